@@ -1,0 +1,139 @@
+/*
+ * mxd_amd.h -- C ABI of the MI355X image resample/crop stage for the mlx-data
+ * Buffer/Stream pipeline.
+ *
+ * The library (mlx-data_amd/libmxd_amd.so) replaces, for the per-pixel hot path
+ * only, these reference interfaces (file:line into ml-explore/mlx-data 0.2.0):
+ *
+ *   core::image::scale(img, double)          mlx/data/core/image/ImageTransform.cpp:33-39
+ *   core::image::resize(img, dw, dh)         mlx/data/core/image/ImageTransform.cpp:41-62
+ *     -> stbir_resize_uint8_linear(...)       (stb_image_resize2, triangle filter, :7-10,49-60)
+ *   core::image::crop(img, x, y, w, h)       mlx/data/core/image/ImageTransform.cpp:64-73
+ *   core::image::hflip(img)                  mlx/data/core/image/ImageTransform.cpp:123-140
+ *   op::ImageResizeSmallestSide::apply_image mlx/data/op/ImageTransform.cpp:78-94
+ *   op::ImageCenterCrop::apply_image         mlx/data/op/ImageTransform.cpp:115-126
+ *   op::ImageRandomCrop / ImageRandomHFlip   mlx/data/op/ImageTransform.cpp:135-158,323-332
+ *   array::batch (NHWC stack + pad)          mlx/data/Array.cpp:465-498
+ *   x.astype("float32") / 255 (normalize)    benchmarks/comparative/caltech101/mlx_data.py:46
+ *
+ * Conventions: plain pointers and sizes only; every function returns an int
+ * status (MXD_OK == 0) and never throws.  On failure the thread-local message
+ * returned by mxd_last_error() holds the reason, using the reference's own
+ * error strings where the reference has one.  All functions are thread-safe.
+ * Streams are HIP streams passed as void* (NULL = the device's null stream).
+ */
+#ifndef MXD_AMD_H
+#define MXD_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MXD_ABI_VERSION 1
+
+enum mxd_status {
+  MXD_OK = 0,
+  MXD_ERR_INVALID = 1,     /* bad argument (reference: std::runtime_error / invalid_argument) */
+  MXD_ERR_UNSUPPORTED = 2, /* valid for the reference, not supported by this build */
+  MXD_ERR_DEVICE = 3,      /* HIP runtime failure */
+  MXD_ERR_NOMEM = 4
+};
+
+/* Output element type of a resample launch. */
+enum mxd_dtype {
+  MXD_U8 = 0,          /* uint8, as core::image::resize + crop produce */
+  MXD_F32_DIV255 = 1   /* float32 q/255.0f of the uint8 result, bit-exact to the
+                          NumPy x.astype("float32")/255 the reference benchmark runs */
+};
+
+/*
+ * One image of a batch: source HWC uint8 in device memory, the resize target
+ * (the dims core::image::scale / resize would produce), the crop window inside
+ * the resized image, and where the (crop_h x crop_w x channels) result goes.
+ *
+ *   src          device pointer to the first byte of row 0
+ *   src_stride   bytes between source rows (>= src_w*channels)
+ *   resize_w/h   resized dims, >= 1 (reference: verify_dimensions, ImageTransform.cpp:23-31)
+ *   crop_x/y/w/h window in resized coordinates; must lie inside the resized image
+ *                (reference: ImageCenterCrop :119-122, array::sub Array.cpp:558-566)
+ *   flip         nonzero: mirror the cropped result horizontally (core::image::hflip)
+ *   dst          device pointer to row 0 of the output image
+ *   dst_stride   bytes between output rows
+ */
+typedef struct mxd_image {
+  const uint8_t* src;
+  int64_t src_stride;
+  int32_t src_w, src_h, channels;
+  int32_t resize_w, resize_h;
+  int32_t crop_x, crop_y, crop_w, crop_h;
+  int32_t flip;
+  void* dst;
+  int64_t dst_stride;
+} mxd_image;
+
+/* ---- library / errors ------------------------------------------------- */
+int mxd_abi_version(void);
+const char* mxd_last_error(void);
+int mxd_device_count(int* count);
+
+/* ---- reference geometry (host only, no device needed) ------------------ */
+
+/* ImageResizeSmallestSide + core::image::scale: target dims of resizing the
+ * smaller side of (w, h) to `size` (lround of a double scale). */
+int mxd_resize_smallest_side_dims(int64_t w, int64_t h, int64_t size, int64_t* out_w, int64_t* out_h);
+
+/* ImageCenterCrop: origin of a (cw x ch) centre crop of a (w x h) image. */
+int mxd_center_crop_origin(int64_t w, int64_t h, int64_t cw, int64_t ch, int64_t* x, int64_t* y);
+
+/* Resampling taps of one axis for output pixels [crop_off, crop_off+crop_len)
+ * of an in_size -> out_size resize: first input index, tap count and weights
+ * (row-major [crop_len][max_taps], zero padded).  *taps_needed receives the
+ * widest tap count; if it exceeds max_taps nothing is written and
+ * MXD_ERR_INVALID is returned. */
+int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t crop_len, int32_t max_taps,
+                  int32_t* first, int32_t* ntaps, float* weights, int32_t* taps_needed);
+
+/* ---- the hot path -------------------------------------------------------- */
+
+/* Fused resize + crop (+ flip) (+ /255 normalize) of n images on `device`,
+ * enqueued on `stream`.  One kernel launch per call; inputs and outputs are in
+ * device memory.  Asynchronous: returns once the work is enqueued. */
+int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream);
+
+/* ---- device memory / streams / events (so a C or C++ host needs no torch) */
+int mxd_set_device(int32_t device);
+int mxd_malloc_device(void** ptr, size_t bytes, int32_t device);
+int mxd_free_device(void* ptr, int32_t device);
+int mxd_malloc_pinned(void** ptr, size_t bytes);
+int mxd_free_pinned(void* ptr);
+int mxd_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);
+int mxd_memcpy_d2h_async(void* dst, const void* src, size_t bytes, void* stream);
+/* 2-D copy: rows of `width` bytes, host pitch spitch -> device pitch dpitch. */
+int mxd_memcpy2d_h2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                           void* stream);
+int mxd_memset_async(void* dst, int value, size_t bytes, void* stream);
+int mxd_stream_create(int32_t device, void** stream);
+int mxd_stream_destroy(void* stream);
+int mxd_stream_synchronize(void* stream);
+int mxd_event_create(void** event);
+int mxd_event_destroy(void* event);
+int mxd_event_record(void* event, void* stream);
+int mxd_event_synchronize(void* event);
+int mxd_event_elapsed_ms(float* ms, void* start, void* stop);
+
+/* ---- host-resident convenience path ------------------------------------ */
+
+/* Host image in, host result out: pinned staging, H2D, fused kernel, D2H on
+ * the calling thread's per-device stream; synchronous.  `images[i].src` and
+ * `images[i].dst` are HOST pointers here.  This is the path the C++ pipeline
+ * ops use when samples live in host memory (mlx-data's default). */
+int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MXD_AMD_H */

@@ -1,0 +1,521 @@
+// capi.cpp -- the C ABI declared in include/mxd_amd.h.
+//
+// Host side of the fused resize+crop stage: validation with the reference's
+// error conditions, per-device caches of the axis tap tables, tiling, a
+// per-stream descriptor workspace, and the launch.  No exceptions cross the
+// ABI: every entry point returns a status and leaves a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "mxd_amd.h"
+#include "resample.h"
+#include "taps.h"
+
+using mxd::ImgDev;
+using mxd::LaunchCfg;
+
+namespace {
+
+thread_local std::string g_error;
+
+int fail(int code, const std::string& msg) {
+  g_error = msg;
+  return code;
+}
+
+#define MXD_HIP(expr)                                                                                    \
+  do {                                                                                                   \
+    hipError_t e_ = (expr);                                                                              \
+    if (e_ != hipSuccess) return fail(MXD_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Restores the calling thread's current device on scope exit.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Device tap tables: one per (device, in_size, out_size), covering every
+// output pixel of the axis, so any crop window is a pointer offset into it.
+struct DevTable {
+  float* ptr = nullptr;
+  int32_t width = 0;
+  std::vector<int32_t> first, count;  // host copy for tiling decisions
+};
+
+class TableCache {
+ public:
+  int get(int32_t device, int32_t in, int32_t out, const DevTable** out_tab) {
+    std::lock_guard<std::mutex> lock(mu_);
+    auto key = std::make_tuple(device, in, out);
+    auto it = map_.find(key);
+    if (it != map_.end()) {
+      *out_tab = it->second.get();
+      return MXD_OK;
+    }
+    mxd::AxisTaps taps;
+    if (!mxd::build_axis_taps(in, out, 0, out, &taps))
+      return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension");
+    const int32_t stride = mxd::kTapHeader + taps.width;
+    std::vector<float> host((size_t)out * stride, 0.0f);
+    for (int32_t i = 0; i < out; i++) {
+      float* e = &host[(size_t)i * stride];
+      std::memcpy(&e[0], &taps.first[i], 4);
+      std::memcpy(&e[1], &taps.count[i], 4);
+      std::memcpy(&e[2], &taps.weight[(size_t)i * taps.width], sizeof(float) * taps.width);
+    }
+    auto tab = std::make_unique<DevTable>();
+    tab->width = taps.width;
+    tab->first = taps.first;
+    tab->count = taps.count;
+    DeviceGuard g(device);
+    MXD_HIP(hipMalloc(&tab->ptr, host.size() * sizeof(float)));
+    MXD_HIP(hipMemcpy(tab->ptr, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    *out_tab = tab.get();
+    map_[key] = std::move(tab);
+    return MXD_OK;
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<std::tuple<int32_t, int32_t, int32_t>, std::unique_ptr<DevTable>> map_;
+};
+
+TableCache& tables() {
+  static TableCache* c = new TableCache();  // leaked on purpose: outlives static teardown
+  return *c;
+}
+
+// ---------------------------------------------------------------------------
+// Per-(device, stream) descriptor workspace: pinned staging + device copy of
+// the ImgDev array.  Re-uploads are skipped when the batch is unchanged.
+struct Workspace {
+  std::mutex mu;
+  ImgDev* host = nullptr;  // pinned
+  ImgDev* dev = nullptr;
+  size_t cap = 0;
+  size_t count = 0;
+  hipEvent_t copied = nullptr;
+};
+
+class WorkspacePool {
+ public:
+  Workspace* get(int32_t device, void* stream) {
+    std::lock_guard<std::mutex> lock(mu_);
+    auto& w = map_[std::make_pair(device, stream)];
+    if (!w) w = std::make_unique<Workspace>();
+    return w.get();
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<std::pair<int32_t, void*>, std::unique_ptr<Workspace>> map_;
+};
+
+WorkspacePool& workspaces() {
+  static WorkspacePool* p = new WorkspacePool();
+  return *p;
+}
+
+// ---------------------------------------------------------------------------
+// Tiling.
+constexpr int32_t kTileRows = 32;          // output rows per tile
+constexpr int32_t kStripBytes = 1536;      // target source-footprint bytes per strip row
+constexpr int32_t kLdsBudget = 40 * 1024;  // bytes of LDS for the f32 row group
+
+int32_t strip_chunks(const DevTable& xt, int32_t crop_x, int32_t crop_w, int32_t ox0, int32_t ox1, bool flip,
+                     int32_t c, int32_t vec) {
+  const int32_t xa = flip ? crop_w - ox1 : ox0;
+  const int32_t xb = flip ? crop_w - 1 - ox0 : ox1 - 1;
+  const int32_t lo = xt.first[crop_x + xa];
+  const int32_t hi = xt.first[crop_x + xb] + xt.count[crop_x + xb] - 1;
+  const int32_t fb0 = (lo * c) & ~(vec - 1);
+  return ((hi + 1) * c - fb0 + vec - 1) / vec;
+}
+
+int validate(const mxd_image& im, int32_t i) {
+  const std::string at = " (image " + std::to_string(i) + ")";
+  if (!im.src || !im.dst) return fail(MXD_ERR_INVALID, "mxd: null src/dst pointer" + at);
+  if (im.src_w <= 0 || im.src_h <= 0)
+    return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
+  if (im.channels <= 0 || im.channels > 4)
+    return fail(MXD_ERR_INVALID, "verifyImage: channels must be 0 <= c <= 4" + at);
+  if (im.channels == 4)
+    return fail(MXD_ERR_UNSUPPORTED, "mxd: 4-channel (STBIR_RGBA alpha-weighted) resize not supported" + at);
+  if (im.resize_w <= 0 || im.resize_h <= 0 || im.crop_w <= 0 || im.crop_h <= 0)
+    return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
+  if (im.crop_x < 0 || im.crop_y < 0 || im.crop_x >= im.resize_w || im.crop_y >= im.resize_h)
+    return fail(MXD_ERR_INVALID, "Array: sub: offset out of bound" + at);
+  if (im.crop_x + im.crop_w > im.resize_w || im.crop_y + im.crop_h > im.resize_h)
+    return fail(MXD_ERR_INVALID, "Array: sub: shape out of bound" + at);
+  if (im.src_stride < (int64_t)im.src_w * im.channels)
+    return fail(MXD_ERR_INVALID, "mxd: src_stride smaller than a row" + at);
+  return MXD_OK;
+}
+
+int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
+  if (n == 0) return MXD_OK;
+  const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
+  const int32_t channels = images[0].channels;
+  bool aligned = true;
+  for (int32_t i = 0; i < n; i++) {
+    if (int rc = validate(images[i], i)) return rc;
+    if (images[i].channels != channels)
+      return fail(MXD_ERR_INVALID, "mxd: all images of a batch must have the same channel count");
+    if (images[i].dst_stride < (int64_t)images[i].crop_w * channels * elem)
+      return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+    aligned = aligned && ((reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride) & 15) == 0;
+  }
+  const int32_t vec = aligned ? 16 : 1;
+
+  LaunchCfg cfg{};
+  cfg.vec = vec;
+  cfg.channels = channels;
+  cfg.f32 = out_dtype == MXD_F32_DIV255;
+  cfg.nimgs = n;
+  std::vector<ImgDev> descs(n);
+  int32_t tiles = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    const DevTable *xt = nullptr, *yt = nullptr;
+    if (int rc = tables().get(device, im.src_w, im.resize_w, &xt)) return rc;
+    if (int rc = tables().get(device, im.src_h, im.resize_h, &yt)) return rc;
+    const bool flip = im.flip != 0;
+    // Column strips: enough that one strip row's footprint is ~kStripBytes.
+    const int32_t full = strip_chunks(*xt, im.crop_x, im.crop_w, 0, im.crop_w, flip, channels, 1);
+    int32_t nstrips = std::max<int32_t>(1, (full + kStripBytes - 1) / kStripBytes);
+    int32_t tx = (im.crop_w + nstrips - 1) / nstrips;
+    tx = std::min<int32_t>(im.crop_w, (tx + 3) & ~3);
+    nstrips = (im.crop_w + tx - 1) / tx;
+    int32_t max_chunks = 0;
+    for (int32_t s = 0; s < nstrips; s++) {
+      const int32_t ox0 = s * tx, ox1 = std::min(ox0 + tx, im.crop_w);
+      max_chunks = std::max(max_chunks, strip_chunks(*xt, im.crop_x, im.crop_w, ox0, ox1, flip, channels, vec));
+    }
+    const int32_t vw = (max_chunks * vec + 3) & ~3;
+    const int32_t ty = std::min(kTileRows, im.crop_h);
+    int32_t group = std::max<int32_t>(1, std::min<int32_t>(8, 512 / std::max(1, max_chunks)));
+    group = std::max<int32_t>(1, std::min<int32_t>(group, kLdsBudget / (vw * 4)));
+    group = std::min(group, ty);
+    const int32_t nbands = (im.crop_h + ty - 1) / ty;
+
+    ImgDev& d = descs[i];
+    d.src = im.src;
+    d.src_stride = im.src_stride;
+    d.dst = im.dst;
+    d.dst_stride = im.dst_stride;
+    d.xwidth = xt->width;
+    d.ywidth = yt->width;
+    d.xtab = xt->ptr + (size_t)im.crop_x * (mxd::kTapHeader + xt->width);
+    d.ytab = yt->ptr + (size_t)im.crop_y * (mxd::kTapHeader + yt->width);
+    d.crop_w = im.crop_w;
+    d.crop_h = im.crop_h;
+    d.flip = flip ? 1 : 0;
+    d.tile_begin = tiles;
+    d.nstrips = nstrips;
+    d.ty = ty;
+    d.tx = tx;
+    d.group = group;
+    tiles += nbands * nstrips;
+    cfg.max_tx = std::max(cfg.max_tx, tx);
+    cfg.max_ty = std::max(cfg.max_ty, ty);
+    cfg.max_xw = std::max(cfg.max_xw, xt->width);
+    cfg.max_yw = std::max(cfg.max_yw, yt->width);
+    cfg.max_vw = std::max(cfg.max_vw, vw);
+    cfg.max_group = std::max(cfg.max_group, group);
+  }
+  cfg.ntiles = tiles;
+  if (mxd::resample_smem_bytes(cfg) > 160 * 1024) return fail(MXD_ERR_UNSUPPORTED, "mxd: tile does not fit in LDS");
+
+  DeviceGuard guard(device);
+  Workspace* ws = workspaces().get(device, stream);
+  std::lock_guard<std::mutex> lock(ws->mu);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t bytes = sizeof(ImgDev) * (size_t)n;
+  const bool same = ws->count == (size_t)n && ws->host && std::memcmp(ws->host, descs.data(), bytes) == 0;
+  if (!same) {
+    if (ws->copied) MXD_HIP(hipEventSynchronize(ws->copied));  // staging no longer read
+    if ((size_t)n > ws->cap) {
+      if (ws->dev) {
+        MXD_HIP(hipStreamSynchronize(s));
+        MXD_HIP(hipFree(ws->dev));
+        MXD_HIP(hipHostFree(ws->host));
+        ws->dev = nullptr;
+        ws->host = nullptr;
+      }
+      const size_t cap = std::max<size_t>(n, 64);
+      MXD_HIP(hipMalloc(reinterpret_cast<void**>(&ws->dev), sizeof(ImgDev) * cap));
+      MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws->host), sizeof(ImgDev) * cap, hipHostMallocDefault));
+      ws->cap = cap;
+    }
+    if (!ws->copied) MXD_HIP(hipEventCreateWithFlags(&ws->copied, hipEventDisableTiming));
+    std::memcpy(ws->host, descs.data(), bytes);
+    MXD_HIP(hipMemcpyAsync(ws->dev, ws->host, bytes, hipMemcpyHostToDevice, s));
+    MXD_HIP(hipEventRecord(ws->copied, s));
+    ws->count = n;
+  }
+  if (int rc = mxd::launch_resample(cfg, ws->dev, stream))
+    return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
+                                    " rc=" + std::to_string(rc));
+  return MXD_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Host-resident path: per-(thread, device) stream + growable buffers.
+struct HostCtx {
+  hipStream_t stream = nullptr;
+  uint8_t* pin_in = nullptr;
+  size_t pin_in_cap = 0;
+  uint8_t* pin_out = nullptr;
+  size_t pin_out_cap = 0;
+  uint8_t* dev_in = nullptr;
+  size_t dev_in_cap = 0;
+  uint8_t* dev_out = nullptr;
+  size_t dev_out_cap = 0;
+};
+
+int grow_pinned(uint8_t** p, size_t* cap, size_t need) {
+  if (need <= *cap) return MXD_OK;
+  if (*p) MXD_HIP(hipHostFree(*p));
+  *p = nullptr;
+  const size_t c = std::max(need, *cap * 2);
+  MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(p), c, hipHostMallocDefault));
+  *cap = c;
+  return MXD_OK;
+}
+
+int grow_device(uint8_t** p, size_t* cap, size_t need) {
+  if (need <= *cap) return MXD_OK;
+  if (*p) MXD_HIP(hipFree(*p));
+  *p = nullptr;
+  const size_t c = std::max(need, *cap * 2);
+  MXD_HIP(hipMalloc(reinterpret_cast<void**>(p), c));
+  *cap = c;
+  return MXD_OK;
+}
+
+HostCtx& host_ctx(int32_t device) {
+  thread_local std::map<int32_t, HostCtx> ctx;
+  return ctx[device];
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxd_abi_version(void) { return MXD_ABI_VERSION; }
+
+const char* mxd_last_error(void) { return g_error.c_str(); }
+
+int mxd_device_count(int* count) {
+  if (!count) return fail(MXD_ERR_INVALID, "mxd: null count");
+  MXD_HIP(hipGetDeviceCount(count));
+  return MXD_OK;
+}
+
+int mxd_resize_smallest_side_dims(int64_t w, int64_t h, int64_t size, int64_t* out_w, int64_t* out_h) {
+  if (!out_w || !out_h) return fail(MXD_ERR_INVALID, "mxd: null output");
+  if (size <= 0)
+    return fail(MXD_ERR_INVALID, "ImageResizeSmallestSide: illegal target size: " + std::to_string(size));
+  if (w <= 0 || h <= 0) return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension");
+  mxd::smallest_side_dims(w, h, size, out_w, out_h);
+  return MXD_OK;
+}
+
+int mxd_center_crop_origin(int64_t w, int64_t h, int64_t cw, int64_t ch, int64_t* x, int64_t* y) {
+  if (!x || !y) return fail(MXD_ERR_INVALID, "mxd: null output");
+  if (ch > h || cw > w) return fail(MXD_ERR_INVALID, "ImageCenterCrop: target image size larger than input image");
+  *x = (w - cw) / 2;
+  *y = (h - ch) / 2;
+  return MXD_OK;
+}
+
+int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t crop_len, int32_t max_taps,
+                  int32_t* first, int32_t* ntaps, float* weights, int32_t* taps_needed) {
+  mxd::AxisTaps t;
+  if (!mxd::build_axis_taps(in_size, out_size, crop_off, crop_len, &t))
+    return fail(MXD_ERR_INVALID, "mxd: invalid axis geometry");
+  if (taps_needed) *taps_needed = t.width;
+  if (t.width > max_taps) return fail(MXD_ERR_INVALID, "mxd: max_taps too small");
+  if (!first || !ntaps || !weights) return fail(MXD_ERR_INVALID, "mxd: null output");
+  for (int32_t i = 0; i < crop_len; i++) {
+    first[i] = t.first[i];
+    ntaps[i] = t.count[i];
+    for (int32_t k = 0; k < max_taps; k++)
+      weights[(size_t)i * max_taps + k] = k < t.width ? t.weight[(size_t)i * t.width + k] : 0.0f;
+  }
+  return MXD_OK;
+}
+
+int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
+  return run_batch(images, n, out_dtype, device, stream);
+}
+
+int mxd_set_device(int32_t device) {
+  MXD_HIP(hipSetDevice(device));
+  return MXD_OK;
+}
+
+int mxd_malloc_device(void** ptr, size_t bytes, int32_t device) {
+  if (!ptr) return fail(MXD_ERR_INVALID, "mxd: null ptr");
+  DeviceGuard g(device);
+  MXD_HIP(hipMalloc(ptr, bytes));
+  return MXD_OK;
+}
+
+int mxd_free_device(void* ptr, int32_t device) {
+  DeviceGuard g(device);
+  MXD_HIP(hipFree(ptr));
+  return MXD_OK;
+}
+
+int mxd_malloc_pinned(void** ptr, size_t bytes) {
+  if (!ptr) return fail(MXD_ERR_INVALID, "mxd: null ptr");
+  MXD_HIP(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+  return MXD_OK;
+}
+
+int mxd_free_pinned(void* ptr) {
+  MXD_HIP(hipHostFree(ptr));
+  return MXD_OK;
+}
+
+int mxd_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+  MXD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_memcpy_d2h_async(void* dst, const void* src, size_t bytes, void* stream) {
+  MXD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_memcpy2d_h2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                           void* stream) {
+  MXD_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyHostToDevice,
+                           reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_memset_async(void* dst, int value, size_t bytes, void* stream) {
+  MXD_HIP(hipMemsetAsync(dst, value, bytes, reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_stream_create(int32_t device, void** stream) {
+  if (!stream) return fail(MXD_ERR_INVALID, "mxd: null stream");
+  DeviceGuard g(device);
+  hipStream_t s = nullptr;
+  MXD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return MXD_OK;
+}
+
+int mxd_stream_destroy(void* stream) {
+  MXD_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_stream_synchronize(void* stream) {
+  MXD_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_event_create(void** event) {
+  if (!event) return fail(MXD_ERR_INVALID, "mxd: null event");
+  hipEvent_t e = nullptr;
+  MXD_HIP(hipEventCreate(&e));
+  *event = e;
+  return MXD_OK;
+}
+
+int mxd_event_destroy(void* event) {
+  MXD_HIP(hipEventDestroy(reinterpret_cast<hipEvent_t>(event)));
+  return MXD_OK;
+}
+
+int mxd_event_record(void* event, void* stream) {
+  MXD_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(event), reinterpret_cast<hipStream_t>(stream)));
+  return MXD_OK;
+}
+
+int mxd_event_synchronize(void* event) {
+  MXD_HIP(hipEventSynchronize(reinterpret_cast<hipEvent_t>(event)));
+  return MXD_OK;
+}
+
+int mxd_event_elapsed_ms(float* ms, void* start, void* stop) {
+  if (!ms) return fail(MXD_ERR_INVALID, "mxd: null ms");
+  MXD_HIP(hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start), reinterpret_cast<hipEvent_t>(stop)));
+  return MXD_OK;
+}
+
+int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (n == 0) return MXD_OK;
+  const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
+  for (int32_t i = 0; i < n; i++)
+    if (int rc = validate(images[i], i)) return rc;
+  DeviceGuard g(device);
+  HostCtx& ctx = host_ctx(device);
+  if (!ctx.stream) MXD_HIP(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+  // Pack every source with a 16-byte aligned pitch so the vector path applies.
+  std::vector<size_t> in_off(n), out_off(n);
+  std::vector<int64_t> pitch(n);
+  size_t in_bytes = 0, out_bytes = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    pitch[i] = ((int64_t)im.src_w * im.channels + 15) & ~(int64_t)15;
+    in_off[i] = in_bytes;
+    in_bytes += ((size_t)pitch[i] * im.src_h + 255) & ~(size_t)255;
+    out_off[i] = out_bytes;
+    out_bytes += ((size_t)im.crop_w * im.channels * elem * im.crop_h + 255) & ~(size_t)255;
+  }
+  if (int rc = grow_pinned(&ctx.pin_in, &ctx.pin_in_cap, in_bytes)) return rc;
+  if (int rc = grow_pinned(&ctx.pin_out, &ctx.pin_out_cap, out_bytes)) return rc;
+  if (int rc = grow_device(&ctx.dev_in, &ctx.dev_in_cap, in_bytes)) return rc;
+  if (int rc = grow_device(&ctx.dev_out, &ctx.dev_out_cap, out_bytes)) return rc;
+  std::vector<mxd_image> dev_imgs(images, images + n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    const size_t row = (size_t)im.src_w * im.channels;
+    uint8_t* stage = ctx.pin_in + in_off[i];
+    for (int32_t r = 0; r < im.src_h; r++) std::memcpy(stage + (size_t)r * pitch[i], im.src + (size_t)r * im.src_stride, row);
+    dev_imgs[i].src = ctx.dev_in + in_off[i];
+    dev_imgs[i].src_stride = pitch[i];
+    dev_imgs[i].dst = ctx.dev_out + out_off[i];
+    dev_imgs[i].dst_stride = (int64_t)im.crop_w * im.channels * elem;
+  }
+  MXD_HIP(hipMemcpyAsync(ctx.dev_in, ctx.pin_in, in_bytes, hipMemcpyHostToDevice, ctx.stream));
+  if (int rc = run_batch(dev_imgs.data(), n, out_dtype, device, ctx.stream)) return rc;
+  MXD_HIP(hipMemcpyAsync(ctx.pin_out, ctx.dev_out, out_bytes, hipMemcpyDeviceToHost, ctx.stream));
+  MXD_HIP(hipStreamSynchronize(ctx.stream));
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    const size_t row = (size_t)im.crop_w * im.channels * elem;
+    uint8_t* d = static_cast<uint8_t*>(im.dst);
+    const uint8_t* s = ctx.pin_out + out_off[i];
+    for (int32_t r = 0; r < im.crop_h; r++) std::memcpy(d + (size_t)r * im.dst_stride, s + r * row, row);
+  }
+  return MXD_OK;
+}
+
+}  // extern "C"

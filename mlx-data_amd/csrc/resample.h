@@ -1,0 +1,45 @@
+// resample.h -- device-side descriptors shared by capi.cpp and resample.hip.
+#pragma once
+
+#include <cstdint>
+
+namespace mxd {
+
+// One entry of a per-axis tap table in device memory: the first input index
+// and tap count stored as int bits, then `width` f32 weights.
+constexpr int kTapHeader = 2;
+
+// Per-image parameters, resolved by the host (geometry already validated).
+// Each image is cut into nbands x nstrips tiles of ty output rows x tx output
+// columns; tiles of all images are numbered consecutively from tile_begin.
+struct ImgDev {
+  const uint8_t* src;
+  int64_t src_stride;
+  void* dst;
+  int64_t dst_stride;
+  const float* ytab;  // crop_h entries of (kTapHeader + ywidth) floats
+  const float* xtab;  // crop_w entries of (kTapHeader + xwidth) floats
+  int32_t ywidth, xwidth;
+  int32_t crop_w, crop_h;
+  int32_t flip;
+  int32_t tile_begin;
+  int32_t nstrips, ty, tx, group;
+};
+static_assert(sizeof(ImgDev) == 88, "ImgDev layout");
+
+struct LaunchCfg {
+  int32_t vec;        // bytes per thread per source row: 16 (16-byte aligned rows) or 1
+  int32_t channels;   // 1..3
+  int32_t f32;        // output f32 /255
+  int32_t nimgs;
+  int32_t ntiles;
+  int32_t max_tx, max_ty, max_xw, max_yw, max_vw, max_group;
+};
+
+// Dynamic LDS bytes the kernel needs for cfg.
+int resample_smem_bytes(const LaunchCfg& cfg);
+
+// Enqueues the fused kernel; imgs is a device pointer to cfg.nimgs entries.
+int launch_resample(const LaunchCfg& cfg, const ImgDev* imgs, void* stream);
+
+}  // namespace mxd

@@ -1,0 +1,222 @@
+"""ctypes binding of the C ABI in include/mxd_amd.h (libmxd_amd.so).
+
+This is the Python-side stub a maintainer would add to bind the library
+(INTEGRATION.md); the C++ pipeline binds the same symbols directly.  Loading
+fails loudly when the library is missing: there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libmxd_amd.so")
+
+MXD_OK = 0
+MXD_U8 = 0
+MXD_F32_DIV255 = 1
+
+# Every symbol include/mxd_amd.h declares.
+EXPORTS = (
+    "mxd_abi_version", "mxd_last_error", "mxd_device_count",
+    "mxd_resize_smallest_side_dims", "mxd_center_crop_origin", "mxd_axis_taps",
+    "mxd_resize_crop_batch",
+    "mxd_set_device", "mxd_malloc_device", "mxd_free_device", "mxd_malloc_pinned", "mxd_free_pinned",
+    "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
+    "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
+    "mxd_event_create", "mxd_event_destroy", "mxd_event_record", "mxd_event_synchronize", "mxd_event_elapsed_ms",
+    "mxd_resize_crop_host",
+)
+
+
+class MxdImage(ctypes.Structure):
+    """struct mxd_image (include/mxd_amd.h)."""
+
+    _fields_ = [
+        ("src", ctypes.c_void_p),
+        ("src_stride", ctypes.c_int64),
+        ("src_w", ctypes.c_int32),
+        ("src_h", ctypes.c_int32),
+        ("channels", ctypes.c_int32),
+        ("resize_w", ctypes.c_int32),
+        ("resize_h", ctypes.c_int32),
+        ("crop_x", ctypes.c_int32),
+        ("crop_y", ctypes.c_int32),
+        ("crop_w", ctypes.c_int32),
+        ("crop_h", ctypes.c_int32),
+        ("flip", ctypes.c_int32),
+        ("dst", ctypes.c_void_p),
+        ("dst_stride", ctypes.c_int64),
+    ]
+
+
+class MxdError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() or `make -C mlx-data_amd`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.mxd_last_error.restype = ctypes.c_char_p
+        for name in ("mxd_malloc_pinned", "mxd_free_pinned", "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async",
+                     "mxd_memset_async"):
+            getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != MXD_OK:
+        raise MxdError(rc, lib().mxd_last_error().decode())
+    return rc
+
+
+def resize_smallest_side_dims(w, h, size):
+    tw, th = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().mxd_resize_smallest_side_dims(ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_int64(size),
+                                              ctypes.byref(tw), ctypes.byref(th)))
+    return tw.value, th.value
+
+
+def center_crop_origin(w, h, cw, ch):
+    x, y = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().mxd_center_crop_origin(ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_int64(cw),
+                                       ctypes.c_int64(ch), ctypes.byref(x), ctypes.byref(y)))
+    return x.value, y.value
+
+
+def axis_taps(in_size, out_size, off=0, length=None):
+    """(first[len], ntaps[len], weights[len, width]) of the product tap builder."""
+    length = out_size - off if length is None else length
+    need = ctypes.c_int32()
+    L = lib()
+    rc = L.mxd_axis_taps(in_size, out_size, off, length, 0, None, None, None, ctypes.byref(need))
+    width = need.value
+    if rc != MXD_OK and width <= 0:
+        check(rc)
+    first = np.zeros(length, np.int32)
+    cnt = np.zeros(length, np.int32)
+    w = np.zeros((length, width), np.float32)
+    check(L.mxd_axis_taps(in_size, out_size, off, length, width,
+                          first.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), None))
+    return first, cnt, w
+
+
+def make_images(entries):
+    """entries: iterable of dicts with the mxd_image fields -> ctypes array."""
+    entries = list(entries)
+    arr = (MxdImage * max(1, len(entries)))()
+    for i, e in enumerate(entries):
+        for k, v in e.items():
+            setattr(arr[i], k, v)
+    return arr, len(entries)
+
+
+def resize_crop_batch(images, n, out_dtype, device=0, stream=None):
+    check(lib().mxd_resize_crop_batch(images, n, out_dtype, device, ctypes.c_void_p(stream)))
+
+
+def resize_crop_host(images, n, out_dtype, device=0):
+    check(lib().mxd_resize_crop_host(images, n, out_dtype, device))
+
+
+class Stream:
+    """A HIP stream owned through the C ABI (NULL = the device's null stream)."""
+
+    def __init__(self, device=0):
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().mxd_stream_create(device, ctypes.byref(h)))
+        self.handle = h.value
+
+    def synchronize(self):
+        check(lib().mxd_stream_synchronize(ctypes.c_void_p(self.handle)))
+
+    def close(self):
+        if self.handle:
+            check(lib().mxd_stream_destroy(ctypes.c_void_p(self.handle)))
+            self.handle = None
+
+
+class Event:
+    def __init__(self):
+        h = ctypes.c_void_p()
+        check(lib().mxd_event_create(ctypes.byref(h)))
+        self.handle = h.value
+
+    def record(self, stream):
+        check(lib().mxd_event_record(ctypes.c_void_p(self.handle), ctypes.c_void_p(stream.handle if stream else None)))
+
+    def synchronize(self):
+        check(lib().mxd_event_synchronize(ctypes.c_void_p(self.handle)))
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        check(lib().mxd_event_elapsed_ms(ctypes.byref(ms), ctypes.c_void_p(self.handle), ctypes.c_void_p(end.handle)))
+        return ms.value
+
+    def close(self):
+        if self.handle:
+            check(lib().mxd_event_destroy(ctypes.c_void_p(self.handle)))
+            self.handle = None
+
+
+class DeviceBuffer:
+    """Raw device allocation with numpy upload/download helpers."""
+
+    def __init__(self, nbytes, device=0):
+        self.device = device
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().mxd_malloc_device(ctypes.byref(p), ctypes.c_size_t(max(1, self.nbytes)), device))
+        self.ptr = p.value
+
+    def upload(self, arr, offset=0, stream=None):
+        arr = np.ascontiguousarray(arr)
+        check(lib().mxd_memcpy_h2d_async(ctypes.c_void_p(self.ptr + offset), arr.ctypes.data_as(ctypes.c_void_p),
+                                         ctypes.c_size_t(arr.nbytes), ctypes.c_void_p(stream.handle if stream else None)))
+        if stream is not None:
+            stream.synchronize()
+        else:
+            check(lib().mxd_stream_synchronize(ctypes.c_void_p(None)))
+
+    def download(self, shape, dtype, offset=0, stream=None):
+        out = np.empty(shape, dtype)
+        check(lib().mxd_memcpy_d2h_async(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(self.ptr + offset),
+                                         ctypes.c_size_t(out.nbytes), ctypes.c_void_p(stream.handle if stream else None)))
+        if stream is not None:
+            stream.synchronize()
+        else:
+            check(lib().mxd_stream_synchronize(ctypes.c_void_p(None)))
+        return out
+
+    def memset(self, value, stream=None):
+        check(lib().mxd_memset_async(ctypes.c_void_p(self.ptr), value, ctypes.c_size_t(self.nbytes),
+                                     ctypes.c_void_p(stream.handle if stream else None)))
+
+    def free(self):
+        if self.ptr:
+            check(lib().mxd_free_device(ctypes.c_void_p(self.ptr), self.device))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def device_count():
+    n = ctypes.c_int()
+    rc = lib().mxd_device_count(ctypes.byref(n))
+    return n.value if rc == MXD_OK else 0

@@ -1,0 +1,52 @@
+"""Batched image functions over the C ABI (host numpy in, numpy out).
+
+These are the functional counterparts of the reference's per-image
+core::image::{scale, resize, crop, hflip} (mlx/data/core/image/ImageTransform.cpp)
+applied to a whole batch in one fused kernel launch; geometry follows
+ImageResizeSmallestSide / ImageCenterCrop (mlx/data/op/ImageTransform.cpp:78-126).
+"""
+import numpy as np
+
+from . import capi
+
+
+def plan_resize_smallest_side_center_crop(w, h, size, cw, ch):
+    """(resize_w, resize_h, crop_x, crop_y) exactly as the reference computes them."""
+    tw, th = capi.resize_smallest_side_dims(w, h, size)
+    x, y = capi.center_crop_origin(tw, th, cw, ch)
+    return tw, th, x, y
+
+
+def resize_crop(images, geoms, out_dtype="uint8", device=0):
+    """Host-resident fused path.
+
+    images: list of (H, W, C) uint8 arrays.
+    geoms:  list of (resize_w, resize_h, crop_x, crop_y, crop_w, crop_h, flip).
+    Returns a list of (crop_h, crop_w, C) arrays (uint8, or float32 q/255).
+    """
+    f32 = out_dtype in ("float32", np.float32)
+    outs, entries = [], []
+    keep = []
+    for img, g in zip(images, geoms):
+        img = np.ascontiguousarray(img, np.uint8)
+        if img.ndim == 2:
+            img = img[:, :, None]
+        rw, rh, x, y, cw, ch, flip = g
+        out = np.empty((ch, cw, img.shape[2]), np.float32 if f32 else np.uint8)
+        keep.append(img)
+        outs.append(out)
+        entries.append(dict(src=img.ctypes.data, src_stride=img.strides[0], src_w=img.shape[1], src_h=img.shape[0],
+                            channels=img.shape[2], resize_w=rw, resize_h=rh, crop_x=x, crop_y=y, crop_w=cw,
+                            crop_h=ch, flip=int(bool(flip)), dst=out.ctypes.data, dst_stride=out.strides[0]))
+    arr, n = capi.make_images(entries)
+    capi.resize_crop_host(arr, n, capi.MXD_F32_DIV255 if f32 else capi.MXD_U8, device)
+    return outs
+
+
+def resize_smallest_side_center_crop(images, size, cw, ch, out_dtype="uint8", device=0):
+    geoms = []
+    for img in images:
+        h, w = img.shape[:2]
+        tw, th, x, y = plan_resize_smallest_side_center_crop(w, h, size, cw, ch)
+        geoms.append((tw, th, x, y, cw, ch, 0))
+    return resize_crop(images, geoms, out_dtype, device)

@@ -1,0 +1,174 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes/numpy face of the CPU oracle.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg
+import this module.  The product path (mlx-data_amd/) never does.
+
+* ``liboracle.so`` (stbir_oracle.c): CPU restatement of
+  core::image::scale/resize/crop/hflip, array::batch and the /255 normalize
+  (reference file:line citations in stbir_oracle.c).  Resize arithmetic is
+  "parity unpinned" by the reference (stb_image_resize2 is not in this image);
+  see DESIGN.md section "Oracle".
+* ``_ref/libmlxref.so`` (ref_harness.cpp + the reference's own Array.cpp,
+  Sample.cpp, core/BatchShape.cpp, core/State.cpp): crop bytes, batch layout
+  and RNG draw streams computed by the reference's code itself.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_f32p = ctypes.POINTER(ctypes.c_float)
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle`")
+        _lib = ctypes.CDLL(path)
+    return _lib
+
+
+def ref_lib():
+    """The reference-code harness, or None when it was never built."""
+    global _ref
+    if _ref is None:
+        path = os.path.join(HERE, "_ref", "libmlxref.so")
+        if not os.path.exists(path):
+            return None
+        _ref = ctypes.CDLL(path)
+    return _ref
+
+
+def _ptr(a, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+def axis_coeffs(in_size, out_size):
+    """(first, last, weights[out, width]) of the restated stbir triangle filter."""
+    L = lib()
+    cw = L.orc_axis_width(in_size, out_size)
+    n0 = np.zeros(out_size, np.int32)
+    n1 = np.zeros(out_size, np.int32)
+    w = np.zeros((out_size, cw), np.float32)
+    rc = L.orc_axis_coeffs(in_size, out_size, cw, _ptr(n0, _i32p), _ptr(n1, _i32p), _ptr(w, _f32p))
+    if rc:
+        raise ValueError("orc_axis_coeffs failed")
+    return n0, n1, w
+
+
+def resize(img, dw, dh):
+    """stbir_resize_uint8_linear restated: (H, W, C) u8 -> (dh, dw, C) u8."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, c = img.shape
+    out = np.zeros((dh, dw, c), np.uint8)
+    if lib().orc_resize_u8(_ptr(img), w, h, c, _ptr(out), dw, dh):
+        raise ValueError("orc_resize_u8 failed")
+    return out
+
+
+def smallest_side_dims(w, h, size):
+    tw, th = ctypes.c_int64(), ctypes.c_int64()
+    if lib().orc_resize_smallest_side_dims(
+        ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_int64(size), ctypes.byref(tw), ctypes.byref(th)
+    ):
+        raise ValueError("ImageResizeSmallestSide: illegal target size")
+    return tw.value, th.value
+
+
+def center_crop_origin(w, h, cw, ch):
+    if ch > h or cw > w:
+        raise ValueError("ImageCenterCrop: target image size larger than input image")
+    return (w - cw) // 2, (h - ch) // 2
+
+
+def crop(img, x, y, cw, ch):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, c = img.shape
+    out = np.zeros((ch, cw, c), np.uint8)
+    if lib().orc_crop_u8(_ptr(img), w, h, c, x, y, cw, ch, _ptr(out)):
+        raise ValueError("crop out of bounds")
+    return out
+
+
+def hflip(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, c = img.shape
+    out = np.zeros_like(img)
+    lib().orc_hflip_u8(_ptr(img), w, h, c, _ptr(out))
+    return out
+
+
+def normalize(q):
+    q = np.ascontiguousarray(q, np.uint8)
+    out = np.zeros(q.shape, np.float32)
+    lib().orc_normalize_u8(_ptr(q), ctypes.c_size_t(q.size), _ptr(out, _f32p))
+    return out
+
+
+def resize_crop(img, size, cw, ch, crop_xy=None, flip=False):
+    """resize_smallest_side(size) -> crop (centre unless crop_xy) -> optional hflip."""
+    h, w = img.shape[:2]
+    tw, th = smallest_side_dims(w, h, size)
+    r = resize(img, tw, th)
+    x, y = center_crop_origin(tw, th, cw, ch) if crop_xy is None else crop_xy
+    out = crop(r, x, y, cw, ch)
+    return hflip(out) if flip else out
+
+
+def batch(arrs, pad=0):
+    """array::batch: stack (H, W, C) u8 arrays into the padded NHWC batch."""
+    shape = [len(arrs)] + [max(a.shape[d] for a in arrs) for d in range(3)]
+    out = np.full(shape, pad, np.uint8)
+    for i, a in enumerate(arrs):
+        out[i, : a.shape[0], : a.shape[1], : a.shape[2]] = a
+    return out
+
+
+# ---- reference-code harness (oracle/_ref) ---------------------------------
+
+
+def ref_crop(img, x, y, cw, ch):
+    R = ref_lib()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, c = img.shape
+    out = np.zeros((ch, cw, c), np.uint8)
+    if R.ref_crop_u8(_ptr(img), w, h, c, x, y, cw, ch, _ptr(out)):
+        raise ValueError("array::sub raised")
+    return out
+
+
+def ref_batch(arrs, pad=0.0):
+    R = ref_lib()
+    arrs = [np.ascontiguousarray(a, np.uint8) for a in arrs]
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * len(arrs))(*[_ptr(a) for a in arrs])
+    shapes = np.array([a.shape for a in arrs], np.int64).reshape(-1)
+    shape = [len(arrs)] + [max(a.shape[d] for a in arrs) for d in range(3)]
+    out = np.zeros(shape, np.uint8)
+    R.ref_batch_u8.restype = ctypes.c_int64
+    n = R.ref_batch_u8(ptrs, _ptr(shapes, _i64p), len(arrs), ctypes.c_double(pad), _ptr(out), ctypes.c_int64(out.size))
+    if n != out.size:
+        raise ValueError("array::batch failed")
+    return out
+
+
+def ref_random_crop_flip(seed, sizes_wh, cw, ch, prob):
+    """Per-sample (x, y, flip) draws of random_crop then random_h_flip after set_state(seed)."""
+    R = ref_lib()
+    wh = np.ascontiguousarray(np.asarray(sizes_wh, np.int64).reshape(-1))
+    n = len(wh) // 2
+    xy = np.zeros(2 * n, np.int64)
+    fl = np.zeros(n, np.int32)
+    R.ref_random_crop_flip_params(
+        ctypes.c_int64(seed), n, _ptr(wh, _i64p), ctypes.c_int64(cw), ctypes.c_int64(ch), ctypes.c_float(prob),
+        _ptr(xy, _i64p), _ptr(fl, _i32p)
+    )
+    return xy.reshape(n, 2), fl

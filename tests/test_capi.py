@@ -1,0 +1,96 @@
+"""CPU-side checks of the C ABI (no device work): the library loads, exports
+every symbol include/mxd_amd.h declares, its host logic (geometry, tap tables,
+argument validation) matches the reference rules and the oracle."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as O
+from mlx_data_amd import capi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    text = open(os.path.join(REPO, "include", "mxd_amd.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mxd_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    L = capi.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(capi.EXPORTS) == syms
+    assert L.mxd_abi_version() == 1
+
+
+@pytest.mark.parametrize("w,h,size", [(1280, 960, 256), (375, 500, 256), (500, 375, 256), (300, 200, 256),
+                                      (3840, 2160, 512), (300, 300, 256), (1, 1, 256), (333, 500, 256),
+                                      (641, 479, 224), (7, 1000, 256)])
+def test_geometry_matches_oracle(w, h, size):
+    assert capi.resize_smallest_side_dims(w, h, size) == O.smallest_side_dims(w, h, size)
+
+
+def test_geometry_errors_use_reference_messages():
+    with pytest.raises(capi.MxdError, match="ImageResizeSmallestSide: illegal target size: 0"):
+        capi.resize_smallest_side_dims(10, 10, 0)
+    with pytest.raises(capi.MxdError, match="ImageCenterCrop: target image size larger than input image"):
+        capi.center_crop_origin(200, 300, 224, 224)
+    assert capi.center_crop_origin(341, 256, 224, 224) == (58, 16)
+
+
+GEOMS = [(1280, 341), (960, 256), (300, 384), (200, 256), (3840, 455), (2160, 256), (3840, 910), (2160, 512),
+         (375, 256), (500, 341), (500, 333), (333, 256), (256, 256), (100, 256), (7, 3), (3, 7), (1, 5), (5, 1),
+         (1000, 999), (999, 1000), (640, 341), (480, 256), (1080, 256), (1920, 455), (2560, 455), (1440, 256)]
+
+
+@pytest.mark.parametrize("i,o", GEOMS)
+def test_tap_tables_bitwise_equal_oracle(i, o):
+    n0, n1, w = O.axis_coeffs(i, o)
+    first, cnt, pw = capi.axis_taps(i, o)
+    assert np.array_equal(first, n0)
+    assert np.array_equal(cnt, n1 - n0 + 1)
+    for j in range(o):
+        k = cnt[j]
+        assert np.array_equal(w[j, :k].view(np.uint32), pw[j, :k].view(np.uint32))
+        assert not pw[j, k:].any()
+
+
+def test_tap_window_is_slice_of_full_axis():
+    f_full, c_full, w_full = capi.axis_taps(1280, 341)
+    f, c, w = capi.axis_taps(1280, 341, 58, 224)
+    assert np.array_equal(f, f_full[58:282]) and np.array_equal(c, c_full[58:282])
+    assert np.array_equal(w[:, : w_full.shape[1]], w_full[58:282, : w.shape[1]])
+
+
+def _one(**kw):
+    e = dict(src=16, src_stride=3 * 100, src_w=100, src_h=80, channels=3, resize_w=100, resize_h=80, crop_x=0,
+             crop_y=0, crop_w=50, crop_h=40, flip=0, dst=16, dst_stride=150)
+    e.update(kw)
+    return capi.make_images([e])
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(crop_w=200), "Array: sub: shape out of bound"),
+    (dict(crop_x=100), "Array: sub: offset out of bound"),
+    (dict(resize_w=0), "image: cannot create image with 0 or negative dimension"),
+    (dict(crop_h=0), "image: cannot create image with 0 or negative dimension"),
+    (dict(channels=0), "verifyImage: channels must be 0 <= c <= 4"),
+    (dict(channels=5), "verifyImage: channels must be 0 <= c <= 4"),
+    (dict(src=0), "null src/dst"),
+])
+def test_batch_validation_rejects_before_touching_the_device(kw, msg):
+    arr, n = _one(**kw)
+    with pytest.raises(capi.MxdError, match=msg):
+        capi.resize_crop_batch(arr, n, capi.MXD_U8)
+
+
+def test_rgba_is_reported_unsupported_not_wrong():
+    arr, n = _one(channels=4, src_stride=400, dst_stride=200)
+    with pytest.raises(capi.MxdError) as e:
+        capi.resize_crop_batch(arr, n, capi.MXD_U8)
+    assert e.value.code == 2
