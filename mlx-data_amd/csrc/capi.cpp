@@ -169,91 +169,19 @@ int validate(const mxd_image& im, int32_t i) {
   return MXD_OK;
 }
 
-int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
-  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
-  if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
-  if (n == 0) return MXD_OK;
-  const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
-  const int32_t channels = images[0].channels;
-  bool aligned = true;
-  for (int32_t i = 0; i < n; i++) {
-    if (int rc = validate(images[i], i)) return rc;
-    if (images[i].channels != channels)
-      return fail(MXD_ERR_INVALID, "mxd: all images of a batch must have the same channel count");
-    if (images[i].dst_stride < (int64_t)images[i].crop_w * channels * elem)
-      return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
-    aligned = aligned && ((reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride) & 15) == 0;
-  }
-  const int32_t vec = aligned ? 16 : 1;
-
-  LaunchCfg cfg{};
-  cfg.vec = vec;
-  cfg.channels = channels;
-  cfg.f32 = out_dtype == MXD_F32_DIV255;
-  cfg.nimgs = n;
-  std::vector<ImgDev> descs(n);
-  int32_t tiles = 0;
-  for (int32_t i = 0; i < n; i++) {
-    const mxd_image& im = images[i];
-    const DevTable *xt = nullptr, *yt = nullptr;
-    if (int rc = tables().get(device, im.src_w, im.resize_w, &xt)) return rc;
-    if (int rc = tables().get(device, im.src_h, im.resize_h, &yt)) return rc;
-    const bool flip = im.flip != 0;
-    // Column strips: enough that one strip row's footprint is ~kStripBytes.
-    const int32_t full = strip_chunks(*xt, im.crop_x, im.crop_w, 0, im.crop_w, flip, channels, 1);
-    int32_t nstrips = std::max<int32_t>(1, (full + kStripBytes - 1) / kStripBytes);
-    int32_t tx = (im.crop_w + nstrips - 1) / nstrips;
-    tx = std::min<int32_t>(im.crop_w, (tx + 3) & ~3);
-    nstrips = (im.crop_w + tx - 1) / tx;
-    int32_t max_chunks = 0;
-    for (int32_t s = 0; s < nstrips; s++) {
-      const int32_t ox0 = s * tx, ox1 = std::min(ox0 + tx, im.crop_w);
-      max_chunks = std::max(max_chunks, strip_chunks(*xt, im.crop_x, im.crop_w, ox0, ox1, flip, channels, vec));
-    }
-    const int32_t vw = (max_chunks * vec + 3) & ~3;
-    const int32_t ty = std::min(kTileRows, im.crop_h);
-    int32_t group = std::max<int32_t>(1, std::min<int32_t>(8, 512 / std::max(1, max_chunks)));
-    group = std::max<int32_t>(1, std::min<int32_t>(group, kLdsBudget / (vw * 4)));
-    group = std::min(group, ty);
-    const int32_t nbands = (im.crop_h + ty - 1) / ty;
-
-    ImgDev& d = descs[i];
-    d.src = im.src;
-    d.src_stride = im.src_stride;
-    d.dst = im.dst;
-    d.dst_stride = im.dst_stride;
-    d.xwidth = xt->width;
-    d.ywidth = yt->width;
-    d.xtab = xt->ptr + (size_t)im.crop_x * (mxd::kTapHeader + xt->width);
-    d.ytab = yt->ptr + (size_t)im.crop_y * (mxd::kTapHeader + yt->width);
-    d.crop_w = im.crop_w;
-    d.crop_h = im.crop_h;
-    d.flip = flip ? 1 : 0;
-    d.tile_begin = tiles;
-    d.nstrips = nstrips;
-    d.ty = ty;
-    d.tx = tx;
-    d.group = group;
-    tiles += nbands * nstrips;
-    cfg.max_tx = std::max(cfg.max_tx, tx);
-    cfg.max_ty = std::max(cfg.max_ty, ty);
-    cfg.max_xw = std::max(cfg.max_xw, xt->width);
-    cfg.max_yw = std::max(cfg.max_yw, yt->width);
-    cfg.max_vw = std::max(cfg.max_vw, vw);
-    cfg.max_group = std::max(cfg.max_group, group);
-  }
-  cfg.ntiles = tiles;
-  if (mxd::resample_smem_bytes(cfg) > 160 * 1024) return fail(MXD_ERR_UNSUPPORTED, "mxd: tile does not fit in LDS");
-
-  DeviceGuard guard(device);
+// Uploads descs to the stream's workspace (skipped when unchanged) and returns
+// the device copy.
+int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream, ImgDev** dev_out,
+                 std::unique_lock<std::mutex>* hold) {
   Workspace* ws = workspaces().get(device, stream);
-  std::lock_guard<std::mutex> lock(ws->mu);
+  *hold = std::unique_lock<std::mutex>(ws->mu);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const size_t bytes = sizeof(ImgDev) * (size_t)n;
-  const bool same = ws->count == (size_t)n && ws->host && std::memcmp(ws->host, descs.data(), bytes) == 0;
+  const size_t n = descs.size();
+  const size_t bytes = sizeof(ImgDev) * n;
+  const bool same = ws->count == n && ws->host && std::memcmp(ws->host, descs.data(), bytes) == 0;
   if (!same) {
     if (ws->copied) MXD_HIP(hipEventSynchronize(ws->copied));  // staging no longer read
-    if ((size_t)n > ws->cap) {
+    if (n > ws->cap) {
       if (ws->dev) {
         MXD_HIP(hipStreamSynchronize(s));
         MXD_HIP(hipFree(ws->dev));
@@ -272,7 +200,176 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventRecord(ws->copied, s));
     ws->count = n;
   }
-  if (int rc = mxd::launch_resample(cfg, ws->dev, stream))
+  *dev_out = ws->dev;
+  return MXD_OK;
+}
+
+struct ImgPlan {
+  const DevTable* xt = nullptr;
+  const DevTable* yt = nullptr;
+  int32_t bucket = -1;   // wave path tap bucket, -1 = not eligible
+  int32_t nstrips = 0, tx = 0;
+};
+
+// Wave path strips: <= 64 output columns and <= wave_row_bytes() of source
+// footprint each (the kernel's fb0 alignment included).
+bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int32_t* tx) {
+  const int32_t c = im.channels, row = mxd::wave_row_bytes();
+  for (int32_t ns = (im.crop_w + 63) / 64; ns <= im.crop_w; ns++) {
+    const int32_t t = (im.crop_w + ns - 1) / ns;
+    bool ok = true;
+    for (int32_t s = 0; s < ns && ok; s++) {
+      const int32_t ox0 = s * t, ox1 = std::min(ox0 + t, im.crop_w);
+      if (ox0 >= ox1) break;
+      const int32_t xa = im.flip ? im.crop_w - ox1 : ox0;
+      const int32_t xb = im.flip ? im.crop_w - 1 - ox0 : ox1 - 1;
+      const int32_t lo = xt.first[im.crop_x + xa];
+      const int32_t hi = xt.first[im.crop_x + xb] + xt.count[im.crop_x + xb] - 1;
+      const int32_t fb0 = (lo * c) / 12 * 12;
+      ok = (hi + 1) * c - fb0 <= row;
+    }
+    if (ok) {
+      *nstrips = (im.crop_w + t - 1) / t;
+      *tx = t;
+      return true;
+    }
+    if (t <= 1) break;
+  }
+  return false;
+}
+
+int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
+  if (n == 0) return MXD_OK;
+  const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
+  const int32_t channels = images[0].channels;
+  bool aligned16 = true, wave_ok = true;
+  for (int32_t i = 0; i < n; i++) {
+    if (int rc = validate(images[i], i)) return rc;
+    if (images[i].channels != channels)
+      return fail(MXD_ERR_INVALID, "mxd: all images of a batch must have the same channel count");
+    if (images[i].dst_stride < (int64_t)images[i].crop_w * channels * elem)
+      return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
+    aligned16 = aligned16 && (a & 15) == 0;
+    wave_ok = wave_ok && (a & 3) == 0;
+  }
+  std::vector<ImgPlan> plans(n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    ImgPlan& p = plans[i];
+    if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
+    if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
+    if (wave_ok) {
+      p.bucket = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
+      wave_ok = p.bucket > 0 && wave_strips(*p.xt, im, &p.nstrips, &p.tx);
+    }
+  }
+  DeviceGuard guard(device);
+  auto fill = [&](ImgDev& d, const mxd_image& im, const ImgPlan& p) {
+    d.src = im.src;
+    d.src_stride = im.src_stride;
+    d.dst = im.dst;
+    d.dst_stride = im.dst_stride;
+    d.xwidth = p.xt->width;
+    d.ywidth = p.yt->width;
+    d.xtab = p.xt->ptr + (size_t)im.crop_x * (mxd::kTapHeader + p.xt->width);
+    d.ytab = p.yt->ptr + (size_t)im.crop_y * (mxd::kTapHeader + p.yt->width);
+    d.crop_w = im.crop_w;
+    d.crop_h = im.crop_h;
+    d.flip = im.flip ? 1 : 0;
+  };
+
+  if (wave_ok) {
+    // One launch per tap bucket; descriptors of all groups share one upload.
+    std::vector<int32_t> order(n);
+    for (int32_t i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return plans[a].bucket < plans[b].bucket; });
+    int64_t strip_rows = 0;
+    for (int32_t i = 0; i < n; i++) strip_rows += (int64_t)plans[i].nstrips * images[i].crop_h;
+    const int32_t ty = (int32_t)std::max<int64_t>(8, std::min<int64_t>(64, (strip_rows + 8191) / 8192));
+    std::vector<ImgDev> descs(n);
+    struct Group { int32_t first, count, units, bucket; };
+    std::vector<Group> groups;
+    for (int32_t k = 0; k < n; k++) {
+      const int32_t i = order[k];
+      if (groups.empty() || groups.back().bucket != plans[i].bucket) groups.push_back({k, 0, 0, plans[i].bucket});
+      Group& g = groups.back();
+      ImgDev& d = descs[k];
+      fill(d, images[i], plans[i]);
+      d.tile_begin = g.units;
+      d.nstrips = plans[i].nstrips;
+      d.tx = plans[i].tx;
+      d.ty = std::min(ty, images[i].crop_h);
+      d.group = 1;
+      g.units += d.nstrips * ((images[i].crop_h + d.ty - 1) / d.ty);
+      g.count++;
+    }
+    ImgDev* dev = nullptr;
+    std::unique_lock<std::mutex> hold;
+    if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
+    for (const Group& g : groups) {
+      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units};
+      if (int rc = mxd::launch_wave(cfg, dev + g.first, stream))
+        return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
+                                        " rc=" + std::to_string(rc));
+    }
+    return MXD_OK;
+  }
+
+  // General path (any alignment, any tap count): workgroup tiles, resample.hip.
+  const int32_t vec = aligned16 ? 16 : 1;
+  LaunchCfg cfg{};
+  cfg.vec = vec;
+  cfg.channels = channels;
+  cfg.f32 = out_dtype == MXD_F32_DIV255;
+  cfg.nimgs = n;
+  std::vector<ImgDev> descs(n);
+  int32_t tiles = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    const DevTable* xt = plans[i].xt;
+    const DevTable* yt = plans[i].yt;
+    const bool flip = im.flip != 0;
+    // Column strips: enough that one strip row's footprint is ~kStripBytes.
+    const int32_t full = strip_chunks(*xt, im.crop_x, im.crop_w, 0, im.crop_w, flip, channels, 1);
+    int32_t nstrips = std::max<int32_t>(1, (full + kStripBytes - 1) / kStripBytes);
+    int32_t tx = (im.crop_w + nstrips - 1) / nstrips;
+    tx = std::min<int32_t>(im.crop_w, (tx + 3) & ~3);
+    nstrips = (im.crop_w + tx - 1) / tx;
+    int32_t max_chunks = 0;
+    for (int32_t s = 0; s < nstrips; s++) {
+      const int32_t ox0 = s * tx, ox1 = std::min(ox0 + tx, im.crop_w);
+      max_chunks = std::max(max_chunks, strip_chunks(*xt, im.crop_x, im.crop_w, ox0, ox1, flip, channels, vec));
+    }
+    const int32_t vw = (max_chunks * vec + 3) & ~3;
+    const int32_t ty = std::min(kTileRows, im.crop_h);
+    int32_t group = std::max<int32_t>(1, std::min<int32_t>(8, 512 / std::max(1, max_chunks)));
+    group = std::max<int32_t>(1, std::min<int32_t>(group, kLdsBudget / (vw * 4)));
+    group = std::min(group, ty);
+    const int32_t nbands = (im.crop_h + ty - 1) / ty;
+    ImgDev& d = descs[i];
+    fill(d, im, plans[i]);
+    d.tile_begin = tiles;
+    d.nstrips = nstrips;
+    d.ty = ty;
+    d.tx = tx;
+    d.group = group;
+    tiles += nbands * nstrips;
+    cfg.max_tx = std::max(cfg.max_tx, tx);
+    cfg.max_ty = std::max(cfg.max_ty, ty);
+    cfg.max_xw = std::max(cfg.max_xw, xt->width);
+    cfg.max_yw = std::max(cfg.max_yw, yt->width);
+    cfg.max_vw = std::max(cfg.max_vw, vw);
+    cfg.max_group = std::max(cfg.max_group, group);
+  }
+  cfg.ntiles = tiles;
+  if (mxd::resample_smem_bytes(cfg) > 160 * 1024) return fail(MXD_ERR_UNSUPPORTED, "mxd: tile does not fit in LDS");
+  ImgDev* dev = nullptr;
+  std::unique_lock<std::mutex> hold;
+  if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
+  if (int rc = mxd::launch_resample(cfg, dev, stream))
     return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
                                     " rc=" + std::to_string(rc));
   return MXD_OK;

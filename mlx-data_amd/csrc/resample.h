@@ -36,6 +36,17 @@ struct LaunchCfg {
   int32_t max_tx, max_ty, max_xw, max_yw, max_vw, max_group;
 };
 
+// Wave-per-unit fast path (wave.hip): sources 4-byte aligned, every strip's
+// footprint <= wave_row_bytes(), taps <= 24.  Units are numbered through
+// ImgDev::tile_begin exactly like tiles; ty = band rows, tx = strip columns.
+struct WaveCfg {
+  int32_t channels, f32, taps, nimgs, nunits;
+};
+int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
+int wave_row_floats(int taps, int channels);
+int wave_row_bytes();
+int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
+
 // Dynamic LDS bytes the kernel needs for cfg.
 int resample_smem_bytes(const LaunchCfg& cfg);
 
