@@ -54,7 +54,9 @@ enum mxd_dtype {
  * (the dims core::image::scale / resize would produce), the crop window inside
  * the resized image, and where the (crop_h x crop_w x channels) result goes.
  *
- *   src          device pointer to the first byte of row 0
+ *   src          device pointer to the first byte of row 0; the buffer must span
+ *                src_stride * src_h bytes (the kernels read whole 4-byte words
+ *                of a row up to src_stride, never past it)
  *   src_stride   bytes between source rows (>= src_w*channels)
  *   resize_w/h   resized dims, >= 1 (reference: verify_dimensions, ImageTransform.cpp:23-31)
  *   crop_x/y/w/h window in resized coordinates; must lie inside the resized image

@@ -211,21 +211,23 @@ struct ImgPlan {
   int32_t nstrips = 0, tx = 0;
 };
 
-// Wave path strips: <= 64 output columns and <= wave_row_bytes() of source
-// footprint each (the kernel's fb0 alignment included).
+// Wave path strips: strip_cols a multiple of 4 (so every strip's first output
+// element is 16-byte aligned), strip_cols*C <= wave_max_outputs() and <=
+// wave_row_bytes() of source footprint (the kernel's 4-byte fb0 alignment
+// included).
 bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int32_t* tx) {
   const int32_t c = im.channels, row = mxd::wave_row_bytes();
-  for (int32_t ns = (im.crop_w + 63) / 64; ns <= im.crop_w; ns++) {
-    const int32_t t = (im.crop_w + ns - 1) / ns;
-    bool ok = true;
-    for (int32_t s = 0; s < ns && ok; s++) {
-      const int32_t ox0 = s * t, ox1 = std::min(ox0 + t, im.crop_w);
-      if (ox0 >= ox1) break;
+  const int32_t max_tx = mxd::wave_max_outputs() / c / 4 * 4;
+  for (int32_t ns = (im.crop_w + max_tx - 1) / max_tx; ns <= im.crop_w; ns++) {
+    const int32_t t = std::min(im.crop_w, ((im.crop_w + ns - 1) / ns + 3) & ~3);
+    bool ok = t * c <= mxd::wave_max_outputs();
+    for (int32_t ox0 = 0; ox0 < im.crop_w && ok; ox0 += t) {
+      const int32_t ox1 = std::min(ox0 + t, im.crop_w);
       const int32_t xa = im.flip ? im.crop_w - ox1 : ox0;
       const int32_t xb = im.flip ? im.crop_w - 1 - ox0 : ox1 - 1;
       const int32_t lo = xt.first[im.crop_x + xa];
       const int32_t hi = xt.first[im.crop_x + xb] + xt.count[im.crop_x + xb] - 1;
-      const int32_t fb0 = (lo * c) / 12 * 12;
+      const int32_t fb0 = (lo * c) & ~3;
       ok = (hi + 1) * c - fb0 <= row;
     }
     if (ok) {
@@ -233,7 +235,7 @@ bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int3
       *tx = t;
       return true;
     }
-    if (t <= 1) break;
+    if (t <= 4) break;
   }
   return false;
 }
@@ -253,7 +255,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
     const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
     aligned16 = aligned16 && (a & 15) == 0;
-    wave_ok = wave_ok && (a & 3) == 0;
+    const uintptr_t o = reinterpret_cast<uintptr_t>(images[i].dst) | (uintptr_t)images[i].dst_stride;
+    wave_ok = wave_ok && (a & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0;
   }
   std::vector<ImgPlan> plans(n);
   for (int32_t i = 0; i < n; i++) {

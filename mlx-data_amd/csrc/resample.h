@@ -36,8 +36,9 @@ struct LaunchCfg {
   int32_t max_tx, max_ty, max_xw, max_yw, max_vw, max_group;
 };
 
-// Wave-per-unit fast path (wave.hip): sources 4-byte aligned, every strip's
-// footprint <= wave_row_bytes(), taps <= 24.  Units are numbered through
+// Wave-per-unit fast path (wave.hip): sources 4-byte aligned, outputs 16-byte
+// (f32) / 4-byte (u8) aligned, every strip's footprint <= wave_row_bytes(),
+// strip_cols*C <= wave_max_outputs(), taps <= 17.  Units are numbered through
 // ImgDev::tile_begin exactly like tiles; ty = band rows, tx = strip columns.
 struct WaveCfg {
   int32_t channels, f32, taps, nimgs, nunits;
@@ -45,6 +46,7 @@ struct WaveCfg {
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
 int wave_row_floats(int taps, int channels);
 int wave_row_bytes();
+int wave_max_outputs();  // output elements per strip row (4 per lane)
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
 
 // Dynamic LDS bytes the kernel needs for cfg.
