@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=512)
+    ap.add_argument("--no-copy", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,6 +191,7 @@ def main():
     alg_bytes = B * (fp + out_bytes)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic()
+    copy_gbs = capi.copy_bandwidth(1 << 30, dev, 20) if not args.no_copy else None
 
     e2e = None
     if not args.no_e2e and world == 1:
@@ -243,7 +245,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_image": fp + out_bytes,
-                         "kernel_ms_per_launch": round(kernel_ms, 5)},
+                         "kernel_ms_per_launch": round(kernel_ms, 5),
+                         "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None},
             "cpu_baseline": cpu,
             "e2e": e2e,
         }

@@ -105,6 +105,10 @@ int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t c
  * device memory.  Asynchronous: returns once the work is enqueued. */
 int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream);
 
+/* Measured device-memory ceiling: a 16-byte-per-lane streaming copy of `bytes`
+ * (read + write counted), averaged over `iters` launches, in GB/s. */
+int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps);
+
 /* ---- device memory / streams / events (so a C or C++ host needs no torch) */
 int mxd_set_device(int32_t device);
 int mxd_malloc_device(void** ptr, size_t bytes, int32_t device);

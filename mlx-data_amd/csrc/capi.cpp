@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -313,7 +314,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     std::unique_lock<std::mutex> hold;
     if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
     for (const Group& g : groups) {
-      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units};
+      static const int ablate = [] {
+        const char* e = std::getenv("MXD_WAVE_ABLATE");
+        return e ? std::atoi(e) : 0;
+      }();
+      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate};
       if (int rc = mxd::launch_wave(cfg, dev + g.first, stream))
         return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
                                         " rc=" + std::to_string(rc));
@@ -467,6 +472,34 @@ int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t c
 
 int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
   return run_batch(images, n, out_dtype, device, stream);
+}
+
+int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps) {
+  if (!gbps || bytes < 16 || iters <= 0) return fail(MXD_ERR_INVALID, "mxd: bad copy_bandwidth arguments");
+  DeviceGuard g(device);
+  void *a = nullptr, *b = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  MXD_HIP(hipMalloc(&a, bytes));
+  MXD_HIP(hipMalloc(&b, bytes));
+  MXD_HIP(hipMemset(a, 1, bytes));
+  MXD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  MXD_HIP(hipEventCreate(&e0));
+  MXD_HIP(hipEventCreate(&e1));
+  mxd::launch_copy(a, b, bytes, s);
+  MXD_HIP(hipEventRecord(e0, s));
+  for (int32_t i = 0; i < iters; i++) mxd::launch_copy(a, b, bytes, s);
+  MXD_HIP(hipEventRecord(e1, s));
+  MXD_HIP(hipEventSynchronize(e1));
+  float ms = 0.0f;
+  MXD_HIP(hipEventElapsedTime(&ms, e0, e1));
+  *gbps = (float)(2.0 * (double)(bytes / 16 * 16) * iters / (ms * 1e-3) / 1e9);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipStreamDestroy(s);
+  hipFree(a);
+  hipFree(b);
+  return MXD_OK;
 }
 
 int mxd_set_device(int32_t device) {

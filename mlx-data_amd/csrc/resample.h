@@ -1,6 +1,7 @@
 // resample.h -- device-side descriptors shared by capi.cpp and resample.hip.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 
 namespace mxd {
@@ -42,12 +43,14 @@ struct LaunchCfg {
 // ImgDev::tile_begin exactly like tiles; ty = band rows, tx = strip columns.
 struct WaveCfg {
   int32_t channels, f32, taps, nimgs, nunits;
+  int32_t mode;  // 0 = product kernel; 1..3 = diagnostic ablations (MXD_WAVE_ABLATE)
 };
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
 int wave_row_floats(int taps, int channels);
 int wave_row_bytes();
 int wave_max_outputs();  // output elements per strip row (4 per lane)
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
+int launch_copy(const void* src, void* dst, size_t bytes, void* stream);
 
 // Dynamic LDS bytes the kernel needs for cfg.
 int resample_smem_bytes(const LaunchCfg& cfg);

@@ -126,7 +126,12 @@ __device__ __forceinline__ void shift_rows_dyn(Chunk* R, int d, int m) {
   }
 }
 
-template <int C, bool F32, int T>
+// MODE: 0 = the product kernel.  Diagnostic ablations (selected only through
+// the MXD_WAVE_ABLATE environment variable, C=3/f32/T=8 only):
+//   1 = no vertical arithmetic (loads kept live with one op per dword),
+//   2 = no source loads (rows synthesised from the lane id),
+//   3 = no horizontal pass (encode of the LDS value at the tap base only).
+template <int C, bool F32, int T, int MODE = 0>
 __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __restrict__ imgs, int nimgs,
                                                                int nunits, int rowf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -199,8 +204,12 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     for (int k = 0; k < T; k++) {
       if (k >= m) {
         const int row = n0 + min(k, nt - 1);
-        if (vact) R[k] = load_chunk(col + row * sstride, nd);
-        else R[k] = Chunk{{0u, 0u, 0u, 0u}};
+        if constexpr (MODE == 2) {
+          R[k] = Chunk{{(uint32_t)(lane * 7 + row), (uint32_t)(row * 3), (uint32_t)lane, (uint32_t)(row ^ lane)}};
+        } else {
+          if (vact) R[k] = load_chunk(col + row * sstride, nd);
+          else R[k] = Chunk{{0u, 0u, 0u, 0u}};
+        }
       }
     }
   };
@@ -214,8 +223,15 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     float acc[kChunk];
 #pragma unroll
     for (int i = 0; i < kChunk; i++) acc[i] = 0.0f;
+    if constexpr (MODE == 1) {
 #pragma unroll
-    for (int k = 0; k < T; k++) fma16(acc, k < nt ? ye[kTapHeader + k] : 0.0f, R[k]);
+      for (int k = 0; k < T; k++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[4 * i] += __uint_as_float(R[k].d[i] & 0x3fffffffu);
+    } else {
+#pragma unroll
+      for (int k = 0; k < T; k++) fma16(acc, k < nt ? ye[kTapHeader + k] : 0.0f, R[k]);
+    }
     float4* dv = reinterpret_cast<float4*>(vrow + lane * kChunk);
     dv[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
     dv[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
@@ -244,8 +260,12 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
 #pragma unroll
     for (int j = 0; j < kOutPerLane; j++) {
       float s = 0.0f;
+      if constexpr (MODE == 3) {
+        s = wx[j][0] * vrow[pos[j]];
+      } else {
 #pragma unroll
-      for (int k = 0; k < T; k++) s = __builtin_fmaf(wx[j][k], vrow[pos[j] + k * C], s);
+        for (int k = 0; k < T; k++) s = __builtin_fmaf(wx[j][k], vrow[pos[j] + k * C], s);
+      }
       out[j] = encode(s);
     }
     const int o0 = kOutPerLane * lane;
@@ -279,11 +299,19 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   }
 }
 
-template <int C, bool F32, int T>
+template <int C, bool F32, int T, int MODE = 0>
 int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
+  if constexpr (MODE == 0 && C == 3 && F32 && T == 8) {
+    switch (cfg.mode) {
+      case 1: return launch_ct<C, F32, T, 1>(cfg, imgs, s);
+      case 2: return launch_ct<C, F32, T, 2>(cfg, imgs, s);
+      case 3: return launch_ct<C, F32, T, 3>(cfg, imgs, s);
+      default: break;
+    }
+  }
   const int rowf = wave_row_floats(cfg.taps, C);
   const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL((resample_wave<C, F32, T>), dim3(blocks), dim3(kWaves * kLanes),
+  hipLaunchKernelGGL((resample_wave<C, F32, T, MODE>), dim3(blocks), dim3(kWaves * kLanes),
                      kWaves * rowf * (int)sizeof(float), s, imgs, cfg.nimgs, cfg.nunits, rowf);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -320,6 +348,19 @@ int wave_row_floats(int taps, int channels) { return (kRowBytes + taps * channel
 int wave_row_bytes() { return kRowBytes; }
 
 int wave_max_outputs() { return kLanes * kOutPerLane; }
+
+// Streaming copy (16 B per lane, grid-stride): the measured HBM ceiling that
+// bench.py reports next to the spec peak.
+__global__ __launch_bounds__(256) void copy_f4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+int launch_copy(const void* src, void* dst, size_t bytes, void* stream) {
+  const size_t n = bytes / 16;
+  hipLaunchKernelGGL(copy_f4, dim3(256 * 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst), n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

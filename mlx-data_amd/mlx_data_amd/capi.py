@@ -20,7 +20,7 @@ MXD_F32_DIV255 = 1
 EXPORTS = (
     "mxd_abi_version", "mxd_last_error", "mxd_device_count",
     "mxd_resize_smallest_side_dims", "mxd_center_crop_origin", "mxd_axis_taps",
-    "mxd_resize_crop_batch",
+    "mxd_resize_crop_batch", "mxd_copy_bandwidth",
     "mxd_set_device", "mxd_malloc_device", "mxd_free_device", "mxd_malloc_pinned", "mxd_free_pinned",
     "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
     "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
@@ -214,6 +214,12 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def copy_bandwidth(nbytes=1 << 30, device=0, iters=20):
+    g = ctypes.c_float()
+    check(lib().mxd_copy_bandwidth(ctypes.c_size_t(nbytes), device, iters, ctypes.byref(g)))
+    return g.value
 
 
 def device_count():
