@@ -351,13 +351,28 @@ int wave_max_outputs() { return kLanes * kOutPerLane; }
 
 // Streaming copy (16 B per lane, grid-stride): the measured HBM ceiling that
 // bench.py reports next to the spec peak.
+// Each thread moves 4 x 16 B per iteration (4 loads in flight before the
+// stores); blocks own contiguous 16 KiB pieces.
 __global__ __launch_bounds__(256) void copy_f4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+  const size_t per_block = 256 * 4;
+  for (size_t base = blockIdx.x * per_block; base < n; base += (size_t)gridDim.x * per_block) {
+    float4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const size_t j = base + i * 256 + threadIdx.x;
+      if (j < n) v[i] = a[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const size_t j = base + i * 256 + threadIdx.x;
+      if (j < n) b[j] = v[i];
+    }
+  }
 }
 
 int launch_copy(const void* src, void* dst, size_t bytes, void* stream) {
   const size_t n = bytes / 16;
-  hipLaunchKernelGGL(copy_f4, dim3(256 * 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(copy_f4, dim3(256 * 8), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst), n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
