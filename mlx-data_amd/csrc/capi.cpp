@@ -56,7 +56,8 @@ struct DeviceGuard {
 // output pixel of the axis, so any crop window is a pointer offset into it.
 struct DevTable {
   float* ptr = nullptr;
-  int32_t width = 0;
+  int32_t width = 0;     // max taps of any output
+  int32_t padded = 0;    // weights per entry in device memory (>= kMinTabWidth)
   std::vector<int32_t> first, count;  // host copy for tiling decisions
 };
 
@@ -73,7 +74,8 @@ class TableCache {
     mxd::AxisTaps taps;
     if (!mxd::build_axis_taps(in, out, 0, out, &taps))
       return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension");
-    const int32_t stride = mxd::kTapHeader + taps.width;
+    const int32_t padded = std::max<int32_t>(taps.width, mxd::kMinTabWidth);
+    const int32_t stride = mxd::kTapHeader + padded;
     std::vector<float> host((size_t)out * stride, 0.0f);
     for (int32_t i = 0; i < out; i++) {
       float* e = &host[(size_t)i * stride];
@@ -83,6 +85,7 @@ class TableCache {
     }
     auto tab = std::make_unique<DevTable>();
     tab->width = taps.width;
+    tab->padded = padded;
     tab->first = taps.first;
     tab->count = taps.count;
     DeviceGuard g(device);
@@ -257,7 +260,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
     aligned16 = aligned16 && (a & 15) == 0;
     const uintptr_t o = reinterpret_cast<uintptr_t>(images[i].dst) | (uintptr_t)images[i].dst_stride;
-    wave_ok = wave_ok && (a & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0;
+    wave_ok = wave_ok && (a & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
+              images[i].src_stride * images[i].src_h < ((int64_t)1 << 31);
   }
   std::vector<ImgPlan> plans(n);
   for (int32_t i = 0; i < n; i++) {
@@ -274,12 +278,14 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   auto fill = [&](ImgDev& d, const mxd_image& im, const ImgPlan& p) {
     d.src = im.src;
     d.src_stride = im.src_stride;
+    d.src_w = im.src_w;
+    d.src_h = im.src_h;
     d.dst = im.dst;
     d.dst_stride = im.dst_stride;
-    d.xwidth = p.xt->width;
-    d.ywidth = p.yt->width;
-    d.xtab = p.xt->ptr + (size_t)im.crop_x * (mxd::kTapHeader + p.xt->width);
-    d.ytab = p.yt->ptr + (size_t)im.crop_y * (mxd::kTapHeader + p.yt->width);
+    d.xwidth = p.xt->padded;
+    d.ywidth = p.yt->padded;
+    d.xtab = p.xt->ptr + (size_t)im.crop_x * (mxd::kTapHeader + p.xt->padded);
+    d.ytab = p.yt->ptr + (size_t)im.crop_y * (mxd::kTapHeader + p.yt->padded);
     d.crop_w = im.crop_w;
     d.crop_h = im.crop_h;
     d.flip = im.flip ? 1 : 0;
@@ -367,8 +373,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     tiles += nbands * nstrips;
     cfg.max_tx = std::max(cfg.max_tx, tx);
     cfg.max_ty = std::max(cfg.max_ty, ty);
-    cfg.max_xw = std::max(cfg.max_xw, xt->width);
-    cfg.max_yw = std::max(cfg.max_yw, yt->width);
+    cfg.max_xw = std::max(cfg.max_xw, xt->padded);
+    cfg.max_yw = std::max(cfg.max_yw, yt->padded);
     cfg.max_vw = std::max(cfg.max_vw, vw);
     cfg.max_group = std::max(cfg.max_group, group);
   }

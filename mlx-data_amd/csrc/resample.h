@@ -7,8 +7,11 @@
 namespace mxd {
 
 // One entry of a per-axis tap table in device memory: the first input index
-// and tap count stored as int bits, then `width` f32 weights.
+// and tap count stored as int bits, then `width` f32 weights, zero padded to
+// at least kMinTabWidth so the wave kernel can read T <= kMinTabWidth
+// weights of any entry unconditionally.
 constexpr int kTapHeader = 2;
+constexpr int kMinTabWidth = 24;
 
 // Per-image parameters, resolved by the host (geometry already validated).
 // Each image is cut into nbands x nstrips tiles of ty output rows x tx output
@@ -25,8 +28,9 @@ struct ImgDev {
   int32_t flip;
   int32_t tile_begin;
   int32_t nstrips, ty, tx, group;
+  int32_t src_w, src_h;
 };
-static_assert(sizeof(ImgDev) == 88, "ImgDev layout");
+static_assert(sizeof(ImgDev) == 96, "ImgDev layout");
 
 struct LaunchCfg {
   int32_t vec;        // bytes per thread per source row: 16 (16-byte aligned rows) or 1

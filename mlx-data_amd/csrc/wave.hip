@@ -5,23 +5,25 @@
 // organised so that no workgroup barrier is ever needed:
 //
 //   one WAVE owns one unit = (image, band of output rows, strip of output
-//   columns).  Lane l holds 16 source bytes of the strip's footprint, so one
-//   wave spans 1024 source bytes of a row (one dwordx4 load per lane, 1 KiB
-//   per wave-instruction).  For each output row y of the band:
+//   columns).  The wave covers a 1024-byte window of each source row: lane l
+//   holds the four dwords at bytes 4l + 256j (j = 0..3) of the window, loaded
+//   with buffer_load_dword through a descriptor spanning the whole image (row
+//   offset in the scalar soffset, so no per-load address arithmetic; reads
+//   past the image return 0).  For each output row y of the band:
 //     V  lane sums its 16 byte columns over the T vertical taps of y from the
-//        T source rows it holds in registers and writes 16 f32 to the wave's
-//        private LDS row.  Then it moves on to y+1: source rows shared by the
-//        taps of y and y+1 (about half of them when downsampling) stay in
-//        registers (shifted by the uniform row advance d); only the new rows
-//        are loaded, and those loads are in flight during
+//        T consecutive source rows it holds in registers and writes 16 f32 to
+//        the wave's private LDS row (four ds_write_b128, lanes 16 bytes apart:
+//        conflict-free).  Then it moves on to y+1: the rows shared by the taps
+//        of y and y+1 stay in registers (shifted by the uniform row advance d),
+//        only the d new rows are loaded, and those loads are in flight during
 //     H  lane l produces output elements 4l..4l+3 of the strip row (C
 //        channels interleaved) from the LDS row with their T horizontal taps
 //        (weights in registers for the whole band), rounds like stbir's encode
 //        and stores 4 f32 (exact q/255, one 16-byte store) or 4 u8.
 //   Waves never wait for each other; the CU interleaves the waves of many
 //   units so that loads of their next rows are always in flight.
-// Tap counts are padded to the template T with zero weights and clamped row
-// indices; the LDS row has a zeroed tail so padded taps read finite values.
+// Tap counts are padded to the template T with zero weights; padded taps read
+// real neighbouring rows/columns (or zeros), so every value is finite.
 #include <hip/hip_runtime.h>
 
 #include "resample.h"
@@ -38,6 +40,8 @@ constexpr int kOutPerLane = 4;              // output elements per lane per row
 #define GLOBAL_PTR(T, p) ((__attribute__((address_space(1))) T*)(p))
 using gfloat = __attribute__((address_space(1))) float;
 using cgfloat = const __attribute__((address_space(1))) float;
+// Constant address space: uniform loads through it are scalar (s_load).
+using kfloat = const __attribute__((address_space(4))) float;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int xcd_remap(int b, int n) {
@@ -57,25 +61,15 @@ __device__ __forceinline__ float div255(float q) {
 // stbir encode: (uint8)trunc(clamp(v*255 + 0.5, 0, 255)), v in byte units here.
 __device__ __forceinline__ float encode(float v) { return truncf(fminf(fmaxf(v + 0.5f, 0.0f), 255.0f)); }
 
-struct alignas(4) Chunk {
+struct Chunk {
   uint32_t d[4];
 };
 
-// Loads the lane's 16 bytes; only the first nd dwords when the chunk would
-// cross src_stride (the last lane of a strip at the right edge of the image,
-// where the bytes past the row may be past the end of the buffer).
-__device__ __forceinline__ Chunk load_chunk(const uint8_t* p, int nd) {
-  const __attribute__((address_space(1))) uint32_t* q = GLOBAL_PTR(const uint32_t, p);
+// The lane's 4 dwords of source row `row`: bytes off + 256j of the row.
+__device__ __forceinline__ Chunk load_chunk(__amdgpu_buffer_rsrc_t rsrc, int off, int row_off) {
   Chunk r;
-  if (nd == 4) {
-    r.d[0] = q[0];
-    r.d[1] = q[1];
-    r.d[2] = q[2];
-    r.d[3] = q[3];
-  } else {
 #pragma unroll
-    for (int i = 0; i < 4; i++) r.d[i] = i < nd ? q[i] : 0u;
-  }
+  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 256 * j, row_off, 0);
   return r;
 }
 
@@ -89,48 +83,49 @@ __device__ __forceinline__ void fma16(float* acc, float w, const Chunk& v) {
   }
 }
 
-// R[k] <- R[k + D] for k < m (m uniform): rows shared by consecutive outputs.
+// Rows for the next output, whose first tap is D rows further down:
+// R[k] <- R[k + D], then load the D rows that are new.
 template <int T, int D>
-__device__ __forceinline__ void shift_rows(Chunk* R, int m) {
+__device__ __forceinline__ void advance_rows(Chunk* R, __amdgpu_buffer_rsrc_t rsrc, int off, int n0, int stride) {
 #pragma unroll
-  for (int k = 0; k + D < T; k++)
-    if (k < m) R[k] = R[k + D];
+  for (int k = 0; k + D < T; k++) R[k] = R[k + D];
+#pragma unroll
+  for (int k = (T > D ? T - D : 0); k < T; k++) R[k] = load_chunk(rsrc, off, (n0 + k) * stride);
 }
 
 template <int T>
-__device__ __forceinline__ void shift_rows_dyn(Chunk* R, int d, int m) {
+__device__ __forceinline__ void advance_rows_dyn(Chunk* R, __amdgpu_buffer_rsrc_t rsrc, int off, int n0, int stride,
+                                                 int d) {
   switch (d) {
-#define MXD_SHIFT_CASE(D)                        \
-  case D:                                        \
-    if constexpr (D < T) shift_rows<T, D>(R, m); \
+    case 0:
+      break;
+#define MXD_ADV_CASE(D)                                            \
+  case D:                                                          \
+    if constexpr (D < T) advance_rows<T, D>(R, rsrc, off, n0, stride); \
     break;
-    MXD_SHIFT_CASE(1)
-    MXD_SHIFT_CASE(2)
-    MXD_SHIFT_CASE(3)
-    MXD_SHIFT_CASE(4)
-    MXD_SHIFT_CASE(5)
-    MXD_SHIFT_CASE(6)
-    MXD_SHIFT_CASE(7)
-    MXD_SHIFT_CASE(8)
-    MXD_SHIFT_CASE(9)
-    MXD_SHIFT_CASE(10)
-    MXD_SHIFT_CASE(11)
-    MXD_SHIFT_CASE(12)
-    MXD_SHIFT_CASE(13)
-    MXD_SHIFT_CASE(14)
-    MXD_SHIFT_CASE(15)
-    MXD_SHIFT_CASE(16)
-#undef MXD_SHIFT_CASE
+    MXD_ADV_CASE(1)
+    MXD_ADV_CASE(2)
+    MXD_ADV_CASE(3)
+    MXD_ADV_CASE(4)
+    MXD_ADV_CASE(5)
+    MXD_ADV_CASE(6)
+    MXD_ADV_CASE(7)
+    MXD_ADV_CASE(8)
+    MXD_ADV_CASE(9)
+    MXD_ADV_CASE(10)
+    MXD_ADV_CASE(11)
+    MXD_ADV_CASE(12)
+    MXD_ADV_CASE(13)
+    MXD_ADV_CASE(14)
+    MXD_ADV_CASE(15)
+    MXD_ADV_CASE(16)
+#undef MXD_ADV_CASE
     default:
+      advance_rows<T, T>(R, rsrc, off, n0, stride);
       break;
   }
 }
 
-// MODE: 0 = the product kernel.  Diagnostic ablations (selected only through
-// the MXD_WAVE_ABLATE environment variable, C=3/f32/T=8 only):
-//   1 = no vertical arithmetic (loads kept live with one op per dword),
-//   2 = no source loads (rows synthesised from the lane id),
-//   3 = no horizontal pass (encode of the LDS value at the tap base only).
 template <int C, bool F32, int T, int MODE = 0>
 __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __restrict__ imgs, int nimgs,
                                                                int nunits, int rowf) {
@@ -156,10 +151,14 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   const int xs = kTapHeader + __builtin_amdgcn_readfirstlane(im.xwidth);
   const int ys = kTapHeader + __builtin_amdgcn_readfirstlane(im.ywidth);
   cgfloat* xtab = GLOBAL_PTR(const float, im.xtab);
-  cgfloat* ytab = GLOBAL_PTR(const float, im.ytab);
-  const uint8_t* src = im.src;
+  // Uniform pointer: the vertical taps are read with scalar loads (lgkmcnt),
+  // which never wait on the vector loads of the next rows.
+  const uint64_t yb = reinterpret_cast<uint64_t>(im.ytab);
+  kfloat* ytab = (kfloat*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(yb >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)yb));
   char* dst = reinterpret_cast<char*>(im.dst);
-  const int64_t sstride = im.src_stride;
+  const int sstride = __builtin_amdgcn_readfirstlane((int)im.src_stride);
+  const int src_h = __builtin_amdgcn_readfirstlane(im.src_h);
   const int64_t dstride = im.dst_stride;
   const int local = unit - __builtin_amdgcn_readfirstlane(im.tile_begin);
   const int band = local / nstrips;
@@ -175,11 +174,17 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   const int px_lo = __float_as_int(xtab[xa * xs]);
   const int px_hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
   const int fb0 = (px_lo * C) & ~3;
-  const bool vact = fb0 + lane * kChunk < (px_hi + 1) * C;
-  const int nd = vact ? (int)min<int64_t>(4, (sstride - (fb0 + lane * kChunk)) / 4) : 0;
+  (void)px_hi;
+  const uint64_t sbase = reinterpret_cast<uint64_t>(im.src);
+  const uint64_t sb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(sb), (short)0, sstride * src_h, 0x00020000);
+  const int loff = fb0 + 4 * lane;  // + 256 j
 
   // Horizontal taps of this lane's 4 output elements, for the whole band.
   const int nout = (ox1 - ox0) * C;
+  const bool partial = (nout & (kOutPerLane - 1)) != 0;
   float wx[kOutPerLane][T];
   int pos[kOutPerLane];
 #pragma unroll
@@ -190,36 +195,31 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     const int ox = ox0 + px;
     const int xc = flip ? crop_w - 1 - ox : ox;
     cgfloat* xe = xtab + xc * xs;
-    const int ntx = __float_as_int(xe[1]);
     pos[j] = __float_as_int(xe[0]) * C - fb0 + c;
 #pragma unroll
-    for (int k = 0; k < T; k++) wx[j][k] = k < ntx ? xe[kTapHeader + k] : 0.0f;
+    for (int k = 0; k < T; k++) wx[j][k] = xe[kTapHeader + k];  // zero padded past the tap count
   }
 
-  const uint8_t* __restrict__ col = src + fb0 + lane * kChunk;
-  Chunk R[T];
-  // Loads rows n0 + min(k, nt-1) for k in [m, T).
-  auto load_rows = [&](int n0, int nt, int m) {
+  // The horizontal weights are loaded once; retire them here so the waits the
+  // compiler places in the row loop only ever cover the row loads.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+  auto load_rows = [&](Chunk* R, int y) {
+    const int n0 = __float_as_int(ytab[y * ys]);
 #pragma unroll
     for (int k = 0; k < T; k++) {
-      if (k >= m) {
-        const int row = n0 + min(k, nt - 1);
-        if constexpr (MODE == 2) {
-          R[k] = Chunk{{(uint32_t)(lane * 7 + row), (uint32_t)(row * 3), (uint32_t)lane, (uint32_t)(row ^ lane)}};
-        } else {
-          if (vact) R[k] = load_chunk(col + row * sstride, nd);
-          else R[k] = Chunk{{0u, 0u, 0u, 0u}};
-        }
+      if constexpr (MODE == 2) {
+        R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
+      } else {
+        R[k] = load_chunk(rsrc, loff, (n0 + k) * sstride);
       }
     }
   };
 
-  cgfloat* ye = ytab + oy0 * ys;
-  int n0 = __float_as_int(ye[0]);
-  int nt = __float_as_int(ye[1]);
-  load_rows(n0, nt, 0);
-  for (int y = oy0; y < oy1; y++) {
+  // One output row from the T source rows in R.
+  auto step = [&](const Chunk* R, int y) {
     // ---- V: vertical taps of row y -> LDS ----
+    kfloat* ye = ytab + y * ys;
     float acc[kChunk];
 #pragma unroll
     for (int i = 0; i < kChunk; i++) acc[i] = 0.0f;
@@ -230,27 +230,13 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
         for (int i = 0; i < 4; i++) acc[4 * i] += __uint_as_float(R[k].d[i] & 0x3fffffffu);
     } else {
 #pragma unroll
-      for (int k = 0; k < T; k++) fma16(acc, k < nt ? ye[kTapHeader + k] : 0.0f, R[k]);
+      for (int k = 0; k < T; k++) fma16(acc, ye[kTapHeader + k], R[k]);  // zero padded past the tap count
     }
-    float4* dv = reinterpret_cast<float4*>(vrow + lane * kChunk);
-    dv[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    dv[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    dv[2] = make_float4(acc[8], acc[9], acc[10], acc[11]);
-    dv[3] = make_float4(acc[12], acc[13], acc[14], acc[15]);
-
-    // ---- rows for y+1: keep the shared ones, load the rest (in flight during H) ----
-    if (y + 1 < oy1) {
-      cgfloat* yn = ye + ys;
-      const int n0n = __float_as_int(yn[0]);
-      const int ntn = __float_as_int(yn[1]);
-      const int d = n0n - n0;
-      const int m = (d > 0) ? min(max(nt - d, 0), ntn) : (d == 0 ? min(nt, ntn) : 0);
-      if (d > 0) shift_rows_dyn<T>(R, d, m);
-      load_rows(n0n, ntn, m);
-      ye = yn;
-      n0 = n0n;
-      nt = ntn;
-    }
+    // floats of bytes 4l + 256j .. +3 go to vrow[4l + 256j]: lanes 16 B apart per store
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      *reinterpret_cast<float4*>(vrow + 4 * lane + 256 * j) =
+          make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -269,33 +255,44 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
       out[j] = encode(s);
     }
     const int o0 = kOutPerLane * lane;
-    if (o0 < nout) {
-      char* drow = dst + (int64_t)y * dstride;
+    char* drow = dst + (int64_t)y * dstride;
+    if (o0 + kOutPerLane <= nout) {  // one store instruction per row (lanes past nout masked)
       if constexpr (F32) {
-        gfloat* d = GLOBAL_PTR(float, drow) + ox0 * C + o0;
-        if (o0 + kOutPerLane <= nout) {
-          f32x4 v = {div255(out[0]), div255(out[1]), div255(out[2]), div255(out[3])};
-          *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(d) = v;
-        } else {
-#pragma unroll
-          for (int j = 0; j < kOutPerLane; j++)
-            if (o0 + j < nout) d[j] = div255(out[j]);
-        }
+        f32x4 v = {div255(out[0]), div255(out[1]), div255(out[2]), div255(out[3])};
+        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(GLOBAL_PTR(float, drow) + ox0 * C + o0) = v;
       } else {
-        __attribute__((address_space(1))) uint8_t* d = GLOBAL_PTR(uint8_t, drow) + ox0 * C + o0;
-        if (o0 + kOutPerLane <= nout) {
-          *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(d) =
-              (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
-        } else {
+        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(GLOBAL_PTR(uint8_t, drow) + ox0 * C + o0) =
+            (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
+      }
+    }
+    if (partial && o0 < nout && o0 + kOutPerLane > nout) {  // ragged strip end (uniform `partial`)
 #pragma unroll
-          for (int j = 0; j < kOutPerLane; j++)
-            if (o0 + j < nout) d[j] = (uint8_t)out[j];
+      for (int j = 0; j < kOutPerLane; j++) {
+        if (o0 + j < nout) {
+          if constexpr (F32) GLOBAL_PTR(float, drow)[ox0 * C + o0 + j] = div255(out[j]);
+          else GLOBAL_PTR(uint8_t, drow)[ox0 * C + o0 + j] = (uint8_t)out[j];
         }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // Double-buffered rows: the loads of row y+1 are issued before row y is
+  // computed, so they fly during the whole V+H of row y.
+  // The prefetch is unconditional (clamped to the last output row) so every
+  // path through the loop has the same loads in flight and the compiler's
+  // counted waits stay partial.
+  Chunk RA[T], RB[T];
+  load_rows(RA, oy0);
+  for (int y = oy0;; y += 2) {
+    load_rows(RB, min(y + 1, crop_h - 1));
+    step(RA, y);
+    if (y + 1 >= oy1) break;
+    load_rows(RA, min(y + 2, crop_h - 1));
+    step(RB, y + 1);
+    if (y + 2 >= oy1) break;
   }
 }
 
