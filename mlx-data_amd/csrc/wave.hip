@@ -210,6 +210,9 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     for (int k = 0; k < T; k++) {
       if constexpr (MODE == 2) {
         R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
+      } else if constexpr (MODE == 4) {
+        if (k >= T / 2) R[k] = load_chunk(rsrc, loff, (n0 + k) * sstride);
+        else R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
       } else {
         R[k] = load_chunk(rsrc, loff, (n0 + k) * sstride);
       }
@@ -303,6 +306,7 @@ int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
       case 1: return launch_ct<C, F32, T, 1>(cfg, imgs, s);
       case 2: return launch_ct<C, F32, T, 2>(cfg, imgs, s);
       case 3: return launch_ct<C, F32, T, 3>(cfg, imgs, s);
+      case 4: return launch_ct<C, F32, T, 4>(cfg, imgs, s);
       default: break;
     }
   }
