@@ -212,6 +212,7 @@ struct ImgPlan {
   const DevTable* xt = nullptr;
   const DevTable* yt = nullptr;
   int32_t bucket = -1;   // wave path tap bucket, -1 = not eligible
+  int32_t scatter = 0;   // vertical taps allow the row-once (scatter) kernel
   int32_t nstrips = 0, tx = 0;
 };
 
@@ -244,6 +245,18 @@ bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int3
   return false;
 }
 
+// The scatter kernel keeps 3 open output rows and closes at most one per
+// source row: every source row must feed <= 3 outputs of the window and the
+// last taps must strictly increase.
+bool scatter_ok(const DevTable& yt, int32_t off, int32_t len) {
+  for (int32_t y = off; y < off + len; y++) {
+    const int32_t last = yt.first[y] + yt.count[y] - 1;
+    if (y + 1 < off + len && yt.first[y + 1] + yt.count[y + 1] - 1 <= last) return false;
+    if (y + 3 < off + len && yt.first[y + 3] <= last) return false;
+  }
+  return true;
+}
+
 int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
@@ -272,6 +285,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (wave_ok) {
       p.bucket = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
       wave_ok = p.bucket > 0 && wave_strips(*p.xt, im, &p.nstrips, &p.tx);
+      static const int no_scatter = [] {
+        const char* e = std::getenv("MXD_NO_SCATTER");
+        return e ? std::atoi(e) : 0;
+      }();
+      p.scatter = !no_scatter && scatter_ok(*p.yt, im.crop_y, im.crop_h) ? 1 : 0;
     }
   }
   DeviceGuard guard(device);
@@ -295,16 +313,18 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     // One launch per tap bucket; descriptors of all groups share one upload.
     std::vector<int32_t> order(n);
     for (int32_t i = 0; i < n; i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return plans[a].bucket < plans[b].bucket; });
+    auto key = [&](int32_t i) { return plans[i].bucket * 2 + plans[i].scatter; };
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
     int64_t strip_rows = 0;
     for (int32_t i = 0; i < n; i++) strip_rows += (int64_t)plans[i].nstrips * images[i].crop_h;
     const int32_t ty = (int32_t)std::max<int64_t>(8, std::min<int64_t>(64, (strip_rows + 8191) / 8192));
     std::vector<ImgDev> descs(n);
-    struct Group { int32_t first, count, units, bucket; };
+    struct Group { int32_t first, count, units, bucket, scatter; };
     std::vector<Group> groups;
     for (int32_t k = 0; k < n; k++) {
       const int32_t i = order[k];
-      if (groups.empty() || groups.back().bucket != plans[i].bucket) groups.push_back({k, 0, 0, plans[i].bucket});
+      if (groups.empty() || groups.back().bucket != plans[i].bucket || groups.back().scatter != plans[i].scatter)
+        groups.push_back({k, 0, 0, plans[i].bucket, plans[i].scatter});
       Group& g = groups.back();
       ImgDev& d = descs[k];
       fill(d, images[i], plans[i]);
@@ -324,7 +344,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         const char* e = std::getenv("MXD_WAVE_ABLATE");
         return e ? std::atoi(e) : 0;
       }();
-      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate};
+      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate, g.scatter};
       if (int rc = mxd::launch_wave(cfg, dev + g.first, stream))
         return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
                                         " rc=" + std::to_string(rc));

@@ -47,7 +47,8 @@ struct LaunchCfg {
 // ImgDev::tile_begin exactly like tiles; ty = band rows, tx = strip columns.
 struct WaveCfg {
   int32_t channels, f32, taps, nimgs, nunits;
-  int32_t mode;  // 0 = product kernel; 1..3 = diagnostic ablations (MXD_WAVE_ABLATE)
+  int32_t mode;     // 0 = product kernel; 1..4 = diagnostic ablations (MXD_WAVE_ABLATE)
+  int32_t scatter;  // every image's rows feed <= 3 outputs, <= 1 output ends per row
 };
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
 int wave_row_floats(int taps, int channels);

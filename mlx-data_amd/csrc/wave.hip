@@ -126,7 +126,7 @@ __device__ __forceinline__ void advance_rows_dyn(Chunk* R, __amdgpu_buffer_rsrc_
   }
 }
 
-template <int C, bool F32, int T, int MODE = 0>
+template <int C, bool F32, int T, int MODE = 0, bool SCATTER = false>
 __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __restrict__ imgs, int nimgs,
                                                                int nunits, int rowf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -219,23 +219,9 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     }
   };
 
-  // One output row from the T source rows in R.
-  auto step = [&](const Chunk* R, int y) {
-    // ---- V: vertical taps of row y -> LDS ----
-    kfloat* ye = ytab + y * ys;
-    float acc[kChunk];
-#pragma unroll
-    for (int i = 0; i < kChunk; i++) acc[i] = 0.0f;
-    if constexpr (MODE == 1) {
-#pragma unroll
-      for (int k = 0; k < T; k++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) acc[4 * i] += __uint_as_float(R[k].d[i] & 0x3fffffffu);
-    } else {
-#pragma unroll
-      for (int k = 0; k < T; k++) fma16(acc, ye[kTapHeader + k], R[k]);  // zero padded past the tap count
-    }
-    // floats of bytes 4l + 256j .. +3 go to vrow[4l + 256j]: lanes 16 B apart per store
+  // V result (16 f32 per lane) -> the wave's LDS row: floats of bytes
+  // 4l + 256j .. +3 go to vrow[4l + 256j], lanes 16 B apart per store.
+  auto write_vrow = [&](const float* acc) {
 #pragma unroll
     for (int j = 0; j < 4; j++)
       *reinterpret_cast<float4*>(vrow + 4 * lane + 256 * j) =
@@ -243,8 +229,10 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
 
-    // ---- H: horizontal taps from LDS, encode, store ----
+  // H: horizontal taps of output row y from the LDS row, encode, store.
+  auto h_store = [&](int y) {
     float out[kOutPerLane];
 #pragma unroll
     for (int j = 0; j < kOutPerLane; j++) {
@@ -282,25 +270,128 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  // Double-buffered rows: the loads of row y+1 are issued before row y is
-  // computed, so they fly during the whole V+H of row y.
-  // The prefetch is unconditional (clamped to the last output row) so every
-  // path through the loop has the same loads in flight and the compiler's
-  // counted waits stay partial.
-  Chunk RA[T], RB[T];
-  load_rows(RA, oy0);
-  for (int y = oy0;; y += 2) {
-    load_rows(RB, min(y + 1, crop_h - 1));
-    step(RA, y);
-    if (y + 1 >= oy1) break;
-    load_rows(RA, min(y + 2, crop_h - 1));
-    step(RB, y + 1);
-    if (y + 2 >= oy1) break;
+  if constexpr (!SCATTER) {
+    // ---- gather: each output row sums its T source rows, loaded for it ----
+    auto step = [&](const Chunk* R, int y) {
+      kfloat* ye = ytab + y * ys;
+      float acc[kChunk];
+#pragma unroll
+      for (int i = 0; i < kChunk; i++) acc[i] = 0.0f;
+      if constexpr (MODE == 1) {
+#pragma unroll
+        for (int k = 0; k < T; k++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[4 * i] += __uint_as_float(R[k].d[i] & 0x3fffffffu);
+      } else {
+#pragma unroll
+        for (int k = 0; k < T; k++) fma16(acc, ye[kTapHeader + k], R[k]);  // zero padded past the tap count
+      }
+      write_vrow(acc);
+      h_store(y);
+    };
+    // Double-buffered rows: the loads of row y+1 are issued before row y is
+    // computed, so they fly during the whole V+H of row y.  The prefetch is
+    // unconditional (clamped to the last output row) so every path through
+    // the loop has the same loads in flight and the compiler's counted waits
+    // stay partial.
+    Chunk RA[T], RB[T];
+    load_rows(RA, oy0);
+    for (int y = oy0;; y += 2) {
+      load_rows(RB, min(y + 1, crop_h - 1));
+      step(RA, y);
+      if (y + 1 >= oy1) break;
+      load_rows(RA, min(y + 2, crop_h - 1));
+      step(RB, y + 1);
+      if (y + 2 >= oy1) break;
+    }
+  } else {
+    // ---- scatter: every source row of the band is loaded once, converted
+    // once and accumulated into the (at most 3) output rows whose taps
+    // contain it; slot 0 is the oldest open output row.  Loads run kDepth
+    // rows ahead in a register ring (static indices: the row loop is
+    // unrolled by kDepth).  Requires: no source row feeds more than 3 output
+    // rows and at most one output row ends per source row (downsampling).
+    constexpr int kDepth = 8;
+    auto entry = [&](int y) { return ytab + min(y, crop_h - 1) * ys; };
+    int y0 = oy0;
+    kfloat* e0 = entry(y0);
+    kfloat* e1 = entry(y0 + 1);
+    kfloat* e2 = entry(y0 + 2);
+    int f0 = __float_as_int(e0[0]), l0 = f0 + __float_as_int(e0[1]) - 1;
+    int f1 = __float_as_int(e1[0]), l1 = f1 + __float_as_int(e1[1]) - 1;
+    int f2 = __float_as_int(e2[0]), l2 = f2 + __float_as_int(e2[1]) - 1;
+    kfloat* elast = entry(oy1 - 1);
+    const int rs = f0;
+    const int re = __float_as_int(elast[0]) + __float_as_int(elast[1]) - 1;
+    float A0[kChunk], A1[kChunk], A2[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; i++) A0[i] = A1[i] = A2[i] = 0.0f;
+    Chunk ring[kDepth];
+#pragma unroll
+    for (int i = 0; i < kDepth; i++) ring[i] = load_chunk(rsrc, loff, min(rs + i, re) * sstride);
+    for (int r = rs; r <= re; r += kDepth) {
+#pragma unroll
+      for (int i = 0; i < kDepth; i++) {
+        const int row = r + i;
+        if (row > re) break;
+        float x[kChunk];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          x[4 * q + 0] = (float)(ring[i].d[q] & 0xffu);
+          x[4 * q + 1] = (float)((ring[i].d[q] >> 8) & 0xffu);
+          x[4 * q + 2] = (float)((ring[i].d[q] >> 16) & 0xffu);
+          x[4 * q + 3] = (float)(ring[i].d[q] >> 24);
+        }
+        ring[i] = load_chunk(rsrc, loff, min(row + kDepth, re) * sstride);
+        {
+          const float w = e0[kTapHeader + max(row - f0, 0)];
+#pragma unroll
+          for (int q = 0; q < kChunk; q++) A0[q] = __builtin_fmaf(w, x[q], A0[q]);
+        }
+        if (row >= f1 && y0 + 1 < oy1) {
+          const float w = e1[kTapHeader + row - f1];
+#pragma unroll
+          for (int q = 0; q < kChunk; q++) A1[q] = __builtin_fmaf(w, x[q], A1[q]);
+        }
+        if (row >= f2 && y0 + 2 < oy1) {
+          const float w = e2[kTapHeader + row - f2];
+#pragma unroll
+          for (int q = 0; q < kChunk; q++) A2[q] = __builtin_fmaf(w, x[q], A2[q]);
+        }
+        if (row == l0) {  // output row y0 is complete
+          write_vrow(A0);
+          h_store(y0);
+#pragma unroll
+          for (int q = 0; q < kChunk; q++) {
+            A0[q] = A1[q];
+            A1[q] = A2[q];
+            A2[q] = 0.0f;
+          }
+          y0++;
+          e0 = e1;
+          f0 = f1;
+          l0 = l1;
+          e1 = e2;
+          f1 = f2;
+          l1 = l2;
+          e2 = entry(y0 + 2);
+          f2 = __float_as_int(e2[0]);
+          l2 = f2 + __float_as_int(e2[1]) - 1;
+        }
+      }
+    }
   }
 }
 
 template <int C, bool F32, int T, int MODE = 0>
 int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
+  if (cfg.scatter) {
+    const int rowf = wave_row_floats(cfg.taps, C);
+    const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL((resample_wave<C, F32, T, 0, true>), dim3(blocks), dim3(kWaves * kLanes),
+                       kWaves * rowf * (int)sizeof(float), s, imgs, cfg.nimgs, cfg.nunits, rowf);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if constexpr (MODE == 0 && C == 3 && F32 && T == 8) {
     switch (cfg.mode) {
       case 1: return launch_ct<C, F32, T, 1>(cfg, imgs, s);
