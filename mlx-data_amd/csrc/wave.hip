@@ -328,7 +328,10 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     for (int i = 0; i < kChunk; i++) A0[i] = A1[i] = A2[i] = 0.0f;
     Chunk ring[kDepth];
 #pragma unroll
-    for (int i = 0; i < kDepth; i++) ring[i] = load_chunk(rsrc, loff, min(rs + i, re) * sstride);
+    for (int i = 0; i < kDepth; i++) {
+      if constexpr (MODE == 2) ring[i] = Chunk{{(uint32_t)(lane * 7 + i), (uint32_t)(rs * 3), (uint32_t)lane, (uint32_t)(i ^ lane)}};
+      else ring[i] = load_chunk(rsrc, loff, min(rs + i, re) * sstride);
+    }
     for (int r = rs; r <= re; r += kDepth) {
 #pragma unroll
       for (int i = 0; i < kDepth; i++) {
@@ -342,18 +345,22 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
           x[4 * q + 2] = (float)((ring[i].d[q] >> 16) & 0xffu);
           x[4 * q + 3] = (float)(ring[i].d[q] >> 24);
         }
-        ring[i] = load_chunk(rsrc, loff, min(row + kDepth, re) * sstride);
-        {
+        if constexpr (MODE == 2) ring[i].d[0] += (uint32_t)row;
+        else ring[i] = load_chunk(rsrc, loff, min(row + kDepth, re) * sstride);
+        if constexpr (MODE == 1) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) A0[q] += __uint_as_float(ring[i].d[q] & 0x3fffffffu);
+        } else {
           const float w = e0[kTapHeader + max(row - f0, 0)];
 #pragma unroll
           for (int q = 0; q < kChunk; q++) A0[q] = __builtin_fmaf(w, x[q], A0[q]);
         }
-        if (row >= f1 && y0 + 1 < oy1) {
+        if (MODE != 1 && row >= f1 && y0 + 1 < oy1) {
           const float w = e1[kTapHeader + row - f1];
 #pragma unroll
           for (int q = 0; q < kChunk; q++) A1[q] = __builtin_fmaf(w, x[q], A1[q]);
         }
-        if (row >= f2 && y0 + 2 < oy1) {
+        if (MODE != 1 && row >= f2 && y0 + 2 < oy1) {
           const float w = e2[kTapHeader + row - f2];
 #pragma unroll
           for (int q = 0; q < kChunk; q++) A2[q] = __builtin_fmaf(w, x[q], A2[q]);
@@ -388,8 +395,13 @@ int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
   if (cfg.scatter) {
     const int rowf = wave_row_floats(cfg.taps, C);
     const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
-    hipLaunchKernelGGL((resample_wave<C, F32, T, 0, true>), dim3(blocks), dim3(kWaves * kLanes),
-                       kWaves * rowf * (int)sizeof(float), s, imgs, cfg.nimgs, cfg.nunits, rowf);
+    auto k = resample_wave<C, F32, T, 0, true>;
+    if constexpr (C == 3 && F32 && T == 8) {
+      if (cfg.mode == 1) k = resample_wave<C, F32, T, 1, true>;
+      if (cfg.mode == 2) k = resample_wave<C, F32, T, 2, true>;
+    }
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), kWaves * rowf * (int)sizeof(float), s, imgs,
+                       cfg.nimgs, cfg.nunits, rowf);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if constexpr (MODE == 0 && C == 3 && F32 && T == 8) {
