@@ -101,6 +101,55 @@ class TableCache {
   std::map<std::tuple<int32_t, int32_t, int32_t>, std::unique_ptr<DevTable>> map_;
 };
 
+// Right-aligned vertical tables for the ring kernel: per output row
+// {last tap row, tap count, w[T]} with the weights aligned so that w[T-1]
+// belongs to the last tap row (zeros in front).  Keyed by (device, in, out, T).
+class RightTableCache {
+ public:
+  int get(int32_t device, const DevTable& base, int32_t in, int32_t out, int32_t t, const DevTable** out_tab) {
+    std::lock_guard<std::mutex> lock(mu_);
+    auto key = std::make_tuple(device, in, out, t);
+    auto it = map_.find(key);
+    if (it != map_.end()) {
+      *out_tab = it->second.get();
+      return MXD_OK;
+    }
+    mxd::AxisTaps taps;
+    if (!mxd::build_axis_taps(in, out, 0, out, &taps) || taps.width > t)
+      return fail(MXD_ERR_INVALID, "mxd: right-aligned table geometry");
+    const int32_t padded = std::max<int32_t>(t, mxd::kMinTabWidth);
+    const int32_t stride = mxd::kTapHeader + padded;
+    std::vector<float> host((size_t)out * stride, 0.0f);
+    for (int32_t i = 0; i < out; i++) {
+      float* e = &host[(size_t)i * stride];
+      const int32_t last = taps.first[i] + taps.count[i] - 1;
+      std::memcpy(&e[0], &last, 4);
+      std::memcpy(&e[1], &taps.count[i], 4);
+      std::memcpy(&e[2 + (t - taps.count[i])], &taps.weight[(size_t)i * taps.width], sizeof(float) * taps.count[i]);
+    }
+    auto tab = std::make_unique<DevTable>();
+    tab->width = taps.width;
+    tab->padded = padded;
+    tab->first = base.first;
+    tab->count = base.count;
+    DeviceGuard g(device);
+    MXD_HIP(hipMalloc(&tab->ptr, host.size() * sizeof(float)));
+    MXD_HIP(hipMemcpy(tab->ptr, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    *out_tab = tab.get();
+    map_[key] = std::move(tab);
+    return MXD_OK;
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<std::tuple<int32_t, int32_t, int32_t, int32_t>, std::unique_ptr<DevTable>> map_;
+};
+
+RightTableCache& right_tables() {
+  static RightTableCache* c = new RightTableCache();
+  return *c;
+}
+
 TableCache& tables() {
   static TableCache* c = new TableCache();  // leaked on purpose: outlives static teardown
   return *c;
@@ -212,7 +261,8 @@ struct ImgPlan {
   const DevTable* xt = nullptr;
   const DevTable* yt = nullptr;
   int32_t bucket = -1;   // wave path tap bucket, -1 = not eligible
-  int32_t scatter = 0;   // vertical taps allow the row-once (scatter) kernel
+  int32_t ring = 0;      // use the row-once register-ring kernel (right-aligned y table)
+  const DevTable* yr = nullptr;
   int32_t nstrips = 0, tx = 0;
 };
 
@@ -245,15 +295,11 @@ bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int3
   return false;
 }
 
-// The scatter kernel keeps 3 open output rows and closes at most one per
-// source row: every source row must feed <= 3 outputs of the window and the
-// last taps must strictly increase.
-bool scatter_ok(const DevTable& yt, int32_t off, int32_t len) {
-  for (int32_t y = off; y < off + len; y++) {
-    const int32_t last = yt.first[y] + yt.count[y] - 1;
-    if (y + 1 < off + len && yt.first[y + 1] + yt.count[y + 1] - 1 <= last) return false;
-    if (y + 3 < off + len && yt.first[y + 3] <= last) return false;
-  }
+// The ring kernel closes at most one output row per source row: the last taps
+// of consecutive output rows in the window must strictly increase.
+bool one_output_per_row(const DevTable& yt, int32_t off, int32_t len) {
+  for (int32_t y = off; y + 1 < off + len; y++)
+    if (yt.first[y + 1] + yt.count[y + 1] <= yt.first[y] + yt.count[y]) return false;
   return true;
 }
 
@@ -285,11 +331,13 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (wave_ok) {
       p.bucket = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
       wave_ok = p.bucket > 0 && wave_strips(*p.xt, im, &p.nstrips, &p.tx);
-      static const int no_scatter = [] {
-        const char* e = std::getenv("MXD_NO_SCATTER");
+      static const int no_ring = [] {
+        const char* e = std::getenv("MXD_NO_RING");
         return e ? std::atoi(e) : 0;
       }();
-      p.scatter = !no_scatter && scatter_ok(*p.yt, im.crop_y, im.crop_h) ? 1 : 0;
+      p.ring = !no_ring && p.bucket <= 12 && one_output_per_row(*p.yt, im.crop_y, im.crop_h) ? 1 : 0;
+      if (wave_ok && p.ring)
+        if (int rc = right_tables().get(device, *p.yt, im.src_h, im.resize_h, p.bucket, &p.yr)) return rc;
     }
   }
   DeviceGuard guard(device);
@@ -313,21 +361,25 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     // One launch per tap bucket; descriptors of all groups share one upload.
     std::vector<int32_t> order(n);
     for (int32_t i = 0; i < n; i++) order[i] = i;
-    auto key = [&](int32_t i) { return plans[i].bucket * 2 + plans[i].scatter; };
+    auto key = [&](int32_t i) { return plans[i].bucket * 2 + plans[i].ring; };
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
     int64_t strip_rows = 0;
     for (int32_t i = 0; i < n; i++) strip_rows += (int64_t)plans[i].nstrips * images[i].crop_h;
     const int32_t ty = (int32_t)std::max<int64_t>(8, std::min<int64_t>(64, (strip_rows + 8191) / 8192));
     std::vector<ImgDev> descs(n);
-    struct Group { int32_t first, count, units, bucket, scatter; };
+    struct Group { int32_t first, count, units, bucket, ring; };
     std::vector<Group> groups;
     for (int32_t k = 0; k < n; k++) {
       const int32_t i = order[k];
-      if (groups.empty() || groups.back().bucket != plans[i].bucket || groups.back().scatter != plans[i].scatter)
-        groups.push_back({k, 0, 0, plans[i].bucket, plans[i].scatter});
+      if (groups.empty() || groups.back().bucket != plans[i].bucket || groups.back().ring != plans[i].ring)
+        groups.push_back({k, 0, 0, plans[i].bucket, plans[i].ring});
       Group& g = groups.back();
       ImgDev& d = descs[k];
       fill(d, images[i], plans[i]);
+      if (plans[i].ring) {
+        d.ywidth = plans[i].yr->padded;
+        d.ytab = plans[i].yr->ptr + (size_t)images[i].crop_y * (mxd::kTapHeader + plans[i].yr->padded);
+      }
       d.tile_begin = g.units;
       d.nstrips = plans[i].nstrips;
       d.tx = plans[i].tx;
@@ -344,7 +396,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         const char* e = std::getenv("MXD_WAVE_ABLATE");
         return e ? std::atoi(e) : 0;
       }();
-      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate, g.scatter};
+      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate, g.ring};
       if (int rc = mxd::launch_wave(cfg, dev + g.first, stream))
         return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
                                         " rc=" + std::to_string(rc));

@@ -48,7 +48,7 @@ struct LaunchCfg {
 struct WaveCfg {
   int32_t channels, f32, taps, nimgs, nunits;
   int32_t mode;     // 0 = product kernel; 1..4 = diagnostic ablations (MXD_WAVE_ABLATE)
-  int32_t scatter;  // every image's rows feed <= 3 outputs, <= 1 output ends per row
+  int32_t ring;     // register-ring kernel; ImgDev::ytab is the right-aligned table
 };
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
 int wave_row_floats(int taps, int channels);

@@ -26,6 +26,9 @@
 // real neighbouring rows/columns (or zeros), so every value is finite.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+#include <utility>
+
 #include "resample.h"
 
 namespace mxd {
@@ -83,6 +86,17 @@ __device__ __forceinline__ void fma16(float* acc, float w, const Chunk& v) {
   }
 }
 
+// Calls f(std::integral_constant<int, I>) for I = 0..N-1 (guaranteed unrolled,
+// so register-array indices derived from I are static).
+template <class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // Rows for the next output, whose first tap is D rows further down:
 // R[k] <- R[k + D], then load the D rows that are new.
 template <int T, int D>
@@ -126,7 +140,7 @@ __device__ __forceinline__ void advance_rows_dyn(Chunk* R, __amdgpu_buffer_rsrc_
   }
 }
 
-template <int C, bool F32, int T, int MODE = 0, bool SCATTER = false>
+template <int C, bool F32, int T, int MODE = 0, bool RING = false>
 __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __restrict__ imgs, int nimgs,
                                                                int nunits, int rowf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  if constexpr (!SCATTER) {
+  if constexpr (!RING) {
     // ---- gather: each output row sums its T source rows, loaded for it ----
     auto step = [&](const Chunk* R, int y) {
       kfloat* ye = ytab + y * ys;
@@ -305,94 +319,67 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
       if (y + 2 >= oy1) break;
     }
   } else {
-    // ---- scatter: every source row of the band is loaded once, converted
-    // once and accumulated into the (at most 3) output rows whose taps
-    // contain it; slot 0 is the oldest open output row.  Loads run kDepth
-    // rows ahead in a register ring (static indices: the row loop is
-    // unrolled by kDepth).  Requires: no source row feeds more than 3 output
-    // rows and at most one output row ends per source row (downsampling).
-    constexpr int kDepth = 8;
-    auto entry = [&](int y) { return ytab + min(y, crop_h - 1) * ys; };
-    int y0 = oy0;
-    kfloat* e0 = entry(y0);
-    kfloat* e1 = entry(y0 + 1);
-    kfloat* e2 = entry(y0 + 2);
-    int f0 = __float_as_int(e0[0]), l0 = f0 + __float_as_int(e0[1]) - 1;
-    int f1 = __float_as_int(e1[0]), l1 = f1 + __float_as_int(e1[1]) - 1;
-    int f2 = __float_as_int(e2[0]), l2 = f2 + __float_as_int(e2[1]) - 1;
-    kfloat* elast = entry(oy1 - 1);
-    const int rs = f0;
-    const int re = __float_as_int(elast[0]) + __float_as_int(elast[1]) - 1;
-    float A0[kChunk], A1[kChunk], A2[kChunk];
+    // ---- ring: every source row of the band is loaded once, kLook rows
+    // ahead, into a register ring of kRing = T + kLook slots; the source-row
+    // loop is unrolled by kRing so every slot index is static.  When row r is
+    // the last tap of output row y, y's taps are exactly the T rows ending at
+    // r (right-aligned weights, zero for the rows before y's first tap), all
+    // resident in the ring: gather them (V), then H and store.  Requires the
+    // last taps of consecutive output rows to strictly increase (at most one
+    // output row ends per source row: downsampling); the host checks it.
+    constexpr int kLook = 6;
+    constexpr int kRing = T + kLook;
+    // right-aligned vertical table: {last row, count, w[T]} per output row
+    kfloat* rtab = ytab;
+    auto last_of = [&](int y) { return __float_as_int(rtab[min(y, crop_h - 1) * ys]); };
+    const int rs = last_of(oy0) - (T - 1);
+    const int re = last_of(oy1 - 1);
+    int y = oy0;
+    int ly = last_of(y);
+    Chunk ring[kRing];
 #pragma unroll
-    for (int i = 0; i < kChunk; i++) A0[i] = A1[i] = A2[i] = 0.0f;
-    Chunk ring[kDepth];
-#pragma unroll
-    for (int i = 0; i < kDepth; i++) {
+    for (int i = 0; i < kLook; i++) {
       if constexpr (MODE == 2) ring[i] = Chunk{{(uint32_t)(lane * 7 + i), (uint32_t)(rs * 3), (uint32_t)lane, (uint32_t)(i ^ lane)}};
       else ring[i] = load_chunk(rsrc, loff, min(rs + i, re) * sstride);
     }
-    for (int r = rs; r <= re; r += kDepth) {
+    for (int base = rs; base <= re; base += kRing) {
+      static_for<kRing>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        __builtin_amdgcn_sched_barrier(0);  // keep each row's work (and its load) in place
+        const int r = base + i;
+        if (r > re) return;
+        // keep kLook rows in flight: slot (i + kLook) % kRing is free (its row
+        // left the tap window of every open output row)
+        if constexpr (MODE == 2) ring[(i + kLook) % kRing].d[0] = (uint32_t)(r + lane);
+        else ring[(i + kLook) % kRing] = load_chunk(rsrc, loff, min(r + kLook, re) * sstride);
+        if (r == ly) {  // output row y ends at source row r (at most one: checked on the host)
+          kfloat* we = rtab + y * ys + kTapHeader;
+          float acc[kChunk];
 #pragma unroll
-      for (int i = 0; i < kDepth; i++) {
-        const int row = r + i;
-        if (row > re) break;
-        float x[kChunk];
+          for (int q = 0; q < kChunk; q++) acc[q] = 0.0f;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          x[4 * q + 0] = (float)(ring[i].d[q] & 0xffu);
-          x[4 * q + 1] = (float)((ring[i].d[q] >> 8) & 0xffu);
-          x[4 * q + 2] = (float)((ring[i].d[q] >> 16) & 0xffu);
-          x[4 * q + 3] = (float)(ring[i].d[q] >> 24);
-        }
-        if constexpr (MODE == 2) ring[i].d[0] += (uint32_t)row;
-        else ring[i] = load_chunk(rsrc, loff, min(row + kDepth, re) * sstride);
-        if constexpr (MODE == 1) {
+          for (int k = 0; k < T; k++) {
+            const Chunk& c = ring[(i + kRing - (T - 1) + k) % kRing];
+            if constexpr (MODE == 1) {
 #pragma unroll
-          for (int q = 0; q < 4; q++) A0[q] += __uint_as_float(ring[i].d[q] & 0x3fffffffu);
-        } else {
-          const float w = e0[kTapHeader + max(row - f0, 0)];
-#pragma unroll
-          for (int q = 0; q < kChunk; q++) A0[q] = __builtin_fmaf(w, x[q], A0[q]);
-        }
-        if (MODE != 1 && row >= f1 && y0 + 1 < oy1) {
-          const float w = e1[kTapHeader + row - f1];
-#pragma unroll
-          for (int q = 0; q < kChunk; q++) A1[q] = __builtin_fmaf(w, x[q], A1[q]);
-        }
-        if (MODE != 1 && row >= f2 && y0 + 2 < oy1) {
-          const float w = e2[kTapHeader + row - f2];
-#pragma unroll
-          for (int q = 0; q < kChunk; q++) A2[q] = __builtin_fmaf(w, x[q], A2[q]);
-        }
-        if (row == l0) {  // output row y0 is complete
-          write_vrow(A0);
-          h_store(y0);
-#pragma unroll
-          for (int q = 0; q < kChunk; q++) {
-            A0[q] = A1[q];
-            A1[q] = A2[q];
-            A2[q] = 0.0f;
+              for (int q = 0; q < 4; q++) acc[4 * q] += __uint_as_float(c.d[q] & 0x3fffffffu);
+            } else {
+              fma16(acc, we[k], c);
+            }
           }
-          y0++;
-          e0 = e1;
-          f0 = f1;
-          l0 = l1;
-          e1 = e2;
-          f1 = f2;
-          l1 = l2;
-          e2 = entry(y0 + 2);
-          f2 = __float_as_int(e2[0]);
-          l2 = f2 + __float_as_int(e2[1]) - 1;
+          write_vrow(acc);
+          h_store(y);
+          ++y;
+          ly = y < oy1 ? last_of(y) : 0x7fffffff;
         }
-      }
+      });
     }
   }
 }
 
 template <int C, bool F32, int T, int MODE = 0>
 int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
-  if (cfg.scatter) {
+  if (cfg.ring) {
     const int rowf = wave_row_floats(cfg.taps, C);
     const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
     auto k = resample_wave<C, F32, T, 0, true>;
