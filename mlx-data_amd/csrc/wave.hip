@@ -386,6 +386,7 @@ int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
     if constexpr (C == 3 && F32 && T == 8) {
       if (cfg.mode == 1) k = resample_wave<C, F32, T, 1, true>;
       if (cfg.mode == 2) k = resample_wave<C, F32, T, 2, true>;
+      if (cfg.mode == 3) k = resample_wave<C, F32, T, 3, true>;
     }
     hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), kWaves * rowf * (int)sizeof(float), s, imgs,
                        cfg.nimgs, cfg.nunits, rowf);
