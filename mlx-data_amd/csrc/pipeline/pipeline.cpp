@@ -1,0 +1,726 @@
+// pipeline.cpp -- see pipeline.h.  Host-side control only: every pixel of the
+// resize / crop / mirror path is produced by the gfx950 kernels behind
+// mxd_resize_crop_host (include/mxd_amd.h); there is no CPU pixel path for
+// uint8 images.
+#include "pipeline.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+
+#include "mxd_amd.h"
+
+namespace mxd {
+namespace pipe {
+
+int64_t itemsize(DType t) {
+  switch (t) {
+    case DType::UInt8:
+    case DType::Int8:
+      return 1;
+    case DType::Int32:
+    case DType::Float:
+      return 4;
+    case DType::Int64:
+    case DType::Double:
+      return 8;
+    default:
+      return 0;
+  }
+}
+
+namespace {
+
+int64_t shape_size(const std::vector<int64_t>& s) {
+  int64_t n = 1;
+  for (auto d : s) n *= d;
+  return n;
+}
+
+std::shared_ptr<void> alloc_bytes(int64_t n) {
+  // 64-byte alignment: batch tensors are handed to numpy / torch as is.
+  void* p = nullptr;
+  if (posix_memalign(&p, 64, std::max<int64_t>(n, 1)) != 0) throw std::bad_alloc();
+  return std::shared_ptr<void>(p, std::free);
+}
+
+void check(int rc) {
+  if (rc != MXD_OK) throw std::runtime_error(mxd_last_error());
+}
+
+// ------------------------------------------------------------ device choice
+std::mutex g_dev_mu;
+std::vector<int> g_devices;
+bool g_devices_set = false;
+std::atomic<uint64_t> g_rr{0};
+
+int next_device() {
+  std::vector<int> d = devices();
+  if (d.empty()) throw std::runtime_error("mxd: no HIP device visible (the image path runs only on the GPU)");
+  return d[g_rr.fetch_add(1) % d.size()];
+}
+
+mxd_image plan_desc(const ImagePlan& p, void* dst, int64_t dst_stride) {
+  const Array& s = *p.src;
+  const int64_t c = s.shape(2);
+  const int64_t stride = s.shape(1) * c;
+  mxd_image d{};
+  d.src = static_cast<const uint8_t*>(s.data()) + p.sy * stride + p.sx * c;
+  d.src_stride = stride;
+  d.src_w = (int32_t)p.sw;
+  d.src_h = (int32_t)p.sh;
+  d.channels = (int32_t)c;
+  d.resize_w = (int32_t)p.resize_w;
+  d.resize_h = (int32_t)p.resize_h;
+  d.crop_x = (int32_t)p.crop_x;
+  d.crop_y = (int32_t)p.crop_y;
+  d.crop_w = (int32_t)p.crop_w;
+  d.crop_h = (int32_t)p.crop_h;
+  d.flip = p.flip ? 1 : 0;
+  d.dst = dst;
+  d.dst_stride = dst_stride;
+  return d;
+}
+
+void run_host(const std::vector<mxd_image>& descs) {
+  if (descs.empty()) return;
+  check(mxd_resize_crop_host(descs.data(), (int32_t)descs.size(), MXD_U8, next_device()));
+}
+
+}  // namespace
+
+int64_t ImagePlan::channels() const { return src->shape(2); }
+
+// ------------------------------------------------------------------ Array
+Array::Array(DType type, std::vector<int64_t> shape) : type_(type), shape_(std::move(shape)) {
+  if (type_ == DType::Any && size() != 0) throw std::runtime_error("Array: cannot create a tensor of undetermined type");
+  if (size() > 0) {
+    data_ = alloc_bytes(nbytes());
+    std::memset(data_.get(), 0, nbytes());
+  }
+}
+
+Array::Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data)
+    : type_(type), shape_(std::move(shape)), data_(std::move(data)) {}
+
+Array::Array(std::shared_ptr<const ImagePlan> plan)
+    : type_(DType::UInt8), shape_({plan->crop_h, plan->crop_w, plan->channels()}), plan_(std::move(plan)) {}
+
+int64_t Array::shape(int d) const {
+  if (d < 0) d += ndim();
+  if (d < 0 || d >= ndim()) throw std::runtime_error("Array: out of bound dimension");
+  return shape_[d];
+}
+
+int64_t Array::size() const { return shape_size(shape_); }
+
+bool Array::pending() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return plan_ && !data_;
+}
+
+void* Array::data() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!data_ && plan_) {
+    auto buf = alloc_bytes(nbytes());
+    const int64_t row = shape_[1] * shape_[2];
+    run_host({plan_desc(*plan_, buf.get(), row)});
+    data_ = buf;
+  }
+  return data_.get();
+}
+
+std::shared_ptr<Array> check_key(const Sample& s, const std::string& key) {
+  auto it = s.find(key);
+  if (it == s.end()) throw std::runtime_error("key <" + key + "> expected");
+  return it->second;
+}
+
+void set_devices(const std::vector<int>& d) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  g_devices = d;
+  g_devices_set = true;
+}
+
+std::vector<int> devices() {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (!g_devices_set) {
+    int n = 0;
+    if (mxd_device_count(&n) != MXD_OK) n = 0;
+    g_devices.clear();
+    for (int i = 0; i < n; i++) g_devices.push_back(i);
+    g_devices_set = true;
+  }
+  return g_devices;
+}
+
+// ------------------------------------------------------------------ state
+// core/State.cpp:9-22: a global generator; each thread takes a copy of it
+// whenever set_state() bumped the version.
+namespace {
+State g_state{std::mt19937(), 0};
+std::mutex g_state_mu;
+}  // namespace
+
+void set_state(int64_t seed) {
+  std::lock_guard<std::mutex> lk(g_state_mu);
+  g_state.gen = std::mt19937(seed);
+  g_state.version++;
+}
+
+std::shared_ptr<State> get_state() {
+  static thread_local std::shared_ptr<State> st;
+  std::lock_guard<std::mutex> lk(g_state_mu);
+  if (!st || st->version != g_state.version) st = std::make_shared<State>(g_state);
+  return st;
+}
+
+// ------------------------------------------------------------------ ops
+Sample KeyTransformOp::apply(const Sample& sample) const {
+  auto x = check_key(sample, ikey_);
+  Sample res = sample;
+  res[okey_.empty() ? ikey_ : okey_] = apply_key(x);
+  return res;
+}
+
+namespace {
+
+// The image (H, W, C) as a plan: a pending one as is, a materialised one as
+// the identity plan over all of it.
+ImagePlan view(const std::shared_ptr<Array>& img) {
+  if (img->plan() && img->pending()) return *img->plan();
+  if (img->type() != DType::UInt8) throw std::invalid_argument("image must be of type UInt8");
+  ImagePlan p;
+  p.src = img;
+  p.sw = p.resize_w = p.crop_w = img->shape(1);
+  p.sh = p.resize_h = p.crop_h = img->shape(0);
+  return p;
+}
+
+void verify_dimensions(int64_t w, int64_t h, int64_t c) {
+  // core/image/ImageTransform.cpp:23-31
+  if (h <= 0 || w <= 0) throw std::runtime_error("image: cannot create image with 0 or negative dimension");
+  if (c <= 0 || c > 4) throw std::runtime_error("image: channels must be 0 < c <= 4");
+}
+
+std::shared_ptr<Array> make(const ImagePlan& p) { return std::make_shared<Array>(std::make_shared<const ImagePlan>(p)); }
+
+// core::image::resize (core/image/ImageTransform.cpp:41-62).
+std::shared_ptr<Array> plan_resize(const std::shared_ptr<Array>& img, int64_t dw, int64_t dh) {
+  verify_dimensions(dw, dh, img->shape(2));
+  ImagePlan p = view(img);
+  const bool identity_so_far = p.resize_w == p.sw && p.resize_h == p.sh && !p.flip;
+  if (identity_so_far) {
+    // crop-then-resize: the crop becomes the source window.
+    p.sx += p.crop_x;
+    p.sy += p.crop_y;
+    p.sw = p.crop_w;
+    p.sh = p.crop_h;
+  } else {
+    // resize of a resized (or mirrored) image: run the first one, resample
+    // its output.
+    img->data();
+    p = view(img);
+  }
+  p.resize_w = p.crop_w = dw;
+  p.resize_h = p.crop_h = dh;
+  p.crop_x = p.crop_y = 0;
+  p.flip = false;
+  if (p.src->shape(2) == 4)
+    throw std::runtime_error("mxd: 4-channel (STBIR_RGBA alpha-weighted) resize not supported");
+  return make(p);
+}
+
+// core::image::crop -> array::sub (Array.cpp:544-583), in the coordinates of
+// the current view.
+std::shared_ptr<Array> plan_crop(const std::shared_ptr<Array>& img, int64_t x, int64_t y, int64_t w, int64_t h) {
+  verify_dimensions(w, h, 3);
+  const int64_t W = img->shape(1), H = img->shape(0);
+  if (y < 0 || x < 0 || y >= H || x >= W) throw std::runtime_error("Array: sub: offset out of bound");
+  if (y + h > H || x + w > W) throw std::runtime_error("Array: sub: shape out of bound");
+  if (img->type() != DType::UInt8) {
+    // Not the image path (the resize kernel is uint8 only, like the
+    // reference's resize): a plain strided sub-array copy.
+    const int64_t c = img->ndim() > 2 ? img->shape(2) : 1, isz = itemsize(img->type());
+    auto out = std::make_shared<Array>(img->type(), std::vector<int64_t>{h, w, c});
+    const auto* s = static_cast<const uint8_t*>(img->data());
+    auto* d = static_cast<uint8_t*>(out->data());
+    for (int64_t r = 0; r < h; r++) std::memcpy(d + r * w * c * isz, s + ((y + r) * W + x) * c * isz, w * c * isz);
+    return out;
+  }
+  ImagePlan p = view(img);
+  p.crop_x = p.flip ? p.crop_x + p.crop_w - x - w : p.crop_x + x;
+  p.crop_y += y;
+  p.crop_w = w;
+  p.crop_h = h;
+  return make(p);
+}
+
+}  // namespace
+
+// op/ImageTransform.cpp:22-31 + core/image/ImageIO.cpp:39-49
+std::shared_ptr<Array> ImageOp::apply_key(const std::shared_ptr<Array>& x) const {
+  if (x->ndim() == 4) throw std::runtime_error("mxd: video (4-d) arrays are not on the image path");
+  if (x->ndim() != 3) throw std::runtime_error("verifyImage: image must be 3 dimension Array (HWC)");
+  if (x->shape(2) == 0 || x->shape(2) > 4) throw std::runtime_error("verifyImage: channels must be 0 <= c <= 4");
+  return apply_image(x);
+}
+
+// op/ImageTransform.cpp:78-94 + core::image::scale :33-39
+std::shared_ptr<Array> ImageResizeSmallestSide::apply_image(const std::shared_ptr<Array>& img) const {
+  if (size_ <= 0) throw std::runtime_error("ImageResizeSmallestSide: illegal target size: " + std::to_string(size_));
+  const int64_t w = img->shape(1), h = img->shape(0);
+  const double scale = h > w ? (double)size_ / w : (double)size_ / h;
+  return plan_resize(img, std::lround(scale * w), std::lround(scale * h));
+}
+
+// op/ImageTransform.cpp:103-106
+std::shared_ptr<Array> ImageResize::apply_image(const std::shared_ptr<Array>& img) const {
+  return plan_resize(img, w_, h_);
+}
+
+// op/ImageTransform.cpp:115-126
+std::shared_ptr<Array> ImageCenterCrop::apply_image(const std::shared_ptr<Array>& img) const {
+  const int64_t w = img->shape(1), h = img->shape(0);
+  if (h_ > h || w_ > w) throw std::runtime_error("ImageCenterCrop: target image size larger than input image");
+  return plan_crop(img, (w - w_) / 2, (h - h_) / 2, w_, h_);
+}
+
+// op/ImageTransform.cpp:135-158 (x drawn before y, int64 uniform ints)
+std::shared_ptr<Array> ImageRandomCrop::apply_image(const std::shared_ptr<Array>& img) const {
+  const int64_t w = img->shape(1), h = img->shape(0);
+  if (h_ > h || w_ > w) throw std::runtime_error("ImageRandomCrop: target image size larger than input image");
+  std::uniform_int_distribution<int64_t> xu{0, w - w_};
+  std::uniform_int_distribution<int64_t> yu{0, h - h_};
+  auto st = get_state();
+  const int64_t x = xu(st->gen);
+  const int64_t y = yu(st->gen);
+  return plan_crop(img, x, y, w_, h_);
+}
+
+// op/ImageTransform.cpp:323-332 + core::image::hflip :123-140
+std::shared_ptr<Array> ImageRandomHFlip::apply_image(const std::shared_ptr<Array>& img) const {
+  std::uniform_real_distribution<float> u{0, 1.0};
+  auto st = get_state();
+  if (u(st->gen) <= prob_) {
+    verify_dimensions(img->shape(1), img->shape(0), img->shape(2));
+    ImagePlan p = view(img);
+    p.flip = !p.flip;
+    return make(p);
+  }
+  return img;
+}
+
+// ------------------------------------------------------------------ load
+namespace {
+std::mutex g_dec_mu;
+ImageDecoder g_decoder;
+}  // namespace
+
+void set_image_decoder(ImageDecoder dec) {
+  std::lock_guard<std::mutex> lk(g_dec_mu);
+  g_decoder = std::move(dec);
+}
+
+LoadImage::LoadImage(std::string ikey, std::string prefix, bool info, std::string format, bool from_memory,
+                     std::string okey)
+    : KeyTransformOp(std::move(ikey), std::move(okey)),
+      prefix_(std::move(prefix)),
+      info_(info),
+      format_(std::move(format)),
+      from_memory_(from_memory) {}
+
+// op/LoadImage.cpp:23-48
+std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) const {
+  std::string path;
+  if (!from_memory_) {
+    if (x->type() != DType::Int8) throw std::runtime_error("LoadImage: char array (int8) expected");
+    std::string filename(static_cast<const char*>(x->data()), x->size());
+    path = prefix_;
+    if (!filename.empty() && filename[0] == '/') path = filename;  // std::filesystem::path operator/
+    else if (!path.empty()) path = (path.back() == '/' ? path : path + "/") + filename;
+    else path = filename;
+  }
+  ImageDecoder dec;
+  {
+    std::lock_guard<std::mutex> lk(g_dec_mu);
+    dec = g_decoder;
+  }
+  if (!dec) throw std::runtime_error("LoadImage: no image decoder installed");
+  auto out = dec(path, x, from_memory_, info_);
+  if (!out) throw std::runtime_error("LoadImage: unable to load image <" + (from_memory_ ? std::string("stream") : path) + ">");
+  return out;
+}
+
+// ------------------------------------------------------------------ batch
+namespace {
+
+// array_copy_linear_to_strided (Array.cpp:405-463): `src` (dense, shape
+// `shape`) into `dst` at element offset `off` with per-dim strides `stride`.
+void copy_to_strided(uint8_t* dst, int64_t off, const uint8_t* src, const std::vector<int64_t>& shape,
+                     const std::vector<int64_t>& stride, int64_t isz) {
+  const int nd = (int)shape.size();
+  if (nd == 0) {
+    std::memcpy(dst + off * isz, src, isz);
+    return;
+  }
+  const int64_t run = shape[nd - 1] * isz;
+  int64_t rows = 1;
+  for (int d = 0; d < nd - 1; d++) rows *= shape[d];
+  std::vector<int64_t> idx(std::max(nd - 1, 0), 0);
+  for (int64_t r = 0; r < rows; r++) {
+    int64_t o = off;
+    for (int d = 0; d < nd - 1; d++) o += idx[d] * stride[d];
+    std::memcpy(dst + o * isz, src + r * run, run);
+    for (int d = nd - 2; d >= 0; d--) {
+      if (++idx[d] < shape[d]) break;
+      idx[d] = 0;
+    }
+  }
+}
+
+template <class T>
+void fill_t(void* p, int64_t n, double v) {
+  std::fill_n(static_cast<T*>(p), n, static_cast<T>(v));
+}
+
+void fill(Array& a, double v) {
+  void* p = a.data();
+  const int64_t n = a.size();
+  switch (a.type()) {
+    case DType::UInt8: fill_t<uint8_t>(p, n, v); break;
+    case DType::Int8: fill_t<int8_t>(p, n, v); break;
+    case DType::Int32: fill_t<int32_t>(p, n, v); break;
+    case DType::Int64: fill_t<int64_t>(p, n, v); break;
+    case DType::Float: fill_t<float>(p, n, v); break;
+    case DType::Double: fill_t<double>(p, n, v); break;
+    default: break;
+  }
+}
+
+}  // namespace
+
+// array::batch (Array.cpp:465-541) + BatchShape::add (core/BatchShape.cpp:26-66).
+std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& arrs, double pad_value, int dim,
+                                    bool has_dim) {
+  const auto type = arrs.front()->type();
+  const int nd = arrs.front()->ndim();
+  if (has_dim) {
+    if (dim < 0) dim += nd;
+    if (dim < 0 || dim >= nd) throw std::runtime_error("Array: out of bound dimension");
+  }
+  std::vector<int64_t> bshape;
+  for (size_t i = 0; i < arrs.size(); i++) {
+    const auto& a = arrs[i];
+    if (a->type() != type) throw std::runtime_error("Array: unexpected different types of arrays in batch");
+    const auto& s = a->shape();
+    if (!has_dim) {
+      if (i == 0) {
+        bshape.assign(1, 0);
+        bshape.insert(bshape.end(), s.begin(), s.end());
+      } else if (s.size() + 1 != bshape.size()) {
+        throw std::runtime_error("BatchShape: batched arrays expected to have consistent shapes");
+      } else {
+        for (size_t d = 0; d < s.size(); d++) bshape[d + 1] = std::max(bshape[d + 1], s[d]);
+      }
+      bshape[0]++;
+    } else {
+      if (dim >= (int)s.size()) throw std::runtime_error("BatchShape: dimension out of bound");
+      if (i == 0) {
+        bshape = s;
+      } else if (s.size() != bshape.size()) {
+        throw std::runtime_error("BatchShape: batched arrays expected to have consistent shapes");
+      } else {
+        for (size_t d = 0; d < s.size(); d++) bshape[d] = d == (size_t)dim ? bshape[d] + s[d] : std::max(bshape[d], s[d]);
+      }
+    }
+  }
+  // Per-array element strides into the result and the per-array step.
+  const int rd = (int)bshape.size();
+  std::vector<int64_t> full_stride(rd);
+  int64_t acc = 1;
+  for (int d = rd - 1; d >= 0; d--) {
+    full_stride[d] = acc;
+    acc *= bshape[d];
+  }
+  std::vector<int64_t> stride(nd);
+  int64_t item = 1;
+  if (!has_dim) {
+    for (int d = 0; d < nd; d++) stride[d] = full_stride[d + 1];
+    item = full_stride[0];
+  } else {
+    for (int d = 0; d < nd; d++) stride[d] = full_stride[d];
+    item = full_stride[dim];
+  }
+
+  auto res = std::make_shared<Array>(type, bshape, alloc_bytes(shape_size(bshape) * itemsize(type)));
+  bool ragged = false;
+  for (const auto& a : arrs)
+    for (int d = 0; d < nd; d++)
+      if (a->shape()[d] != (has_dim ? bshape[d] : bshape[d + 1]) && !(has_dim && d == dim)) ragged = true;
+  if (ragged) fill(*res, pad_value);
+
+  auto* base = static_cast<uint8_t*>(res->data());
+  const int64_t isz = itemsize(type);
+  std::vector<mxd_image> launch;
+  int64_t off = 0;
+  for (const auto& a : arrs) {
+    // Pending uint8 HWC images in the default stacking layout go to the
+    // fused kernel, which writes rows straight into the batch.
+    if (!has_dim && a->pending() && nd == 3) {
+      launch.push_back(plan_desc(*a->plan(), base + off, stride[0]));
+    } else {
+      copy_to_strided(base, off, static_cast<const uint8_t*>(a->data()), a->shape(), stride, isz);
+    }
+    off += has_dim ? item * a->shape(dim) : item;
+  }
+  run_host(launch);
+  return res;
+}
+
+// core::merge_batch (core/Utils.cpp:209-252)
+Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<std::string, double>& pad,
+                   const std::unordered_map<std::string, int>& dims) {
+  std::vector<std::string> keys;
+  std::vector<std::vector<std::shared_ptr<Array>>> values;
+  for (const auto& s : samples) {
+    if (keys.empty()) {
+      for (const auto& kv : s) keys.push_back(kv.first);
+      values.resize(keys.size());
+    }
+    for (size_t k = 0; k < keys.size(); k++) {
+      auto it = s.find(keys[k]);
+      if (it == s.end())
+        throw std::runtime_error("mergeBatch: inconsistent sample keys in batch (unknown key: <" + keys[k] + ">)");
+      values[k].push_back(it->second);
+    }
+  }
+  Sample out;
+  for (size_t k = 0; k < keys.size(); k++) {
+    auto p = pad.find(keys[k]);
+    auto d = dims.find(keys[k]);
+    out[keys[k]] = batch_arrays(values[k], p == pad.end() ? 0.0 : p->second, d == dims.end() ? 0 : d->second,
+                                d != dims.end());
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ pool
+ThreadPool::ThreadPool(int n) {
+  n = std::max(n, 1);
+  for (int i = 0; i < n; i++) {
+    workers_.emplace_back([this] {
+      for (;;) {
+        std::packaged_task<Sample()> task;
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [this] { return stop_ || !tasks_.empty(); });
+          if (stop_ && tasks_.empty()) return;
+          task = std::move(tasks_.front());
+          tasks_.pop();
+        }
+        task();
+      }
+    });
+  }
+}
+
+ThreadPool::~ThreadPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& w : workers_) w.join();
+}
+
+std::future<Sample> ThreadPool::enqueue(std::function<Sample()> fn) {
+  std::packaged_task<Sample()> task(std::move(fn));
+  auto fut = task.get_future();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stop_) throw std::runtime_error("ThreadPool: enqueue on stopped pool");
+    tasks_.push(std::move(task));
+  }
+  cv_.notify_one();
+  return fut;
+}
+
+// ------------------------------------------------------------------ buffers
+// buffer/FromVector.cpp
+Sample FromVector::get(int64_t idx) const {
+  if (idx < 0 || idx >= (int64_t)data_.size()) throw std::out_of_range("FromVector: index out of range");
+  return data_[idx];
+}
+
+Perm::Perm(std::shared_ptr<Buffer> b, std::vector<int64_t> perm) : b_(std::move(b)), perm_(std::move(perm)) {
+  for (auto i : perm_)
+    if (i < 0 || i >= b_->size()) throw std::runtime_error("Perm: index out of range");
+}
+
+Sample Perm::get(int64_t idx) const {
+  if (idx < 0 || idx >= (int64_t)perm_.size()) throw std::runtime_error("Perm: index out of range");
+  return b_->get(perm_[idx]);
+}
+
+// buffer/Shuffle.cpp:13-24
+std::shared_ptr<Buffer> shuffle_buffer(const std::shared_ptr<Buffer>& b) {
+  std::vector<int64_t> perm(b->size());
+  std::iota(perm.begin(), perm.end(), 0);
+  auto st = get_state();
+  std::shuffle(perm.begin(), perm.end(), st->gen);
+  return std::make_shared<Perm>(b, std::move(perm));
+}
+
+// buffer/Transform.cpp:21-33
+Sample BufferTransform::get(int64_t idx) const {
+  Sample s = b_->get(idx);
+  if (s.empty()) throw std::runtime_error("Transform: cannot return empty sample");
+  s = op_->apply(s);
+  if (s.empty()) throw std::runtime_error("Transform: cannot return empty sample");
+  return s;
+}
+
+// buffer/Batch.cpp:10-25,52-68
+BufferBatch::BufferBatch(std::shared_ptr<Buffer> b, int64_t batch_size, std::unordered_map<std::string, double> pad,
+                         std::unordered_map<std::string, int> dims)
+    : b_(std::move(b)), bs_(batch_size), pad_(std::move(pad)), dims_(std::move(dims)) {
+  if (bs_ <= 0) throw std::runtime_error("Batch: batch size must be positive");
+  size_ = (b_->size() + bs_ - 1) / bs_;
+}
+
+Sample BufferBatch::get(int64_t idx) const {
+  if (idx < 0 || idx >= size_) throw std::runtime_error("Batch: index out of range");
+  const int64_t n = std::min(bs_, b_->size() - idx * bs_);
+  std::vector<Sample> samples(n);
+  for (int64_t i = 0; i < n; i++) samples[i] = b_->get(idx * bs_ + i);
+  return merge_batch(samples, pad_, dims_);
+}
+
+// ------------------------------------------------------------------ streams
+// stream/FromBuffer.cpp:12-30
+Sample FromBuffer::next() const {
+  int64_t idx = -1;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (idx_ < b_->size()) idx = idx_++;
+  }
+  return idx < 0 ? Sample() : b_->get(idx);
+}
+
+void FromBuffer::reset() {
+  std::lock_guard<std::mutex> lk(mu_);
+  idx_ = 0;
+}
+
+// stream/Transform.cpp:21-47: skip samples an op drops.
+Sample StreamTransform::next() const {
+  Sample res;
+  while (res.empty()) {
+    Sample s = s_->next();
+    if (s.empty()) break;
+    res = op_->apply(s);
+  }
+  return res;
+}
+
+// stream/Batch.cpp:10-39
+StreamBatch::StreamBatch(std::shared_ptr<Stream> s, int64_t batch_size, std::unordered_map<std::string, double> pad,
+                         std::unordered_map<std::string, int> dims)
+    : s_(std::move(s)), bs_(batch_size), pad_(std::move(pad)), dims_(std::move(dims)) {
+  if (bs_ <= 0) throw std::runtime_error("Batch: batch size must be positive");
+}
+
+Sample StreamBatch::next() const {
+  std::vector<Sample> samples;
+  for (int64_t i = 0; i < bs_; i++) {
+    Sample s = s_->next();
+    if (s.empty()) break;
+    samples.push_back(std::move(s));
+  }
+  return samples.empty() ? Sample() : merge_batch(samples, pad_, dims_);
+}
+
+// stream/Prefetch.cpp:9-66
+Prefetch::Prefetch(std::shared_ptr<Stream> s, int prefetch_size, int num_threads)
+    : s_(std::move(s)), pool_(std::make_unique<ThreadPool>(num_threads)), size_(prefetch_size) {
+  if (size_ < 0) throw std::runtime_error("Prefetch: prefetch size must be positive");
+}
+
+Prefetch::~Prefetch() {
+  std::lock_guard<std::mutex> lk(mu_);
+  while (!cache_.empty()) {
+    cache_.front().wait();
+    cache_.pop();
+  }
+}
+
+Sample Prefetch::next() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (size_ == 0) return s_->next();
+  if ((int)cache_.size() < size_)
+    for (int i = 0; i < size_; i++) cache_.push(pool_->enqueue([s = s_] { return s->next(); }));
+  Sample res;
+  for (int i = 0; i < size_; i++) {
+    auto f = std::move(cache_.front());
+    cache_.pop();
+    cache_.push(pool_->enqueue([s = s_] { return s->next(); }));
+    res = f.get();
+    if (!res.empty()) break;
+  }
+  return res;
+}
+
+void Prefetch::reset() {
+  std::lock_guard<std::mutex> lk(mu_);
+  while (!cache_.empty()) {
+    cache_.front().wait();
+    cache_.pop();
+  }
+  s_->reset();
+}
+
+// stream/OrderedPrefetch.cpp:8-80
+OrderedPrefetch::OrderedPrefetch(std::shared_ptr<Buffer> b, int prefetch_size, int num_threads)
+    : b_(std::move(b)), pool_(std::make_unique<ThreadPool>(num_threads)), size_(prefetch_size) {
+  if (size_ <= 0) throw std::runtime_error("Prefetch: prefetch size must be strictly positive");
+}
+
+OrderedPrefetch::~OrderedPrefetch() {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& f : cache_)
+    if (f.valid()) f.wait();
+  cache_.clear();
+}
+
+Sample OrderedPrefetch::next() const {
+  std::unique_lock<std::mutex> lk(mu_);
+  const int64_t n = b_->size();
+  if (cache_.empty()) {
+    cache_.resize(size_);
+    for (int64_t i = idx_; i < std::min<int64_t>(idx_ + size_, n); i++)
+      cache_[i % size_] = pool_->enqueue([b = b_, i] { return b->get(i); });
+  }
+  if (idx_ >= n) return Sample();
+  const int64_t idx = idx_++;
+  auto f = std::move(cache_[idx % size_]);
+  const int64_t nxt = idx + size_;
+  if (nxt < n) cache_[idx % size_] = pool_->enqueue([b = b_, nxt] { return b->get(nxt); });
+  lk.unlock();
+  return f.get();
+}
+
+void OrderedPrefetch::reset() {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& f : cache_)
+    if (f.valid()) f.wait();
+  cache_.clear();
+  idx_ = 0;
+}
+
+}  // namespace pipe
+}  // namespace mxd

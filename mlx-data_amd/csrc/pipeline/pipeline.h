@@ -1,0 +1,354 @@
+// pipeline.h -- the mlx-data Buffer/Stream operator surface for the image
+// path, with the pixel work of image_resize_smallest_side / image_resize /
+// image_center_crop / image_random_crop / image_random_h_flip deferred to the
+// batch and executed by the fused gfx950 kernel through the C ABI
+// (include/mxd_amd.h).
+//
+// Mirrors (semantics, error conditions, RNG draw order) of mlx-data 0.2.0:
+//   Array / batch         mlx/data/Array.{h,cpp} (batch :465-498, sub :544-583)
+//   Sample, check_key     mlx/data/Sample.{h,cpp}:13,18-29
+//   Op / KeyTransformOp   mlx/data/op/{Op,KeyTransform}.{h,cpp}
+//   image ops             mlx/data/op/ImageTransform.cpp:22-158,317-332
+//   LoadImage             mlx/data/op/LoadImage.cpp:23-48
+//   buffers               mlx/data/buffer/{FromVector,Perm,Shuffle,Transform,Batch}.cpp
+//   streams               mlx/data/stream/{FromBuffer,Transform,Batch,Prefetch,OrderedPrefetch}.cpp
+//   state                 mlx/data/core/State.cpp:9-22
+//   merge_batch           mlx/data/core/Utils.cpp:209-252, BatchShape.cpp:26-66
+#pragma once
+
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <future>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace mxd {
+namespace pipe {
+
+// Same order as mlx::data::ArrayType.
+enum class DType { Any, UInt8, Int8, Int32, Int64, Float, Double };
+int64_t itemsize(DType t);
+
+class Array;
+
+// Pixel work that has not run yet: take the window (sx, sy, sw, sh) of `src`,
+// resize it to resize_w x resize_h (identity when equal), keep the crop window
+// of that, mirror it if `flip`.  The output is `crop_h x crop_w x C` uint8.
+// It materialises on the GPU -- one launch for a whole batch when the batch
+// node sees plans, one launch per image when something reads it directly.
+struct ImagePlan {
+  std::shared_ptr<Array> src;  // (H, W, C) uint8, materialised
+  int64_t sx = 0, sy = 0, sw = 0, sh = 0;
+  int64_t resize_w = 0, resize_h = 0;
+  int64_t crop_x = 0, crop_y = 0, crop_w = 0, crop_h = 0;
+  bool flip = false;
+  int64_t channels() const;
+};
+
+class Array {
+ public:
+  Array(DType type, std::vector<int64_t> shape);                      // zero-initialised storage
+  Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data);
+  explicit Array(std::shared_ptr<const ImagePlan> plan);              // lazy image
+
+  DType type() const { return type_; }
+  const std::vector<int64_t>& shape() const { return shape_; }
+  int64_t shape(int d) const;
+  int ndim() const { return (int)shape_.size(); }
+  int64_t size() const;
+  int64_t nbytes() const { return size() * itemsize(type_); }
+  // Materialises a pending image plan (one GPU launch) on first use.
+  void* data() const;
+  const std::shared_ptr<const ImagePlan>& plan() const { return plan_; }
+  bool pending() const;
+
+ private:
+  DType type_;
+  std::vector<int64_t> shape_;
+  mutable std::shared_ptr<void> data_;
+  std::shared_ptr<const ImagePlan> plan_;
+  mutable std::mutex mu_;
+};
+
+using Sample = std::unordered_map<std::string, std::shared_ptr<Array>>;
+
+std::shared_ptr<Array> check_key(const Sample& s, const std::string& key);
+
+// Devices the fused kernel may use (default: all visible).  Batches are
+// spread over them round-robin.
+void set_devices(const std::vector<int>& devices);
+std::vector<int> devices();
+
+// ---------------------------------------------------------------- state
+struct State {
+  std::mt19937 gen;
+  int64_t version = 0;
+};
+void set_state(int64_t seed);
+std::shared_ptr<State> get_state();
+
+// ---------------------------------------------------------------- ops
+class Op {
+ public:
+  virtual ~Op() = default;
+  virtual Sample apply(const Sample& sample) const = 0;
+};
+
+class KeyTransformOp : public Op {
+ public:
+  KeyTransformOp(std::string ikey, std::string okey) : ikey_(std::move(ikey)), okey_(std::move(okey)) {}
+  Sample apply(const Sample& sample) const override;
+  virtual std::shared_ptr<Array> apply_key(const std::shared_ptr<Array>& x) const = 0;
+
+ protected:
+  std::string ikey_, okey_;
+};
+
+class KeyTransform : public KeyTransformOp {
+ public:
+  using Fn = std::function<std::shared_ptr<Array>(const std::shared_ptr<Array>&)>;
+  KeyTransform(std::string ikey, Fn fn, std::string okey) : KeyTransformOp(std::move(ikey), std::move(okey)), fn_(std::move(fn)) {}
+  std::shared_ptr<Array> apply_key(const std::shared_ptr<Array>& x) const override { return fn_(x); }
+
+ private:
+  Fn fn_;
+};
+
+class ImageOp : public KeyTransformOp {
+ public:
+  using KeyTransformOp::KeyTransformOp;
+  std::shared_ptr<Array> apply_key(const std::shared_ptr<Array>& x) const override;
+  virtual std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const = 0;
+};
+
+class ImageResizeSmallestSide : public ImageOp {
+ public:
+  ImageResizeSmallestSide(std::string ikey, int64_t size, std::string okey)
+      : ImageOp(std::move(ikey), std::move(okey)), size_(size) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  int64_t size_;
+};
+
+class ImageResize : public ImageOp {
+ public:
+  ImageResize(std::string ikey, int64_t w, int64_t h, std::string okey)
+      : ImageOp(std::move(ikey), std::move(okey)), w_(w), h_(h) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  int64_t w_, h_;
+};
+
+class ImageCenterCrop : public ImageOp {
+ public:
+  ImageCenterCrop(std::string ikey, int64_t w, int64_t h, std::string okey)
+      : ImageOp(std::move(ikey), std::move(okey)), w_(w), h_(h) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  int64_t w_, h_;
+};
+
+class ImageRandomCrop : public ImageOp {
+ public:
+  ImageRandomCrop(std::string ikey, int64_t w, int64_t h, std::string okey)
+      : ImageOp(std::move(ikey), std::move(okey)), w_(w), h_(h) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  int64_t w_, h_;
+};
+
+class ImageRandomHFlip : public ImageOp {
+ public:
+  ImageRandomHFlip(std::string ikey, float prob, std::string okey)
+      : ImageOp(std::move(ikey), std::move(okey)), prob_(prob) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  float prob_;
+};
+
+// Decoder hook: (path or encoded bytes, from_memory) -> (H, W, 3) uint8, or
+// nullptr when the image cannot be decoded.  Installed by the binding.
+using ImageDecoder = std::function<std::shared_ptr<Array>(const std::string& path, const std::shared_ptr<Array>& bytes,
+                                                          bool from_memory, bool info)>;
+void set_image_decoder(ImageDecoder dec);
+
+class LoadImage : public KeyTransformOp {
+ public:
+  LoadImage(std::string ikey, std::string prefix, bool info, std::string format, bool from_memory, std::string okey);
+  std::shared_ptr<Array> apply_key(const std::shared_ptr<Array>& x) const override;
+
+ private:
+  std::string prefix_;
+  bool info_;
+  std::string format_;
+  bool from_memory_;
+};
+
+// ---------------------------------------------------------------- batching
+// array::batch semantics (pad with pad_value to the max shape; optional
+// concatenation dim).  Pending image plans of one key become one fused launch.
+std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& arrs, double pad_value, int dim,
+                                    bool has_dim);
+Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<std::string, double>& pad,
+                   const std::unordered_map<std::string, int>& dims);
+
+// ---------------------------------------------------------------- threads
+class ThreadPool {
+ public:
+  explicit ThreadPool(int n);
+  ~ThreadPool();
+  std::future<Sample> enqueue(std::function<Sample()> fn);
+
+ private:
+  std::vector<std::thread> workers_;
+  std::queue<std::packaged_task<Sample()>> tasks_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+// ---------------------------------------------------------------- buffers
+class Buffer {
+ public:
+  virtual ~Buffer() = default;
+  virtual int64_t size() const = 0;
+  virtual Sample get(int64_t idx) const = 0;
+};
+
+class FromVector : public Buffer {
+ public:
+  explicit FromVector(std::vector<Sample> data) : data_(std::move(data)) {}
+  int64_t size() const override { return (int64_t)data_.size(); }
+  Sample get(int64_t idx) const override;
+
+ private:
+  std::vector<Sample> data_;
+};
+
+class Perm : public Buffer {
+ public:
+  Perm(std::shared_ptr<Buffer> b, std::vector<int64_t> perm);
+  int64_t size() const override { return (int64_t)perm_.size(); }
+  Sample get(int64_t idx) const override;
+
+ private:
+  std::shared_ptr<Buffer> b_;
+  std::vector<int64_t> perm_;
+};
+std::shared_ptr<Buffer> shuffle_buffer(const std::shared_ptr<Buffer>& b);
+
+class BufferTransform : public Buffer {
+ public:
+  BufferTransform(std::shared_ptr<Buffer> b, std::shared_ptr<Op> op) : b_(std::move(b)), op_(std::move(op)) {}
+  int64_t size() const override { return b_->size(); }
+  Sample get(int64_t idx) const override;
+
+ private:
+  std::shared_ptr<Buffer> b_;
+  std::shared_ptr<Op> op_;
+};
+
+class BufferBatch : public Buffer {
+ public:
+  BufferBatch(std::shared_ptr<Buffer> b, int64_t batch_size, std::unordered_map<std::string, double> pad,
+              std::unordered_map<std::string, int> dims);
+  int64_t size() const override { return size_; }
+  Sample get(int64_t idx) const override;
+
+ private:
+  std::shared_ptr<Buffer> b_;
+  int64_t bs_, size_;
+  std::unordered_map<std::string, double> pad_;
+  std::unordered_map<std::string, int> dims_;
+};
+
+// ---------------------------------------------------------------- streams
+class Stream {
+ public:
+  virtual ~Stream() = default;
+  virtual Sample next() const = 0;
+  virtual void reset() = 0;
+};
+
+class FromBuffer : public Stream {
+ public:
+  explicit FromBuffer(std::shared_ptr<Buffer> b) : b_(std::move(b)) {}
+  Sample next() const override;
+  void reset() override;
+
+ private:
+  std::shared_ptr<Buffer> b_;
+  mutable std::mutex mu_;
+  mutable int64_t idx_ = 0;
+};
+
+class StreamTransform : public Stream {
+ public:
+  StreamTransform(std::shared_ptr<Stream> s, std::shared_ptr<Op> op) : s_(std::move(s)), op_(std::move(op)) {}
+  Sample next() const override;
+  void reset() override { s_->reset(); }
+
+ private:
+  std::shared_ptr<Stream> s_;
+  std::shared_ptr<Op> op_;
+};
+
+class StreamBatch : public Stream {
+ public:
+  StreamBatch(std::shared_ptr<Stream> s, int64_t batch_size, std::unordered_map<std::string, double> pad,
+              std::unordered_map<std::string, int> dims);
+  Sample next() const override;
+  void reset() override { s_->reset(); }
+
+ private:
+  std::shared_ptr<Stream> s_;
+  int64_t bs_;
+  std::unordered_map<std::string, double> pad_;
+  std::unordered_map<std::string, int> dims_;
+};
+
+class Prefetch : public Stream {
+ public:
+  Prefetch(std::shared_ptr<Stream> s, int prefetch_size, int num_threads);
+  ~Prefetch() override;
+  Sample next() const override;
+  void reset() override;
+
+ private:
+  std::shared_ptr<Stream> s_;
+  std::unique_ptr<ThreadPool> pool_;
+  int size_;
+  mutable std::mutex mu_;
+  mutable std::queue<std::future<Sample>> cache_;
+};
+
+class OrderedPrefetch : public Stream {
+ public:
+  OrderedPrefetch(std::shared_ptr<Buffer> b, int prefetch_size, int num_threads);
+  ~OrderedPrefetch() override;
+  Sample next() const override;
+  void reset() override;
+
+ private:
+  std::shared_ptr<Buffer> b_;
+  std::unique_ptr<ThreadPool> pool_;
+  int size_;
+  mutable std::mutex mu_;
+  mutable std::vector<std::future<Sample>> cache_;
+  mutable int64_t idx_ = 0;
+};
+
+}  // namespace pipe
+}  // namespace mxd

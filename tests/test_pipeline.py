@@ -1,0 +1,232 @@
+"""CPU tests of the operator surface (mlx_data_amd.data): dataset plumbing,
+batch semantics, plan geometry, RNG draw order and error behaviour.
+
+Nothing here reads pixels of a resized image (that needs the GPU; see
+test_gpu_pipeline.py).  Expected values come from the reference's own code
+(golden fixtures made with oracle/_ref) or from the oracle's geometry.
+Reference anchors: op/ImageTransform.cpp:78-158,317-332, Array.cpp:465-541,
+stream/{Batch,Prefetch,OrderedPrefetch}.cpp, buffer/{Batch,Shuffle}.cpp,
+op/LoadImage.cpp:23-48.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from mlx_data_amd import data as dx
+from mlx_data_amd import _pipeline as P
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden.npz"))
+
+
+def has_gpu():
+    return len(dx.devices()) > 0
+
+
+def test_sample_conversion():
+    b = dx.buffer_from_vector([dict(a=3, f=2.5, s=b"abc", n=np.arange(4, dtype=np.int32), u=np.ones((2, 2), np.uint8))])
+    s = b[0]
+    assert s["a"].dtype == np.int64 and s["a"].shape == () and int(s["a"]) == 3
+    assert s["f"].dtype == np.float64 and float(s["f"]) == 2.5
+    assert s["s"].dtype == np.int8 and bytes(s["s"]) == b"abc"
+    assert s["n"].dtype == np.int32 and list(s["n"]) == [0, 1, 2, 3]
+    assert s["u"].dtype == np.uint8 and s["u"].shape == (2, 2)
+    with pytest.raises(ValueError, match="Cannot convert strings"):
+        dx.buffer_from_vector([dict(a="x")])
+    with pytest.raises(RuntimeError, match="unexpected empty sample"):
+        dx.buffer_from_vector([dict()])
+    with pytest.raises(RuntimeError, match="Contiguous array expected"):
+        dx.buffer_from_vector([dict(a=np.zeros((4, 4))[:, ::2])])
+
+
+def test_batch_matches_reference_array_batch():
+    """Ragged uint8 crops batched with pad 0: bytes equal the reference's
+    array::batch output (golden refbatch, made by oracle/_ref)."""
+    shapes = GOLD["refbatch_shapes"]
+    crops = [GOLD["rc_caltech_200x300"], GOLD["rc_small_97x131"][:200, :210], GOLD["rc_tiny_48x64"][:150, :224]]
+    assert [c.shape for c in crops] == [tuple(s) for s in shapes]
+    b = dx.buffer_from_vector([dict(image=np.ascontiguousarray(c)) for c in crops]).batch(3)
+    out = b[0]["image"]
+    assert out.shape == GOLD["refbatch"].shape
+    assert np.array_equal(out, GOLD["refbatch"])
+
+
+def test_batch_pad_and_dim():
+    xs = [np.arange(n, dtype=np.int64) + 10 * n for n in (1, 3, 2)]
+    b = dx.buffer_from_vector([dict(x=x, y=float(i)) for i, x in enumerate(xs)])
+    s = b.batch(3, pad={"x": -7})[0]
+    assert s["x"].tolist() == [[10, -7, -7], [30, 31, 32], [20, 21, -7]]
+    assert s["y"].tolist() == [0.0, 1.0, 2.0]
+    # dim: concatenation along an existing axis (Array.cpp:500-541)
+    m = [np.full((2, n), n, np.int32) for n in (1, 3)]
+    s = dx.buffer_from_vector([dict(m=a) for a in m]).batch(2, dim={"m": 1})[0]
+    assert s["m"].tolist() == [[1, 3, 3, 3], [1, 3, 3, 3]]
+    s = dx.buffer_from_vector([dict(m=a) for a in [np.ones((1, 2), np.int32), np.ones((2, 1), np.int32)]]).batch(
+        2, dim={"m": 0}, pad={"m": 5})[0]
+    assert s["m"].tolist() == [[1, 1], [1, 5], [1, 5]]
+    with pytest.raises(RuntimeError, match="consistent shapes"):
+        dx.buffer_from_vector([dict(x=np.zeros(2)), dict(x=np.zeros((2, 2)))]).batch(2)[0]
+    with pytest.raises(RuntimeError, match="different types"):
+        dx.buffer_from_vector([dict(x=np.zeros(2)), dict(x=np.zeros(2, np.int32))]).batch(2)[0]
+    with pytest.raises(RuntimeError, match="inconsistent sample keys"):
+        dx.buffer_from_vector([dict(x=1), dict(y=1)]).batch(2)[0]
+    with pytest.raises(RuntimeError, match="batch size must be positive"):
+        dx.buffer_from_vector([dict(x=1)]).batch(0)
+
+
+def test_buffer_batch_sizes_and_short_last():
+    b = dx.buffer_from_vector([dict(i=i) for i in range(10)]).batch(4)
+    assert len(b) == 3
+    assert [s["i"].tolist() for s in b] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+    with pytest.raises(RuntimeError, match="index out of range"):
+        b[3]
+
+
+def test_stream_batch_prefetch_and_reset():
+    s = dx.buffer_from_vector([dict(i=i) for i in range(11)]).to_stream().batch(3)
+    assert [x["i"].tolist() for x in s] == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10]]
+    assert s.next() == {}
+    s.reset()
+    assert s.next()["i"].tolist() == [0, 1, 2]
+    # prefetch: every batch exactly once (order between workers is free)
+    p = dx.buffer_from_vector([dict(i=i) for i in range(100)]).to_stream().batch(7).prefetch(4, 3)
+    got = sorted(v for x in p for v in x["i"].tolist())
+    assert got == list(range(100))
+    # ordered_prefetch keeps buffer order
+    o = dx.buffer_from_vector([dict(i=i) for i in range(50)]).batch(4).ordered_prefetch(3, 4)
+    assert [v for x in o for v in x["i"].tolist()] == list(range(50))
+    o.reset()
+    assert o.next()["i"].tolist() == [0, 1, 2, 3]
+
+
+def test_shuffle_is_seeded_permutation():
+    b = dx.buffer_from_vector([dict(i=i) for i in range(64)])
+    dx.set_state(7)
+    a = [int(s["i"]) for s in b.shuffle()]
+    dx.set_state(7)
+    c = [int(s["i"]) for s in b.shuffle()]
+    assert a == c and sorted(a) == list(range(64)) and a != list(range(64))
+
+
+def test_key_transform_and_if_variants():
+    b = dx.buffer_from_vector([dict(x=np.arange(3, dtype=np.float32))])
+    t = b.key_transform("x", lambda v: v * 2, output_key="y")
+    s = t[0]
+    assert s["x"].tolist() == [0, 1, 2] and s["y"].tolist() == [0, 2, 4]
+    assert b.key_transform_if(False, "x", lambda v: v + 1)[0]["x"].tolist() == [0, 1, 2]
+    assert b.key_transform_if(True, "x", lambda v: v + 1)[0]["x"].tolist() == [1, 2, 3]
+    with pytest.raises(RuntimeError, match="key <nope> expected"):
+        b.key_transform("nope", lambda v: v)[0]
+
+
+IMGS = sorted(k[4:] for k in GOLD.files if k.startswith("img_"))
+
+
+@pytest.mark.parametrize("name", IMGS)
+def test_plan_geometry_matches_oracle(name):
+    img = np.ascontiguousarray(GOLD[f"img_{name}"])
+    h, w = img.shape[:2]
+    b = dx.buffer_from_vector([dict(image=img)])
+    t = b.image_resize_smallest_side("image", 256)
+    tw, th = O.smallest_side_dims(w, h, 256)
+    p = P._plan(t, 0, "image")
+    assert p["resize"] == (tw, th) and p["window"] == (0, 0, w, h) and p["shape"] == [th, tw, img.shape[2]]
+    if tw >= 224 and th >= 224:
+        c = t.image_center_crop("image", 224, 224)
+        x, y = O.center_crop_origin(tw, th, 224, 224)
+        p = P._plan(c, 0, "image")
+        assert p["crop"] == (x, y, 224, 224) and p["shape"] == [224, 224, img.shape[2]] and not p["flip"]
+
+
+def test_random_crop_flip_draws_match_reference():
+    """set_state(1234) then random_crop(448) + random_h_flip(0.5) on 910x512
+    images: the (x, y, flip) stream equals the reference's (golden rng_*)."""
+    img = np.zeros((512, 910, 3), np.uint8)
+    b = dx.buffer_from_vector([dict(image=img)] * 64)
+    t = b.image_random_crop("image", 448, 448).image_random_h_flip("image", 0.5)
+    dx.set_state(1234)
+    got = [P._plan(t, i, "image") for i in range(64)]
+    xy = [g["crop"][:2] for g in got]
+    fl = [int(g["flip"]) for g in got]
+    assert np.array_equal(np.array(xy), GOLD["rng_xy"])
+    assert np.array_equal(np.array(fl), GOLD["rng_flip"])
+
+
+def test_plan_composition():
+    img = np.zeros((100, 200, 3), np.uint8)
+    b = dx.buffer_from_vector([dict(image=img)])
+    # crop -> resize: the crop becomes the source window
+    p = P._plan(b.image_center_crop("image", 50, 40).image_resize("image", 25, 20), 0, "image")
+    assert p["window"] == (75, 30, 50, 40) and p["resize"] == (25, 20) and p["crop"] == (0, 0, 25, 20)
+    # crop of a mirrored view maps back into unmirrored coordinates
+    b2 = dx.buffer_from_vector([dict(image=img)] * 2)
+    dx.set_state(0)
+    f = b2.image_random_h_flip("image", 1.0).image_center_crop("image", 60, 100)
+    p = P._plan(f, 0, "image")
+    assert p["flip"] and p["crop"] == (70, 0, 60, 100)
+    g = P._plan(b.image_random_h_flip("image", 1.0).image_random_crop("image", 10, 10), 0, "image")
+    assert g["flip"]
+    # flip twice = identity mirror
+    p = P._plan(b.image_random_h_flip("image", 1.0).image_random_h_flip("image", 1.0), 0, "image")
+    assert not p["flip"]
+
+
+def test_image_op_errors():
+    img = np.zeros((20, 30, 3), np.uint8)
+    b = dx.buffer_from_vector([dict(image=img)])
+    with pytest.raises(RuntimeError, match="ImageResizeSmallestSide: illegal target size: 0"):
+        b.image_resize_smallest_side("image", 0)[0]
+    with pytest.raises(RuntimeError, match="ImageCenterCrop: target image size larger than input image"):
+        b.image_center_crop("image", 31, 10)[0]
+    with pytest.raises(RuntimeError, match="ImageRandomCrop: target image size larger than input image"):
+        b.image_random_crop("image", 10, 21)[0]
+    with pytest.raises(RuntimeError, match="cannot create image with 0 or negative dimension"):
+        b.image_resize("image", 0, 5)[0]
+    with pytest.raises(RuntimeError, match="image must be 3 dimension"):
+        dx.buffer_from_vector([dict(image=np.zeros((4, 4), np.uint8))]).image_resize("image", 2, 2)[0]
+    with pytest.raises(RuntimeError, match="channels must be 0 <= c <= 4"):
+        dx.buffer_from_vector([dict(image=np.zeros((4, 4, 5), np.uint8))]).image_resize("image", 2, 2)[0]
+    with pytest.raises(ValueError, match="UInt8"):
+        dx.buffer_from_vector([dict(image=np.zeros((4, 4, 3), np.float32))]).image_resize("image", 2, 2)[0]
+
+
+def test_non_uint8_crop_is_a_sub_array():
+    a = np.arange(4 * 6 * 2, dtype=np.float32).reshape(4, 6, 2)
+    s = dx.buffer_from_vector([dict(image=a)]).image_center_crop("image", 2, 2)[0]
+    assert np.array_equal(s["image"], a[1:3, 2:4])
+
+
+@pytest.mark.skipif(has_gpu(), reason="checks the no-GPU behaviour")
+def test_pixels_need_the_gpu():
+    img = np.zeros((20, 30, 3), np.uint8)
+    b = dx.buffer_from_vector([dict(image=img)] * 2)
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        b.image_resize("image", 10, 10)[0]
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        b.image_center_crop("image", 10, 10).batch(2)[0]
+
+
+def test_load_image(tmp_path):
+    from PIL import Image
+
+    rng = np.random.default_rng(3)
+    arr = rng.integers(0, 256, (40, 60, 3), dtype=np.uint8)
+    Image.fromarray(arr).save(tmp_path / "a.jpg", quality=90)
+    Image.fromarray(arr[:, :, 0]).save(tmp_path / "g.png")
+    Image.fromarray(arr).save(tmp_path / "c.png")
+    expect = np.asarray(Image.open(tmp_path / "a.jpg").convert("RGB"))
+    b = dx.buffer_from_vector([dict(f=b"a.jpg"), dict(f=b"g.png"), dict(f=b"c.png")])
+    s = b.load_image("f", prefix=str(tmp_path), output_key="image")
+    assert np.array_equal(s[0]["image"], expect)
+    assert s[1]["image"].shape == (40, 60, 1) and np.array_equal(s[1]["image"][:, :, 0], arr[:, :, 0])
+    assert np.array_equal(s[2]["image"], arr)
+    info = b.load_image("f", prefix=str(tmp_path), info=True)[0]["f"]
+    assert info.tolist() == [60, 40]
+    raw = (tmp_path / "a.jpg").read_bytes()
+    m = dx.buffer_from_vector([dict(f=np.frombuffer(raw, np.uint8))]).load_image("f", from_memory=True)
+    assert np.array_equal(m[0]["f"], expect)
+    with pytest.raises(RuntimeError, match=r"LoadImage: unable to load image <.*missing.jpg>"):
+        dx.buffer_from_vector([dict(f=b"missing.jpg")]).load_image("f", prefix=str(tmp_path))[0]
+    with pytest.raises(RuntimeError, match=r"char array \(int8\) expected"):
+        dx.buffer_from_vector([dict(f=np.zeros(3, np.uint8))]).load_image("f")[0]
