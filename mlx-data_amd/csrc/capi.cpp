@@ -303,6 +303,53 @@ bool one_output_per_row(const DevTable& yt, int32_t off, int32_t len) {
   return true;
 }
 
+// Output rows per wave unit.  The units of one launch all do about the same
+// work, so the launch runs best as whole "rounds" of the device's concurrent
+// wave slots: a last round that is only partly filled leaves the HBM queue
+// short of loads while it drains.  Pick the fewest rounds whose band height
+// stays <= kMaxBand, then the smallest band height whose unit count fits them.
+// MXD_BAND_ROWS overrides (tuning).
+int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_t capacity) {
+  constexpr int32_t kMinBand = 8, kMaxBand = 64;
+  static const int forced = [] {
+    const char* e = std::getenv("MXD_BAND_ROWS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0) return forced;
+  int64_t rows = 0;
+  int32_t max_h = 1;
+  for (auto& s : strips) {
+    rows += (int64_t)s.first * s.second;
+    max_h = std::max(max_h, s.second);
+  }
+  auto units = [&](int32_t ty) {
+    int64_t u = 0;
+    for (auto& s : strips) u += (int64_t)s.first * ((s.second + std::min(ty, s.second) - 1) / std::min(ty, s.second));
+    return u;
+  };
+  if (capacity <= 0) capacity = 4096;
+  for (int64_t rounds = 1;; rounds++) {
+    const int64_t slots = rounds * capacity;
+    int32_t ty = (int32_t)std::max<int64_t>(kMinBand, (rows + slots - 1) / slots);
+    if (ty > kMaxBand) continue;
+    while (ty < max_h && units(ty) > slots) ty++;
+    if (units(ty) <= slots || ty >= max_h) return std::min(ty, max_h);
+  }
+}
+
+int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int, int, int>, int32_t> cache;
+  const auto key = std::make_tuple(device, cfg.channels, cfg.f32, cfg.taps, cfg.ring, cfg.mode);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  DeviceGuard g(device);
+  const int32_t c = mxd::wave_capacity(cfg, device);
+  cache[key] = c;
+  return c;
+}
+
 int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
@@ -363,39 +410,45 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     for (int32_t i = 0; i < n; i++) order[i] = i;
     auto key = [&](int32_t i) { return plans[i].bucket * 2 + plans[i].ring; };
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
-    int64_t strip_rows = 0;
-    for (int32_t i = 0; i < n; i++) strip_rows += (int64_t)plans[i].nstrips * images[i].crop_h;
-    const int32_t ty = (int32_t)std::max<int64_t>(8, std::min<int64_t>(64, (strip_rows + 8191) / 8192));
+    static const int ablate = [] {
+      const char* e = std::getenv("MXD_WAVE_ABLATE");
+      return e ? std::atoi(e) : 0;
+    }();
     std::vector<ImgDev> descs(n);
-    struct Group { int32_t first, count, units, bucket, ring; };
+    struct Group { int32_t first, count, units, bucket, ring, ty; };
     std::vector<Group> groups;
     for (int32_t k = 0; k < n; k++) {
       const int32_t i = order[k];
       if (groups.empty() || groups.back().bucket != plans[i].bucket || groups.back().ring != plans[i].ring)
-        groups.push_back({k, 0, 0, plans[i].bucket, plans[i].ring});
-      Group& g = groups.back();
-      ImgDev& d = descs[k];
-      fill(d, images[i], plans[i]);
-      if (plans[i].ring) {
-        d.ywidth = plans[i].yr->padded;
-        d.ytab = plans[i].yr->ptr + (size_t)images[i].crop_y * (mxd::kTapHeader + plans[i].yr->padded);
+        groups.push_back({k, 0, 0, plans[i].bucket, plans[i].ring, 0});
+      groups.back().count++;
+    }
+    for (Group& g : groups) {
+      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, 0, ablate, g.ring};
+      std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
+      for (int32_t k = g.first; k < g.first + g.count; k++)
+        strips.push_back({plans[order[k]].nstrips, images[order[k]].crop_h});
+      g.ty = band_rows(strips, wave_capacity_cached(cfg, device));
+      for (int32_t k = g.first; k < g.first + g.count; k++) {
+        const int32_t i = order[k];
+        ImgDev& d = descs[k];
+        fill(d, images[i], plans[i]);
+        if (plans[i].ring) {
+          d.ywidth = plans[i].yr->padded;
+          d.ytab = plans[i].yr->ptr + (size_t)images[i].crop_y * (mxd::kTapHeader + plans[i].yr->padded);
+        }
+        d.tile_begin = g.units;
+        d.nstrips = plans[i].nstrips;
+        d.tx = plans[i].tx;
+        d.ty = std::min(g.ty, images[i].crop_h);
+        d.group = 1;
+        g.units += d.nstrips * ((images[i].crop_h + d.ty - 1) / d.ty);
       }
-      d.tile_begin = g.units;
-      d.nstrips = plans[i].nstrips;
-      d.tx = plans[i].tx;
-      d.ty = std::min(ty, images[i].crop_h);
-      d.group = 1;
-      g.units += d.nstrips * ((images[i].crop_h + d.ty - 1) / d.ty);
-      g.count++;
     }
     ImgDev* dev = nullptr;
     std::unique_lock<std::mutex> hold;
     if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
     for (const Group& g : groups) {
-      static const int ablate = [] {
-        const char* e = std::getenv("MXD_WAVE_ABLATE");
-        return e ? std::atoi(e) : 0;
-      }();
       mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate, g.ring};
       if (int rc = mxd::launch_wave(cfg, dev + g.first, stream))
         return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
@@ -572,11 +625,11 @@ int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps)
   float ms = 0.0f;
   MXD_HIP(hipEventElapsedTime(&ms, e0, e1));
   *gbps = (float)(2.0 * (double)(bytes / 16 * 16) * iters / (ms * 1e-3) / 1e9);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipStreamDestroy(s);
-  hipFree(a);
-  hipFree(b);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
+  (void)hipFree(a);
+  (void)hipFree(b);
   return MXD_OK;
 }
 

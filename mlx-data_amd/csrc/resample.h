@@ -55,6 +55,8 @@ int wave_row_floats(int taps, int channels);
 int wave_row_bytes();
 int wave_max_outputs();  // output elements per strip row (4 per lane)
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
+// Waves of this configuration the device runs at once (occupancy x CUs), 0 if unknown.
+int wave_capacity(const WaveCfg& cfg, int device);
 int launch_copy(const void* src, void* dst, size_t bytes, void* stream);
 
 // Dynamic LDS bytes the kernel needs for cfg.

@@ -68,11 +68,17 @@ struct Chunk {
   uint32_t d[4];
 };
 
-// The lane's 4 dwords of source row `row`: bytes off + 256j of the row.
-__device__ __forceinline__ Chunk load_chunk(__amdgpu_buffer_rsrc_t rsrc, int off, int row_off) {
+// A voffset past any image (images are < 2^31 bytes): the buffer range check
+// turns the load into a zero without a memory request.
+constexpr int kNoLoad = 0x7ffffff0;
+
+// The lane's 4 dwords of source row `row_off / stride` (byte offsets voff[j]
+// of the row, kNoLoad for dwords outside the strip's footprint), or four
+// zeros without memory traffic when !live (uniform).
+__device__ __forceinline__ Chunk load_chunk_if(__amdgpu_buffer_rsrc_t rsrc, const int* voff, int row_off, bool live) {
   Chunk r;
 #pragma unroll
-  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 256 * j, row_off, 0);
+  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, live ? voff[j] : kNoLoad, row_off, 0);
   return r;
 }
 
@@ -95,49 +101,6 @@ __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int
 template <int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// Rows for the next output, whose first tap is D rows further down:
-// R[k] <- R[k + D], then load the D rows that are new.
-template <int T, int D>
-__device__ __forceinline__ void advance_rows(Chunk* R, __amdgpu_buffer_rsrc_t rsrc, int off, int n0, int stride) {
-#pragma unroll
-  for (int k = 0; k + D < T; k++) R[k] = R[k + D];
-#pragma unroll
-  for (int k = (T > D ? T - D : 0); k < T; k++) R[k] = load_chunk(rsrc, off, (n0 + k) * stride);
-}
-
-template <int T>
-__device__ __forceinline__ void advance_rows_dyn(Chunk* R, __amdgpu_buffer_rsrc_t rsrc, int off, int n0, int stride,
-                                                 int d) {
-  switch (d) {
-    case 0:
-      break;
-#define MXD_ADV_CASE(D)                                            \
-  case D:                                                          \
-    if constexpr (D < T) advance_rows<T, D>(R, rsrc, off, n0, stride); \
-    break;
-    MXD_ADV_CASE(1)
-    MXD_ADV_CASE(2)
-    MXD_ADV_CASE(3)
-    MXD_ADV_CASE(4)
-    MXD_ADV_CASE(5)
-    MXD_ADV_CASE(6)
-    MXD_ADV_CASE(7)
-    MXD_ADV_CASE(8)
-    MXD_ADV_CASE(9)
-    MXD_ADV_CASE(10)
-    MXD_ADV_CASE(11)
-    MXD_ADV_CASE(12)
-    MXD_ADV_CASE(13)
-    MXD_ADV_CASE(14)
-    MXD_ADV_CASE(15)
-    MXD_ADV_CASE(16)
-#undef MXD_ADV_CASE
-    default:
-      advance_rows<T, T>(R, rsrc, off, n0, stride);
-      break;
-  }
 }
 
 template <int C, bool F32, int T, int MODE = 0, bool RING = false>
@@ -188,13 +151,16 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   const int px_lo = __float_as_int(xtab[xa * xs]);
   const int px_hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
   const int fb0 = (px_lo * C) & ~3;
-  (void)px_hi;
+  const int need = (px_hi + 1) * C - fb0;  // footprint bytes of the strip (<= kRowBytes)
   const uint64_t sbase = reinterpret_cast<uint64_t>(im.src);
   const uint64_t sb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>(sb), (short)0, sstride * src_h, 0x00020000);
-  const int loff = fb0 + 4 * lane;  // + 256 j
+  // Only the dwords that hold footprint bytes are fetched.
+  int voff[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) voff[j] = 4 * lane + 256 * j < need ? fb0 + 4 * lane + 256 * j : kNoLoad;
 
   // Horizontal taps of this lane's 4 output elements, for the whole band.
   const int nout = (ox1 - ox0) * C;
@@ -218,17 +184,17 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   // compiler places in the row loop only ever cover the row loads.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 
-  auto load_rows = [&](Chunk* R, int y) {
+  auto load_rows = [&](Chunk* R, int y, bool live) {
     const int n0 = __float_as_int(ytab[y * ys]);
 #pragma unroll
     for (int k = 0; k < T; k++) {
       if constexpr (MODE == 2) {
         R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
       } else if constexpr (MODE == 4) {
-        if (k >= T / 2) R[k] = load_chunk(rsrc, loff, (n0 + k) * sstride);
+        if (k >= T / 2) R[k] = load_chunk_if(rsrc, voff, (n0 + k) * sstride, live);
         else R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
       } else {
-        R[k] = load_chunk(rsrc, loff, (n0 + k) * sstride);
+        R[k] = load_chunk_if(rsrc, voff, (n0 + k) * sstride, live);
       }
     }
   };
@@ -309,12 +275,12 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     // the loop has the same loads in flight and the compiler's counted waits
     // stay partial.
     Chunk RA[T], RB[T];
-    load_rows(RA, oy0);
+    load_rows(RA, oy0, true);
     for (int y = oy0;; y += 2) {
-      load_rows(RB, min(y + 1, crop_h - 1));
+      load_rows(RB, min(y + 1, crop_h - 1), y + 1 < oy1);
       step(RA, y);
       if (y + 1 >= oy1) break;
-      load_rows(RA, min(y + 2, crop_h - 1));
+      load_rows(RA, min(y + 2, crop_h - 1), y + 2 < oy1);
       step(RB, y + 1);
       if (y + 2 >= oy1) break;
     }
@@ -340,7 +306,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
 #pragma unroll
     for (int i = 0; i < kLook; i++) {
       if constexpr (MODE == 2) ring[i] = Chunk{{(uint32_t)(lane * 7 + i), (uint32_t)(rs * 3), (uint32_t)lane, (uint32_t)(i ^ lane)}};
-      else ring[i] = load_chunk(rsrc, loff, min(rs + i, re) * sstride);
+      else ring[i] = load_chunk_if(rsrc, voff, min(rs + i, re) * sstride, rs + i <= re);
     }
     for (int base = rs; base <= re; base += kRing) {
       static_for<kRing>([&](auto ic) {
@@ -351,7 +317,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
         // keep kLook rows in flight: slot (i + kLook) % kRing is free (its row
         // left the tap window of every open output row)
         if constexpr (MODE == 2) ring[(i + kLook) % kRing].d[0] = (uint32_t)(r + lane);
-        else ring[(i + kLook) % kRing] = load_chunk(rsrc, loff, min(r + kLook, re) * sstride);
+        else ring[(i + kLook) % kRing] = load_chunk_if(rsrc, voff, min(r + kLook, re) * sstride, r + kLook <= re);
         if (r == ly) {  // output row y ends at source row r (at most one: checked on the host)
           kfloat* we = rtab + y * ys + kTapHeader;
           float acc[kChunk];
@@ -377,54 +343,58 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   }
 }
 
-template <int C, bool F32, int T, int MODE = 0>
-int launch_ct(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
+using WaveKernel = void (*)(const ImgDev*, int, int, int);
+
+template <int C, bool F32, int T>
+WaveKernel select_ct(const WaveCfg& cfg) {
   if (cfg.ring) {
-    const int rowf = wave_row_floats(cfg.taps, C);
-    const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
-    auto k = resample_wave<C, F32, T, 0, true>;
     if constexpr (C == 3 && F32 && T == 8) {
-      if (cfg.mode == 1) k = resample_wave<C, F32, T, 1, true>;
-      if (cfg.mode == 2) k = resample_wave<C, F32, T, 2, true>;
-      if (cfg.mode == 3) k = resample_wave<C, F32, T, 3, true>;
+      if (cfg.mode == 1) return resample_wave<C, F32, T, 1, true>;
+      if (cfg.mode == 2) return resample_wave<C, F32, T, 2, true>;
+      if (cfg.mode == 3) return resample_wave<C, F32, T, 3, true>;
     }
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), kWaves * rowf * (int)sizeof(float), s, imgs,
-                       cfg.nimgs, cfg.nunits, rowf);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return resample_wave<C, F32, T, 0, true>;
   }
-  if constexpr (MODE == 0 && C == 3 && F32 && T == 8) {
-    switch (cfg.mode) {
-      case 1: return launch_ct<C, F32, T, 1>(cfg, imgs, s);
-      case 2: return launch_ct<C, F32, T, 2>(cfg, imgs, s);
-      case 3: return launch_ct<C, F32, T, 3>(cfg, imgs, s);
-      case 4: return launch_ct<C, F32, T, 4>(cfg, imgs, s);
-      default: break;
-    }
+  if constexpr (C == 3 && F32 && T == 8) {
+    if (cfg.mode == 1) return resample_wave<C, F32, T, 1>;
+    if (cfg.mode == 2) return resample_wave<C, F32, T, 2>;
+    if (cfg.mode == 3) return resample_wave<C, F32, T, 3>;
+    if (cfg.mode == 4) return resample_wave<C, F32, T, 4>;
   }
-  const int rowf = wave_row_floats(cfg.taps, C);
-  const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL((resample_wave<C, F32, T, MODE>), dim3(blocks), dim3(kWaves * kLanes),
-                     kWaves * rowf * (int)sizeof(float), s, imgs, cfg.nimgs, cfg.nunits, rowf);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return resample_wave<C, F32, T, 0>;
 }
 
 template <int C, bool F32>
-int launch_c(const WaveCfg& cfg, const ImgDev* imgs, hipStream_t s) {
+WaveKernel select_c(const WaveCfg& cfg) {
   switch (cfg.taps) {
-    case 2: return launch_ct<C, F32, 2>(cfg, imgs, s);
-    case 3: return launch_ct<C, F32, 3>(cfg, imgs, s);
-    case 4: return launch_ct<C, F32, 4>(cfg, imgs, s);
-    case 5: return launch_ct<C, F32, 5>(cfg, imgs, s);
-    case 6: return launch_ct<C, F32, 6>(cfg, imgs, s);
-    case 8: return launch_ct<C, F32, 8>(cfg, imgs, s);
-    case 9: return launch_ct<C, F32, 9>(cfg, imgs, s);
-    case 10: return launch_ct<C, F32, 10>(cfg, imgs, s);
-    case 12: return launch_ct<C, F32, 12>(cfg, imgs, s);
-    case 14: return launch_ct<C, F32, 14>(cfg, imgs, s);
-    case 17: return launch_ct<C, F32, 17>(cfg, imgs, s);
-    default: return -2;
+    case 2: return select_ct<C, F32, 2>(cfg);
+    case 3: return select_ct<C, F32, 3>(cfg);
+    case 4: return select_ct<C, F32, 4>(cfg);
+    case 5: return select_ct<C, F32, 5>(cfg);
+    case 6: return select_ct<C, F32, 6>(cfg);
+    case 8: return select_ct<C, F32, 8>(cfg);
+    case 9: return select_ct<C, F32, 9>(cfg);
+    case 10: return select_ct<C, F32, 10>(cfg);
+    case 12: return select_ct<C, F32, 12>(cfg);
+    case 14: return select_ct<C, F32, 14>(cfg);
+    case 17: return select_ct<C, F32, 17>(cfg);
+    default: return nullptr;
   }
 }
+
+WaveKernel select_kernel(const WaveCfg& cfg) {
+  switch (cfg.channels * 2 + (cfg.f32 ? 1 : 0)) {
+    case 2: return select_c<1, false>(cfg);
+    case 3: return select_c<1, true>(cfg);
+    case 4: return select_c<2, false>(cfg);
+    case 5: return select_c<2, true>(cfg);
+    case 6: return select_c<3, false>(cfg);
+    case 7: return select_c<3, true>(cfg);
+    default: return nullptr;
+  }
+}
+
+int lds_bytes(const WaveCfg& cfg) { return kWaves * wave_row_floats(cfg.taps, cfg.channels) * (int)sizeof(float); }
 
 }  // namespace
 
@@ -470,16 +440,23 @@ int launch_copy(const void* src, void* dst, size_t bytes, void* stream) {
 }
 
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  switch (cfg.channels * 2 + (cfg.f32 ? 1 : 0)) {
-    case 2: return launch_c<1, false>(cfg, imgs, s);
-    case 3: return launch_c<1, true>(cfg, imgs, s);
-    case 4: return launch_c<2, false>(cfg, imgs, s);
-    case 5: return launch_c<2, true>(cfg, imgs, s);
-    case 6: return launch_c<3, false>(cfg, imgs, s);
-    case 7: return launch_c<3, true>(cfg, imgs, s);
-    default: return -2;
-  }
+  const WaveKernel k = select_kernel(cfg);
+  if (!k) return -2;
+  const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
+                     imgs, cfg.nimgs, cfg.nunits, wave_row_floats(cfg.taps, cfg.channels));
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int wave_capacity(const WaveCfg& cfg, int device) {
+  const WaveKernel k = select_kernel(cfg);
+  if (!k) return 0;
+  int blocks = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(k), kWaves * kLanes,
+                                                   lds_bytes(cfg)) != hipSuccess)
+    return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return blocks * kWaves * cus;
 }
 
 }  // namespace mxd

@@ -78,4 +78,4 @@ def synth(h, w, c, seed):
     xi = np.minimum((np.arange(w) * (gw - 1)) // max(1, w - 1), gw - 2)
     f = grid[yi][:, xi] * 0.6 + grid[yi + 1][:, xi + 1] * 0.4
     f += rng.normal(0, 16, f.shape).astype(np.float32)
-    return np.clip(f, 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(np.clip(f, 0, 255).astype(np.uint8))
