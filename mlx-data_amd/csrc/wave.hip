@@ -92,6 +92,14 @@ __device__ __forceinline__ void fma16(float* acc, float w, const Chunk& v) {
   }
 }
 
+// Diagnostic (MODE 5): one 16-byte load per lane instead of four dwords --
+// same bytes per wave, wrong lane order (timing only).
+__device__ __forceinline__ Chunk load_x4_if(__amdgpu_buffer_rsrc_t rsrc, int off, int row_off, bool live) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, live ? off : kNoLoad, row_off, 0);
+  return Chunk{{(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w}};
+}
+
 // Calls f(std::integral_constant<int, I>) for I = 0..N-1 (guaranteed unrolled,
 // so register-array indices derived from I are static).
 template <class F, int... Is>
@@ -293,7 +301,8 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     // resident in the ring: gather them (V), then H and store.  Requires the
     // last taps of consecutive output rows to strictly increase (at most one
     // output row ends per source row: downsampling); the host checks it.
-    constexpr int kLook = 6;
+    // rows loaded ahead (MODE 6/7/8: lookahead experiments)
+    constexpr int kLook = MODE == 6 ? 9 : MODE == 7 ? 4 : MODE == 8 ? 12 : 6;
     constexpr int kRing = T + kLook;
     // right-aligned vertical table: {last row, count, w[T]} per output row
     kfloat* rtab = ytab;
@@ -306,6 +315,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
 #pragma unroll
     for (int i = 0; i < kLook; i++) {
       if constexpr (MODE == 2) ring[i] = Chunk{{(uint32_t)(lane * 7 + i), (uint32_t)(rs * 3), (uint32_t)lane, (uint32_t)(i ^ lane)}};
+      else if constexpr (MODE == 5) ring[i] = load_x4_if(rsrc, fb0 + 16 * lane, min(rs + i, re) * sstride, rs + i <= re);
       else ring[i] = load_chunk_if(rsrc, voff, min(rs + i, re) * sstride, rs + i <= re);
     }
     for (int base = rs; base <= re; base += kRing) {
@@ -317,6 +327,8 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
         // keep kLook rows in flight: slot (i + kLook) % kRing is free (its row
         // left the tap window of every open output row)
         if constexpr (MODE == 2) ring[(i + kLook) % kRing].d[0] = (uint32_t)(r + lane);
+        else if constexpr (MODE == 5)
+          ring[(i + kLook) % kRing] = load_x4_if(rsrc, fb0 + 16 * lane, min(r + kLook, re) * sstride, r + kLook <= re);
         else ring[(i + kLook) % kRing] = load_chunk_if(rsrc, voff, min(r + kLook, re) * sstride, r + kLook <= re);
         if (r == ly) {  // output row y ends at source row r (at most one: checked on the host)
           kfloat* we = rtab + y * ys + kTapHeader;
@@ -352,6 +364,10 @@ WaveKernel select_ct(const WaveCfg& cfg) {
       if (cfg.mode == 1) return resample_wave<C, F32, T, 1, true>;
       if (cfg.mode == 2) return resample_wave<C, F32, T, 2, true>;
       if (cfg.mode == 3) return resample_wave<C, F32, T, 3, true>;
+      if (cfg.mode == 5) return resample_wave<C, F32, T, 5, true>;
+      if (cfg.mode == 6) return resample_wave<C, F32, T, 6, true>;
+      if (cfg.mode == 7) return resample_wave<C, F32, T, 7, true>;
+      if (cfg.mode == 8) return resample_wave<C, F32, T, 8, true>;
     }
     return resample_wave<C, F32, T, 0, true>;
   }

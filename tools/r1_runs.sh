@@ -12,7 +12,7 @@ run() {  # name limit cmd...
   if [ $rc -gt 1 ]; then echo "stopping"; exit $rc; fi
 }
 run pytest 600 python -m pytest tests -x -q -m gpu
-for m in 0 5 2; do
+for m in 0 5 6 7 8 2; do
   MXD_WAVE_ABLATE=$m run abl_m$m 300 python bench.py --steps 30 --warmup 3 --no-cpu --no-e2e
 done
 for w in c3 c5; do run bench_$w 300 python bench.py --workload $w --steps 20 --warmup 3 --no-cpu; done
