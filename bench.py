@@ -249,7 +249,7 @@ def main():
     offs, total = [], 0
     for (sw, sh) in sizes:
         offs.append(total)
-        total += (sw * C * sh + 255) // 256 * 256
+        total += (sw * C * sh + 255) // 256 * 256 + int(os.environ.get("MXD_BENCH_SLOT_PAD", "0"))
     out_bytes = [g[4] * g[5] * C * elem for g in geoms]
     out_offs = np.concatenate([[0], np.cumsum(out_bytes)[:-1]]).astype(np.int64)
     rng = np.random.default_rng(1000 + ranks.rank)

@@ -75,10 +75,11 @@ constexpr int kNoLoad = 0x7ffffff0;
 // The lane's 4 dwords of source row `row_off / stride` (byte offsets voff[j]
 // of the row, kNoLoad for dwords outside the strip's footprint), or four
 // zeros without memory traffic when !live (uniform).
+template <int AUX = 0>
 __device__ __forceinline__ Chunk load_chunk_if(__amdgpu_buffer_rsrc_t rsrc, const int* voff, int row_off, bool live) {
   Chunk r;
 #pragma unroll
-  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, live ? voff[j] : kNoLoad, row_off, 0);
+  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, live ? voff[j] : kNoLoad, row_off, AUX);
   return r;
 }
 
@@ -235,10 +236,18 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     }
     const int o0 = kOutPerLane * lane;
     char* drow = dst + (int64_t)y * dstride;
+    // MODE 9/10 (timing only): no stores (nimgs is never negative)
+    if ((MODE != 9 && MODE != 10) || nimgs < 0)
     if (o0 + kOutPerLane <= nout) {  // one store instruction per row (lanes past nout masked)
       if constexpr (F32) {
         f32x4 v = {div255(out[0]), div255(out[1]), div255(out[2]), div255(out[3])};
-        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(GLOBAL_PTR(float, drow) + ox0 * C + o0) = v;
+        const int ob = (ox0 * C + o0) * 4;  // MODE 14: only whole 128-B lines of the strip's row segment
+        if (MODE != 14 || (ob >= ((ox0 * C * 4 + 127) & ~127) && ob + 16 <= ((ox1 * C * 4) & ~127))) {
+          if constexpr (MODE == 11 || MODE == 13)
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(reinterpret_cast<float*>(drow) + ox0 * C + o0));
+          else
+            *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(GLOBAL_PTR(float, drow) + ox0 * C + o0) = v;
+        }
       } else {
         *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(GLOBAL_PTR(uint8_t, drow) + ox0 * C + o0) =
             (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
@@ -316,7 +325,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     for (int i = 0; i < kLook; i++) {
       if constexpr (MODE == 2) ring[i] = Chunk{{(uint32_t)(lane * 7 + i), (uint32_t)(rs * 3), (uint32_t)lane, (uint32_t)(i ^ lane)}};
       else if constexpr (MODE == 5) ring[i] = load_x4_if(rsrc, fb0 + 16 * lane, min(rs + i, re) * sstride, rs + i <= re);
-      else ring[i] = load_chunk_if(rsrc, voff, min(rs + i, re) * sstride, rs + i <= re);
+      else ring[i] = load_chunk_if<(MODE == 12 || MODE == 13) ? 2 : 0>(rsrc, voff, min(rs + i, re) * sstride, rs + i <= re);
     }
     for (int base = rs; base <= re; base += kRing) {
       static_for<kRing>([&](auto ic) {
@@ -329,7 +338,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
         if constexpr (MODE == 2) ring[(i + kLook) % kRing].d[0] = (uint32_t)(r + lane);
         else if constexpr (MODE == 5)
           ring[(i + kLook) % kRing] = load_x4_if(rsrc, fb0 + 16 * lane, min(r + kLook, re) * sstride, r + kLook <= re);
-        else ring[(i + kLook) % kRing] = load_chunk_if(rsrc, voff, min(r + kLook, re) * sstride, r + kLook <= re);
+        else ring[(i + kLook) % kRing] = load_chunk_if<(MODE == 12 || MODE == 13) ? 2 : 0>(rsrc, voff, min(r + kLook, re) * sstride, r + kLook <= re);
         if (r == ly) {  // output row y ends at source row r (at most one: checked on the host)
           kfloat* we = rtab + y * ys + kTapHeader;
           float acc[kChunk];
@@ -338,7 +347,7 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
 #pragma unroll
           for (int k = 0; k < T; k++) {
             const Chunk& c = ring[(i + kRing - (T - 1) + k) % kRing];
-            if constexpr (MODE == 1) {
+            if constexpr (MODE == 1 || MODE == 10) {
 #pragma unroll
               for (int q = 0; q < 4; q++) acc[4 * q] += __uint_as_float(c.d[q] & 0x3fffffffu);
             } else {
@@ -368,6 +377,12 @@ WaveKernel select_ct(const WaveCfg& cfg) {
       if (cfg.mode == 6) return resample_wave<C, F32, T, 6, true>;
       if (cfg.mode == 7) return resample_wave<C, F32, T, 7, true>;
       if (cfg.mode == 8) return resample_wave<C, F32, T, 8, true>;
+      if (cfg.mode == 9) return resample_wave<C, F32, T, 9, true>;
+      if (cfg.mode == 10) return resample_wave<C, F32, T, 10, true>;
+      if (cfg.mode == 11) return resample_wave<C, F32, T, 11, true>;
+      if (cfg.mode == 12) return resample_wave<C, F32, T, 12, true>;
+      if (cfg.mode == 13) return resample_wave<C, F32, T, 13, true>;
+      if (cfg.mode == 14) return resample_wave<C, F32, T, 14, true>;
     }
     return resample_wave<C, F32, T, 0, true>;
   }
