@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -59,6 +60,7 @@ struct DevTable {
   int32_t width = 0;     // max taps of any output
   int32_t padded = 0;    // weights per entry in device memory (>= kMinTabWidth)
   std::vector<int32_t> first, count;  // host copy for tiling decisions
+  std::vector<float> w;               // host copy of the weights, `width` per output (scatter schedules)
 };
 
 class TableCache {
@@ -88,6 +90,7 @@ class TableCache {
     tab->padded = padded;
     tab->first = taps.first;
     tab->count = taps.count;
+    tab->w = taps.weight;
     DeviceGuard g(device);
     MXD_HIP(hipMalloc(&tab->ptr, host.size() * sizeof(float)));
     MXD_HIP(hipMemcpy(tab->ptr, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -261,10 +264,147 @@ struct ImgPlan {
   const DevTable* xt = nullptr;
   const DevTable* yt = nullptr;
   int32_t bucket = -1;   // wave path tap bucket, -1 = not eligible
-  int32_t ring = 0;      // use the row-once register-ring kernel (right-aligned y table)
-  const DevTable* yr = nullptr;
+  int32_t kind = 0;      // wave kernel: 0 gather, 1 register ring, 2 scatter
+  int32_t s = 0, dmax = 0, p = 0;  // scatter shape (ScatterShape)
+  const DevTable* yr = nullptr;    // ring: right-aligned vertical table
   int32_t nstrips = 0, tx = 0;
 };
+
+// Shape of the scatter schedule for crop rows [off, off+len) of a vertical
+// table, valid for bands starting at any row: dmax = most source rows that are
+// new for one output row (after the previous row's last tap), p = prologue
+// groups (the first output of a band needs all its taps), s = most output rows
+// a source row's weights must reach from its group (accumulator slots).
+// s = 0: taps not monotone (not a geometry the scatter kernel handles).
+struct ScatterShape {
+  int32_t s = 0, dmax = 0, p = 0;
+};
+
+ScatterShape scatter_shape_uncached(const DevTable& t, int32_t off, int32_t len) {
+  ScatterShape sh;
+  auto first = [&](int32_t u) { return t.first[off + u]; };
+  auto last = [&](int32_t u) { return t.first[off + u] + t.count[off + u] - 1; };
+  int32_t dmax = 1;
+  for (int32_t u = 1; u < len; u++) {
+    if (first(u) < first(u - 1) || last(u) < last(u - 1)) return sh;
+    dmax = std::max(dmax, last(u) - last(u - 1));
+  }
+  int32_t p = 0;
+  for (int32_t u = 0; u < len; u++) p = std::max(p, (t.count[off + u] + dmax - 1) / dmax - 1);
+  int32_t s = 1;
+  for (int32_t b = 0; b < len; b++) {
+    // prologue rows of a band starting at b: slot = (output - b) + (last(b) - r) / dmax
+    for (int32_t r = first(b); r <= last(b); r++)
+      for (int32_t u = b; u < len && first(u) <= r; u++)
+        if (r <= last(u)) s = std::max(s, u - b + (last(b) - r) / dmax + 1);
+    // rows new for output b (b > 0 as a non-first output): slot = output - b
+    if (b > 0)
+      for (int32_t r = last(b - 1) + 1; r <= last(b); r++)
+        for (int32_t u = b; u < len && first(u) <= r; u++)
+          if (r <= last(u)) s = std::max(s, u - b + 1);
+  }
+  sh.s = s;
+  sh.dmax = dmax;
+  sh.p = p;
+  return sh;
+}
+
+// Cached per (table, crop rows): computing the shape walks every crop row.
+ScatterShape scatter_shape(const DevTable& t, int32_t off, int32_t len) {
+  static std::mutex mu;
+  static std::map<std::tuple<const DevTable*, int32_t, int32_t>, ScatterShape> cache;
+  const auto key = std::make_tuple(&t, off, len);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  return cache[key] = scatter_shape_uncached(t, off, len);
+}
+
+// Scatter schedules (layout: wave.hip) in device memory, one per
+// (device, vertical geometry, crop rows, band height, shape).
+struct DevSched {
+  int32_t* ptr = nullptr;
+  int32_t band_words = 0;  // words per band
+  int32_t entry_off = 0;   // word offset of the iteration entries in a band
+};
+
+class SchedCache {
+ public:
+  int get(int32_t device, const DevTable& yt, int32_t src_h, int32_t resize_h, int32_t crop_y, int32_t crop_h,
+          int32_t ty, const ScatterShape& sh, const DevSched** out) {
+    std::lock_guard<std::mutex> lock(mu_);
+    const auto key = std::make_tuple(device, src_h, resize_h, crop_y, crop_h, ty, sh.s, sh.dmax, sh.p);
+    auto it = map_.find(key);
+    if (it != map_.end()) {
+      *out = it->second.get();
+      return MXD_OK;
+    }
+    auto sched = std::make_unique<DevSched>();
+    std::vector<int32_t> words;
+    if (!build(yt, crop_y, crop_h, ty, sh, &words, sched.get()))
+      return fail(MXD_ERR_INVALID, "mxd: scatter schedule does not fit its shape");
+    DeviceGuard g(device);
+    MXD_HIP(hipMalloc(reinterpret_cast<void**>(&sched->ptr), words.size() * sizeof(int32_t)));
+    MXD_HIP(hipMemcpy(sched->ptr, words.data(), words.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    *out = sched.get();
+    map_[key] = std::move(sched);
+    return MXD_OK;
+  }
+
+ private:
+  static bool build(const DevTable& yt, int32_t crop_y, int32_t crop_h, int32_t ty, const ScatterShape& sh,
+                    std::vector<int32_t>* words, DevSched* d) {
+    const int32_t S = sh.s, D = sh.dmax, P = sh.p;
+    const int32_t la = mxd::scatter_ring_slots(D) - 1, bg = mxd::scatter_block_groups(S, D);
+    const int32_t E = mxd::scatter_entry_words(S);
+    const int32_t nb = (crop_h + ty - 1) / ty;
+    const int32_t gmax = (P + ty + bg - 1) / bg * bg;
+    const int32_t gwords = (1 + gmax + 3) & ~3;
+    const int32_t iters = gmax * D + la;
+    d->band_words = gwords + iters * E;
+    d->entry_off = gwords;
+    words->assign((size_t)nb * d->band_words, 0);
+    auto first = [&](int32_t y) { return yt.first[crop_y + y]; };
+    auto last = [&](int32_t y) { return yt.first[crop_y + y] + yt.count[crop_y + y] - 1; };
+    for (int32_t b = 0; b < nb; b++) {
+      int32_t* w = words->data() + (size_t)b * d->band_words;
+      const int32_t y0 = b * ty, n = std::min(ty, crop_h - y0);
+      w[0] = (P + n + bg - 1) / bg * bg;
+      for (int32_t g = 0; g < gmax; g++) w[1 + g] = g >= P && g - P < n ? y0 + g - P : -1;
+      int32_t* ent = w + gwords;
+      for (int32_t i = 0; i < iters; i++) ent[i * E] = -1;
+      std::vector<int32_t> fill(gmax, 0);
+      bool ok = true;
+      auto add_row = [&](int32_t g, int32_t r) {
+        if (g < 0 || g >= gmax || fill[g] >= D) return void(ok = false);
+        int32_t* e = ent + (size_t)(g * D + fill[g]++) * E;
+        e[0] = r;
+        for (int32_t u = 0; u < n; u++) {
+          if (r < first(y0 + u) || r > last(y0 + u)) continue;
+          const int32_t k = P + u - g;
+          if (k < 0 || k >= S) return void(ok = false);
+          const float wt = yt.w[(size_t)(crop_y + y0 + u) * yt.width + (r - first(y0 + u))];
+          std::memcpy(&e[1 + k], &wt, sizeof(float));
+        }
+      };
+      for (int32_t r = first(y0); r <= last(y0); r++) add_row(P - (last(y0) - r) / D, r);
+      for (int32_t u = 1; u < n; u++)
+        for (int32_t r = last(y0 + u - 1) + 1; r <= last(y0 + u); r++) add_row(P + u, r);
+      if (!ok) return false;
+    }
+    return true;
+  }
+
+  std::mutex mu_;
+  std::map<std::tuple<int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t>,
+           std::unique_ptr<DevSched>>
+      map_;
+};
+
+SchedCache& schedules() {
+  static SchedCache* c = new SchedCache();
+  return *c;
+}
 
 // Wave path strips: strip_cols a multiple of 4 (so every strip's first output
 // element is 16-byte aligned), strip_cols*C <= wave_max_outputs() and <=
@@ -339,8 +479,8 @@ int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_
 
 int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, int, int>, int32_t> cache;
-  const auto key = std::make_tuple(device, cfg.channels, cfg.f32, cfg.taps, cfg.ring, cfg.mode);
+  static std::map<std::tuple<int, int, int, int, int, int, int, int>, int32_t> cache;
+  const auto key = std::make_tuple(device, cfg.channels, cfg.f32, cfg.taps, cfg.kind, cfg.s, cfg.dmax, cfg.mode);
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
@@ -348,6 +488,11 @@ int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
   const int32_t c = mxd::wave_capacity(cfg, device);
   cache[key] = c;
   return c;
+}
+
+int env_int(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : 0;
 }
 
 int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
@@ -369,22 +514,34 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     wave_ok = wave_ok && (a & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
               images[i].src_stride * images[i].src_h < ((int64_t)1 << 31);
   }
+  static const int no_ring = env_int("MXD_NO_RING");
+  static const int no_scatter = env_int("MXD_NO_SCATTER");
+  static const int ablate = env_int("MXD_WAVE_ABLATE");
+  const int32_t f32 = out_dtype == MXD_F32_DIV255 ? 1 : 0;
   std::vector<ImgPlan> plans(n);
   for (int32_t i = 0; i < n; i++) {
     const mxd_image& im = images[i];
     ImgPlan& p = plans[i];
     if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
     if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
-    if (wave_ok) {
-      p.bucket = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
-      wave_ok = p.bucket > 0 && wave_strips(*p.xt, im, &p.nstrips, &p.tx);
-      static const int no_ring = [] {
-        const char* e = std::getenv("MXD_NO_RING");
-        return e ? std::atoi(e) : 0;
-      }();
-      p.ring = !no_ring && p.bucket <= 12 && one_output_per_row(*p.yt, im.crop_y, im.crop_h) ? 1 : 0;
-      if (wave_ok && p.ring)
-        if (int rc = right_tables().get(device, *p.yt, im.src_h, im.resize_h, p.bucket, &p.yr)) return rc;
+    if (!wave_ok) continue;
+    p.bucket = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
+    wave_ok = p.bucket > 0 && wave_strips(*p.xt, im, &p.nstrips, &p.tx);
+    if (!wave_ok) continue;
+    // Scatter when the vertical axis downsamples into a shape with a kernel;
+    // else the register ring (<= 1 output row per source row); else gather.
+    const ScatterShape sh = no_scatter ? ScatterShape{} : scatter_shape(*p.yt, im.crop_y, im.crop_h);
+    const int32_t xb = mxd::wave_taps_bucket(p.xt->width);
+    if (sh.s > 0 && xb > 0 &&
+        mxd::wave_has_kernel(mxd::WaveCfg{channels, f32, xb, 0, 0, ablate, 2, sh.s, sh.dmax})) {
+      p.kind = 2;
+      p.bucket = xb;
+      p.s = sh.s;
+      p.dmax = sh.dmax;
+      p.p = sh.p;
+    } else if (!no_ring && p.bucket <= 12 && one_output_per_row(*p.yt, im.crop_y, im.crop_h)) {
+      p.kind = 1;
+      if (int rc = right_tables().get(device, *p.yt, im.src_h, im.resize_h, p.bucket, &p.yr)) return rc;
     }
   }
   DeviceGuard guard(device);
@@ -405,52 +562,70 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   };
 
   if (wave_ok) {
-    // One launch per tap bucket; descriptors of all groups share one upload.
+    // One launch per kernel (kind, tap bucket, scatter shape); descriptors of
+    // all launches share one upload.
+    auto key = [&](int32_t i) {
+      const ImgPlan& p = plans[i];
+      return std::make_tuple(p.kind, p.bucket, p.s, p.dmax);
+    };
     std::vector<int32_t> order(n);
     for (int32_t i = 0; i < n; i++) order[i] = i;
-    auto key = [&](int32_t i) { return plans[i].bucket * 2 + plans[i].ring; };
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
-    static const int ablate = [] {
-      const char* e = std::getenv("MXD_WAVE_ABLATE");
-      return e ? std::atoi(e) : 0;
-    }();
     std::vector<ImgDev> descs(n);
-    struct Group { int32_t first, count, units, bucket, ring, ty; };
+    struct Group {
+      int32_t first, count, units, ty;
+      mxd::WaveCfg cfg;
+    };
     std::vector<Group> groups;
     for (int32_t k = 0; k < n; k++) {
-      const int32_t i = order[k];
-      if (groups.empty() || groups.back().bucket != plans[i].bucket || groups.back().ring != plans[i].ring)
-        groups.push_back({k, 0, 0, plans[i].bucket, plans[i].ring, 0});
+      const ImgPlan& p = plans[order[k]];
+      if (groups.empty() || key(order[groups.back().first]) != key(order[k]))
+        groups.push_back({k, 0, 0, 0, mxd::WaveCfg{channels, f32, p.bucket, 0, 0, ablate, p.kind, p.s, p.dmax}});
       groups.back().count++;
     }
     for (Group& g : groups) {
-      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, 0, ablate, g.ring};
+      g.cfg.nimgs = g.count;
       std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
       for (int32_t k = g.first; k < g.first + g.count; k++)
         strips.push_back({plans[order[k]].nstrips, images[order[k]].crop_h});
-      g.ty = band_rows(strips, wave_capacity_cached(cfg, device));
+      g.ty = band_rows(strips, wave_capacity_cached(g.cfg, device));
       for (int32_t k = g.first; k < g.first + g.count; k++) {
         const int32_t i = order[k];
+        const mxd_image& im = images[i];
+        const ImgPlan& p = plans[i];
         ImgDev& d = descs[k];
-        fill(d, images[i], plans[i]);
-        if (plans[i].ring) {
-          d.ywidth = plans[i].yr->padded;
-          d.ytab = plans[i].yr->ptr + (size_t)images[i].crop_y * (mxd::kTapHeader + plans[i].yr->padded);
+        fill(d, im, p);
+        d.ty = std::min(g.ty, im.crop_h);
+        if (p.kind == 1) {
+          d.ywidth = p.yr->padded;
+          d.ytab = p.yr->ptr + (size_t)im.crop_y * (mxd::kTapHeader + p.yr->padded);
+        } else if (p.kind == 2) {
+          const DevSched* sc = nullptr;
+          if (int rc = schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
+                                       ScatterShape{p.s, p.dmax, p.p}, &sc))
+            return rc;
+          d.ytab = reinterpret_cast<const float*>(sc->ptr);
+          d.ywidth = sc->band_words;
+          d.group = sc->entry_off;
         }
         d.tile_begin = g.units;
-        d.nstrips = plans[i].nstrips;
-        d.tx = plans[i].tx;
-        d.ty = std::min(g.ty, images[i].crop_h);
-        d.group = 1;
-        g.units += d.nstrips * ((images[i].crop_h + d.ty - 1) / d.ty);
+        d.nstrips = p.nstrips;
+        d.tx = p.tx;
+        if (p.kind != 2) d.group = 1;
+        g.units += d.nstrips * ((im.crop_h + d.ty - 1) / d.ty);
       }
+      g.cfg.nunits = g.units;
     }
     ImgDev* dev = nullptr;
     std::unique_lock<std::mutex> hold;
     if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
+    static const int debug = env_int("MXD_DEBUG");
     for (const Group& g : groups) {
-      mxd::WaveCfg cfg{channels, out_dtype == MXD_F32_DIV255 ? 1 : 0, g.bucket, g.count, g.units, ablate, g.ring};
-      if (int rc = mxd::launch_wave(cfg, dev + g.first, stream))
+      if (debug)
+        std::fprintf(stderr, "mxd: launch kind=%d taps=%d s=%d dmax=%d f32=%d imgs=%d units=%d band_rows=%d capacity=%d\n",
+                     g.cfg.kind, g.cfg.taps, g.cfg.s, g.cfg.dmax, g.cfg.f32, g.cfg.nimgs, g.cfg.nunits, g.ty,
+                     wave_capacity_cached(g.cfg, device));
+      if (int rc = mxd::launch_wave(g.cfg, dev + g.first, stream))
         return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
                                         " rc=" + std::to_string(rc));
     }

@@ -41,20 +41,38 @@ struct LaunchCfg {
   int32_t max_tx, max_ty, max_xw, max_yw, max_vw, max_group;
 };
 
-// Wave-per-unit fast path (wave.hip): sources 4-byte aligned, outputs 16-byte
+// Wave-per-unit fast paths (wave.hip): sources 4-byte aligned, outputs 16-byte
 // (f32) / 4-byte (u8) aligned, every strip's footprint <= wave_row_bytes(),
 // strip_cols*C <= wave_max_outputs(), taps <= 17.  Units are numbered through
 // ImgDev::tile_begin exactly like tiles; ty = band rows, tx = strip columns.
+// kind: 0 = gather, 1 = register ring (ImgDev::ytab is the right-aligned
+// table), 2 = scatter (ImgDev::ytab is the schedule, ywidth its words per band,
+// group the offset of its iteration entries).  taps = horizontal (and, for
+// gather / ring, vertical) tap bucket; s / dmax = scatter shape.
 struct WaveCfg {
   int32_t channels, f32, taps, nimgs, nunits;
-  int32_t mode;     // 0 = product kernel; 1..4 = diagnostic ablations (MXD_WAVE_ABLATE)
-  int32_t ring;     // register-ring kernel; ImgDev::ytab is the right-aligned table
+  int32_t mode;  // 0 = product kernel; 1, 2, 9 = timing-only ablations (MXD_WAVE_ABLATE)
+  int32_t kind;
+  int32_t s, dmax;
 };
+
+// Scatter schedule geometry, shared by the kernel and the host builder:
+// register ring slots for DMAX iterations per group, groups per unrolled
+// block (a multiple of S whose iterations are a multiple of the ring), words
+// per iteration entry (row + S weights).
+constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; }
+constexpr int scatter_ring_slots(int dmax) { return 12 % dmax == 0 ? 12 : (2 * dmax <= 12 ? 2 * dmax : dmax); }
+constexpr int scatter_block_groups(int s, int dmax) {
+  return scatter_ring_slots(dmax) / scatter_gcd(scatter_ring_slots(dmax), s * dmax) * s;
+}
+constexpr int scatter_entry_words(int s) { return s <= 3 ? 4 : 8; }
+
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
 int wave_row_floats(int taps, int channels);
 int wave_row_bytes();
 int wave_max_outputs();  // output elements per strip row (4 per lane)
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
+bool wave_has_kernel(const WaveCfg& cfg);
 // Waves of this configuration the device runs at once (occupancy x CUs), 0 if unknown.
 int wave_capacity(const WaveCfg& cfg, int device);
 int launch_copy(const void* src, void* dst, size_t bytes, void* stream);

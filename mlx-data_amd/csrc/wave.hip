@@ -1,29 +1,48 @@
-// wave.hip -- the fast path of the fused resize + crop (+ hflip) (+ /255) stage.
+// wave.hip -- the fast paths of the fused resize + crop (+ hflip) (+ /255) stage.
 //
-// Same arithmetic as resample.hip (stbir triangle taps from the shared tables,
-// vertical pass first in byte units, f32 FMA accumulation, stbir encode), but
-// organised so that no workgroup barrier is ever needed:
+// Arithmetic (shared with resample.hip): stbir triangle taps from the shared
+// tables, vertical pass first in byte units, f32 FMA accumulation in tap order
+// starting from 0, stbir's encode, exact q/255.
 //
-//   one WAVE owns one unit = (image, band of output rows, strip of output
-//   columns).  The wave covers a 1024-byte window of each source row: lane l
-//   holds the four dwords at bytes 4l + 256j (j = 0..3) of the window, loaded
-//   with buffer_load_dword through a descriptor spanning the whole image (row
-//   offset in the scalar soffset, so no per-load address arithmetic; reads
-//   past the image return 0).  For each output row y of the band:
-//     V  lane sums its 16 byte columns over the T vertical taps of y from the
-//        T consecutive source rows it holds in registers and writes 16 f32 to
-//        the wave's private LDS row (four ds_write_b128, lanes 16 bytes apart:
-//        conflict-free).  Then it moves on to y+1: the rows shared by the taps
-//        of y and y+1 stay in registers (shifted by the uniform row advance d),
-//        only the d new rows are loaded, and those loads are in flight during
-//     H  lane l produces output elements 4l..4l+3 of the strip row (C
-//        channels interleaved) from the LDS row with their T horizontal taps
-//        (weights in registers for the whole band), rounds like stbir's encode
-//        and stores 4 f32 (exact q/255, one 16-byte store) or 4 u8.
-//   Waves never wait for each other; the CU interleaves the waves of many
-//   units so that loads of their next rows are always in flight.
-// Tap counts are padded to the template T with zero weights; padded taps read
-// real neighbouring rows/columns (or zeros), so every value is finite.
+// One WAVE owns one unit = (image, band of output rows, strip of output
+// columns); no workgroup barriers.  The wave covers a 1024-byte window of each
+// source row: lane l holds the four dwords at bytes 4l + 256j (j = 0..3) of the
+// window, loaded with buffer_load_dword through a descriptor spanning the
+// image (row offset in the scalar soffset; dwords outside the strip's
+// footprint are not fetched, reads past the image return 0).  The vertical (V)
+// pass yields 16 f32 per lane for an output row; they go to the wave's private
+// LDS row (four ds_write_b128, lanes 16 B apart: conflict-free).  The
+// horizontal (H) pass gives lane l the output elements 4l..4l+3 of the strip
+// row (C channels interleaved) from the LDS row with their T horizontal taps
+// (in registers for the whole band, paired for v_pk_fma_f32), rounds like
+// stbir's encode and stores 4 f32 (exact q/255, one 16-byte store) or 4 u8.
+//
+// Three ways to run the V pass over a band (KIND):
+//   kGather  each output row loads its T tap rows, double-buffered one output
+//            row ahead.  Any geometry (upsampling included).
+//   kRing    every source row of the band is loaded once, kLook rows ahead,
+//            into a register ring; when a row is the last tap of an output row
+//            the T ring rows ending there are converted and summed
+//            (right-aligned taps).  Downsampling, <= 1 output row per source row.
+//   kScatter every source row is loaded once and converted to f32 ONCE, then
+//            FMA'd into each open output row whose taps contain it, following
+//            a host-built schedule (below).  The downsampling fast path: about
+//            half the VALU work of kRing for the same bytes.
+//
+// Scatter schedule (capi.cpp builds it per image crop and band height): a
+// sequence of GROUPS of DMAX iterations.  An iteration carries one source row
+// (or -1, a bubble) and its weights for the output rows of groups g, g+1, ...,
+// g+S-1; group g completes one output row (or none).  Group g accumulates in
+// slot g mod S, so with the group loop unrolled by a multiple of S every
+// accumulator index is static.  Rows are loaded R-1 iterations ahead into a
+// ring of R register slots, and the unrolled block is a multiple of R
+// iterations, so every ring slot index is static too.  Rows are visited in
+// ascending order, so each output row's sum runs in tap order from 0 exactly
+// as in kGather / kRing: the three kinds give bit-identical results.
+// Per band: word 0 = groups to run (a multiple of the block's groups), words
+// 1.. = the output row each group completes (-1: none), then at word
+// ImgDev::group the iteration entries (scatter_entry_words(S) words each:
+// row, then S f32 weights).
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -41,11 +60,12 @@ constexpr int kRowBytes = kLanes * kChunk;  // 1024 source bytes per wave row
 constexpr int kOutPerLane = 4;              // output elements per lane per row
 
 #define GLOBAL_PTR(T, p) ((__attribute__((address_space(1))) T*)(p))
-using gfloat = __attribute__((address_space(1))) float;
 using cgfloat = const __attribute__((address_space(1))) float;
 // Constant address space: uniform loads through it are scalar (s_load).
 using kfloat = const __attribute__((address_space(4))) float;
+using kint = const __attribute__((address_space(4))) int;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int xcd_remap(int b, int n) {
   const int q = n >> 3, r = n & 7;
@@ -64,6 +84,14 @@ __device__ __forceinline__ float div255(float q) {
 // stbir encode: (uint8)trunc(clamp(v*255 + 0.5, 0, 255)), v in byte units here.
 __device__ __forceinline__ float encode(float v) { return truncf(fminf(fmaxf(v + 0.5f, 0.0f), 255.0f)); }
 
+// A uniform pointer held in scalar registers.
+template <class P>
+__device__ __forceinline__ P uniform_ptr(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  return (P)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
+}
+
 struct Chunk {
   uint32_t d[4];
 };
@@ -75,30 +103,49 @@ constexpr int kNoLoad = 0x7ffffff0;
 // The lane's 4 dwords of source row `row_off / stride` (byte offsets voff[j]
 // of the row, kNoLoad for dwords outside the strip's footprint), or four
 // zeros without memory traffic when !live (uniform).
-template <int AUX = 0>
 __device__ __forceinline__ Chunk load_chunk_if(__amdgpu_buffer_rsrc_t rsrc, const int* voff, int row_off, bool live) {
   Chunk r;
 #pragma unroll
-  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, live ? voff[j] : kNoLoad, row_off, AUX);
+  for (int j = 0; j < 4; j++) r.d[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, live ? voff[j] : kNoLoad, row_off, 0);
   return r;
 }
 
-__device__ __forceinline__ void fma16(float* acc, float w, const Chunk& v) {
+// Bytes -> f32 in pairs: x[2j] = bytes 0,1 of dword j, x[2j+1] = bytes 2,3.
+__device__ __forceinline__ void chunk_to_f32(const Chunk& v, f32x2* x) {
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    acc[4 * i + 0] = __builtin_fmaf(w, (float)(v.d[i] & 0xffu), acc[4 * i + 0]);
-    acc[4 * i + 1] = __builtin_fmaf(w, (float)((v.d[i] >> 8) & 0xffu), acc[4 * i + 1]);
-    acc[4 * i + 2] = __builtin_fmaf(w, (float)((v.d[i] >> 16) & 0xffu), acc[4 * i + 2]);
-    acc[4 * i + 3] = __builtin_fmaf(w, (float)(v.d[i] >> 24), acc[4 * i + 3]);
+  for (int j = 0; j < 4; j++) {
+    x[2 * j] = f32x2{(float)(v.d[j] & 0xffu), (float)((v.d[j] >> 8) & 0xffu)};
+    x[2 * j + 1] = f32x2{(float)((v.d[j] >> 16) & 0xffu), (float)(v.d[j] >> 24)};
   }
 }
 
-// Diagnostic (MODE 5): one 16-byte load per lane instead of four dwords --
-// same bytes per wave, wrong lane order (timing only).
-__device__ __forceinline__ Chunk load_x4_if(__amdgpu_buffer_rsrc_t rsrc, int off, int row_off, bool live) {
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, live ? off : kNoLoad, row_off, 0);
-  return Chunk{{(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w}};
+// acc += w * x over the lane's 16 bytes (8 v_pk_fma_f32).
+__device__ __forceinline__ void fma_row(f32x2* acc, float w, const f32x2* x) {
+  const f32x2 ww = {w, w};
+#pragma unroll
+  for (int p = 0; p < 8; p++) acc[p] = __builtin_elementwise_fma(ww, x[p], acc[p]);
+}
+
+__device__ __forceinline__ void fma_chunk(f32x2* acc, float w, const Chunk& v) {
+  f32x2 x[8];
+  chunk_to_f32(v, x);
+  fma_row(acc, w, x);
+}
+
+// Timing-only ablation (MODE 1): keep the loads live without the V math.
+__device__ __forceinline__ void touch_chunk(f32x2* acc, const Chunk& v) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) acc[j].x += __uint_as_float(v.d[j] & 0x3fffffffu);
+}
+
+__device__ __forceinline__ Chunk fake_chunk(int lane, int r) {
+  return Chunk{{(uint32_t)(lane * 7 + r), (uint32_t)(r * 3), (uint32_t)lane, (uint32_t)(r ^ lane)}};
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Calls f(std::integral_constant<int, I>) for I = 0..N-1 (guaranteed unrolled,
@@ -112,9 +159,13 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int C, bool F32, int T, int MODE = 0, bool RING = false>
-__global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __restrict__ imgs, int nimgs,
-                                                               int nunits, int rowf) {
+enum Kind { kGather = 0, kRing = 1, kScatter = 2 };
+
+// Timing-only ablations (MXD_WAVE_ABLATE, instantiated for the C2 scatter
+// kernel only): 1 = no V math, 2 = no source loads, 9 = no stores.
+template <int C, bool F32, int T, int KIND, int S, int DMAX, int MODE>
+__global__ __launch_bounds__(kWaves* kLanes, KIND == kScatter && T <= 12 ? 3 : 1) void resample_wave(
+    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int rowf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & (kLanes - 1);
   const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
@@ -137,11 +188,9 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   const int xs = kTapHeader + __builtin_amdgcn_readfirstlane(im.xwidth);
   const int ys = kTapHeader + __builtin_amdgcn_readfirstlane(im.ywidth);
   cgfloat* xtab = GLOBAL_PTR(const float, im.xtab);
-  // Uniform pointer: the vertical taps are read with scalar loads (lgkmcnt),
-  // which never wait on the vector loads of the next rows.
-  const uint64_t yb = reinterpret_cast<uint64_t>(im.ytab);
-  kfloat* ytab = (kfloat*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(yb >> 32)) << 32) |
-                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)yb));
+  // The vertical taps / schedule are read with scalar loads (lgkmcnt), which
+  // never wait on the vector loads of the next rows.
+  kfloat* ytab = uniform_ptr<kfloat*>(im.ytab);
   char* dst = reinterpret_cast<char*>(im.dst);
   const int sstride = __builtin_amdgcn_readfirstlane((int)im.src_stride);
   const int src_h = __builtin_amdgcn_readfirstlane(im.src_h);
@@ -161,20 +210,18 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
   const int px_hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
   const int fb0 = (px_lo * C) & ~3;
   const int need = (px_hi + 1) * C - fb0;  // footprint bytes of the strip (<= kRowBytes)
-  const uint64_t sbase = reinterpret_cast<uint64_t>(im.src);
-  const uint64_t sb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sbase >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(sb), (short)0, sstride * src_h, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.src), (short)0, sstride * src_h, 0x00020000);
   // Only the dwords that hold footprint bytes are fetched.
   int voff[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) voff[j] = 4 * lane + 256 * j < need ? fb0 + 4 * lane + 256 * j : kNoLoad;
 
-  // Horizontal taps of this lane's 4 output elements, for the whole band.
+  // Horizontal taps of this lane's 4 output elements, for the whole band,
+  // paired (elements 0,1 and 2,3) for v_pk_fma_f32.
   const int nout = (ox1 - ox0) * C;
   const bool partial = (nout & (kOutPerLane - 1)) != 0;
-  float wx[kOutPerLane][T];
+  f32x2 wx[2][T];
   int pos[kOutPerLane];
 #pragma unroll
   for (int j = 0; j < kOutPerLane; j++) {
@@ -186,103 +233,71 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
     cgfloat* xe = xtab + xc * xs;
     pos[j] = __float_as_int(xe[0]) * C - fb0 + c;
 #pragma unroll
-    for (int k = 0; k < T; k++) wx[j][k] = xe[kTapHeader + k];  // zero padded past the tap count
+    for (int k = 0; k < T; k++) wx[j >> 1][k][j & 1] = xe[kTapHeader + k];  // zero padded past the tap count
   }
 
   // The horizontal weights are loaded once; retire them here so the waits the
   // compiler places in the row loop only ever cover the row loads.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 
-  auto load_rows = [&](Chunk* R, int y, bool live) {
-    const int n0 = __float_as_int(ytab[y * ys]);
-#pragma unroll
-    for (int k = 0; k < T; k++) {
-      if constexpr (MODE == 2) {
-        R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
-      } else if constexpr (MODE == 4) {
-        if (k >= T / 2) R[k] = load_chunk_if(rsrc, voff, (n0 + k) * sstride, live);
-        else R[k] = Chunk{{(uint32_t)(lane * 7 + k + n0), (uint32_t)(k * 3), (uint32_t)lane, (uint32_t)(k ^ lane)}};
-      } else {
-        R[k] = load_chunk_if(rsrc, voff, (n0 + k) * sstride, live);
-      }
-    }
-  };
-
   // V result (16 f32 per lane) -> the wave's LDS row: floats of bytes
   // 4l + 256j .. +3 go to vrow[4l + 256j], lanes 16 B apart per store.
-  auto write_vrow = [&](const float* acc) {
+  auto write_vrow = [&](const f32x2* acc) {
 #pragma unroll
     for (int j = 0; j < 4; j++)
       *reinterpret_cast<float4*>(vrow + 4 * lane + 256 * j) =
-          make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          make_float4(acc[2 * j].x, acc[2 * j].y, acc[2 * j + 1].x, acc[2 * j + 1].y);
+    wave_lds_sync();
   };
 
   // H: horizontal taps of output row y from the LDS row, encode, store.
   auto h_store = [&](int y) {
-    float out[kOutPerLane];
+    f32x2 s0 = {0.0f, 0.0f}, s1 = {0.0f, 0.0f};
 #pragma unroll
-    for (int j = 0; j < kOutPerLane; j++) {
-      float s = 0.0f;
-      if constexpr (MODE == 3) {
-        s = wx[j][0] * vrow[pos[j]];
-      } else {
-#pragma unroll
-        for (int k = 0; k < T; k++) s = __builtin_fmaf(wx[j][k], vrow[pos[j] + k * C], s);
-      }
-      out[j] = encode(s);
+    for (int k = 0; k < T; k++) {
+      s0 = __builtin_elementwise_fma(wx[0][k], f32x2{vrow[pos[0] + k * C], vrow[pos[1] + k * C]}, s0);
+      s1 = __builtin_elementwise_fma(wx[1][k], f32x2{vrow[pos[2] + k * C], vrow[pos[3] + k * C]}, s1);
     }
+    const float out[kOutPerLane] = {encode(s0.x), encode(s0.y), encode(s1.x), encode(s1.y)};
     const int o0 = kOutPerLane * lane;
     char* drow = dst + (int64_t)y * dstride;
-    // MODE 9/10 (timing only): no stores (nimgs is never negative)
-    if ((MODE != 9 && MODE != 10) || nimgs < 0)
-    if (o0 + kOutPerLane <= nout) {  // one store instruction per row (lanes past nout masked)
-      if constexpr (F32) {
-        f32x4 v = {div255(out[0]), div255(out[1]), div255(out[2]), div255(out[3])};
-        const int ob = (ox0 * C + o0) * 4;  // MODE 14: only whole 128-B lines of the strip's row segment
-        if (MODE != 14 || (ob >= ((ox0 * C * 4 + 127) & ~127) && ob + 16 <= ((ox1 * C * 4) & ~127))) {
-          if constexpr (MODE == 11 || MODE == 13)
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(reinterpret_cast<float*>(drow) + ox0 * C + o0));
-          else
-            *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(GLOBAL_PTR(float, drow) + ox0 * C + o0) = v;
+    if (MODE != 9 || nimgs < 0) {  // MODE 9: no stores (nimgs is never negative)
+      if (o0 + kOutPerLane <= nout) {  // one store instruction per row (lanes past nout masked)
+        if constexpr (F32) {
+          f32x4 v = {div255(out[0]), div255(out[1]), div255(out[2]), div255(out[3])};
+          *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(GLOBAL_PTR(float, drow) + ox0 * C + o0) = v;
+        } else {
+          *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(GLOBAL_PTR(uint8_t, drow) + ox0 * C + o0) =
+              (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
         }
-      } else {
-        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(GLOBAL_PTR(uint8_t, drow) + ox0 * C + o0) =
-            (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
       }
-    }
-    if (partial && o0 < nout && o0 + kOutPerLane > nout) {  // ragged strip end (uniform `partial`)
+      if (partial && o0 < nout && o0 + kOutPerLane > nout) {  // ragged strip end (uniform `partial`)
 #pragma unroll
-      for (int j = 0; j < kOutPerLane; j++) {
-        if (o0 + j < nout) {
-          if constexpr (F32) GLOBAL_PTR(float, drow)[ox0 * C + o0 + j] = div255(out[j]);
-          else GLOBAL_PTR(uint8_t, drow)[ox0 * C + o0 + j] = (uint8_t)out[j];
+        for (int j = 0; j < kOutPerLane; j++) {
+          if (o0 + j < nout) {
+            if constexpr (F32) GLOBAL_PTR(float, drow)[ox0 * C + o0 + j] = div255(out[j]);
+            else GLOBAL_PTR(uint8_t, drow)[ox0 * C + o0 + j] = (uint8_t)out[j];
+          }
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_sync();
   };
 
-  if constexpr (!RING) {
+  if constexpr (KIND == kGather) {
     // ---- gather: each output row sums its T source rows, loaded for it ----
+    auto load_rows = [&](Chunk* R, int y, bool live) {
+      const int n0 = __float_as_int(ytab[y * ys]);
+#pragma unroll
+      for (int k = 0; k < T; k++) R[k] = load_chunk_if(rsrc, voff, (n0 + k) * sstride, live);
+    };
     auto step = [&](const Chunk* R, int y) {
       kfloat* ye = ytab + y * ys;
-      float acc[kChunk];
+      f32x2 acc[8];
 #pragma unroll
-      for (int i = 0; i < kChunk; i++) acc[i] = 0.0f;
-      if constexpr (MODE == 1) {
+      for (int p = 0; p < 8; p++) acc[p] = f32x2{0.0f, 0.0f};
 #pragma unroll
-        for (int k = 0; k < T; k++)
-#pragma unroll
-          for (int i = 0; i < 4; i++) acc[4 * i] += __uint_as_float(R[k].d[i] & 0x3fffffffu);
-      } else {
-#pragma unroll
-        for (int k = 0; k < T; k++) fma16(acc, ye[kTapHeader + k], R[k]);  // zero padded past the tap count
-      }
+      for (int k = 0; k < T; k++) fma_chunk(acc, ye[kTapHeader + k], R[k]);  // zero padded past the tap count
       write_vrow(acc);
       h_store(y);
     };
@@ -301,32 +316,29 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
       step(RB, y + 1);
       if (y + 2 >= oy1) break;
     }
-  } else {
+  } else if constexpr (KIND == kRing) {
     // ---- ring: every source row of the band is loaded once, kLook rows
     // ahead, into a register ring of kRing = T + kLook slots; the source-row
     // loop is unrolled by kRing so every slot index is static.  When row r is
     // the last tap of output row y, y's taps are exactly the T rows ending at
     // r (right-aligned weights, zero for the rows before y's first tap), all
-    // resident in the ring: gather them (V), then H and store.  Requires the
-    // last taps of consecutive output rows to strictly increase (at most one
-    // output row ends per source row: downsampling); the host checks it.
-    // rows loaded ahead (MODE 6/7/8: lookahead experiments)
-    constexpr int kLook = MODE == 6 ? 9 : MODE == 7 ? 4 : MODE == 8 ? 12 : 6;
+    // resident in the ring: convert and sum them (V), then H and store.
+    // Requires the last taps of consecutive output rows to strictly increase
+    // (at most one output row ends per source row); the host checks it.
+    constexpr int kLook = 6;
     constexpr int kRing = T + kLook;
-    // right-aligned vertical table: {last row, count, w[T]} per output row
-    kfloat* rtab = ytab;
+    kfloat* rtab = ytab;  // right-aligned vertical table: {last row, count, w[T]} per output row
     auto last_of = [&](int y) { return __float_as_int(rtab[min(y, crop_h - 1) * ys]); };
     const int rs = last_of(oy0) - (T - 1);
     const int re = last_of(oy1 - 1);
     int y = oy0;
     int ly = last_of(y);
     Chunk ring[kRing];
-#pragma unroll
-    for (int i = 0; i < kLook; i++) {
-      if constexpr (MODE == 2) ring[i] = Chunk{{(uint32_t)(lane * 7 + i), (uint32_t)(rs * 3), (uint32_t)lane, (uint32_t)(i ^ lane)}};
-      else if constexpr (MODE == 5) ring[i] = load_x4_if(rsrc, fb0 + 16 * lane, min(rs + i, re) * sstride, rs + i <= re);
-      else ring[i] = load_chunk_if<(MODE == 12 || MODE == 13) ? 2 : 0>(rsrc, voff, min(rs + i, re) * sstride, rs + i <= re);
-    }
+    static_for<kLook>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's counted waits assume it
+      ring[i] = load_chunk_if(rsrc, voff, min(rs + i, re) * sstride, rs + i <= re);
+    });
     for (int base = rs; base <= re; base += kRing) {
       static_for<kRing>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -335,30 +347,78 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
         if (r > re) return;
         // keep kLook rows in flight: slot (i + kLook) % kRing is free (its row
         // left the tap window of every open output row)
-        if constexpr (MODE == 2) ring[(i + kLook) % kRing].d[0] = (uint32_t)(r + lane);
-        else if constexpr (MODE == 5)
-          ring[(i + kLook) % kRing] = load_x4_if(rsrc, fb0 + 16 * lane, min(r + kLook, re) * sstride, r + kLook <= re);
-        else ring[(i + kLook) % kRing] = load_chunk_if<(MODE == 12 || MODE == 13) ? 2 : 0>(rsrc, voff, min(r + kLook, re) * sstride, r + kLook <= re);
+        ring[(i + kLook) % kRing] = load_chunk_if(rsrc, voff, min(r + kLook, re) * sstride, r + kLook <= re);
         if (r == ly) {  // output row y ends at source row r (at most one: checked on the host)
           kfloat* we = rtab + y * ys + kTapHeader;
-          float acc[kChunk];
+          f32x2 acc[8];
 #pragma unroll
-          for (int q = 0; q < kChunk; q++) acc[q] = 0.0f;
+          for (int p = 0; p < 8; p++) acc[p] = f32x2{0.0f, 0.0f};
 #pragma unroll
-          for (int k = 0; k < T; k++) {
-            const Chunk& c = ring[(i + kRing - (T - 1) + k) % kRing];
-            if constexpr (MODE == 1 || MODE == 10) {
-#pragma unroll
-              for (int q = 0; q < 4; q++) acc[4 * q] += __uint_as_float(c.d[q] & 0x3fffffffu);
-            } else {
-              fma16(acc, we[k], c);
-            }
-          }
+          for (int k = 0; k < T; k++) fma_chunk(acc, we[k], ring[(i + kRing - (T - 1) + k) % kRing]);
           write_vrow(acc);
           h_store(y);
           ++y;
           ly = y < oy1 ? last_of(y) : 0x7fffffff;
         }
+      });
+    }
+  } else {
+    // ---- scatter: follow the band's schedule (see the top of the file) ----
+    constexpr int R = scatter_ring_slots(DMAX);
+    constexpr int LA = R - 1;  // iterations loaded ahead
+    constexpr int BG = scatter_block_groups(S, DMAX);
+    constexpr int E = scatter_entry_words(S);
+    kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
+    const int ngroups = sched[0];
+    kint* gout = sched + 1;
+    kint* itab = sched + __builtin_amdgcn_readfirstlane(im.group);
+    auto load_it = [&](kint* e, int i) {
+      const int r = e[i * E];
+      if constexpr (MODE == 2) return fake_chunk(lane, r);
+      return load_chunk_if(rsrc, voff, r >= 0 ? r * sstride : 0, r >= 0);
+    };
+    f32x2 acc[S][8];
+#pragma unroll
+    for (int s = 0; s < S; s++)
+#pragma unroll
+      for (int p = 0; p < 8; p++) acc[s][p] = f32x2{0.0f, 0.0f};
+    Chunk ring[R];
+    static_for<LA>([&](auto ic) {
+      __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's counted waits assume it
+      ring[decltype(ic)::value] = load_it(itab, decltype(ic)::value);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    for (int gb = 0; gb < ngroups; gb += BG) {
+      kint* blk = itab + gb * DMAX * E;
+      static_for<BG>([&](auto gc) {
+        constexpr int gi = decltype(gc)::value;
+        static_for<DMAX>([&](auto jc) {
+          constexpr int i = gi * DMAX + decltype(jc)::value;
+          __builtin_amdgcn_sched_barrier(0);  // keep each row's work (and its load) in place
+          // slot (i + LA) % R was consumed by the previous iteration
+          ring[(i + LA) % R] = load_it(blk, i + LA);
+          kint* e = blk + i * E;
+          if (e[0] >= 0) {
+            if constexpr (MODE == 1) {
+              touch_chunk(acc[gi % S], ring[i % R]);
+            } else {
+              f32x2 x[8];
+              chunk_to_f32(ring[i % R], x);
+              static_for<S>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                const float w = __int_as_float(e[1 + k]);
+                if (k == 0 || w != 0.0f) fma_row(acc[(gi + k) % S], w, x);
+              });
+            }
+          }
+        });
+        const int y = gout[gb + gi];
+        if (y >= 0) {
+          write_vrow(acc[gi % S]);
+          h_store(y);
+        }
+#pragma unroll
+        for (int p = 0; p < 8; p++) acc[gi % S][p] = f32x2{0.0f, 0.0f};
       });
     }
   }
@@ -367,53 +427,57 @@ __global__ __launch_bounds__(kWaves* kLanes) void resample_wave(const ImgDev* __
 using WaveKernel = void (*)(const ImgDev*, int, int, int);
 
 template <int C, bool F32, int T>
-WaveKernel select_ct(const WaveCfg& cfg) {
-  if (cfg.ring) {
-    if constexpr (C == 3 && F32 && T == 8) {
-      if (cfg.mode == 1) return resample_wave<C, F32, T, 1, true>;
-      if (cfg.mode == 2) return resample_wave<C, F32, T, 2, true>;
-      if (cfg.mode == 3) return resample_wave<C, F32, T, 3, true>;
-      if (cfg.mode == 5) return resample_wave<C, F32, T, 5, true>;
-      if (cfg.mode == 6) return resample_wave<C, F32, T, 6, true>;
-      if (cfg.mode == 7) return resample_wave<C, F32, T, 7, true>;
-      if (cfg.mode == 8) return resample_wave<C, F32, T, 8, true>;
-      if (cfg.mode == 9) return resample_wave<C, F32, T, 9, true>;
-      if (cfg.mode == 10) return resample_wave<C, F32, T, 10, true>;
-      if (cfg.mode == 11) return resample_wave<C, F32, T, 11, true>;
-      if (cfg.mode == 12) return resample_wave<C, F32, T, 12, true>;
-      if (cfg.mode == 13) return resample_wave<C, F32, T, 13, true>;
-      if (cfg.mode == 14) return resample_wave<C, F32, T, 14, true>;
-    }
-    return resample_wave<C, F32, T, 0, true>;
-  }
-  if constexpr (C == 3 && F32 && T == 8) {
-    if (cfg.mode == 1) return resample_wave<C, F32, T, 1>;
-    if (cfg.mode == 2) return resample_wave<C, F32, T, 2>;
-    if (cfg.mode == 3) return resample_wave<C, F32, T, 3>;
-    if (cfg.mode == 4) return resample_wave<C, F32, T, 4>;
-  }
-  return resample_wave<C, F32, T, 0>;
+WaveKernel select_gr(const WaveCfg& cfg) {
+  if (cfg.kind == kRing) return resample_wave<C, F32, T, kRing, 1, 1, 0>;
+  return resample_wave<C, F32, T, kGather, 1, 1, 0>;
 }
 
 template <int C, bool F32>
 WaveKernel select_c(const WaveCfg& cfg) {
   switch (cfg.taps) {
-    case 2: return select_ct<C, F32, 2>(cfg);
-    case 3: return select_ct<C, F32, 3>(cfg);
-    case 4: return select_ct<C, F32, 4>(cfg);
-    case 5: return select_ct<C, F32, 5>(cfg);
-    case 6: return select_ct<C, F32, 6>(cfg);
-    case 8: return select_ct<C, F32, 8>(cfg);
-    case 9: return select_ct<C, F32, 9>(cfg);
-    case 10: return select_ct<C, F32, 10>(cfg);
-    case 12: return select_ct<C, F32, 12>(cfg);
-    case 14: return select_ct<C, F32, 14>(cfg);
-    case 17: return select_ct<C, F32, 17>(cfg);
+    case 2: return select_gr<C, F32, 2>(cfg);
+    case 3: return select_gr<C, F32, 3>(cfg);
+    case 4: return select_gr<C, F32, 4>(cfg);
+    case 5: return select_gr<C, F32, 5>(cfg);
+    case 6: return select_gr<C, F32, 6>(cfg);
+    case 8: return select_gr<C, F32, 8>(cfg);
+    case 9: return select_gr<C, F32, 9>(cfg);
+    case 10: return select_gr<C, F32, 10>(cfg);
+    case 12: return select_gr<C, F32, 12>(cfg);
+    case 14: return select_gr<C, F32, 14>(cfg);
+    case 17: return select_gr<C, F32, 17>(cfg);
     default: return nullptr;
   }
 }
 
+// Scatter kernels exist for RGB and the (S, DMAX, horizontal taps) shapes of
+// resize_smallest_side 256/512 from 200p..4K sources.
+template <bool F32>
+WaveKernel select_scatter(const WaveCfg& cfg) {
+  if (cfg.channels != 3) return nullptr;
+#define MXD_SCATTER(S_, D_, T_) \
+  if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_) return resample_wave<3, F32, T_, kScatter, S_, D_, 0>;
+  if (cfg.s == 2 && cfg.dmax == 4 && cfg.taps == 8) {  // C2 (960 -> 256): ablation builds
+    if (cfg.mode == 1) return resample_wave<3, F32, 8, kScatter, 2, 4, 1>;
+    if (cfg.mode == 2) return resample_wave<3, F32, 8, kScatter, 2, 4, 2>;
+    if (cfg.mode == 9) return resample_wave<3, F32, 8, kScatter, 2, 4, 9>;
+  }
+  // Downsampling by the tent filter reaches each source row from at most two
+  // output rows (S = 2); DMAX = ceil(in / out).
+  MXD_SCATTER(2, 4, 8)   // 960 -> 256
+  MXD_SCATTER(2, 5, 9)   // 1080 -> 256, 2160 -> 512
+  MXD_SCATTER(2, 6, 12)  // 1440 -> 256
+  MXD_SCATTER(2, 9, 17)  // 2160 -> 256
+  MXD_SCATTER(2, 3, 6)   // 720 -> 256
+  MXD_SCATTER(2, 2, 4)   // 480 -> 256
+  MXD_SCATTER(2, 2, 3)   // 375 / 333 -> 256
+  MXD_SCATTER(3, 1, 2)   // upsampling (200 -> 256)
+#undef MXD_SCATTER
+  return nullptr;
+}
+
 WaveKernel select_kernel(const WaveCfg& cfg) {
+  if (cfg.kind == kScatter) return cfg.f32 ? select_scatter<true>(cfg) : select_scatter<false>(cfg);
   switch (cfg.channels * 2 + (cfg.f32 ? 1 : 0)) {
     case 2: return select_c<1, false>(cfg);
     case 3: return select_c<1, true>(cfg);
@@ -441,6 +505,8 @@ int wave_row_floats(int taps, int channels) { return (kRowBytes + taps * channel
 int wave_row_bytes() { return kRowBytes; }
 
 int wave_max_outputs() { return kLanes * kOutPerLane; }
+
+bool wave_has_kernel(const WaveCfg& cfg) { return select_kernel(cfg) != nullptr; }
 
 // Streaming copy (16 B per lane, grid-stride): the measured HBM ceiling that
 // bench.py reports next to the spec peak.
