@@ -264,7 +264,7 @@ struct ImgPlan {
   const DevTable* xt = nullptr;
   const DevTable* yt = nullptr;
   int32_t bucket = -1;   // wave path tap bucket, -1 = not eligible
-  int32_t kind = 0;      // wave kernel: 0 gather, 1 register ring, 2 scatter
+  int32_t kind = 0;      // wave kernel: 0 gather, 1 register ring, 2 scatter, 3 band
   int32_t s = 0, dmax = 0, p = 0;  // scatter shape (ScatterShape)
   const DevTable* yr = nullptr;    // ring: right-aligned vertical table
   int32_t nstrips = 0, tx = 0;
@@ -372,25 +372,27 @@ class SchedCache {
       w[0] = (P + n + bg - 1) / bg * bg;
       for (int32_t g = 0; g < gmax; g++) w[1 + g] = g >= P && g - P < n ? y0 + g - P : -1;
       int32_t* ent = w + gwords;
-      for (int32_t i = 0; i < iters; i++) ent[i * E] = -1;
+      for (int32_t i = 0; i < iters; i++) ent[i * E] = ent[i * E + 1] = -1;
       std::vector<int32_t> fill(gmax, 0);
       bool ok = true;
       auto add_row = [&](int32_t g, int32_t r) {
         if (g < 0 || g >= gmax || fill[g] >= D) return void(ok = false);
         int32_t* e = ent + (size_t)(g * D + fill[g]++) * E;
-        e[0] = r;
+        e[1] = r;
         for (int32_t u = 0; u < n; u++) {
           if (r < first(y0 + u) || r > last(y0 + u)) continue;
           const int32_t k = P + u - g;
           if (k < 0 || k >= S) return void(ok = false);
           const float wt = yt.w[(size_t)(crop_y + y0 + u) * yt.width + (r - first(y0 + u))];
-          std::memcpy(&e[1 + k], &wt, sizeof(float));
+          std::memcpy(&e[2 + k], &wt, sizeof(float));
         }
       };
       for (int32_t r = first(y0); r <= last(y0); r++) add_row(P - (last(y0) - r) / D, r);
       for (int32_t u = 1; u < n; u++)
         for (int32_t r = last(y0 + u - 1) + 1; r <= last(y0 + u); r++) add_row(P + u, r);
       if (!ok) return false;
+      // word 0 of iteration i: the row iteration i + la loads into the ring
+      for (int32_t i = 0; i + la < iters; i++) ent[i * E] = ent[(i + la) * E + 1];
     }
     return true;
   }
@@ -514,8 +516,12 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     wave_ok = wave_ok && (a & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
               images[i].src_stride * images[i].src_h < ((int64_t)1 << 31);
   }
-  static const int no_ring = env_int("MXD_NO_RING");
-  static const int no_scatter = env_int("MXD_NO_SCATTER");
+  // Kernel-kind switches (tuning, tests) are read on every call.
+  const int no_ring = env_int("MXD_NO_RING");
+  const int no_scatter = env_int("MXD_NO_SCATTER");
+  // Band workgroups are opt-in (MXD_BAND=1): measured 261 us vs 162 us for
+  // plain scatter waves on C2 -- the one H/store wave per workgroup serializes.
+  const int no_band = !env_int("MXD_BAND") || env_int("MXD_NO_BAND");
   static const int ablate = env_int("MXD_WAVE_ABLATE");
   const int32_t f32 = out_dtype == MXD_F32_DIV255 ? 1 : 0;
   std::vector<ImgPlan> plans(n);
@@ -539,6 +545,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       p.s = sh.s;
       p.dmax = sh.dmax;
       p.p = sh.p;
+      // Band workgroups (scatter V waves + one H/store wave) when the crop's
+      // strips fit one workgroup and the shape has a band kernel.
+      if (!no_band && p.nstrips <= mxd::wave_band_strips() &&
+          mxd::wave_has_kernel(mxd::WaveCfg{channels, f32, xb, 0, 0, ablate, 3, sh.s, sh.dmax}))
+        p.kind = 3;
     } else if (!no_ring && p.bucket <= 12 && one_output_per_row(*p.yt, im.crop_y, im.crop_h)) {
       p.kind = 1;
       if (int rc = right_tables().get(device, *p.yt, im.src_h, im.resize_h, p.bucket, &p.yr)) return rc;
@@ -587,7 +598,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       g.cfg.nimgs = g.count;
       std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
       for (int32_t k = g.first; k < g.first + g.count; k++)
-        strips.push_back({plans[order[k]].nstrips, images[order[k]].crop_h});
+        strips.push_back({g.cfg.kind == 3 ? 1 : plans[order[k]].nstrips, images[order[k]].crop_h});
       g.ty = band_rows(strips, wave_capacity_cached(g.cfg, device));
       for (int32_t k = g.first; k < g.first + g.count; k++) {
         const int32_t i = order[k];
@@ -599,7 +610,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         if (p.kind == 1) {
           d.ywidth = p.yr->padded;
           d.ytab = p.yr->ptr + (size_t)im.crop_y * (mxd::kTapHeader + p.yr->padded);
-        } else if (p.kind == 2) {
+        } else if (p.kind == 2 || p.kind == 3) {
           const DevSched* sc = nullptr;
           if (int rc = schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
                                        ScatterShape{p.s, p.dmax, p.p}, &sc))
@@ -611,8 +622,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         d.tile_begin = g.units;
         d.nstrips = p.nstrips;
         d.tx = p.tx;
-        if (p.kind != 2) d.group = 1;
-        g.units += d.nstrips * ((im.crop_h + d.ty - 1) / d.ty);
+        if (p.kind < 2) d.group = 1;
+        g.units += (p.kind == 3 ? 1 : d.nstrips) * ((im.crop_h + d.ty - 1) / d.ty);
       }
       g.cfg.nunits = g.units;
     }

@@ -65,12 +65,13 @@ constexpr int scatter_ring_slots(int dmax) { return 12 % dmax == 0 ? 12 : (2 * d
 constexpr int scatter_block_groups(int s, int dmax) {
   return scatter_ring_slots(dmax) / scatter_gcd(scatter_ring_slots(dmax), s * dmax) * s;
 }
-constexpr int scatter_entry_words(int s) { return s <= 3 ? 4 : 8; }
+constexpr int scatter_entry_words(int s) { return s <= 2 ? 4 : 8; }  // prefetch row, row, s weights
 
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
 int wave_row_floats(int taps, int channels);
 int wave_row_bytes();
 int wave_max_outputs();  // output elements per strip row (4 per lane)
+int wave_band_strips();  // strips one band workgroup (kind 3) covers
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
 bool wave_has_kernel(const WaveCfg& cfg);
 // Waves of this configuration the device runs at once (occupancy x CUs), 0 if unknown.

@@ -16,7 +16,10 @@ from collections import defaultdict
 
 tag, out = sys.argv[1], sys.argv[2]
 kern = sys.argv[3] if len(sys.argv) > 3 else "resample_wave"
-vals = defaultdict(list)
+# Per kernel (name) the average over its dispatches, then the sum over the
+# kernels: a batch of mixed sizes runs one launch per kernel shape, so a
+# "launch" of the bench (one batch) is one dispatch of each kernel.
+vals = defaultdict(lambda: defaultdict(list))
 names = set()
 for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/run_counter_collection.csv")):
     per = defaultdict(float)
@@ -24,15 +27,15 @@ for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/run_counter_collection.csv")):
         if kern not in row["Kernel_Name"]:
             continue
         names.add(row["Kernel_Name"])
-        per[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
-    for (d, c), v in per.items():
-        vals[c].append(v)
-avg = {c: sum(v) / len(v) for c, v in vals.items()}
+        per[(row["Kernel_Name"], row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+    for (k, d, c), v in per.items():
+        vals[c][k].append(v)
+avg = {c: sum(sum(v) / len(v) for v in ks.values()) for c, ks in vals.items()}
 res = {
     "tag": tag,
     "kernels": sorted(names),
-    "dispatches": {c: len(v) for c, v in vals.items()},
-    "counters_avg_per_dispatch": avg,
+    "dispatches": {c: sum(len(v) for v in ks.values()) for c, ks in vals.items()},
+    "counters_per_launch": avg,
 }
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     rd = avg["FETCH_SIZE"] * 1024 * 2
