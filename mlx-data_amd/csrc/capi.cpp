@@ -424,8 +424,9 @@ bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int3
       const int32_t xb = im.flip ? im.crop_w - 1 - ox0 : ox1 - 1;
       const int32_t lo = xt.first[im.crop_x + xa];
       const int32_t hi = xt.first[im.crop_x + xb] + xt.count[im.crop_x + xb] - 1;
-      const int32_t fb0 = (lo * c) & ~3;
-      ok = (hi + 1) * c - fb0 <= row;
+      const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(im.src) & 3);
+      const int32_t fb0 = (lo * c + shift) & ~3;
+      ok = (hi + 1) * c + shift - fb0 <= row;
     }
     if (ok) {
       *nstrips = (im.crop_w + t - 1) / t;
@@ -513,7 +514,12 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
     aligned16 = aligned16 && (a & 15) == 0;
     const uintptr_t o = reinterpret_cast<uintptr_t>(images[i].dst) | (uintptr_t)images[i].dst_stride;
-    wave_ok = wave_ok && (a & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
+    // The wave path reads through the 4-byte aligned address below `src` and
+    // shifts its column bytes by the remainder (a source window at any x,
+    // e.g. random_area_crop); rows must stay 4-byte aligned.
+    wave_ok = wave_ok && (images[i].src_stride & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
+              (int64_t)(reinterpret_cast<uintptr_t>(images[i].src) & 3) + (int64_t)images[i].src_w * channels <=
+                  images[i].src_stride &&
               images[i].src_stride * images[i].src_h < ((int64_t)1 << 31);
   }
   // Kernel-kind switches (tuning, tests) are read on every call.
@@ -571,6 +577,12 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     d.crop_h = im.crop_h;
     d.flip = im.flip ? 1 : 0;
   };
+  // Wave path: aligned base + byte shift (ImgDev::flip bits 8..).
+  auto align_src = [](ImgDev& d) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d.src);
+    d.src = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
+    d.flip |= (int32_t)(a & 3) << 8;
+  };
 
   if (wave_ok) {
     // One launch per kernel (kind, tap bucket, scatter shape); descriptors of
@@ -606,6 +618,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         const ImgPlan& p = plans[i];
         ImgDev& d = descs[k];
         fill(d, im, p);
+        align_src(d);
         d.ty = std::min(g.ty, im.crop_h);
         if (p.kind == 1) {
           d.ywidth = p.yr->padded;

@@ -315,6 +315,67 @@ std::shared_ptr<Array> ImageRandomHFlip::apply_image(const std::shared_ptr<Array
   return img;
 }
 
+// op/ImageTransform.cpp:184-212 (constructor checks, same messages)
+ImageRandomAreaCrop::ImageRandomAreaCrop(std::string ikey, std::pair<float, float> area_range,
+                                         std::pair<float, float> aspect_ratio_range, int num_trial, std::string okey)
+    : ImageOp(std::move(ikey), std::move(okey)), area_(area_range), aspect_(aspect_ratio_range), trials_(num_trial) {
+  const char* bad = nullptr;
+  if (area_.first <= 0 || area_.first > area_.second || area_.second > 1.0)
+    bad = "ImageRandomAreaCrop: invalid area range";
+  else if (aspect_.first <= 0 || aspect_.first > aspect_.second)
+    bad = "ImageRandomAreaCrop: invalid aspect ratio range";
+  else if (area_.first * aspect_.first > 1 || area_.first > aspect_.second)
+    bad = "ImageRandomAreaCrop: provided area range and aspect ratio range cannot be fullfilled";
+  else if (trials_ <= 0)
+    bad = "ImageRandomAreaCrop: number of trial must be positive";
+  if (bad) throw std::runtime_error(bad);
+}
+
+// op/ImageTransform.cpp:214-280 (generate_random_crop_).  The arithmetic keeps
+// the reference's types step for step -- float ranges times float image sizes,
+// int64 draws from std::uniform_int_distribution on the thread's mt19937 --
+// so the draws and the accept/reject decisions are the same.  Order of draws:
+// per trial a width, then (if its height range is non-empty) a height; after
+// the trials x, then y.
+std::array<int64_t, 4> ImageRandomAreaCrop::draw(int64_t w, int64_t h) const {
+  const std::array<int64_t, 4> none{0, 0, 0, 0};
+  if (w == 0 || h == 0) return none;
+  const float fw = static_cast<float>(w), fh = static_cast<float>(h);
+  const float ratio = fw / fh;
+  auto st = get_state();
+  const int64_t lo_w = std::ceil(std::sqrt(area_.first * aspect_.first) * fw);
+  const int64_t hi_w = std::floor(std::min(std::sqrt(area_.second * aspect_.second) * fw, fw));
+  if (lo_w > hi_w) return none;
+  std::uniform_int_distribution<int64_t> wdist{lo_w, hi_w};
+  int64_t cw = 0, ch = 0;
+  for (int t = 0; t < trials_; t++) {
+    cw = wdist(st->gen);
+    const float h_by_aspect_lo = 1.0f / (ratio * aspect_.second) * cw;
+    const float h_by_aspect_hi = 1.0f / (ratio * aspect_.first) * cw;
+    const float h_by_area_lo = area_.first * fw * fh / cw;
+    const float h_by_area_hi = area_.second * fw * fh / cw;
+    const int64_t lo_h = std::ceil(std::max(h_by_aspect_lo, h_by_area_lo));
+    const int64_t hi_h = std::floor(std::min(std::min(h_by_aspect_hi, h_by_area_hi), fh));
+    if (lo_h > hi_h) continue;
+    ch = std::uniform_int_distribution<int64_t>{lo_h, hi_h}(st->gen);
+    const float crop_ratio = static_cast<float>(cw) / static_cast<float>(ch);
+    const bool area_ok = !(area_.first * w * h > cw * ch) && !(area_.second * w * h < cw * ch);
+    const bool aspect_ok = !(aspect_.first * ratio > crop_ratio) && !(aspect_.second * ratio < crop_ratio);
+    if (area_ok && aspect_ok && cw > 0 && cw <= w && ch > 0 && ch <= h) break;
+  }
+  if (cw == 0 || ch == 0) return none;
+  const int64_t x = std::uniform_int_distribution<int64_t>{0, w - cw}(st->gen);
+  const int64_t y = std::uniform_int_distribution<int64_t>{0, h - ch}(st->gen);
+  return {x, y, cw, ch};
+}
+
+// op/ImageTransform.cpp:282-291
+std::shared_ptr<Array> ImageRandomAreaCrop::apply_image(const std::shared_ptr<Array>& img) const {
+  const auto c = draw(img->shape(1), img->shape(0));
+  if (c[2] == 0 || c[3] == 0) return img;
+  return plan_crop(img, c[0], c[1], c[2], c[3]);
+}
+
 // ------------------------------------------------------------------ load
 namespace {
 std::mutex g_dec_mu;

@@ -16,6 +16,7 @@
 //   merge_batch           mlx/data/core/Utils.cpp:209-252, BatchShape.cpp:26-66
 #pragma once
 
+#include <array>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -176,6 +177,22 @@ class ImageRandomHFlip : public ImageOp {
 
  private:
   float prob_;
+};
+
+// op/ImageTransform.h ImageRandomAreaCrop: a crop whose area and aspect ratio
+// are drawn by rejection sampling (Inception-style); the image unchanged when
+// no trial meets the constraints.
+class ImageRandomAreaCrop : public ImageOp {
+ public:
+  ImageRandomAreaCrop(std::string ikey, std::pair<float, float> area_range, std::pair<float, float> aspect_ratio_range,
+                      int num_trial, std::string okey);
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+  // (x, y, w, h) of the crop for a w x h image, all 0 when none was found.
+  std::array<int64_t, 4> draw(int64_t w, int64_t h) const;
+
+ private:
+  std::pair<float, float> area_, aspect_;
+  int trials_;
 };
 
 // Decoder hook: (path or encoded bytes, from_memory) -> (H, W, 3) uint8, or

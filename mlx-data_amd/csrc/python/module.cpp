@@ -204,7 +204,16 @@ void dataset_ops(py::class_<D, std::shared_ptr<D>>& cls, Wrap wrap) {
           [wrap](const Self& self, const std::string& key, float prob, const std::string& output_key) {
             return wrap(self, std::make_shared<ImageRandomHFlip>(key, prob, output_key));
           },
-          py::arg("key"), py::arg("prob"), py::arg("output_key") = "");
+          py::arg("key"), py::arg("prob"), py::arg("output_key") = "")
+      .def(
+          "image_random_area_crop",
+          [wrap](const Self& self, const std::string& key, std::pair<float, float> area_range,
+                 std::pair<float, float> aspect_ratio_range, int num_trial, const std::string& output_key) {
+            return wrap(self, std::make_shared<ImageRandomAreaCrop>(key, area_range, aspect_ratio_range, num_trial,
+                                                                    output_key));
+          },
+          py::arg("key"), py::arg("area_range"), py::arg("aspect_ratio_range"), py::arg("num_trial") = 10,
+          py::arg("output_key") = "");
 }
 
 using PadMap = std::unordered_map<std::string, double>;

@@ -25,7 +25,8 @@ struct ImgDev {
   const float* xtab;  // crop_w entries of (kTapHeader + xwidth) floats
   int32_t ywidth, xwidth;
   int32_t crop_w, crop_h;
-  int32_t flip;
+  int32_t flip;  // bit 0: mirror; wave path: bits 8.. = byte offset of the
+                 // source window past the 4-byte aligned `src` (0..3)
   int32_t tile_begin;
   int32_t nstrips, ty, tx, group;
   int32_t src_w, src_h;

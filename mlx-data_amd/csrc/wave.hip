@@ -219,14 +219,14 @@ __device__ __forceinline__ const ImgDev& find_image(const ImgDev* imgs, int nimg
 // Source footprint of output columns [ox0, ox1) (taps are monotone in the crop
 // column): first byte fb0 (4-byte aligned) and byte count (<= kRowBytes).
 template <int C>
-__device__ __forceinline__ void strip_footprint(cgfloat* xtab, int xs, int crop_w, int flip, int ox0, int ox1,
-                                                int* fb0, int* need) {
+__device__ __forceinline__ void strip_footprint(cgfloat* xtab, int xs, int crop_w, int flip, int shift, int ox0,
+                                                int ox1, int* fb0, int* need) {
   const int xa = flip ? crop_w - ox1 : ox0;
   const int xb = flip ? crop_w - 1 - ox0 : ox1 - 1;
   const int px_lo = __float_as_int(xtab[xa * xs]);
   const int px_hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
-  *fb0 = (px_lo * C) & ~3;
-  *need = (px_hi + 1) * C - *fb0;
+  *fb0 = (px_lo * C + shift) & ~3;
+  *need = (px_hi + 1) * C + shift - *fb0;
 }
 
 // Per-lane byte offsets of the strip window: only the dwords that hold
@@ -244,8 +244,8 @@ struct HStrip {
   int pos[kOutPerLane];
   int ox0, nout;
 
-  __device__ __forceinline__ void init(cgfloat* xtab, int xs, int crop_w, int flip, int ox0_, int ox1, int fb0,
-                                       int lane) {
+  __device__ __forceinline__ void init(cgfloat* xtab, int xs, int crop_w, int flip, int shift, int ox0_, int ox1,
+                                       int fb0, int lane) {
     ox0 = ox0_;
     nout = (ox1 - ox0) * C;
 #pragma unroll
@@ -256,7 +256,7 @@ struct HStrip {
       const int ox = ox0 + px;
       const int xc = flip ? crop_w - 1 - ox : ox;
       cgfloat* xe = xtab + xc * xs;
-      pos[j] = __float_as_int(xe[0]) * C - fb0 + c;
+      pos[j] = __float_as_int(xe[0]) * C + shift - fb0 + c;
 #pragma unroll
       for (int k = 0; k < T; k++) wx[j >> 1][k][j & 1] = xe[kTapHeader + k];  // zero padded past the tap count
     }
@@ -372,7 +372,8 @@ __global__ __launch_bounds__(kWaves* kLanes, KIND == kScatter && T <= 12 ? 3 : 1
   const int nstrips = __builtin_amdgcn_readfirstlane(im.nstrips);
   const int crop_w = __builtin_amdgcn_readfirstlane(im.crop_w);
   const int crop_h = __builtin_amdgcn_readfirstlane(im.crop_h);
-  const int flip = __builtin_amdgcn_readfirstlane(im.flip);
+  const int flip_shift = __builtin_amdgcn_readfirstlane(im.flip);
+  const int flip = flip_shift & 1, shift = flip_shift >> 8;  // see ImgDev::flip
   const int band_rows = __builtin_amdgcn_readfirstlane(im.ty);
   const int strip_cols = __builtin_amdgcn_readfirstlane(im.tx);
   const int xs = kTapHeader + __builtin_amdgcn_readfirstlane(im.xwidth);
@@ -392,13 +393,13 @@ __global__ __launch_bounds__(kWaves* kLanes, KIND == kScatter && T <= 12 ? 3 : 1
   const int ox1 = min(ox0 + strip_cols, crop_w);
 
   int fb0, need;
-  strip_footprint<C>(xtab, xs, crop_w, flip, ox0, ox1, &fb0, &need);
+  strip_footprint<C>(xtab, xs, crop_w, flip, shift, ox0, ox1, &fb0, &need);
   const Src src = make_src(im);
   int voff[4];
   window_offsets(fb0, need, lane, voff);
 
   HStrip<C, F32, T> hs;
-  hs.init(xtab, xs, crop_w, flip, ox0, ox1, fb0, lane);
+  hs.init(xtab, xs, crop_w, flip, shift, ox0, ox1, fb0, lane);
   // The horizontal weights are loaded once; retire them here so the waits the
   // compiler places in the row loop only ever cover the row loads.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -518,7 +519,8 @@ __global__ __launch_bounds__(kWaves* kLanes, 4) void resample_band(const ImgDev*
   const ImgDev& im = find_image(imgs, nimgs, unit);
   const int nstrips = __builtin_amdgcn_readfirstlane(im.nstrips);
   const int crop_w = __builtin_amdgcn_readfirstlane(im.crop_w);
-  const int flip = __builtin_amdgcn_readfirstlane(im.flip);
+  const int flip_shift = __builtin_amdgcn_readfirstlane(im.flip);
+  const int flip = flip_shift & 1, shift = flip_shift >> 8;  // see ImgDev::flip
   const int strip_cols = __builtin_amdgcn_readfirstlane(im.tx);
   const int xs = kTapHeader + __builtin_amdgcn_readfirstlane(im.xwidth);
   cgfloat* xtab = GLOBAL_PTR(const float, im.xtab);
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(kWaves* kLanes, 4) void resample_band(const ImgDev*
     // ---- vertical wave of strip `wave` ----
     int fb0 = 0, need = 0;  // a wave without a strip loads nothing
     if (wave < nstrips)
-      strip_footprint<C>(xtab, xs, crop_w, flip, wave * strip_cols, min((wave + 1) * strip_cols, crop_w), &fb0, &need);
+      strip_footprint<C>(xtab, xs, crop_w, flip, shift, wave * strip_cols, min((wave + 1) * strip_cols, crop_w), &fb0, &need);
     const Src src = make_src(im);
     int voff[4];
     window_offsets(fb0, need, lane, voff);
@@ -549,8 +551,8 @@ __global__ __launch_bounds__(kWaves* kLanes, 4) void resample_band(const ImgDev*
       if (s < nstrips) {
         const int ox0 = s * strip_cols, ox1 = min(ox0 + strip_cols, crop_w);
         int fb0, need;
-        strip_footprint<C>(xtab, xs, crop_w, flip, ox0, ox1, &fb0, &need);
-        hs[s].init(xtab, xs, crop_w, flip, ox0, ox1, fb0, lane);
+        strip_footprint<C>(xtab, xs, crop_w, flip, shift, ox0, ox1, &fb0, &need);
+        hs[s].init(xtab, xs, crop_w, flip, shift, ox0, ox1, fb0, lane);
       }
     });
     const int ngroups = sched[0];

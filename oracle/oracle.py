@@ -172,3 +172,17 @@ def ref_random_crop_flip(seed, sizes_wh, cw, ch, prob):
         _ptr(xy, _i64p), _ptr(fl, _i32p)
     )
     return xy.reshape(n, 2), fl
+
+
+def ref_random_area_crop(seed, sizes_wh, area_range, aspect_range, trials=10):
+    """Per-sample (x, y, w, h) draws of image_random_area_crop after set_state(seed)
+    (zeros: no crop found), from the reference's State (oracle/ref_harness.cpp)."""
+    R = ref_lib()
+    wh = np.ascontiguousarray(np.asarray(sizes_wh, np.int64).reshape(-1))
+    n = len(wh) // 2
+    out = np.zeros(4 * n, np.int64)
+    R.ref_random_area_crop_params(
+        ctypes.c_int64(seed), n, _ptr(wh, _i64p), ctypes.c_float(area_range[0]), ctypes.c_float(area_range[1]),
+        ctypes.c_float(aspect_range[0]), ctypes.c_float(aspect_range[1]), int(trials), _ptr(out, _i64p)
+    )
+    return out.reshape(n, 4)

@@ -14,6 +14,8 @@
 //                  (:323-332), in the per-sample order a pipeline applies them.
 // core/image/ImageTransform.cpp itself (resize/hflip) needs stb_image_resize2.h,
 // which this image lacks, so it is not built.
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <random>
@@ -75,6 +77,47 @@ void ref_random_crop_flip_params(int64_t seed, int n, const int64_t* wh, int64_t
     out_xy[2 * i + 1] = yu(state->randomGenerator);
     std::uniform_real_distribution<float> u{0, 1.0};
     out_flip[i] = u(state->randomGenerator) <= prob ? 1 : 0;
+  }
+}
+
+// Per sample, the draws of ImageRandomAreaCrop::generate_random_crop_
+// (op/ImageTransform.cpp:214-280) after set_state(seed), restated on the
+// reference's own State: out[4i..4i+3] = (x, y, w, h), zeros when none.
+void ref_random_area_crop_params(int64_t seed, int n, const int64_t* wh, float a0, float a1, float r0, float r1,
+                                 int trials, int64_t* out) {
+  mlx::data::core::set_state(seed);
+  for (int i = 0; i < n; i++) {
+    const int64_t w = wh[2 * i], h = wh[2 * i + 1];
+    int64_t* o = out + 4 * i;
+    o[0] = o[1] = o[2] = o[3] = 0;
+    if (w == 0 || h == 0) continue;
+    const float wf = (float)w, hf = (float)h, r = wf / hf;
+    auto state = mlx::data::core::get_state();
+    int64_t wmin = std::ceil(std::sqrt(a0 * r0) * wf);
+    int64_t wmax = std::floor(std::min(std::sqrt(a1 * r1) * wf, wf));
+    if (wmin > wmax) continue;
+    std::uniform_int_distribution<int64_t> wu{wmin, wmax};
+    int64_t tw = 0, th = 0;
+    for (int t = 0; t < trials; t++) {
+      tw = wu(state->randomGenerator);
+      int64_t hmin = std::ceil(std::max(1.0f / (r * r1) * tw, a0 * wf * hf / tw));
+      int64_t hmax = std::floor(std::min(std::min(1.0f / (r * r0) * tw, a1 * wf * hf / tw), hf));
+      if (hmin > hmax) continue;
+      std::uniform_int_distribution<int64_t> hu{hmin, hmax};
+      th = hu(state->randomGenerator);
+      float tr = (float)tw / (float)th;
+      if (a0 * w * h > tw * th || a1 * w * h < tw * th) continue;
+      if (r0 * r > tr || r1 * r < tr) continue;
+      if (tw <= 0 || tw > w || th <= 0 || th > h) continue;
+      break;
+    }
+    if (tw == 0 || th == 0) continue;
+    std::uniform_int_distribution<int64_t> xu{0, w - tw};
+    std::uniform_int_distribution<int64_t> yu{0, h - th};
+    o[0] = xu(state->randomGenerator);
+    o[1] = yu(state->randomGenerator);
+    o[2] = tw;
+    o[3] = th;
   }
 }
 

@@ -1,9 +1,9 @@
 """GPU: the wave-kernel kinds of mlx-data_amd/csrc/wave.hip -- band workgroups,
 scatter, register ring, gather -- give bit-identical outputs on the same inputs
 (each sums an output row's taps in the same order from 0), and the default
-choice matches the oracle (+-1 per channel, < 0.2 % of channels differing).
-The kind is forced through MXD_NO_BAND / MXD_NO_SCATTER / MXD_NO_RING, which
-the C ABI reads on every call."""
+choice (scatter) matches the oracle (+-1 per channel, < 0.2 % of channels
+differing).  The kind is chosen through MXD_BAND (opt-in) / MXD_NO_SCATTER /
+MXD_NO_RING, which the C ABI reads on every call."""
 import numpy as np
 import pytest
 
@@ -12,12 +12,12 @@ from gpu_util import center_geom, compare, oracle_out, run_device, synth
 
 pytestmark = pytest.mark.gpu
 
-SWITCHES = ("MXD_NO_BAND", "MXD_NO_SCATTER", "MXD_NO_RING")
+SWITCHES = ("MXD_BAND", "MXD_NO_BAND", "MXD_NO_SCATTER", "MXD_NO_RING")
 KINDS = [
-    ("default", ()),
-    ("scatter", ("MXD_NO_BAND",)),
-    ("ring", ("MXD_NO_BAND", "MXD_NO_SCATTER")),
-    ("gather", SWITCHES),
+    ("band", {"MXD_BAND": "1"}),
+    ("default", {}),
+    ("ring", {"MXD_NO_SCATTER": "1"}),
+    ("gather", {"MXD_NO_SCATTER": "1", "MXD_NO_RING": "1"}),
 ]
 
 
@@ -43,10 +43,10 @@ CASES = {"c2": c2, "mixed": mixed, "c5": c5}
 
 def run_kinds(monkeypatch, imgs, geoms, f32):
     outs = {}
-    for name, off in KINDS:
+    for name, env in KINDS:
         for k in SWITCHES:
-            if k in off:
-                monkeypatch.setenv(k, "1")
+            if k in env:
+                monkeypatch.setenv(k, env[k])
             else:
                 monkeypatch.delenv(k, raising=False)
         outs[name] = run_device(imgs, geoms, f32=f32)

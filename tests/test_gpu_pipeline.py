@@ -174,3 +174,32 @@ def test_prefetch_threads_share_devices():
             check(x["image"][k], oracle_center(imgs[i]))
             n += 1
     assert n == 32
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_random_area_crop_resize(flip):
+    """Inception-style train augmentation:
+    image_random_area_crop((0.08, 1), (3/4, 4/3)) -> image_resize(224, 224)
+    [-> random_h_flip(1.0)] -> batch.  The crop is the resize's source window
+    at any x (byte-shifted wave path), checked against the oracle resize of
+    the numpy crop."""
+    from mlx_data_amd import _pipeline as P
+
+    sizes = [(960, 1280), (375, 500), (500, 333), (1080, 1920), (2160, 3840), (300, 200), (720, 1280), (481, 641)]
+    imgs = [synth(h, w, 3, 40 + i) for i, (h, w) in enumerate(sizes)]
+    b = dx.buffer_from_vector([dict(image=im) for im in imgs])
+    t = b.image_random_area_crop("image", (0.08, 1.0), (0.75, 4 / 3)).image_resize("image", 224, 224)
+    if flip:
+        t = t.image_random_h_flip("image", 1.0)
+    dx.set_state(99)
+    plans = [P._plan(t, i, "image") for i in range(len(imgs))]
+    dx.set_state(99)
+    got = [s for s in t.batch(len(imgs))][0]["image"]
+    assert got.shape == (len(imgs), 224, 224, 3)
+    shifted = 0
+    for k, (im, p) in enumerate(zip(imgs, plans)):
+        x, y, w, h = p["window"]
+        shifted += (x * 3) % 4 != 0
+        ref = O.resize(np.ascontiguousarray(im[y:y + h, x:x + w]), 224, 224)
+        check(got[k], ref[:, ::-1] if flip else ref)
+    assert shifted > 0  # some windows start off a 4-byte boundary

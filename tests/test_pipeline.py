@@ -230,3 +230,56 @@ def test_load_image(tmp_path):
         dx.buffer_from_vector([dict(f=b"missing.jpg")]).load_image("f", prefix=str(tmp_path))[0]
     with pytest.raises(RuntimeError, match=r"char array \(int8\) expected"):
         dx.buffer_from_vector([dict(f=np.zeros(3, np.uint8))]).load_image("f")[0]
+
+
+AREA = np.load(os.path.join(os.path.dirname(__file__), "golden", "rng_area.npz"))
+AREA_CASES = sorted({int(k.split("_")[1]) for k in AREA.files})
+
+
+@pytest.mark.parametrize("case", AREA_CASES)
+def test_random_area_crop_draws_match_reference(case):
+    """image_random_area_crop (op/ImageTransform.cpp:214-291) after set_state:
+    the crop windows equal the reference State's draws (golden rng_area.npz);
+    where no crop was found the image passes unchanged."""
+    seed, trials, a0, a1, r0, r1 = AREA[f"area_{case}_in"]
+    wh = AREA[f"area_{case}_wh"]
+    ref = AREA[f"area_{case}_out"]
+    b = dx.buffer_from_vector([dict(image=np.zeros((h, w, 3), np.uint8)) for w, h in wh])
+    t = b.image_random_area_crop("image", (a0, a1), (r0, r1), num_trial=int(trials))
+    dx.set_state(int(seed))
+    for i, (w, h) in enumerate(wh):
+        p = P._plan(t, i, "image")
+        if ref[i][2] == 0:  # unchanged: the source array itself, no plan
+            assert p is None or p["crop"] == (0, 0, int(w), int(h)), (i, w, h, p)
+        else:
+            assert p is not None and p["crop"] == tuple(int(v) for v in ref[i]), (i, w, h, p, ref[i])
+
+
+def test_random_area_crop_then_resize_plan():
+    """Inception-style random_area_crop -> image_resize: the crop becomes the
+    resize's source window (one fused launch)."""
+    img = np.zeros((375, 500, 3), np.uint8)
+    t = dx.buffer_from_vector([dict(image=img)]).image_random_area_crop("image", (0.08, 1.0), (0.75, 4 / 3))
+    dx.set_state(1234)
+    c = P._plan(t, 0, "image")["crop"]
+    r = t.image_resize("image", 224, 224)
+    dx.set_state(1234)
+    p = P._plan(r, 0, "image")
+    assert p["window"] == c and p["resize"] == (224, 224) and p["crop"] == (0, 0, 224, 224)
+
+
+def test_random_area_crop_errors():
+    b = dx.buffer_from_vector([dict(image=np.zeros((8, 8, 3), np.uint8))])
+    cases = [
+        (((0.0, 1.0), (1.0, 1.0), 10), "invalid area range"),
+        (((0.6, 0.5), (1.0, 1.0), 10), "invalid area range"),
+        (((0.5, 1.1), (1.0, 1.0), 10), "invalid area range"),
+        (((0.5, 1.0), (0.0, 1.0), 10), "invalid aspect ratio range"),
+        (((0.5, 1.0), (2.0, 1.0), 10), "invalid aspect ratio range"),
+        (((0.6, 1.0), (2.0, 3.0), 10), "cannot be fullfilled"),
+        (((0.5, 1.0), (0.1, 0.4), 10), "cannot be fullfilled"),
+        (((0.5, 1.0), (1.0, 1.0), 0), "number of trial must be positive"),
+    ]
+    for (a, r, n), msg in cases:
+        with pytest.raises(RuntimeError, match=msg):
+            b.image_random_area_crop("image", a, r, num_trial=n)
