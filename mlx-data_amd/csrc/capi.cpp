@@ -168,6 +168,12 @@ struct Workspace {
   size_t cap = 0;
   size_t count = 0;
   hipEvent_t copied = nullptr;
+  // Fork/join helpers: the launches of a mixed batch (one per kernel shape)
+  // run concurrently on these streams, so one launch's tail overlaps the
+  // next instead of idling the CUs between serialized launches.
+  static constexpr int kHelpers = 3;
+  hipStream_t helper[kHelpers] = {};
+  hipEvent_t fork = nullptr, join[kHelpers] = {};
 };
 
 class WorkspacePool {
@@ -228,8 +234,9 @@ int validate(const mxd_image& im, int32_t i) {
 // Uploads descs to the stream's workspace (skipped when unchanged) and returns
 // the device copy.
 int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream, ImgDev** dev_out,
-                 std::unique_lock<std::mutex>* hold) {
+                 std::unique_lock<std::mutex>* hold, Workspace** ws_out = nullptr) {
   Workspace* ws = workspaces().get(device, stream);
+  if (ws_out) *ws_out = ws;
   *hold = std::unique_lock<std::mutex>(ws->mu);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t n = descs.size();
@@ -642,16 +649,44 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     }
     ImgDev* dev = nullptr;
     std::unique_lock<std::mutex> hold;
-    if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
+    Workspace* ws = nullptr;
+    if (int rc = upload_descs(descs, device, stream, &dev, &hold, &ws)) return rc;
     static const int debug = env_int("MXD_DEBUG");
-    for (const Group& g : groups) {
+    // Several launches: fork them over the caller's stream and the
+    // workspace's helper streams (largest first), join back before return.
+    const int nfork = env_int("MXD_NO_FORK") ? 0 : std::min<int>((int)groups.size() - 1, Workspace::kHelpers);
+    std::vector<int32_t> by_size(groups.size());
+    for (size_t i = 0; i < groups.size(); i++) by_size[i] = (int32_t)i;
+    std::stable_sort(by_size.begin(), by_size.end(),
+                     [&](int32_t a, int32_t b) { return groups[a].units > groups[b].units; });
+    if (nfork > 0) {
+      if (!ws->fork) {
+        MXD_HIP(hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming));
+        for (int h = 0; h < Workspace::kHelpers; h++) {
+          MXD_HIP(hipStreamCreateWithFlags(&ws->helper[h], hipStreamNonBlocking));
+          MXD_HIP(hipEventCreateWithFlags(&ws->join[h], hipEventDisableTiming));
+        }
+      }
+      MXD_HIP(hipEventRecord(ws->fork, reinterpret_cast<hipStream_t>(stream)));
+      for (int h = 0; h < nfork; h++) MXD_HIP(hipStreamWaitEvent(ws->helper[h], ws->fork, 0));
+    }
+    for (size_t k = 0; k < by_size.size(); k++) {
+      const Group& g = groups[by_size[k]];
+      const int lane = nfork > 0 ? (int)(k % (size_t)(nfork + 1)) : 0;
+      void* s = lane == 0 ? stream : reinterpret_cast<void*>(ws->helper[lane - 1]);
       if (debug)
-        std::fprintf(stderr, "mxd: launch kind=%d taps=%d s=%d dmax=%d f32=%d imgs=%d units=%d band_rows=%d capacity=%d\n",
+        std::fprintf(stderr,
+                     "mxd: launch kind=%d taps=%d s=%d dmax=%d f32=%d imgs=%d units=%d band_rows=%d capacity=%d "
+                     "lane=%d\n",
                      g.cfg.kind, g.cfg.taps, g.cfg.s, g.cfg.dmax, g.cfg.f32, g.cfg.nimgs, g.cfg.nunits, g.ty,
-                     wave_capacity_cached(g.cfg, device));
-      if (int rc = mxd::launch_wave(g.cfg, dev + g.first, stream))
+                     wave_capacity_cached(g.cfg, device), lane);
+      if (int rc = mxd::launch_wave(g.cfg, dev + g.first, s))
         return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
                                         " rc=" + std::to_string(rc));
+    }
+    for (int h = 0; h < nfork; h++) {
+      MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
+      MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
     }
     return MXD_OK;
   }
