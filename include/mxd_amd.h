@@ -138,6 +138,49 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop);
  * ops use when samples live in host memory (mlx-data's default). */
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device);
 
+/* ---- pixel maps: rotate / affine and channel reduction --
+ *
+ *   core::image::affine(img, mx, crop)       mlx/data/core/image/ImageTransform.cpp:75-110
+ *   core::image::rotate(img, angle, crop)    mlx/data/core/image/ImageTransform.cpp:112-121
+ *   core::image::channel_reduction(img,b,m)  mlx/data/core/image/ImageTransform.cpp:142-180
+ *   op::ImageRotate / ImageChannelReduction  mlx/data/op/ImageTransform.cpp:334-421
+ *
+ * One uint8 image of a pixel-map launch.  Affine: dst is dst_h x dst_w x
+ * channels, dst(tx,ty) = src(x,y) at the reference's nearest-pixel inverse map
+ * (0 outside the source).  Channel reduction: channels must be 3, dst is
+ * src_h x src_w x 1.  params: affine mx[0..5]; channel reduction
+ * {bias, m0, m1, m2} as floats (the reference's 16.16 fixed point is derived
+ * from them exactly as core::image::channel_reduction does). */
+typedef struct mxd_pixmap {
+  const uint8_t* src;
+  int64_t src_stride;
+  int32_t src_w, src_h, channels;
+  int32_t dst_w, dst_h;
+  void* dst;
+  int64_t dst_stride;
+  float params[6];
+} mxd_pixmap;
+
+enum mxd_pixop { MXD_AFFINE = 0, MXD_CHANNEL_REDUCTION = 1 };
+
+/* core::image::rotate's matrix and core::image::affine's output dims for a
+ * (w x h) image rotated by `angle` degrees (crop: keep w x h). */
+int mxd_rotate_geometry(int64_t w, int64_t h, double angle, int32_t crop, float* mx6, int64_t* out_w,
+                        int64_t* out_h);
+
+/* op::ImageChannelReduction presets (op/ImageTransform.cpp:362-392):
+ * "default", "rec601", "rec709", "rec2020", "green" -> {bias, m0, m1, m2}.
+ * Unknown name: MXD_ERR_INVALID with the reference's message. */
+int mxd_channel_reduction_preset(const char* preset, float* params4);
+
+/* n pixel maps of kind `op` on `device`, one kernel launch, enqueued on
+ * `stream`; src/dst are device pointers. */
+int mxd_pixmap_batch(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, void* stream);
+
+/* Host pointers in and out (pinned staging, synchronous), like
+ * mxd_resize_crop_host. */
+int mxd_pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "mxd_amd.h"
+#include "pixmap.h"
 #include "resample.h"
 #include "taps.h"
 
@@ -749,6 +751,115 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
 }
 
 // ---------------------------------------------------------------------------
+// Pixel maps (rotate / channel reduction): validation with the reference's
+// messages, host-side derivation of the per-image constants, descriptor upload
+// through a per-(device, stream) pinned/device pair guarded like Workspace.
+struct PixWorkspace {
+  std::mutex mu;
+  mxd::PixDev* host = nullptr;
+  mxd::PixDev* dev = nullptr;
+  size_t cap = 0;
+  hipEvent_t copied = nullptr;
+};
+
+PixWorkspace* pix_workspace(int32_t device, void* stream) {
+  static std::mutex mu;
+  static auto* map = new std::map<std::pair<int32_t, void*>, std::unique_ptr<PixWorkspace>>();
+  std::lock_guard<std::mutex> lk(mu);
+  auto& w = (*map)[std::make_pair(device, stream)];
+  if (!w) w = std::make_unique<PixWorkspace>();
+  return w.get();
+}
+
+int pix_validate(const mxd_pixmap& im, int32_t op, int32_t i) {
+  const std::string at = " (image " + std::to_string(i) + ")";
+  if (!im.src || !im.dst) return fail(MXD_ERR_INVALID, "mxd: null src/dst pointer" + at);
+  if (op != MXD_AFFINE && op != MXD_CHANNEL_REDUCTION) return fail(MXD_ERR_INVALID, "mxd: unknown pixmap op" + at);
+  if (im.src_w <= 0 || im.src_h <= 0 || im.dst_w <= 0 || im.dst_h <= 0)
+    return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
+  if (im.channels <= 0 || im.channels > 4)
+    return fail(MXD_ERR_INVALID, "image: channels must be 0 < c <= 4" + at);
+  if (op == MXD_CHANNEL_REDUCTION) {
+    if (im.channels != 3)
+      return fail(MXD_ERR_INVALID, "image::channelReduction: expected a 3 channel uint8 array" + at);
+    if (im.dst_w != im.src_w || im.dst_h != im.src_h)
+      return fail(MXD_ERR_INVALID, "mxd: channel reduction keeps the image size" + at);
+  }
+  if (im.src_stride < (int64_t)im.src_w * im.channels)
+    return fail(MXD_ERR_INVALID, "mxd: src_stride smaller than a row" + at);
+  const int64_t out_row = (int64_t)im.dst_w * (op == MXD_AFFINE ? im.channels : 1);
+  if (im.dst_stride < out_row) return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than a row" + at);
+  return MXD_OK;
+}
+
+mxd::PixDev pix_desc(const mxd_pixmap& im, int32_t op) {
+  mxd::PixDev d{};
+  d.src = im.src;
+  d.dst = static_cast<uint8_t*>(im.dst);
+  d.src_stride = im.src_stride;
+  d.dst_stride = im.dst_stride;
+  d.src_w = im.src_w;
+  d.src_h = im.src_h;
+  d.dst_w = im.dst_w;
+  d.dst_h = im.dst_h;
+  d.c = im.channels;
+  d.groups = (im.dst_w + 3) / 4;
+  const bool dst4 = ((uintptr_t)im.dst & 3) == 0 && (im.dst_stride & 3) == 0;
+  const bool src4 = ((uintptr_t)im.src & 3) == 0 && (im.src_stride & 3) == 0;
+  d.fast = op == MXD_AFFINE ? dst4 : (dst4 && src4);
+  if (op == MXD_AFFINE) {
+    // core/image/ImageTransform.cpp:88-91 (double halves narrowed to float)
+    for (int k = 0; k < 6; k++) d.mx[k] = im.params[k];
+    d.twh = (float)(im.dst_w / 2.0);
+    d.thh = (float)(im.dst_h / 2.0);
+    d.wh = (float)(im.src_w / 2.0);
+    d.hh = (float)(im.src_h / 2.0);
+  } else {
+    // core/image/ImageTransform.cpp:158-163: float * 65536 truncated to int
+    const int scale = 256 * 256;
+    d.bias = (int)(im.params[0] * scale);
+    for (int k = 0; k < 3; k++) d.m[k] = (int)(im.params[1 + k] * scale);
+  }
+  return d;
+}
+
+int run_pixmap(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, void* stream) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (n == 0) return MXD_OK;
+  for (int32_t i = 0; i < n; i++)
+    if (int rc = pix_validate(images[i], op, i)) return rc;
+  DeviceGuard g(device);
+  PixWorkspace* ws = pix_workspace(device, stream);
+  std::lock_guard<std::mutex> lk(ws->mu);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ws->copied) MXD_HIP(hipEventSynchronize(ws->copied));  // staging free again
+  if ((size_t)n > ws->cap) {
+    if (ws->dev) {
+      MXD_HIP(hipStreamSynchronize(s));
+      MXD_HIP(hipFree(ws->dev));
+      MXD_HIP(hipHostFree(ws->host));
+      ws->dev = nullptr;
+      ws->host = nullptr;
+    }
+    const size_t cap = std::max<size_t>(n, 64);
+    MXD_HIP(hipMalloc(reinterpret_cast<void**>(&ws->dev), sizeof(mxd::PixDev) * cap));
+    MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws->host), sizeof(mxd::PixDev) * cap, hipHostMallocDefault));
+    ws->cap = cap;
+  }
+  if (!ws->copied) MXD_HIP(hipEventCreateWithFlags(&ws->copied, hipEventDisableTiming));
+  int64_t max_units = 0;
+  for (int32_t i = 0; i < n; i++) {
+    ws->host[i] = pix_desc(images[i], op);
+    max_units = std::max(max_units, (int64_t)ws->host[i].dst_h * ws->host[i].groups);
+  }
+  MXD_HIP(hipMemcpyAsync(ws->dev, ws->host, sizeof(mxd::PixDev) * n, hipMemcpyHostToDevice, s));
+  MXD_HIP(hipEventRecord(ws->copied, s));
+  if (mxd::launch_pixmap(op, ws->dev, n, max_units, stream))
+    return fail(MXD_ERR_DEVICE, std::string("pixmap launch: ") + hipGetErrorString(hipGetLastError()));
+  return MXD_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Host-resident path: per-(thread, device) stream + growable buffers.
 struct HostCtx {
   hipStream_t stream = nullptr;
@@ -1012,6 +1123,105 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
     uint8_t* d = static_cast<uint8_t*>(im.dst);
     const uint8_t* s = ctx.pin_out + out_off[i];
     for (int32_t r = 0; r < im.crop_h; r++) std::memcpy(d + (size_t)r * im.dst_stride, s + r * row, row);
+  }
+  return MXD_OK;
+}
+
+int mxd_rotate_geometry(int64_t w, int64_t h, double angle, int32_t crop, float* mx6, int64_t* out_w,
+                        int64_t* out_h) {
+#pragma clang fp contract(off)
+  if (!mx6 || !out_w || !out_h) return fail(MXD_ERR_INVALID, "mxd: null output");
+  // core/image/ImageTransform.cpp:112-121: pi, the radian angle, cos and sin in float
+  const float pi = std::atan(1.0) * 4;
+  const float rangle = angle * pi / 180.;
+  const float c = std::cos(rangle);
+  const float s = std::sin(rangle);
+  const float mx[6] = {c, s, 0, -s, c, 0};
+  for (int k = 0; k < 6; k++) mx6[k] = mx[k];
+  // :81-86 (float products, truncated to int64)
+  int64_t tw = w, th = h;
+  if (!crop) {
+    tw = (int64_t)((float)w * std::fabs(mx[0]) + (float)h * std::fabs(mx[1]));
+    th = (int64_t)((float)h * std::fabs(mx[3]) + (float)w * std::fabs(mx[4]));
+  }
+  *out_w = tw;
+  *out_h = th;
+  if (tw <= 0 || th <= 0) return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension");
+  return MXD_OK;
+}
+
+int mxd_channel_reduction_preset(const char* preset, float* params4) {
+  if (!preset || !params4) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  // op/ImageTransform.cpp:362-392
+  struct P {
+    const char* name;
+    float bias, m[3];
+  };
+  static const P presets[] = {{"default", 0, {0.299, 0.587, 0.114}},
+                              {"rec601", 0, {0.299, 0.587, 0.114}},
+                              {"rec709", 0, {0.2126, 0.7152, 0.0722}},
+                              {"rec2020", 0, {0.2627, 0.678, 0.0593}},
+                              {"green", 0, {0, 1, 0}}};
+  for (const P& p : presets)
+    if (std::strcmp(p.name, preset) == 0) {
+      params4[0] = p.bias;
+      for (int k = 0; k < 3; k++) params4[1 + k] = p.m[k];
+      return MXD_OK;
+    }
+  return fail(MXD_ERR_INVALID, std::string("ImageChannelReduction: unable to find preset ") + preset);
+}
+
+int mxd_pixmap_batch(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, void* stream) {
+  return run_pixmap(images, n, op, device, stream);
+}
+
+int mxd_pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (n == 0) return MXD_OK;
+  for (int32_t i = 0; i < n; i++)
+    if (int rc = pix_validate(images[i], op, i)) return rc;
+  DeviceGuard g(device);
+  HostCtx& ctx = host_ctx(device);
+  if (!ctx.stream) MXD_HIP(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+  std::vector<size_t> in_off(n), out_off(n);
+  std::vector<int64_t> in_pitch(n), out_pitch(n);
+  size_t in_bytes = 0, out_bytes = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_pixmap& im = images[i];
+    const int64_t oc = op == MXD_AFFINE ? im.channels : 1;
+    in_pitch[i] = ((int64_t)im.src_w * im.channels + 15) & ~(int64_t)15;
+    out_pitch[i] = ((int64_t)im.dst_w * oc + 15) & ~(int64_t)15;
+    in_off[i] = in_bytes;
+    in_bytes += ((size_t)in_pitch[i] * im.src_h + 255) & ~(size_t)255;
+    out_off[i] = out_bytes;
+    out_bytes += ((size_t)out_pitch[i] * im.dst_h + 255) & ~(size_t)255;
+  }
+  if (int rc = grow_pinned(&ctx.pin_in, &ctx.pin_in_cap, in_bytes)) return rc;
+  if (int rc = grow_pinned(&ctx.pin_out, &ctx.pin_out_cap, out_bytes)) return rc;
+  if (int rc = grow_device(&ctx.dev_in, &ctx.dev_in_cap, in_bytes)) return rc;
+  if (int rc = grow_device(&ctx.dev_out, &ctx.dev_out_cap, out_bytes)) return rc;
+  std::vector<mxd_pixmap> dev_imgs(images, images + n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_pixmap& im = images[i];
+    const size_t row = (size_t)im.src_w * im.channels;
+    uint8_t* stage = ctx.pin_in + in_off[i];
+    for (int32_t r = 0; r < im.src_h; r++)
+      std::memcpy(stage + (size_t)r * in_pitch[i], im.src + (size_t)r * im.src_stride, row);
+    dev_imgs[i].src = ctx.dev_in + in_off[i];
+    dev_imgs[i].src_stride = in_pitch[i];
+    dev_imgs[i].dst = ctx.dev_out + out_off[i];
+    dev_imgs[i].dst_stride = out_pitch[i];
+  }
+  MXD_HIP(hipMemcpyAsync(ctx.dev_in, ctx.pin_in, in_bytes, hipMemcpyHostToDevice, ctx.stream));
+  if (int rc = run_pixmap(dev_imgs.data(), n, op, device, ctx.stream)) return rc;
+  MXD_HIP(hipMemcpyAsync(ctx.pin_out, ctx.dev_out, out_bytes, hipMemcpyDeviceToHost, ctx.stream));
+  MXD_HIP(hipStreamSynchronize(ctx.stream));
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_pixmap& im = images[i];
+    const size_t row = (size_t)im.dst_w * (op == MXD_AFFINE ? im.channels : 1);
+    uint8_t* d = static_cast<uint8_t*>(im.dst);
+    const uint8_t* s = ctx.pin_out + out_off[i];
+    for (int32_t r = 0; r < im.dst_h; r++) std::memcpy(d + (size_t)r * im.dst_stride, s + (size_t)r * out_pitch[i], row);
   }
   return MXD_OK;
 }

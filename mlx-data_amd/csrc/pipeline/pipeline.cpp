@@ -315,6 +315,55 @@ std::shared_ptr<Array> ImageRandomHFlip::apply_image(const std::shared_ptr<Array
   return img;
 }
 
+namespace {
+// A materialised, contiguous (H, W, C) uint8 image through one pixel-map
+// launch on the next device.
+std::shared_ptr<Array> run_pixmap(const std::shared_ptr<Array>& img, int32_t op, const float* params, int64_t dw,
+                                  int64_t dh, int64_t dc) {
+  if (img->type() != DType::UInt8) throw std::invalid_argument("image must be of type UInt8");
+  const int64_t w = img->shape(1), h = img->shape(0), c = img->shape(2);
+  auto out = std::make_shared<Array>(DType::UInt8, std::vector<int64_t>{dh, dw, dc});
+  mxd_pixmap d{};
+  d.src = static_cast<const uint8_t*>(img->data());
+  d.src_stride = w * c;
+  d.src_w = (int32_t)w;
+  d.src_h = (int32_t)h;
+  d.channels = (int32_t)c;
+  d.dst_w = (int32_t)dw;
+  d.dst_h = (int32_t)dh;
+  d.dst = out->data();
+  d.dst_stride = dw * dc;
+  for (int k = 0; k < 6; k++) d.params[k] = params[k];
+  check(mxd_pixmap_host(&d, 1, op, next_device()));
+  return out;
+}
+}  // namespace
+
+// op/ImageTransform.cpp:334-343 -> core/image/ImageTransform.cpp:75-121
+std::shared_ptr<Array> ImageRotate::apply_image(const std::shared_ptr<Array>& img) const {
+  const int64_t w = img->shape(1), h = img->shape(0), c = img->shape(2);
+  float mx[6];
+  int64_t tw = 0, th = 0;
+  (void)mxd_rotate_geometry(w, h, angle_, crop_ ? 1 : 0, mx, &tw, &th);  // dims are set even when invalid
+  verify_dimensions(tw, th, c);
+  return run_pixmap(img, MXD_AFFINE, mx, tw, th, c);
+}
+
+// op/ImageTransform.cpp:394-421 -> core/image/ImageTransform.cpp:142-180
+ImageChannelReduction::ImageChannelReduction(std::string ikey, const std::string& preset, std::string okey)
+    : ImageOp(std::move(ikey), std::move(okey)) {
+  if (mxd_channel_reduction_preset(preset.c_str(), params_) != MXD_OK)
+    throw std::runtime_error(std::string("ImageChannelReduction: unable to find preset ") + preset);
+}
+
+std::shared_ptr<Array> ImageChannelReduction::apply_image(const std::shared_ptr<Array>& img) const {
+  const int64_t w = img->shape(1), h = img->shape(0), c = img->shape(2);
+  if (c != 3) throw std::runtime_error("image::channelReduction: expected a 3 channel uint8 array");
+  verify_dimensions(w, h, 1);
+  const float p[6] = {params_[0], params_[1], params_[2], params_[3], 0, 0};
+  return run_pixmap(img, MXD_CHANNEL_REDUCTION, p, w, h, 1);
+}
+
 // op/ImageTransform.cpp:184-212 (constructor checks, same messages)
 ImageRandomAreaCrop::ImageRandomAreaCrop(std::string ikey, std::pair<float, float> area_range,
                                          std::pair<float, float> aspect_ratio_range, int num_trial, std::string okey)

@@ -179,6 +179,30 @@ class ImageRandomHFlip : public ImageOp {
   float prob_;
 };
 
+// op/ImageTransform.h:139-152 ImageRotate: nearest-pixel rotation about the
+// centre (core::image::rotate -> affine), one GPU pixel-map launch.
+class ImageRotate : public ImageOp {
+ public:
+  ImageRotate(std::string ikey, double angle, bool crop, std::string okey)
+      : ImageOp(std::move(ikey), std::move(okey)), angle_(angle), crop_(crop) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  double angle_;
+  bool crop_;
+};
+
+// op/ImageTransform.h:154-167 ImageChannelReduction: RGB -> (H, W, 1) gray in
+// 16.16 fixed point with a named preset; unknown presets throw at construction.
+class ImageChannelReduction : public ImageOp {
+ public:
+  ImageChannelReduction(std::string ikey, const std::string& preset, std::string okey);
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+
+ private:
+  float params_[4];  // bias, m0, m1, m2
+};
+
 // op/ImageTransform.h ImageRandomAreaCrop: a crop whose area and aspect ratio
 // are drawn by rejection sampling (Inception-style); the image unchanged when
 // no trial meets the constraints.

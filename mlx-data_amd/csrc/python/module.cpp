@@ -213,7 +213,19 @@ void dataset_ops(py::class_<D, std::shared_ptr<D>>& cls, Wrap wrap) {
                                                                     output_key));
           },
           py::arg("key"), py::arg("area_range"), py::arg("aspect_ratio_range"), py::arg("num_trial") = 10,
-          py::arg("output_key") = "");
+          py::arg("output_key") = "")
+      .def(
+          "image_rotate",
+          [wrap](const Self& self, const std::string& key, double angle, bool crop, const std::string& output_key) {
+            return wrap(self, std::make_shared<ImageRotate>(key, angle, crop, output_key));
+          },
+          py::arg("key"), py::arg("angle"), py::arg("crop") = false, py::arg("output_key") = "")
+      .def(
+          "image_channel_reduction",
+          [wrap](const Self& self, const std::string& key, const std::string& preset, const std::string& output_key) {
+            return wrap(self, std::make_shared<ImageChannelReduction>(key, preset, output_key));
+          },
+          py::arg("key"), py::arg("preset") = "default", py::arg("output_key") = "");
 }
 
 using PadMap = std::unordered_map<std::string, double>;

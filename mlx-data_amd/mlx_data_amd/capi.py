@@ -26,7 +26,11 @@ EXPORTS = (
     "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
     "mxd_event_create", "mxd_event_destroy", "mxd_event_record", "mxd_event_synchronize", "mxd_event_elapsed_ms",
     "mxd_resize_crop_host",
+    "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
 )
+
+MXD_AFFINE = 0
+MXD_CHANNEL_REDUCTION = 1
 
 
 class MxdImage(ctypes.Structure):
@@ -47,6 +51,23 @@ class MxdImage(ctypes.Structure):
         ("flip", ctypes.c_int32),
         ("dst", ctypes.c_void_p),
         ("dst_stride", ctypes.c_int64),
+    ]
+
+
+class MxdPixmap(ctypes.Structure):
+    """struct mxd_pixmap (include/mxd_amd.h): rotate / channel reduction."""
+
+    _fields_ = [
+        ("src", ctypes.c_void_p),
+        ("src_stride", ctypes.c_int64),
+        ("src_w", ctypes.c_int32),
+        ("src_h", ctypes.c_int32),
+        ("channels", ctypes.c_int32),
+        ("dst_w", ctypes.c_int32),
+        ("dst_h", ctypes.c_int32),
+        ("dst", ctypes.c_void_p),
+        ("dst_stride", ctypes.c_int64),
+        ("params", ctypes.c_float * 6),
     ]
 
 
@@ -128,6 +149,44 @@ def resize_crop_batch(images, n, out_dtype, device=0, stream=None):
 
 def resize_crop_host(images, n, out_dtype, device=0):
     check(lib().mxd_resize_crop_host(images, n, out_dtype, device))
+
+
+def rotate_geometry(w, h, angle, crop=False):
+    """(mx[6] float32, out_w, out_h) of core::image::rotate for a w x h image."""
+    mx = np.zeros(6, np.float32)
+    tw, th = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().mxd_rotate_geometry(ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_double(angle), int(bool(crop)),
+                                    mx.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(tw),
+                                    ctypes.byref(th)))
+    return mx, tw.value, th.value
+
+
+def channel_reduction_preset(preset):
+    p = np.zeros(4, np.float32)
+    check(lib().mxd_channel_reduction_preset(preset.encode(), p.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return p
+
+
+def make_pixmaps(entries):
+    """entries: iterable of dicts with the mxd_pixmap fields -> ctypes array."""
+    entries = list(entries)
+    arr = (MxdPixmap * max(1, len(entries)))()
+    for i, e in enumerate(entries):
+        for k, v in e.items():
+            if k == "params":
+                for j, x in enumerate(v):
+                    arr[i].params[j] = float(x)
+            else:
+                setattr(arr[i], k, v)
+    return arr, len(entries)
+
+
+def pixmap_batch(images, n, op, device=0, stream=None):
+    check(lib().mxd_pixmap_batch(images, n, op, device, ctypes.c_void_p(stream)))
+
+
+def pixmap_host(images, n, op, device=0):
+    check(lib().mxd_pixmap_host(images, n, op, device))
 
 
 class Stream:

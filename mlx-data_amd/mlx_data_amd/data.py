@@ -65,7 +65,8 @@ def _add_if_variants(cls):
     """``<op>_if(cond, ...)``: the op when ``cond`` holds, else the dataset
     unchanged (``Dataset::*_if``, ``Dataset.cpp``)."""
     for name in ("key_transform", "load_image", "image_resize_smallest_side", "image_resize",
-                 "image_center_crop", "image_random_crop", "image_random_h_flip", "image_random_area_crop"):
+                 "image_center_crop", "image_random_crop", "image_random_h_flip", "image_random_area_crop",
+                 "image_rotate", "image_channel_reduction"):
         def op_if(self, cond, *args, _name=name, **kwargs):
             return getattr(self, _name)(*args, **kwargs) if cond else self
 

@@ -186,3 +186,47 @@ def ref_random_area_crop(seed, sizes_wh, area_range, aspect_range, trials=10):
         ctypes.c_float(aspect_range[0]), ctypes.c_float(aspect_range[1]), int(trials), _ptr(out, _i64p)
     )
     return out.reshape(n, 4)
+
+
+# ---- rotate / channel reduction -------------------------
+CHANNEL_PRESETS = {  # op/ImageTransform.cpp:362-392 (float literals)
+    "default": (0.0, (0.299, 0.587, 0.114)),
+    "rec601": (0.0, (0.299, 0.587, 0.114)),
+    "rec709": (0.0, (0.2126, 0.7152, 0.0722)),
+    "rec2020": (0.0, (0.2627, 0.678, 0.0593)),
+    "green": (0.0, (0.0, 1.0, 0.0)),
+}
+
+
+def rotate_geometry(w, h, angle, crop=False):
+    mx = np.zeros(6, np.float32)
+    tw, th = ctypes.c_int64(), ctypes.c_int64()
+    bad = lib().orc_rotate_geometry(ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_double(angle), int(bool(crop)),
+                                    _ptr(mx, _f32p), ctypes.byref(tw), ctypes.byref(th))
+    return mx, tw.value, th.value, bool(bad)
+
+
+def rotate(img, angle, crop=False):
+    """core::image::rotate (core/image/ImageTransform.cpp:112-121)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, c = img.shape
+    mx, tw, th, bad = rotate_geometry(w, h, angle, crop)
+    if bad:
+        raise ValueError("image: cannot create image with 0 or negative dimension")
+    out = np.zeros((th, tw, c), np.uint8)
+    lib().orc_affine_u8(_ptr(img), ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_int64(c), _ptr(mx, _f32p),
+                        ctypes.c_int64(tw), ctypes.c_int64(th), _ptr(out))
+    return out
+
+
+def channel_reduction(img, preset="default"):
+    """core::image::channel_reduction (core/image/ImageTransform.cpp:142-180)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, c = img.shape
+    assert c == 3
+    bias, m = CHANNEL_PRESETS[preset]
+    mm = np.array(m, np.float32)
+    out = np.zeros((h, w, 1), np.uint8)
+    lib().orc_channel_reduction_u8(_ptr(img), ctypes.c_int64(w), ctypes.c_int64(h), ctypes.c_float(bias),
+                                   _ptr(mm, _f32p), _ptr(out))
+    return out

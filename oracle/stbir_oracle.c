@@ -20,6 +20,9 @@
  *   - core::image::hflip             core/image/ImageTransform.cpp:123-140
  *   - array::batch (fill pad + copy) Array.cpp:465-498
  *   - x.astype("float32") / 255      benchmarks/comparative/caltech101/mlx_data.py:46
+ *   - core::image::rotate / affine   core/image/ImageTransform.cpp:75-121
+ *   - core::image::channel_reduction core/image/ImageTransform.cpp:142-180
+ *       (+ op::ImageChannelReduction presets, op/ImageTransform.cpp:362-392)
  *
  * Parity status: crop / hflip / batch / normalize are pinned bit-exact against
  * the reference's own Array.cpp compiled by oracle/Makefile (oracle/_ref).
@@ -355,4 +358,61 @@ int orc_resize_smallest_side_center_crop(const uint8_t* src, int w, int h, int c
   if (!rc) rc = orc_crop_u8(tmp, (int)tw, (int)th, c, (int)x, (int)y, cw, ch, dst);
   free(tmp);
   return rc;
+}
+
+/* ---- rotate / affine (core/image/ImageTransform.cpp:75-121) -------------
+ * Parity status: the reference file needs stb_image_resize2.h and is not
+ * buildable here, so this is a line-by-line restatement of its integer /
+ * float arithmetic (pinned by tests/golden/pixmap.npz, generated from this
+ * file, and by the GPU kernels agreeing bit for bit).  fabs is taken in
+ * float (the <cmath> float overload). */
+int orc_rotate_geometry(int64_t w, int64_t h, double angle, int crop, float* mx, int64_t* tw, int64_t* th) {
+  const float pi = (float)(atan(1.0) * 4);
+  const float rangle = (float)(angle * (double)pi / 180.);
+  const float c = cosf(rangle);
+  const float s = sinf(rangle);
+  mx[0] = c; mx[1] = s; mx[2] = 0; mx[3] = -s; mx[4] = c; mx[5] = 0;
+  *tw = w;
+  *th = h;
+  if (!crop) {
+    *tw = (int64_t)((float)w * fabsf(mx[0]) + (float)h * fabsf(mx[1]));
+    *th = (int64_t)((float)h * fabsf(mx[3]) + (float)w * fabsf(mx[4]));
+  }
+  return (*tw <= 0 || *th <= 0) ? 1 : 0;
+}
+
+void orc_affine_u8(const uint8_t* src, int64_t w, int64_t h, int64_t c, const float* mx, int64_t tw, int64_t th,
+                   uint8_t* dst) {
+  const float twh = (float)(tw / 2.0);
+  const float thh = (float)(th / 2.0);
+  const float wh = (float)(w / 2.0);
+  const float hh = (float)(h / 2.0);
+  for (int64_t ty = 0; ty < th; ty++) {
+    for (int64_t tx = 0; tx < tw; tx++) {
+      const float fx = (float)tx - twh, fy = (float)ty - thh;
+      const float sx = mx[0] * fx + mx[1] * fy + mx[2];
+      const float sy = mx[3] * fx + mx[4] * fy + mx[5];
+      const int64_t x = (int64_t)((double)sx + 0.5 + (double)wh);
+      const int64_t y = (int64_t)((double)sy + 0.5 + (double)hh);
+      uint8_t* o = dst + (ty * tw + tx) * c;
+      if (x < 0 || y < 0 || x >= w || y >= h)
+        memset(o, 0, (size_t)c);
+      else
+        memcpy(o, src + (y * w + x) * c, (size_t)c);
+    }
+  }
+}
+
+/* ---- channel reduction (core/image/ImageTransform.cpp:142-180) ---------- */
+void orc_channel_reduction_u8(const uint8_t* src, int64_t w, int64_t h, float bias, const float* mult, uint8_t* dst) {
+  const int scale = 256 * 256;
+  const int ib = (int)(bias * (float)scale);
+  int m[3];
+  for (int i = 0; i < 3; i++) m[i] = (int)(mult[i] * (float)scale);
+  for (int64_t i = 0; i < w * h; i++) {
+    int v = (src[3 * i] * m[0] + src[3 * i + 1] * m[1] + src[3 * i + 2] * m[2] + ib) / scale;
+    v = v <= 255 ? v : 255;
+    v = v >= 0 ? v : 0;
+    dst[i] = (uint8_t)v;
+  }
 }
