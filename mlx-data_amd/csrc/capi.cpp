@@ -787,6 +787,8 @@ int pix_validate(const mxd_pixmap& im, int32_t op, int32_t i) {
   }
   if (im.src_stride < (int64_t)im.src_w * im.channels)
     return fail(MXD_ERR_INVALID, "mxd: src_stride smaller than a row" + at);
+  if ((int64_t)im.dst_w * im.dst_h >= ((int64_t)1 << 31))
+    return fail(MXD_ERR_UNSUPPORTED, "mxd: pixel map output of 2^31 pixels or more" + at);
   const int64_t out_row = (int64_t)im.dst_w * (op == MXD_AFFINE ? im.channels : 1);
   if (im.dst_stride < out_row) return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than a row" + at);
   return MXD_OK;
@@ -803,10 +805,14 @@ mxd::PixDev pix_desc(const mxd_pixmap& im, int32_t op) {
   d.dst_w = im.dst_w;
   d.dst_h = im.dst_h;
   d.c = im.channels;
-  d.groups = (im.dst_w + 3) / 4;
-  const bool dst4 = ((uintptr_t)im.dst & 3) == 0 && (im.dst_stride & 3) == 0;
-  const bool src4 = ((uintptr_t)im.src & 3) == 0 && (im.src_stride & 3) == 0;
-  d.fast = op == MXD_AFFINE ? dst4 : (dst4 && src4);
+  // affine: 4-pixel groups, dword stores; reduction: 16-pixel groups, 16-B
+  // loads and stores (pixmap.hip)
+  const int gp = op == MXD_AFFINE ? 4 : 16;
+  d.groups = (im.dst_w + gp - 1) / gp;
+  const uintptr_t am = op == MXD_AFFINE ? 3 : 15;  // dword stores / 16-byte loads and stores
+  const bool dst_al = ((uintptr_t)im.dst & am) == 0 && ((uintptr_t)im.dst_stride & am) == 0;
+  const bool src_al = ((uintptr_t)im.src & am) == 0 && ((uintptr_t)im.src_stride & am) == 0;
+  d.fast = op == MXD_AFFINE ? dst_al : (dst_al && src_al);
   if (op == MXD_AFFINE) {
     // core/image/ImageTransform.cpp:88-91 (double halves narrowed to float)
     for (int k = 0; k < 6; k++) d.mx[k] = im.params[k];
@@ -850,7 +856,9 @@ int run_pixmap(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, 
   int64_t max_units = 0;
   for (int32_t i = 0; i < n; i++) {
     ws->host[i] = pix_desc(images[i], op);
-    max_units = std::max(max_units, (int64_t)ws->host[i].dst_h * ws->host[i].groups);
+    const int64_t u = op == MXD_AFFINE ? (int64_t)ws->host[i].dst_h * ws->host[i].dst_w
+                                       : (int64_t)ws->host[i].dst_h * ws->host[i].groups;
+    max_units = std::max(max_units, u);
   }
   MXD_HIP(hipMemcpyAsync(ws->dev, ws->host, sizeof(mxd::PixDev) * n, hipMemcpyHostToDevice, s));
   MXD_HIP(hipEventRecord(ws->copied, s));

@@ -23,7 +23,7 @@ struct PixDev {
 };
 
 // op: 0 affine, 1 channel reduction.  c: 1..4 (affine), 3 (reduction).
-// max_units = max over images of dst_h * groups.
+// max_units = max over images of dst_h * dst_w (affine) or dst_h * groups.
 int launch_pixmap(int op, const PixDev* imgs, int n, int64_t max_units, void* stream);
 
 }  // namespace mxd
