@@ -262,12 +262,51 @@ std::shared_ptr<Array> plan_crop(const std::shared_ptr<Array>& img, int64_t x, i
 
 }  // namespace
 
-// op/ImageTransform.cpp:22-31 + core/image/ImageIO.cpp:39-49
+// op/ImageTransform.cpp:22-31 + core/image/ImageIO.cpp:39-49 + core/video/Video.cpp:69-79
 std::shared_ptr<Array> ImageOp::apply_key(const std::shared_ptr<Array>& x) const {
-  if (x->ndim() == 4) throw std::runtime_error("mxd: video (4-d) arrays are not on the image path");
+  if (x->ndim() == 4) {
+    if (x->shape(3) == 0 || x->shape(3) > 4) throw std::runtime_error("verifyVideo: channels must be 0 <= c <= 4");
+    return apply_video(x);
+  }
   if (x->ndim() != 3) throw std::runtime_error("verifyImage: image must be 3 dimension Array (HWC)");
   if (x->shape(2) == 0 || x->shape(2) > 4) throw std::runtime_error("verifyImage: channels must be 0 <= c <= 4");
   return apply_image(x);
+}
+
+std::shared_ptr<Array> video_frame(const std::shared_ptr<Array>& video, int64_t i) {
+  const int64_t h = video->shape(1), w = video->shape(2), c = video->shape(3);
+  const int64_t bytes = h * w * c * itemsize(video->type());
+  auto* base = static_cast<uint8_t*>(video->data()) + i * bytes;
+  return std::make_shared<Array>(video->type(), std::vector<int64_t>{h, w, c},
+                                 std::shared_ptr<void>(video, static_cast<void*>(base)));
+}
+
+std::shared_ptr<Array> stack_frames(const std::vector<std::shared_ptr<Array>>& frames) {
+  const auto& f0 = frames.at(0);
+  const int64_t h = f0->shape(0), w = f0->shape(1), c = f0->shape(2);
+  for (const auto& f : frames)
+    if (f->shape(0) != h || f->shape(1) != w)
+      throw std::runtime_error("applyVideo: frame size inconsistent during transform");
+  auto out = std::make_shared<Array>(f0->type(), std::vector<int64_t>{(int64_t)frames.size(), h, w, c});
+  const int64_t bytes = h * w * c * itemsize(f0->type());
+  auto* dst = static_cast<uint8_t*>(out->data());
+  std::vector<mxd_image> descs;
+  for (size_t i = 0; i < frames.size(); i++) {
+    const auto& f = frames[i];
+    if (f->plan() && f->pending())
+      descs.push_back(plan_desc(*f->plan(), dst + i * bytes, w * c));
+    else
+      std::memcpy(dst + i * bytes, f->data(), bytes);
+  }
+  run_host(descs);  // every pending frame in one launch
+  return out;
+}
+
+std::shared_ptr<Array> ImageOp::apply_video(const std::shared_ptr<Array>& video) const {
+  std::vector<std::shared_ptr<Array>> frames;
+  for (int64_t i = 0; i < video->shape(0); i++) frames.push_back(apply_image(video_frame(video, i)));
+  if (frames.empty()) throw std::runtime_error("applyVideo: empty video");
+  return stack_frames(frames);
 }
 
 // op/ImageTransform.cpp:78-94 + core::image::scale :33-39
@@ -300,6 +339,37 @@ std::shared_ptr<Array> ImageRandomCrop::apply_image(const std::shared_ptr<Array>
   const int64_t x = xu(st->gen);
   const int64_t y = yu(st->gen);
   return plan_crop(img, x, y, w_, h_);
+}
+
+// op/ImageTransform.cpp:160-182: one draw, the same window for every frame
+std::shared_ptr<Array> ImageRandomCrop::apply_video(const std::shared_ptr<Array>& video) const {
+  const int64_t w = video->shape(2), h = video->shape(1);
+  if (h_ > h || w_ > w) throw std::runtime_error("ImageRandomCrop: target image size larger than input image");
+  std::uniform_int_distribution<int64_t> xu{0, w - w_};
+  std::uniform_int_distribution<int64_t> yu{0, h - h_};
+  auto st = get_state();
+  const int64_t x = xu(st->gen);
+  const int64_t y = yu(st->gen);
+  if (w_ == 0 || h_ == 0) return video;
+  std::vector<std::shared_ptr<Array>> frames;
+  for (int64_t i = 0; i < video->shape(0); i++) frames.push_back(plan_crop(video_frame(video, i), x, y, w_, h_));
+  return stack_frames(frames);
+}
+
+// op/ImageTransform.cpp:334-356: one draw, every frame mirrored or none
+std::shared_ptr<Array> ImageRandomHFlip::apply_video(const std::shared_ptr<Array>& video) const {
+  std::uniform_real_distribution<float> u{0, 1.0};
+  auto st = get_state();
+  if (!(u(st->gen) <= prob_)) return video;
+  std::vector<std::shared_ptr<Array>> frames;
+  for (int64_t i = 0; i < video->shape(0); i++) {
+    auto f = video_frame(video, i);
+    verify_dimensions(f->shape(1), f->shape(0), f->shape(2));
+    ImagePlan p = view(f);
+    p.flip = !p.flip;
+    frames.push_back(make(p));
+  }
+  return stack_frames(frames);
 }
 
 // op/ImageTransform.cpp:323-332 + core::image::hflip :123-140
@@ -423,6 +493,15 @@ std::shared_ptr<Array> ImageRandomAreaCrop::apply_image(const std::shared_ptr<Ar
   const auto c = draw(img->shape(1), img->shape(0));
   if (c[2] == 0 || c[3] == 0) return img;
   return plan_crop(img, c[0], c[1], c[2], c[3]);
+}
+
+// op/ImageTransform.cpp:293-315: one draw, the same window for every frame
+std::shared_ptr<Array> ImageRandomAreaCrop::apply_video(const std::shared_ptr<Array>& video) const {
+  const auto c = draw(video->shape(2), video->shape(1));
+  if (c[2] == 0 || c[3] == 0) return video;
+  std::vector<std::shared_ptr<Array>> frames;
+  for (int64_t i = 0; i < video->shape(0); i++) frames.push_back(plan_crop(video_frame(video, i), c[0], c[1], c[2], c[3]));
+  return stack_frames(frames);
 }
 
 // ------------------------------------------------------------------ load

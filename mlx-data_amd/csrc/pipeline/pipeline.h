@@ -127,7 +127,16 @@ class ImageOp : public KeyTransformOp {
   using KeyTransformOp::KeyTransformOp;
   std::shared_ptr<Array> apply_key(const std::shared_ptr<Array>& x) const override;
   virtual std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const = 0;
+  // (F, H, W, C) video: op/ImageTransform.cpp:33-70 -- apply_image per frame,
+  // every frame the size of the first; pending frame plans run as one batched
+  // launch writing straight into the result.
+  virtual std::shared_ptr<Array> apply_video(const std::shared_ptr<Array>& video) const;
 };
+
+// Frame i of a materialised (F, H, W, C) video, sharing its storage.
+std::shared_ptr<Array> video_frame(const std::shared_ptr<Array>& video, int64_t i);
+// Stacks per-frame results (pending plans in one launch) into (F, h, w, c).
+std::shared_ptr<Array> stack_frames(const std::vector<std::shared_ptr<Array>>& frames);
 
 class ImageResizeSmallestSide : public ImageOp {
  public:
@@ -163,6 +172,7 @@ class ImageRandomCrop : public ImageOp {
  public:
   ImageRandomCrop(std::string ikey, int64_t w, int64_t h, std::string okey)
       : ImageOp(std::move(ikey), std::move(okey)), w_(w), h_(h) {}
+  std::shared_ptr<Array> apply_video(const std::shared_ptr<Array>& video) const override;
   std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
 
  private:
@@ -174,6 +184,7 @@ class ImageRandomHFlip : public ImageOp {
   ImageRandomHFlip(std::string ikey, float prob, std::string okey)
       : ImageOp(std::move(ikey), std::move(okey)), prob_(prob) {}
   std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+  std::shared_ptr<Array> apply_video(const std::shared_ptr<Array>& video) const override;
 
  private:
   float prob_;
@@ -211,6 +222,7 @@ class ImageRandomAreaCrop : public ImageOp {
   ImageRandomAreaCrop(std::string ikey, std::pair<float, float> area_range, std::pair<float, float> aspect_ratio_range,
                       int num_trial, std::string okey);
   std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
+  std::shared_ptr<Array> apply_video(const std::shared_ptr<Array>& video) const override;
   // (x, y, w, h) of the crop for a w x h image, all 0 when none was found.
   std::array<int64_t, 4> draw(int64_t w, int64_t h) const;
 

@@ -126,3 +126,11 @@ def test_pipeline_ops_construct_and_check():
     assert b.image_rotate_if(False, "image", 10.0) is b
     with pytest.raises(RuntimeError, match="expected a 3 channel uint8 array"):
         dx.buffer_from_vector([dict(image=np.zeros((4, 4, 1), np.uint8))]).image_channel_reduction("image")[0]
+
+
+def test_video_channel_check_on_cpu():
+    from mlx_data_amd import data as dx
+
+    v = np.zeros((2, 4, 4, 5), np.uint8)
+    with pytest.raises(RuntimeError, match="verifyVideo: channels must be 0 <= c <= 4"):
+        dx.buffer_from_vector([dict(video=v)]).image_center_crop("video", 2, 2)[0]
