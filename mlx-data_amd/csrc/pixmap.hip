@@ -40,12 +40,18 @@ __device__ void affine_tiles(const PixDev& d) {
   const int32_t tiles_x = (d.groups + kTileGroups - 1) / kTileGroups;
   const int32_t ntiles = tiles_x * ((d.dst_h + kTileRows - 1) / kTileRows);
   const int32_t r = threadIdx.x / kTileGroups, gq = threadIdx.x % kTileGroups;
-  // Gathers read the pixel's bytes with one 8-byte load from the 4-byte
-  // aligned word containing it (from an aligned base); the last bytes of the
-  // image fall back to byte loads so nothing reads past the source.
+  // Gathers: every pixel of the thread's group is read with one unconditional
+  // 12-byte load from a 4-byte aligned word at or before it, clamped to end at
+  // the aligned word holding the source's last byte (a dword never straddles
+  // a page, so that word is always readable); out-of-range pixels read the
+  // first word and are masked.  A thread's four loads are thus in flight
+  // together.  Sources under 12 bytes take byte loads.
   const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(d.src) & ~(uintptr_t)3);
   const int64_t skew = d.src - base;
-  const int64_t limit = skew + (int64_t)(d.src_h - 1) * d.src_stride + (int64_t)d.src_w * C - 8;
+  const int64_t total = skew + (int64_t)(d.src_h - 1) * d.src_stride + (int64_t)d.src_w * C;
+  const int64_t end4 = (total + 3) & ~(int64_t)3;
+  const bool tiny = end4 < 12;
+  const int64_t last = end4 - 12;
   for (int32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int32_t tyb = t / tiles_x;
     const int32_t ty = tyb * kTileRows + r;
@@ -57,31 +63,49 @@ __device__ void affine_tiles(const PixDev& d) {
     const float ey = d.mx[4] * fy;
     uint32_t w[C] = {};
     const int cnt = min(4, d.dst_w - tx0);
+    int64_t off[4];
+    bool ok[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      if (k < cnt) {
-        const float fx = (float)(tx0 + k) - d.twh;
-        const float sx = d.mx[0] * fx + by + d.mx[2];
-        const float sy = d.mx[3] * fx + ey + d.mx[5];
-        // (int64_t) of the double sum, as v_cvt_i32_f64 (truncating; it
-        // saturates only far outside any image, where both are rejected)
-        const int32_t x = __double2int_rz((double)sx + 0.5 + (double)d.wh);
-        const int32_t y = __double2int_rz((double)sy + 0.5 + (double)d.hh);
-        if (x >= 0 && y >= 0 && x < d.src_w && y < d.src_h) {
-          const int64_t o = skew + (int64_t)y * d.src_stride + x * C;
-          const int64_t a = o & ~(int64_t)3;
-          if (a <= limit) {
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(base + a);
-            const uint64_t v = ((uint64_t)q[1] << 32 | q[0]) >> (8 * (o & 3));
+      const float fx = (float)(tx0 + k) - d.twh;
+      const float sx = d.mx[0] * fx + by + d.mx[2];
+      const float sy = d.mx[3] * fx + ey + d.mx[5];
+      // (int64_t) of the double sum, as v_cvt_i32_f64 (truncating; it
+      // saturates only far outside any image, where both are rejected)
+      const int32_t x = __double2int_rz((double)sx + 0.5 + (double)d.wh);
+      const int32_t y = __double2int_rz((double)sy + 0.5 + (double)d.hh);
+      ok[k] = k < cnt && x >= 0 && y >= 0 && x < d.src_w && y < d.src_h;
+      off[k] = ok[k] ? skew + (int64_t)y * d.src_stride + (int64_t)x * C : skew;
+    }
+    if (!tiny) {
+      uint32_t q[4][3];
 #pragma unroll
-            for (int ch = 0; ch < C; ch++) put_byte(w, k * C + ch, (uint32_t)(v >> (8 * ch)) & 255);
-          } else {
-            const uint8_t* p = base + o;
+      for (int k = 0; k < 4; k++) {
+        const int64_t a = min(off[k] & ~(int64_t)3, last);
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(base + a);
+        q[k][0] = p[0];
+        q[k][1] = p[1];
+        q[k][2] = p[2];
+        off[k] -= a;  // byte position of the pixel in the 12 loaded bytes
+      }
 #pragma unroll
-            for (int ch = 0; ch < C; ch++) put_byte(w, k * C + ch, p[ch]);
+      for (int k = 0; k < 4; k++) {
+        if (ok[k]) {
+          const int32_t sh = (int32_t)off[k];
+#pragma unroll
+          for (int ch = 0; ch < C; ch++) {
+            const int32_t bpos = sh + ch;
+            const uint32_t dw = bpos < 4 ? q[k][0] : (bpos < 8 ? q[k][1] : q[k][2]);
+            put_byte(w, k * C + ch, (dw >> (8 * (bpos & 3))) & 255);
           }
         }
       }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (ok[k])
+#pragma unroll
+          for (int ch = 0; ch < C; ch++) put_byte(w, k * C + ch, base[off[k] + ch]);
     }
     uint8_t* out = d.dst + (int64_t)ty * d.dst_stride + (int64_t)tx0 * C;
     if (d.fast && cnt == 4) {
