@@ -253,6 +253,7 @@ PYBIND11_MODULE(_pipeline, m) {
              Sample s;
              {
                py::gil_scoped_release nogil;
+               idx = idx < 0 ? idx + b->size() : idx;  // wrap_buffer.cpp:62
                s = b->get(idx);
              }
              return to_dict(s);
