@@ -9,9 +9,11 @@ for N > 1); every rank processes its own batch (weak scaling, no collective on
 the data path; gloo only for the barrier and the max-over-ranks time);
 `value` = images processed by all ranks / max-over-ranks wall time.
 
-`--workload c3` (configs[2]: 512 mixed 480p-4K images -> 256 -> 224 u8) and
-`--workload c5` (configs[4]: 128 4K frames -> 512 -> random_crop 448 + hflip,
-u8) are the other device-resident configurations; DESIGN.md quotes them.
+`--workload c3` (configs[2]: 512 mixed 480p-4K images -> 256 -> 224 u8),
+`--workload c4` (configs[3], device part: 128 ImageNet-shape images per GPU ->
+256 -> 224 f32; e2e adds the pinned copies) and `--workload c5` (configs[4]:
+128 4K frames -> 512 -> random_crop 448 + hflip, u8) are the other
+device-resident configurations; DESIGN.md quotes them.
 
 Extra fields:
   roofline      HBM roofline of the fused kernel: algorithmic bytes per launch
@@ -53,11 +55,16 @@ WORKLOADS = {
     "c3": dict(batch=512, f32=False,
                desc="C3: 512 RGB u8 in HBM, sizes uniform over {640x480, 1280x720, 1280x960, 1920x1080, 2560x1440, "
                     "3840x2160} (seed 1) -> resize_smallest_side 256 -> center_crop 224, u8"),
+    "c4": dict(batch=128, f32=True,
+               desc="C4 (device part): 128 ImageNet-shape RGB u8 per GPU in HBM, sizes uniform over {500x375, "
+                    "375x500, 500x333} (seed 2) -> resize_smallest_side 256 -> center_crop 224 -> f32/255 "
+                    "(host JPEG decode not included; e2e adds pinned H2D/D2H)"),
     "c5": dict(batch=128, f32=False,
                desc="C5: 128 x 3840x2160 RGB u8 in HBM -> resize_smallest_side 512 -> random_crop 448 -> "
                     "random_h_flip 0.5 (seeded), u8"),
 }
 C3_SIZES = [(640, 480), (1280, 720), (1280, 960), (1920, 1080), (2560, 1440), (3840, 2160)]
+C4_SIZES = [(500, 375), (375, 500), (500, 333)]
 
 
 def footprint_bytes(src_w, src_h, c, rw, rh, cx, cy, cw, ch):
@@ -76,6 +83,9 @@ def make_workload(name, batch, rank):
     elif name == "c3":
         rng = np.random.default_rng(1)
         sizes = [C3_SIZES[i] for i in rng.integers(0, len(C3_SIZES), batch)]
+    elif name == "c4":
+        rng = np.random.default_rng(2)
+        sizes = [C4_SIZES[i] for i in rng.integers(0, len(C4_SIZES), batch)]
     else:
         sizes = [(3840, 2160)] * batch
     rng = np.random.default_rng(3 + rank)
@@ -245,11 +255,13 @@ def main():
     sizes, geoms, f32 = make_workload(args.workload, B, ranks.rank)
     elem = 4 if f32 else 1
 
-    # Sources packed in one device buffer (256-B aligned slots), outputs NHWC.
-    offs, total = [], 0
+    # Sources packed in one device buffer (256-B aligned slots, rows padded to
+    # 16 B as mxd_resize_crop_host stages them), outputs NHWC.
+    offs, pitches, total = [], [], 0
     for (sw, sh) in sizes:
         offs.append(total)
-        total += (sw * C * sh + 255) // 256 * 256 + int(os.environ.get("MXD_BENCH_SLOT_PAD", "0"))
+        pitches.append((sw * C + 15) // 16 * 16)
+        total += (pitches[-1] * sh + 255) // 256 * 256 + int(os.environ.get("MXD_BENCH_SLOT_PAD", "0"))
     out_bytes = [g[4] * g[5] * C * elem for g in geoms]
     out_offs = np.concatenate([[0], np.cumsum(out_bytes)[:-1]]).astype(np.int64)
     rng = np.random.default_rng(1000 + ranks.rank)
@@ -258,16 +270,16 @@ def main():
         host[:] = rng.integers(0, 256, total, dtype=np.uint8)
     else:  # one random 4K frame; every image is a slice of it (timing is data-independent)
         base = rng.integers(0, 256, 2160 * 3840 * C, dtype=np.uint8)
-        for (sw, sh), o in zip(sizes, offs):
-            host[o:o + sw * sh * C] = base[:sw * sh * C]
+        for (sw, sh), o, pt in zip(sizes, offs, pitches):
+            host[o:o + pt * sh] = base[:pt * sh]
     stream = capi.Stream(dev)
     src = capi.DeviceBuffer(total, dev)
     dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
     src.upload(host, stream=stream)
-    entries = [dict(src=src.ptr + o, src_stride=sw * C, src_w=sw, src_h=sh, channels=C,
+    entries = [dict(src=src.ptr + o, src_stride=pt, src_w=sw, src_h=sh, channels=C,
                     resize_w=g[0], resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6],
                     dst=dst.ptr + int(oo), dst_stride=g[4] * C * elem)
-               for (sw, sh), o, g, oo in zip(sizes, offs, geoms, out_offs)]
+               for (sw, sh), o, pt, g, oo in zip(sizes, offs, pitches, geoms, out_offs)]
     imgs, n = capi.make_images(entries)
     L = capi.lib()
     hs = ctypes.c_void_p(stream.handle)
@@ -321,8 +333,41 @@ def main():
         e2e = {"value": round(B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
                "note": f"pinned H2D of the {B} sources ({in_b / 1e6:.1f} MB) + fused kernel + D2H of the outputs "
                        f"({out_b / 1e6:.1f} MB), serialized on one stream"}
+        # Double-buffered: two streams, each with its own device batch, so the
+        # H2D of one batch overlaps the kernel and D2H of the other (PCIe is
+        # full duplex).
+        stream2 = capi.Stream(dev)
+        hs2 = ctypes.c_void_p(stream2.handle)
+        src2 = capi.DeviceBuffer(total, dev)
+        dst2 = capi.DeviceBuffer(out_b, dev)
+        pin_dst2 = ctypes.c_void_p()
+        capi.check(L.mxd_malloc_pinned(ctypes.byref(pin_dst2), ctypes.c_size_t(out_b)))
+        imgs2, _ = capi.make_images([dict(e, src=e["src"] - src.ptr + src2.ptr, dst=e["dst"] - dst.ptr + dst2.ptr)
+                                     for e in entries])
+        sets = ((src, dst, imgs, hs, pin_dst), (src2, dst2, imgs2, hs2, pin_dst2))
+
+        def overlap_step():
+            for s_buf, d_buf, im, h, pd in sets:
+                capi.check(L.mxd_memcpy_h2d_async(ctypes.c_void_p(s_buf.ptr), pin_src, ctypes.c_size_t(in_b), h))
+                capi.check(L.mxd_resize_crop_batch(im, n, mode, dev, h))
+                capi.check(L.mxd_memcpy_d2h_async(pd, ctypes.c_void_p(d_buf.ptr), ctypes.c_size_t(out_b), h))
+
+        overlap_step()
+        stream.synchronize()
+        stream2.synchronize()
+        ta = time.perf_counter()
+        for _ in range(k):
+            overlap_step()
+        stream.synchronize()
+        stream2.synchronize()
+        tb = time.perf_counter()
+        e2e["overlapped"] = {"value": round(2 * B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
+                             "note": "two streams, two device batches: H2D of one overlaps kernel + D2H of the other"}
         capi.check(L.mxd_free_pinned(pin_src))
         capi.check(L.mxd_free_pinned(pin_dst))
+        capi.check(L.mxd_free_pinned(pin_dst2))
+        src2.free()
+        dst2.free()
 
     cpu = None
     if ranks.rank == 0 and ranks.world == 1 and not args.no_cpu and args.workload == "c2":

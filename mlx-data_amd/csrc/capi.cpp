@@ -507,6 +507,16 @@ int env_int(const char* name) {
   return e ? std::atoi(e) : 0;
 }
 
+// The wave path reads through the 4-byte aligned address below `src` and
+// shifts its column bytes by the remainder (a source window at any x, e.g.
+// random_area_crop); rows must stay 4-byte aligned.
+bool wave_layout_ok(const mxd_image& im, int32_t out_dtype) {
+  const uintptr_t o = reinterpret_cast<uintptr_t>(im.dst) | (uintptr_t)im.dst_stride;
+  return (im.src_stride & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
+         (int64_t)(reinterpret_cast<uintptr_t>(im.src) & 3) + (int64_t)im.src_w * im.channels <= im.src_stride &&
+         im.src_stride * im.src_h < ((int64_t)1 << 31);
+}
+
 int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
@@ -522,14 +532,18 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
     const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
     aligned16 = aligned16 && (a & 15) == 0;
-    const uintptr_t o = reinterpret_cast<uintptr_t>(images[i].dst) | (uintptr_t)images[i].dst_stride;
-    // The wave path reads through the 4-byte aligned address below `src` and
-    // shifts its column bytes by the remainder (a source window at any x,
-    // e.g. random_area_crop); rows must stay 4-byte aligned.
-    wave_ok = wave_ok && (images[i].src_stride & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
-              (int64_t)(reinterpret_cast<uintptr_t>(images[i].src) & 3) + (int64_t)images[i].src_w * channels <=
-                  images[i].src_stride &&
-              images[i].src_stride * images[i].src_h < ((int64_t)1 << 31);
+    wave_ok = wave_ok && wave_layout_ok(images[i], out_dtype);
+  }
+  if (!wave_ok) {
+    // Mixed layouts: the images whose rows suit the wave kernels go there, the
+    // rest to the general kernel -- two calls on the same stream (the second
+    // call's descriptor upload is stream-ordered after the first launches).
+    std::vector<mxd_image> fast, slow;
+    for (int32_t i = 0; i < n; i++) (wave_layout_ok(images[i], out_dtype) ? fast : slow).push_back(images[i]);
+    if (!fast.empty() && !slow.empty()) {
+      if (int rc = run_batch(fast.data(), (int32_t)fast.size(), out_dtype, device, stream)) return rc;
+      return run_batch(slow.data(), (int32_t)slow.size(), out_dtype, device, stream);
+    }
   }
   // Kernel-kind switches (tuning, tests) are read on every call.
   const int no_ring = env_int("MXD_NO_RING");

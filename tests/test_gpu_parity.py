@@ -73,6 +73,26 @@ def test_ragged_mixed_resolution_batch():
         check(o, oracle_out(img, g))
 
 
+@pytest.mark.parametrize("f32", [False, True])
+def test_mixed_row_alignment_batch(f32):
+    """Tightly packed rows: 500- and 1280-wide rows stay 4-byte aligned, 375-
+    and 333-wide rows do not -- one call, split between the wave and the
+    general kernels by image."""
+    sizes = [(375, 500), (500, 375), (500, 333), (960, 1280), (200, 333), (375, 500)]
+    imgs = [synth(h, w, 3, 40 + i) for i, (h, w) in enumerate(sizes)]
+    geoms = [center_geom(i) for i in imgs]
+    outs = run_device(imgs, geoms, f32=f32, src_align=1)
+    lut = (np.arange(256, dtype=np.uint8).astype("float32") / 255).view(np.uint32)
+    for img, g, o in zip(imgs, geoms, outs):
+        ref = oracle_out(img, g)
+        if f32:
+            q = np.rint(o * 255).astype(np.uint8)
+            assert np.array_equal(o.view(np.uint32), lut[q])
+            check(q, ref)
+        else:
+            check(o, ref)
+
+
 @pytest.mark.parametrize("c", [1, 2, 3])
 def test_channels_and_unaligned_rows(c):
     img = synth(301, 457, c, c)  # odd width: rows not 16-byte aligned -> byte path
