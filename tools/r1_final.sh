@@ -19,6 +19,7 @@ run pytest 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-me
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 run bench 400 python bench.py
 run bench_c3 300 python bench.py --workload c3 --steps 20 --warmup 3 --no-cpu
+run bench_c4 300 python bench.py --workload c4 --steps 20 --warmup 3 --no-cpu
 run bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu
 run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-e2e --no-copy
 cut -c1-220 gpurun_out/${TAG}_prof/run_kernel_stats.csv
