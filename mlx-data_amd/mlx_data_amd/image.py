@@ -1,4 +1,5 @@
-"""Batched image functions over the C ABI (host numpy in, numpy out).
+"""Batched image functions over the C ABI (host numpy in, numpy out):
+resize+crop (the hot path) and the pixel maps rotate / channel_reduction.
 
 These are the functional counterparts of the reference's per-image
 core::image::{scale, resize, crop, hflip} (mlx/data/core/image/ImageTransform.cpp)
@@ -50,3 +51,42 @@ def resize_smallest_side_center_crop(images, size, cw, ch, out_dtype="uint8", de
         tw, th, x, y = plan_resize_smallest_side_center_crop(w, h, size, cw, ch)
         geoms.append((tw, th, x, y, cw, ch, 0))
     return resize_crop(images, geoms, out_dtype, device)
+
+
+def _pixmap(images, op, params_of, dims_of, out_c, device):
+    entries, outs, keep = [], [], []
+    for img in images:
+        img = np.ascontiguousarray(img, np.uint8)
+        if img.ndim == 2:
+            img = img[:, :, None]
+        h, w, c = img.shape
+        dw, dh = dims_of(w, h)
+        out = np.empty((dh, dw, out_c(c)), np.uint8)
+        keep.append(img)
+        outs.append(out)
+        entries.append(dict(src=img.ctypes.data, src_stride=img.strides[0], src_w=w, src_h=h, channels=c, dst_w=dw,
+                            dst_h=dh, dst=out.ctypes.data, dst_stride=out.strides[0], params=params_of(w, h)))
+    if entries:
+        arr, n = capi.make_pixmaps(entries)
+        capi.pixmap_host(arr, n, op, device)
+    return outs
+
+
+def rotate(images, angle, crop=False, device=0):
+    """core::image::rotate (core/image/ImageTransform.cpp:112-121) of a batch:
+    one pixel-map launch.  Returns a list of uint8 arrays."""
+    geo = {}
+
+    def g(w, h):
+        if (w, h) not in geo:
+            geo[(w, h)] = capi.rotate_geometry(w, h, angle, crop)
+        return geo[(w, h)]
+
+    return _pixmap(images, capi.MXD_AFFINE, lambda w, h: g(w, h)[0], lambda w, h: g(w, h)[1:], lambda c: c, device)
+
+
+def channel_reduction(images, preset="default", device=0):
+    """core::image::channel_reduction (core/image/ImageTransform.cpp:142-180)
+    of a batch of RGB images: one launch.  Returns (H, W, 1) uint8 arrays."""
+    p = capi.channel_reduction_preset(preset)
+    return _pixmap(images, capi.MXD_CHANNEL_REDUCTION, lambda w, h: p, lambda w, h: (w, h), lambda c: 1, device)

@@ -149,3 +149,15 @@ def test_pipeline_rotate_and_gray():
     base = np.asarray(b.image_resize_smallest_side("image", 256).image_center_crop("image", 224, 224)[0]["image"])
     got = np.asarray(c[0]["image"])
     assert np.array_equal(got, O.rotate(base, 45.0, True))
+
+
+def test_functional_batch_api():
+    from mlx_data_amd import image
+
+    rng = np.random.default_rng(15)
+    imgs = [rng.integers(0, 256, s, dtype=np.uint8) for s in [(37, 53, 3), (64, 48, 3), (120, 90, 3)]]
+    for a, crop in [(30.0, False), (-12.5, True)]:
+        for got, img in zip(image.rotate(imgs, a, crop), imgs):
+            assert np.array_equal(got, O.rotate(img, a, crop))
+    for got, img in zip(image.channel_reduction(imgs, "rec2020"), imgs):
+        assert np.array_equal(got, O.channel_reduction(img, "rec2020"))
