@@ -4,35 +4,46 @@ Default workload (BASELINE.json configs[1], the metric's configuration): a batch
 of 256 synthetic 1280x960 RGB uint8 images already resident in HBM ->
 image_resize_smallest_side(256) -> image_center_crop(224, 224) -> float32 / 255,
 one fused kernel launch per step over the whole batch (one "step" = one pass
-of the hot path over one batch).  One process per GPU (torch.distributed.run
-for N > 1); every rank processes its own batch (weak scaling, no collective on
-the data path; gloo only for the barrier and the max-over-ranks time);
-`value` = images processed by all ranks / max-over-ranks wall time.
+of the hot path over one batch).  Two source sets and two output batches
+alternate step by step (different HBM addresses), so no step re-reads bytes
+the previous one left in the 256 MiB Infinity Cache.
+
+Multi-GPU: one process per GPU.  `--gpus N` without a launcher spawns N rank
+processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
+environment, before any GPU call); under torch.distributed.run the ranks come
+from the environment.  Every rank processes its own batch on its own device
+(weak scaling, no collective on the data path; gloo only for the barrier and
+the max-over-ranks time); `value` = images of all ranks / max-over-ranks wall.
 
 `--workload c3` (configs[2]: 512 mixed 480p-4K images -> 256 -> 224 u8),
 `--workload c4` (configs[3], device part: 128 ImageNet-shape images per GPU ->
-256 -> 224 f32; e2e adds the pinned copies) and `--workload c5` (configs[4]:
-128 4K frames -> 512 -> random_crop 448 + hflip, u8) are the other
-device-resident configurations; DESIGN.md quotes them.
+256 -> 224 f32) and `--workload c5` (configs[4]: 128 4K frames -> 512 ->
+random_crop 448 + hflip, u8) are the other device-resident configurations;
+DESIGN.md quotes them.
 
 Extra fields:
   roofline      HBM roofline of the fused kernel: algorithmic bytes per launch
                 (source footprint the kept window depends on + output bytes, per
                 image, summed over the batch) / average launch time from HIP
                 events recorded on the kernel's own stream; `traffic` = HBM bytes
-                per launch from the committed rocprofv3 PMC summary
-                (profiles/**/*<workload>*pmc*.json, tools/pmc_traffic.py).
+                per launch from the PMC summary recorded for this workload in
+                profiles/traffic.json; `copy_ceiling_gbs` = the measured
+                streaming-copy rate of this box.
   cpu_baseline  the oracle's C restatement of the reference CPU path
                 (stbir-semantics resize -> crop -> batch -> numpy /255) on a
-                bounded sample, on this host's cores (rank 0, N = 1, c2 only).
-  e2e           the same batch including pinned H2D of the sources and D2H of
-                the outputs (PCIe-inclusive rate; never `value`).
+                bounded sample at 1, 8 and all of this rank's cores (rank 0,
+                N = 1, c2 only), with Pillow BILINEAR as an independent CPU point.
+  e2e           the product's host-resident path (mxd_resize_crop_host: host
+                images in, host batch out, pinned staging of each image's
+                source footprint, H2D / kernel / D2H overlapped in chunks):
+                the PCIe-inclusive rate, never `value`.
 """
 import argparse
 import ctypes
-import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -41,8 +52,6 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mlx-data_amd"))
 
 import numpy as np  # noqa: E402
-
-from mlx_data_amd import capi  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 C = 3
@@ -58,7 +67,7 @@ WORKLOADS = {
     "c4": dict(batch=128, f32=True,
                desc="C4 (device part): 128 ImageNet-shape RGB u8 per GPU in HBM, sizes uniform over {500x375, "
                     "375x500, 500x333} (seed 2) -> resize_smallest_side 256 -> center_crop 224 -> f32/255 "
-                    "(host JPEG decode not included; e2e adds pinned H2D/D2H)"),
+                    "(host JPEG decode not included; e2e adds the host path)"),
     "c5": dict(batch=128, f32=False,
                desc="C5: 128 x 3840x2160 RGB u8 in HBM -> resize_smallest_side 512 -> random_crop 448 -> "
                     "random_h_flip 0.5 (seeded), u8"),
@@ -67,7 +76,7 @@ C3_SIZES = [(640, 480), (1280, 720), (1280, 960), (1920, 1080), (2560, 1440), (3
 C4_SIZES = [(500, 375), (375, 500), (500, 333)]
 
 
-def footprint_bytes(src_w, src_h, c, rw, rh, cx, cy, cw, ch):
+def footprint_bytes(capi, src_w, src_h, c, rw, rh, cx, cy, cw, ch):
     """Source bytes the kept window depends on (rows x cols of the tap footprint)."""
     fx, nx, _ = capi.axis_taps(src_w, rw, cx, cw)
     fy, ny, _ = capi.axis_taps(src_h, rh, cy, ch)
@@ -76,7 +85,7 @@ def footprint_bytes(src_w, src_h, c, rw, rh, cx, cy, cw, ch):
     return rows * cols * c
 
 
-def make_workload(name, batch, rank):
+def make_workload(capi, name, batch, rank):
     """(sizes [(w, h)], geoms [(rw, rh, cx, cy, cw, ch, flip)], f32) for one rank."""
     if name == "c2":
         sizes = [(1280, 960)] * batch
@@ -103,67 +112,106 @@ def make_workload(name, batch, rank):
 
 
 def load_traffic(workload):
-    """HBM bytes per launch measured for this workload's kernel (committed PMC summary)."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", f"*{workload}*pmc*.json"), recursive=True))
-    if not files:
-        return None
+    """HBM bytes per launch measured for this workload's kernel: the record
+    profiles/traffic.json names for it (file, tag and corrected bytes)."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
     try:
-        with open(files[-1]) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except Exception:
+        with open(path) as f:
+            rec = json.load(f).get(workload)
+    except (OSError, ValueError):
         return None
+    return None if rec is None else rec.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(threads, sample):
-    """Reference-algorithm CPU restatement (oracle) on `threads` host threads, C2 shapes."""
+def host_cores():
+    """Cores this rank may use: the box's per-GPU CPU share when OMP_NUM_THREADS
+    states it, else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return min(int(env), len(os.sched_getaffinity(0)))
+    return len(os.sched_getaffinity(0))
+
+
+def _pool_rate(threads, total, work):
+    """Images/s of `work(batch_index)` over `total` batches on `threads` threads
+    (each task builds a whole batch, like stream/Prefetch.cpp:29-56)."""
+    nxt = [0]
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                b = nxt[0]
+                nxt[0] += 1
+            if b >= total:
+                return
+            work(b)
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(sample_per_thread=24):
+    """Reference-algorithm CPU restatement (oracle C code, GIL released) on C2
+    shapes, at 1, 8 and all of this rank's cores, plus Pillow BILINEAR."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
     lib = O.lib()
     u8p = ctypes.POINTER(ctypes.c_uint8)
     rng = np.random.default_rng(123)
-    srcs = [rng.integers(0, 256, (960, 1280, C), dtype=np.uint8) for _ in range(min(16, sample))]
-    per_batch = 32
-    nb = sample // per_batch
+    srcs = [rng.integers(0, 256, (960, 1280, C), dtype=np.uint8) for _ in range(8)]
+    per_batch = 8
 
-    def work(bidx, out):
+    def port_batch(b):
         crops = np.empty((per_batch, 224, 224, C), np.uint8)
         for i in range(per_batch):
-            s = srcs[(bidx * per_batch + i) % len(srcs)]
+            s = srcs[(b * per_batch + i) % len(srcs)]
             rc = lib.orc_resize_smallest_side_center_crop(s.ctypes.data_as(u8p), 1280, 960, C, 256, 224, 224,
                                                           crops[i].ctypes.data_as(u8p))
             assert rc == 0
-        batch = O.batch(list(crops), 0)
-        out[bidx] = batch.astype("float32") / 255
+        return O.batch(list(crops), 0).astype("float32") / 255
 
-    outs = [None] * nb
-    t0 = time.perf_counter()
-    next_b = [0]
-    lock = threading.Lock()
+    cores = host_cores()
+    points = {}
+    for n in sorted({1, min(8, cores), cores}):
+        nb = max(1, n * sample_per_thread // per_batch)
+        dt = _pool_rate(n, nb, port_batch)
+        points[str(n)] = round(nb * per_batch / dt, 2)
+    pil = None
+    try:
+        from PIL import Image
 
-    def worker():
-        while True:
-            with lock:
-                b = next_b[0]
-                next_b[0] += 1
-            if b >= nb:
-                return
-            work(b, outs)
+        pims = [Image.fromarray(s) for s in srcs]
 
-    ts = [threading.Thread(target=worker) for _ in range(threads)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    dt = time.perf_counter() - t0
-    return {"value": round(nb * per_batch / dt, 2), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{nb * per_batch} images 1280x960 -> resize 256 -> crop 224 -> batch {per_batch} -> f32/255 "
-                      f"(oracle C restatement of stbir + numpy normalize, {threads} threads, GIL released in C)"}
+        def pil_batch(b):
+            out = np.empty((per_batch, 224, 224, C), np.uint8)
+            for i in range(per_batch):
+                r = pims[(b * per_batch + i) % len(pims)].resize((341, 256), Image.BILINEAR)
+                out[i] = np.asarray(r)[16:240, 58:282]
+            return out.astype("float32") / 255
+
+        nb = max(1, cores * sample_per_thread // per_batch)
+        dt = _pool_rate(cores, nb, pil_batch)
+        pil = round(nb * per_batch / dt, 2)
+    except ImportError:
+        pass
+    return {"value": points[str(cores)], "unit": "images/s", "cores": cores, "kind": "port",
+            "points": points, "pillow_bilinear": pil,
+            "sample": f"C2 shapes (1280x960 -> resize 256 -> crop 224 -> batch {per_batch} -> f32/255), "
+                      f"{sample_per_thread} images per thread per point; oracle C restatement of stbir + numpy "
+                      f"normalize, threads = cores; pillow_bilinear = Pillow resize(BILINEAR) + crop + /255 "
+                      f"on all cores (independent CPU point)"}
 
 
 class Ranks:
     """Rank bookkeeping: one process per GPU, gloo for the barrier and the
-    max-over-ranks time only (no collective on the data path)."""
+    max-over-ranks time only (no collective on the data path, no torch GPU use)."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,8 +251,8 @@ def timed_steps(ranks, step, sync, steps):
     ranks.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    for i in range(steps):
+        step(i)
     sync()
     t1 = time.perf_counter()
     ranks.barrier()
@@ -227,11 +275,37 @@ def bench_line(workload, world, batch, steps, warmup, wall, roofline, cpu, e2e):
         "dtype": "u8->f32" if w["f32"] else "u8",
         "data": "synthetic (seeded uniform random uint8 RGB, resident in HBM)",
         "config": {"workload": w["desc"], "global_batch": world * batch, "per_gpu_batch": batch,
-                   "parallelism": f"replicas x{world} (no collective)"},
+                   "parallelism": f"dp{world} (one process per GPU, batch per rank, no collective)"},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "e2e": e2e,
     }
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """--gpus N without a launcher: N rank processes of this script, one per
+    GPU, started before this process touches any GPU.  Rank 0's stdout (the
+    JSON line) passes through; the exit code is the first failing rank's."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    return rc
 
 
 def main():
@@ -243,25 +317,41 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (default: the workload's)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-copy", action="store_true")
+    # timing plumbing without a GPU (tests/test_bench_dist.py): each step sleeps
+    ap.add_argument("--simulate", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    capi.lib()  # bind /opt/rocm's HIP runtime before torch (which bundles its own) loads
-    ranks = Ranks()
-    dev = ranks.local
-    capi.check(capi.lib().mxd_set_device(dev))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+
     B = args.batch or WORKLOADS[args.workload]["batch"]
-    sizes, geoms, f32 = make_workload(args.workload, B, ranks.rank)
+    if args.simulate > 0:
+        ranks = Ranks()
+        wall, _ = timed_steps(ranks, lambda i: time.sleep(args.simulate * (1 + ranks.rank)), lambda: None,
+                              args.steps)
+        if ranks.rank == 0:
+            print(json.dumps(bench_line(args.workload, ranks.world, B, args.steps, args.warmup, wall, None, None,
+                                        None)), flush=True)
+        ranks.close()
+        return
+
+    from mlx_data_amd import capi
+
+    capi.lib()  # bind /opt/rocm's HIP runtime first (torch, for gloo, bundles its own)
+    ranks = Ranks()
+    dev = int(os.environ.get("MXD_BENCH_DEVICE", ranks.local))  # rehearsal: several ranks on one GPU
+    capi.check(capi.lib().mxd_set_device(dev))
+    sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank)
     elem = 4 if f32 else 1
 
-    # Sources packed in one device buffer (256-B aligned slots, rows padded to
-    # 16 B as mxd_resize_crop_host stages them), outputs NHWC.
+    # Sources packed in one device buffer per set (256-B aligned slots, rows
+    # padded to 16 B), outputs NHWC; two sets alternate step by step.
     offs, pitches, total = [], [], 0
     for (sw, sh) in sizes:
         offs.append(total)
         pitches.append((sw * C + 15) // 16 * 16)
-        total += (pitches[-1] * sh + 255) // 256 * 256 + int(os.environ.get("MXD_BENCH_SLOT_PAD", "0"))
+        total += (pitches[-1] * sh + 255) // 256 * 256
     out_bytes = [g[4] * g[5] * C * elem for g in geoms]
     out_offs = np.concatenate([[0], np.cumsum(out_bytes)[:-1]]).astype(np.int64)
     rng = np.random.default_rng(1000 + ranks.rank)
@@ -273,23 +363,27 @@ def main():
         for (sw, sh), o, pt in zip(sizes, offs, pitches):
             host[o:o + pt * sh] = base[:pt * sh]
     stream = capi.Stream(dev)
-    src = capi.DeviceBuffer(total, dev)
-    dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
-    src.upload(host, stream=stream)
-    entries = [dict(src=src.ptr + o, src_stride=pt, src_w=sw, src_h=sh, channels=C,
-                    resize_w=g[0], resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6],
-                    dst=dst.ptr + int(oo), dst_stride=g[4] * C * elem)
-               for (sw, sh), o, pt, g, oo in zip(sizes, offs, pitches, geoms, out_offs)]
-    imgs, n = capi.make_images(entries)
+    mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
     L = capi.lib()
     hs = ctypes.c_void_p(stream.handle)
-    mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
+    sets = []
+    for _ in range(2):
+        src = capi.DeviceBuffer(total, dev)
+        dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
+        src.upload(host, stream=stream)
+        entries = [dict(src=src.ptr + o, src_stride=pt, src_w=sw, src_h=sh, channels=C,
+                        resize_w=g[0], resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6],
+                        dst=dst.ptr + int(oo), dst_stride=g[4] * C * elem)
+                   for (sw, sh), o, pt, g, oo in zip(sizes, offs, pitches, geoms, out_offs)]
+        imgs, n = capi.make_images(entries)
+        sets.append((src, dst, imgs, n))
 
-    def step():
+    def step(i):
+        _, _, imgs, n = sets[i & 1]
         capi.check(L.mxd_resize_crop_batch(imgs, n, mode, dev, hs))
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     e0, e1 = capi.Event(), capi.Event()
     stream.synchronize()
     e0.record(stream)
@@ -300,83 +394,57 @@ def main():
     # barrier and host syncs between them add no device work).
     kernel_ms = e0.elapsed_ms(e1) / args.steps
 
-    alg_bytes = sum(footprint_bytes(sw, sh, C, *g[:6]) for (sw, sh), g in zip(sizes, geoms)) + sum(out_bytes)
+    alg_bytes = sum(footprint_bytes(capi, sw, sh, C, *g[:6]) for (sw, sh), g in zip(sizes, geoms)) + sum(out_bytes)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     copy_gbs = capi.copy_bandwidth(1 << 30, dev, 20) if not args.no_copy else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.workload),
                 "alg_bytes_per_launch": int(alg_bytes), "alg_bytes_per_image": round(alg_bytes / B, 1),
                 "kernel_ms_per_launch": round(kernel_ms, 5),
-                "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None}
+                "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
+                "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None}
 
     e2e = None
     if not args.no_e2e and ranks.world == 1:
-        in_b, out_b = total, int(sum(out_bytes))
-        pin_src, pin_dst = ctypes.c_void_p(), ctypes.c_void_p()
-        capi.check(L.mxd_malloc_pinned(ctypes.byref(pin_src), ctypes.c_size_t(in_b)))
-        capi.check(L.mxd_malloc_pinned(ctypes.byref(pin_dst), ctypes.c_size_t(out_b)))
-        ctypes.memmove(pin_src, host.ctypes.data, in_b)
-        k = max(3, args.steps // 10)
-
-        def e2e_step():
-            capi.check(L.mxd_memcpy_h2d_async(ctypes.c_void_p(src.ptr), pin_src, ctypes.c_size_t(in_b), hs))
-            step()
-            capi.check(L.mxd_memcpy_d2h_async(pin_dst, ctypes.c_void_p(dst.ptr), ctypes.c_size_t(out_b), hs))
-
-        e2e_step()
-        stream.synchronize()
-        ta = time.perf_counter()
-        for _ in range(k):
-            e2e_step()
-        stream.synchronize()
-        tb = time.perf_counter()
-        e2e = {"value": round(B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
-               "note": f"pinned H2D of the {B} sources ({in_b / 1e6:.1f} MB) + fused kernel + D2H of the outputs "
-                       f"({out_b / 1e6:.1f} MB), serialized on one stream"}
-        # Double-buffered: two streams, each with its own device batch, so the
-        # H2D of one batch overlaps the kernel and D2H of the other (PCIe is
-        # full duplex).
-        stream2 = capi.Stream(dev)
-        hs2 = ctypes.c_void_p(stream2.handle)
-        src2 = capi.DeviceBuffer(total, dev)
-        dst2 = capi.DeviceBuffer(out_b, dev)
-        pin_dst2 = ctypes.c_void_p()
-        capi.check(L.mxd_malloc_pinned(ctypes.byref(pin_dst2), ctypes.c_size_t(out_b)))
-        imgs2, _ = capi.make_images([dict(e, src=e["src"] - src.ptr + src2.ptr, dst=e["dst"] - dst.ptr + dst2.ptr)
-                                     for e in entries])
-        sets = ((src, dst, imgs, hs, pin_dst), (src2, dst2, imgs2, hs2, pin_dst2))
-
-        def overlap_step():
-            for s_buf, d_buf, im, h, pd in sets:
-                capi.check(L.mxd_memcpy_h2d_async(ctypes.c_void_p(s_buf.ptr), pin_src, ctypes.c_size_t(in_b), h))
-                capi.check(L.mxd_resize_crop_batch(im, n, mode, dev, h))
-                capi.check(L.mxd_memcpy_d2h_async(pd, ctypes.c_void_p(d_buf.ptr), ctypes.c_size_t(out_b), h))
-
-        overlap_step()
-        stream.synchronize()
-        stream2.synchronize()
-        ta = time.perf_counter()
-        for _ in range(k):
-            overlap_step()
-        stream.synchronize()
-        stream2.synchronize()
-        tb = time.perf_counter()
-        e2e["overlapped"] = {"value": round(2 * B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
-                             "note": "two streams, two device batches: H2D of one overlaps kernel + D2H of the other"}
-        capi.check(L.mxd_free_pinned(pin_src))
-        capi.check(L.mxd_free_pinned(pin_dst))
-        capi.check(L.mxd_free_pinned(pin_dst2))
-        src2.free()
-        dst2.free()
+        e2e = e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev)
 
     cpu = None
     if ranks.rank == 0 and ranks.world == 1 and not args.no_cpu and args.workload == "c2":
-        cpu = cpu_baseline(min(16, os.cpu_count() or 1), args.cpu_sample)
+        cpu = cpu_baseline()
 
+    for src, dst, _, _ in sets:
+        src.free()
+        dst.free()
     if ranks.rank == 0:
         print(json.dumps(bench_line(args.workload, ranks.world, B, args.steps, args.warmup, wall, roofline, cpu,
                                     e2e)), flush=True)
     ranks.close()
+
+
+def e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev):
+    """The product host path (mxd_resize_crop_host): host sources in, host
+    batch out, synchronous per call."""
+    elem = 4 if f32 else 1
+    outs = np.empty(sum(g[4] * g[5] * C for g in geoms), np.float32 if f32 else np.uint8)
+    o = 0
+    entries = []
+    for (sw, sh), so, pt, g in zip(sizes, offs, pitches, geoms):
+        entries.append(dict(src=host.ctypes.data + so, src_stride=pt, src_w=sw, src_h=sh, channels=C,
+                            resize_w=g[0], resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5],
+                            flip=g[6], dst=outs.ctypes.data + o * elem, dst_stride=g[4] * C * elem))
+        o += g[4] * g[5] * C
+    imgs, n = capi.make_images(entries)
+    mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
+    capi.resize_crop_host(imgs, n, mode, dev)
+    k = max(3, args.steps // 10)
+    ta = time.perf_counter()
+    for _ in range(k):
+        capi.resize_crop_host(imgs, n, mode, dev)
+    tb = time.perf_counter()
+    B = len(sizes)
+    return {"value": round(B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
+            "note": "mxd_resize_crop_host: pinned staging of each image's source footprint, H2D / fused kernel / "
+                    "D2H overlapped over chunks of the batch, host batch out; synchronous per call"}
 
 
 if __name__ == "__main__":

@@ -105,6 +105,20 @@ int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t c
  * device memory.  Asynchronous: returns once the work is enqueued. */
 int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream);
 
+/* Kernel policy: a process-wide switch between kernels that compute
+ * bit-identical results (for tests and tuning; default 0 = automatic choice).
+ * MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
+ * of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
+ * general workgroup-tile kernel.  Returns the previous policy. */
+enum mxd_policy { MXD_POLICY_AUTO = 0, MXD_POLICY_NO_SCATTER = 1, MXD_POLICY_NO_WAVE = 2 };
+int mxd_set_kernel_policy(int32_t policy);
+
+/* The kernel mxd_resize_crop_batch would run for one image on `device`
+ * (diagnostics, tests): info[0] = 1 wave kernel / 0 general kernel, then kind
+ * (0 gather, 2 scatter), tap bucket, scatter S, scatter DMAX, output pixels
+ * per lane, strips, source pixels per lane.  Host only: needs no device. */
+int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device, int32_t* info8);
+
 /* Measured device-memory ceiling: a 16-byte-per-lane streaming copy of `bytes`
  * (read + write counted), averaged over `iters` launches, in GB/s. */
 int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps);

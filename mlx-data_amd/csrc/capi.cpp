@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -67,6 +68,8 @@ struct DevTable {
 
 class TableCache {
  public:
+  // upload = false: host copies only (ptr stays null), for planning without a device.
+  explicit TableCache(bool upload = true) : upload_(upload) {}
   int get(int32_t device, int32_t in, int32_t out, const DevTable** out_tab) {
     std::lock_guard<std::mutex> lock(mu_);
     auto key = std::make_tuple(device, in, out);
@@ -93,70 +96,29 @@ class TableCache {
     tab->first = taps.first;
     tab->count = taps.count;
     tab->w = taps.weight;
-    DeviceGuard g(device);
-    MXD_HIP(hipMalloc(&tab->ptr, host.size() * sizeof(float)));
-    MXD_HIP(hipMemcpy(tab->ptr, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (upload_) {
+      DeviceGuard g(device);
+      MXD_HIP(hipMalloc(&tab->ptr, host.size() * sizeof(float)));
+      MXD_HIP(hipMemcpy(tab->ptr, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     *out_tab = tab.get();
     map_[key] = std::move(tab);
     return MXD_OK;
   }
 
  private:
+  bool upload_;
   std::mutex mu_;
   std::map<std::tuple<int32_t, int32_t, int32_t>, std::unique_ptr<DevTable>> map_;
 };
 
-// Right-aligned vertical tables for the ring kernel: per output row
-// {last tap row, tap count, w[T]} with the weights aligned so that w[T-1]
-// belongs to the last tap row (zeros in front).  Keyed by (device, in, out, T).
-class RightTableCache {
- public:
-  int get(int32_t device, const DevTable& base, int32_t in, int32_t out, int32_t t, const DevTable** out_tab) {
-    std::lock_guard<std::mutex> lock(mu_);
-    auto key = std::make_tuple(device, in, out, t);
-    auto it = map_.find(key);
-    if (it != map_.end()) {
-      *out_tab = it->second.get();
-      return MXD_OK;
-    }
-    mxd::AxisTaps taps;
-    if (!mxd::build_axis_taps(in, out, 0, out, &taps) || taps.width > t)
-      return fail(MXD_ERR_INVALID, "mxd: right-aligned table geometry");
-    const int32_t padded = std::max<int32_t>(t, mxd::kMinTabWidth);
-    const int32_t stride = mxd::kTapHeader + padded;
-    std::vector<float> host((size_t)out * stride, 0.0f);
-    for (int32_t i = 0; i < out; i++) {
-      float* e = &host[(size_t)i * stride];
-      const int32_t last = taps.first[i] + taps.count[i] - 1;
-      std::memcpy(&e[0], &last, 4);
-      std::memcpy(&e[1], &taps.count[i], 4);
-      std::memcpy(&e[2 + (t - taps.count[i])], &taps.weight[(size_t)i * taps.width], sizeof(float) * taps.count[i]);
-    }
-    auto tab = std::make_unique<DevTable>();
-    tab->width = taps.width;
-    tab->padded = padded;
-    tab->first = base.first;
-    tab->count = base.count;
-    DeviceGuard g(device);
-    MXD_HIP(hipMalloc(&tab->ptr, host.size() * sizeof(float)));
-    MXD_HIP(hipMemcpy(tab->ptr, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
-    *out_tab = tab.get();
-    map_[key] = std::move(tab);
-    return MXD_OK;
-  }
-
- private:
-  std::mutex mu_;
-  std::map<std::tuple<int32_t, int32_t, int32_t, int32_t>, std::unique_ptr<DevTable>> map_;
-};
-
-RightTableCache& right_tables() {
-  static RightTableCache* c = new RightTableCache();
+TableCache& tables() {
+  static TableCache* c = new TableCache();  // leaked on purpose: outlives static teardown
   return *c;
 }
 
-TableCache& tables() {
-  static TableCache* c = new TableCache();  // leaked on purpose: outlives static teardown
+TableCache& host_tables() {
+  static TableCache* c = new TableCache(false);
   return *c;
 }
 
@@ -272,12 +234,17 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
 struct ImgPlan {
   const DevTable* xt = nullptr;
   const DevTable* yt = nullptr;
-  int32_t bucket = -1;   // wave path tap bucket, -1 = not eligible
-  int32_t kind = 0;      // wave kernel: 0 gather, 1 register ring, 2 scatter, 3 band
+  bool wave = false;     // runs on a wave kernel (wave.hip), else the general tile kernel
+  int32_t bucket = -1;   // wave kernel tap bucket
+  int32_t kind = 0;      // wave kernel: 0 gather, 2 scatter
   int32_t s = 0, dmax = 0, p = 0;  // scatter shape (ScatterShape)
-  const DevTable* yr = nullptr;    // ring: right-aligned vertical table
-  int32_t nstrips = 0, tx = 0;
+  int32_t nstrips = 0, tx = 0, q = 0, shift = 0;
+  int32_t pp = 0;  // source pixels per lane
 };
+
+// Kernel policy (mxd_set_kernel_policy): a process-wide tuning / test switch
+// between kernels that compute identical results.
+std::atomic<int32_t> g_policy{0};
 
 // Shape of the scatter schedule for crop rows [off, off+len) of a vertical
 // table, valid for bands starting at any row: dmax = most source rows that are
@@ -417,42 +384,37 @@ SchedCache& schedules() {
   return *c;
 }
 
-// Wave path strips: strip_cols a multiple of 4 (so every strip's first output
-// element is 16-byte aligned), strip_cols*C <= wave_max_outputs() and <=
-// wave_row_bytes() of source footprint (the kernel's 4-byte fb0 alignment
-// included).
-bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t* nstrips, int32_t* tx) {
-  const int32_t c = im.channels, row = mxd::wave_row_bytes();
-  const int32_t max_tx = mxd::wave_max_outputs() / c / 4 * 4;
-  for (int32_t ns = (im.crop_w + max_tx - 1) / max_tx; ns <= im.crop_w; ns++) {
-    const int32_t t = std::min(im.crop_w, ((im.crop_w + ns - 1) / ns + 3) & ~3);
-    bool ok = t * c <= mxd::wave_max_outputs();
-    for (int32_t ox0 = 0; ox0 < im.crop_w && ok; ox0 += t) {
-      const int32_t ox1 = std::min(ox0 + t, im.crop_w);
-      const int32_t xa = im.flip ? im.crop_w - ox1 : ox0;
-      const int32_t xb = im.flip ? im.crop_w - 1 - ox0 : ox1 - 1;
-      const int32_t lo = xt.first[im.crop_x + xa];
-      const int32_t hi = xt.first[im.crop_x + xb] + xt.count[im.crop_x + xb] - 1;
-      const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(im.src) & 3);
-      const int32_t fb0 = (lo * c + shift) & ~3;
-      ok = (hi + 1) * c + shift - fb0 <= row;
+// Wave path strips: q output pixels per lane (strip_cols <= 64 q) and every
+// strip's source window (start aligned down to wave_window_align()) within
+// wave_window_px() pixels.  Fewest strips first (least halo re-reading and
+// fewest units), then the smallest q.
+bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t pp, int32_t* nstrips, int32_t* tx, int32_t* q) {
+  const int32_t c = im.channels, wpx = mxd::wave_window_px(c, pp), al = mxd::wave_window_align(c);
+  int32_t best = 0;
+  for (int32_t qq : {1, 2, 4}) {
+    const int32_t max_tx = mxd::wave_lanes() * qq;
+    for (int32_t ns = (im.crop_w + max_tx - 1) / max_tx; ns <= im.crop_w && (best == 0 || ns < best); ns++) {
+      const int32_t t = (im.crop_w + ns - 1) / ns;
+      if ((im.crop_w + t - 1) / t != ns) continue;  // equal strips of t columns give another count
+      bool ok = true;
+      for (int32_t ox0 = 0; ox0 < im.crop_w && ok; ox0 += t) {
+        const int32_t ox1 = std::min(ox0 + t, im.crop_w);
+        const int32_t xa = im.flip ? im.crop_w - ox1 : ox0;
+        const int32_t xb = im.flip ? im.crop_w - 1 - ox0 : ox1 - 1;
+        const int32_t lo = xt.first[im.crop_x + xa] & ~(al - 1);
+        const int32_t hi = xt.first[im.crop_x + xb] + xt.count[im.crop_x + xb] - 1;
+        ok = hi + 1 - lo <= wpx;
+      }
+      if (ok) {
+        best = ns;
+        *nstrips = ns;
+        *tx = t;
+        *q = qq;
+        break;
+      }
     }
-    if (ok) {
-      *nstrips = (im.crop_w + t - 1) / t;
-      *tx = t;
-      return true;
-    }
-    if (t <= 4) break;
   }
-  return false;
-}
-
-// The ring kernel closes at most one output row per source row: the last taps
-// of consecutive output rows in the window must strictly increase.
-bool one_output_per_row(const DevTable& yt, int32_t off, int32_t len) {
-  for (int32_t y = off; y + 1 < off + len; y++)
-    if (yt.first[y + 1] + yt.count[y + 1] <= yt.first[y] + yt.count[y]) return false;
-  return true;
+  return best > 0;
 }
 
 // Output rows per wave unit.  The units of one launch all do about the same
@@ -460,14 +422,8 @@ bool one_output_per_row(const DevTable& yt, int32_t off, int32_t len) {
 // wave slots: a last round that is only partly filled leaves the HBM queue
 // short of loads while it drains.  Pick the fewest rounds whose band height
 // stays <= kMaxBand, then the smallest band height whose unit count fits them.
-// MXD_BAND_ROWS overrides (tuning).
 int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_t capacity) {
   constexpr int32_t kMinBand = 8, kMaxBand = 64;
-  static const int forced = [] {
-    const char* e = std::getenv("MXD_BAND_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced > 0) return forced;
   int64_t rows = 0;
   int32_t max_h = 1;
   for (auto& s : strips) {
@@ -491,8 +447,9 @@ int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_
 
 int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, int, int, int, int>, int32_t> cache;
-  const auto key = std::make_tuple(device, cfg.channels, cfg.f32, cfg.taps, cfg.kind, cfg.s, cfg.dmax, cfg.mode);
+  static std::map<std::tuple<int, int, int, int, int, int, int, int, int, int>, int32_t> cache;
+  const auto key =
+      std::make_tuple(device, cfg.channels, cfg.f32, cfg.taps, cfg.kind, cfg.s, cfg.dmax, cfg.q, cfg.shift, cfg.p);
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
@@ -502,19 +459,61 @@ int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
   return c;
 }
 
-int env_int(const char* name) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : 0;
-}
-
 // The wave path reads through the 4-byte aligned address below `src` and
 // shifts its column bytes by the remainder (a source window at any x, e.g.
-// random_area_crop); rows must stay 4-byte aligned.
+// random_area_crop); rows must stay 4-byte aligned.  f32 outputs are stored
+// per pixel (4-byte aligned), u8 outputs per byte.
 bool wave_layout_ok(const mxd_image& im, int32_t out_dtype) {
   const uintptr_t o = reinterpret_cast<uintptr_t>(im.dst) | (uintptr_t)im.dst_stride;
-  return (im.src_stride & 3) == 0 && (o & (out_dtype == MXD_F32_DIV255 ? 15 : 3)) == 0 &&
+  return im.channels <= 3 && (im.src_stride & 3) == 0 && (out_dtype != MXD_F32_DIV255 || (o & 3) == 0) &&
          (int64_t)(reinterpret_cast<uintptr_t>(im.src) & 3) + (int64_t)im.src_w * im.channels <= im.src_stride &&
-         im.src_stride * im.src_h < ((int64_t)1 << 31);
+         im.src_stride * (int64_t)im.src_h < ((int64_t)1 << 31);
+}
+
+// Chooses the wave kernel of one image (p.wave = false: the general kernel):
+// over the lane widths available for its channel count, the one that cuts
+// the crop into the fewest strips (narrow strips read more halo and more,
+// shorter row pieces), then the narrower lane width.
+void plan_wave(const mxd_image& im, int32_t f32, int32_t out_dtype, ImgPlan& p) {
+  p.wave = false;
+  if (!wave_layout_ok(im, out_dtype)) return;
+  const int32_t c = im.channels;
+  const int32_t shift = (reinterpret_cast<uintptr_t>(im.src) & 3) != 0 ? 1 : 0;
+  // Scatter when the vertical axis downsamples into a shape with a kernel,
+  // else gather.
+  const ScatterShape sh =
+      (g_policy.load() & MXD_POLICY_NO_SCATTER) ? ScatterShape{} : scatter_shape(*p.yt, im.crop_y, im.crop_h);
+  const int32_t xb = mxd::wave_taps_bucket(p.xt->width);
+  const int32_t gb = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
+  const int32_t dp = mxd::wave_default_p(c);
+  const int32_t widths[2] = {dp, c == 3 ? 8 : dp};
+  for (int32_t pp : widths) {
+    if (p.wave && pp == p.pp) continue;
+    int32_t ns = 0, tx = 0, q = 0;
+    if (!wave_strips(*p.xt, im, pp, &ns, &tx, &q)) continue;
+    if (p.wave && ns >= p.nstrips) continue;
+    ImgPlan cand = p;
+    cand.nstrips = ns;
+    cand.tx = tx;
+    cand.q = q;
+    cand.pp = pp;
+    cand.shift = shift;
+    if (sh.s > 0 && xb > 0 &&
+        mxd::wave_has_kernel(mxd::WaveCfg{c, f32, xb, 0, 0, 2, sh.s, sh.dmax, q, shift, pp})) {
+      cand.kind = 2;
+      cand.bucket = xb;
+      cand.s = sh.s;
+      cand.dmax = sh.dmax;
+      cand.p = sh.p;
+    } else if (gb > 0 && mxd::wave_has_kernel(mxd::WaveCfg{c, f32, gb, 0, 0, 0, 0, 0, q, shift, pp})) {
+      cand.kind = 0;
+      cand.bucket = gb;
+    } else {
+      continue;
+    }
+    cand.wave = true;
+    p = cand;
+  }
 }
 
 int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
@@ -523,69 +522,28 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   if (n == 0) return MXD_OK;
   const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
   const int32_t channels = images[0].channels;
-  bool aligned16 = true, wave_ok = true;
   for (int32_t i = 0; i < n; i++) {
     if (int rc = validate(images[i], i)) return rc;
     if (images[i].channels != channels)
       return fail(MXD_ERR_INVALID, "mxd: all images of a batch must have the same channel count");
     if (images[i].dst_stride < (int64_t)images[i].crop_w * channels * elem)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
-    const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
-    aligned16 = aligned16 && (a & 15) == 0;
-    wave_ok = wave_ok && wave_layout_ok(images[i], out_dtype);
   }
-  if (!wave_ok) {
-    // Mixed layouts: the images whose rows suit the wave kernels go there, the
-    // rest to the general kernel -- two calls on the same stream (the second
-    // call's descriptor upload is stream-ordered after the first launches).
-    std::vector<mxd_image> fast, slow;
-    for (int32_t i = 0; i < n; i++) (wave_layout_ok(images[i], out_dtype) ? fast : slow).push_back(images[i]);
-    if (!fast.empty() && !slow.empty()) {
-      if (int rc = run_batch(fast.data(), (int32_t)fast.size(), out_dtype, device, stream)) return rc;
-      return run_batch(slow.data(), (int32_t)slow.size(), out_dtype, device, stream);
-    }
-  }
-  // Kernel-kind switches (tuning, tests) are read on every call.
-  const int no_ring = env_int("MXD_NO_RING");
-  const int no_scatter = env_int("MXD_NO_SCATTER");
-  // Band workgroups are opt-in (MXD_BAND=1): measured 261 us vs 162 us for
-  // plain scatter waves on C2 -- the one H/store wave per workgroup serializes.
-  const int no_band = !env_int("MXD_BAND") || env_int("MXD_NO_BAND");
-  static const int ablate = env_int("MXD_WAVE_ABLATE");
   const int32_t f32 = out_dtype == MXD_F32_DIV255 ? 1 : 0;
+  const bool no_wave = (g_policy.load() & MXD_POLICY_NO_WAVE) != 0;
   std::vector<ImgPlan> plans(n);
+  std::vector<int32_t> slow;  // images for the general kernel
   for (int32_t i = 0; i < n; i++) {
     const mxd_image& im = images[i];
     ImgPlan& p = plans[i];
     if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
     if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
-    if (!wave_ok) continue;
-    p.bucket = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
-    wave_ok = p.bucket > 0 && wave_strips(*p.xt, im, &p.nstrips, &p.tx);
-    if (!wave_ok) continue;
-    // Scatter when the vertical axis downsamples into a shape with a kernel;
-    // else the register ring (<= 1 output row per source row); else gather.
-    const ScatterShape sh = no_scatter ? ScatterShape{} : scatter_shape(*p.yt, im.crop_y, im.crop_h);
-    const int32_t xb = mxd::wave_taps_bucket(p.xt->width);
-    if (sh.s > 0 && xb > 0 &&
-        mxd::wave_has_kernel(mxd::WaveCfg{channels, f32, xb, 0, 0, ablate, 2, sh.s, sh.dmax})) {
-      p.kind = 2;
-      p.bucket = xb;
-      p.s = sh.s;
-      p.dmax = sh.dmax;
-      p.p = sh.p;
-      // Band workgroups (scatter V waves + one H/store wave) when the crop's
-      // strips fit one workgroup and the shape has a band kernel.
-      if (!no_band && p.nstrips <= mxd::wave_band_strips() &&
-          mxd::wave_has_kernel(mxd::WaveCfg{channels, f32, xb, 0, 0, ablate, 3, sh.s, sh.dmax}))
-        p.kind = 3;
-    } else if (!no_ring && p.bucket <= 12 && one_output_per_row(*p.yt, im.crop_y, im.crop_h)) {
-      p.kind = 1;
-      if (int rc = right_tables().get(device, *p.yt, im.src_h, im.resize_h, p.bucket, &p.yr)) return rc;
-    }
+    if (!no_wave) plan_wave(im, f32, out_dtype, p);
+    if (!p.wave) slow.push_back(i);
   }
   DeviceGuard guard(device);
   auto fill = [&](ImgDev& d, const mxd_image& im, const ImgPlan& p) {
+    d = ImgDev{};
     d.src = im.src;
     d.src_stride = im.src_stride;
     d.src_w = im.src_w;
@@ -600,167 +558,168 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     d.crop_h = im.crop_h;
     d.flip = im.flip ? 1 : 0;
   };
-  // Wave path: aligned base + byte shift (ImgDev::flip bits 8..).
-  auto align_src = [](ImgDev& d) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(d.src);
-    d.src = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
-    d.flip |= (int32_t)(a & 3) << 8;
-  };
 
-  if (wave_ok) {
-    // One launch per kernel (kind, tap bucket, scatter shape); descriptors of
-    // all launches share one upload.
-    auto key = [&](int32_t i) {
+  // Wave launches: one per kernel (kind, tap bucket, scatter shape, q,
+  // shift); their descriptors come first in the one upload, the general
+  // kernel's after them.
+  auto key = [&](int32_t i) {
+    const ImgPlan& p = plans[i];
+    return std::make_tuple(p.kind, p.bucket, p.s, p.dmax, p.q, p.shift, p.pp);
+  };
+  std::vector<int32_t> order;
+  for (int32_t i = 0; i < n; i++)
+    if (plans[i].wave) order.push_back(i);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
+  const int32_t nw = (int32_t)order.size();
+  std::vector<ImgDev> descs(n);
+  struct Group {
+    int32_t first, count, units, ty;
+    mxd::WaveCfg cfg;
+  };
+  std::vector<Group> groups;
+  for (int32_t k = 0; k < nw; k++) {
+    const ImgPlan& p = plans[order[k]];
+    if (groups.empty() || key(order[groups.back().first]) != key(order[k]))
+      groups.push_back(
+          {k, 0, 0, 0, mxd::WaveCfg{channels, f32, p.bucket, 0, 0, p.kind, p.s, p.dmax, p.q, p.shift, p.pp}});
+    groups.back().count++;
+  }
+  for (Group& g : groups) {
+    g.cfg.nimgs = g.count;
+    std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
+    for (int32_t k = g.first; k < g.first + g.count; k++) strips.push_back({plans[order[k]].nstrips, images[order[k]].crop_h});
+    g.ty = band_rows(strips, wave_capacity_cached(g.cfg, device));
+    for (int32_t k = g.first; k < g.first + g.count; k++) {
+      const int32_t i = order[k];
+      const mxd_image& im = images[i];
       const ImgPlan& p = plans[i];
-      return std::make_tuple(p.kind, p.bucket, p.s, p.dmax);
-    };
-    std::vector<int32_t> order(n);
-    for (int32_t i = 0; i < n; i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
-    std::vector<ImgDev> descs(n);
-    struct Group {
-      int32_t first, count, units, ty;
-      mxd::WaveCfg cfg;
-    };
-    std::vector<Group> groups;
-    for (int32_t k = 0; k < n; k++) {
-      const ImgPlan& p = plans[order[k]];
-      if (groups.empty() || key(order[groups.back().first]) != key(order[k]))
-        groups.push_back({k, 0, 0, 0, mxd::WaveCfg{channels, f32, p.bucket, 0, 0, ablate, p.kind, p.s, p.dmax}});
-      groups.back().count++;
-    }
-    for (Group& g : groups) {
-      g.cfg.nimgs = g.count;
-      std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
-      for (int32_t k = g.first; k < g.first + g.count; k++)
-        strips.push_back({g.cfg.kind == 3 ? 1 : plans[order[k]].nstrips, images[order[k]].crop_h});
-      g.ty = band_rows(strips, wave_capacity_cached(g.cfg, device));
-      for (int32_t k = g.first; k < g.first + g.count; k++) {
-        const int32_t i = order[k];
-        const mxd_image& im = images[i];
-        const ImgPlan& p = plans[i];
-        ImgDev& d = descs[k];
-        fill(d, im, p);
-        align_src(d);
-        d.ty = std::min(g.ty, im.crop_h);
-        if (p.kind == 1) {
-          d.ywidth = p.yr->padded;
-          d.ytab = p.yr->ptr + (size_t)im.crop_y * (mxd::kTapHeader + p.yr->padded);
-        } else if (p.kind == 2 || p.kind == 3) {
-          const DevSched* sc = nullptr;
-          if (int rc = schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
-                                       ScatterShape{p.s, p.dmax, p.p}, &sc))
-            return rc;
-          d.ytab = reinterpret_cast<const float*>(sc->ptr);
-          d.ywidth = sc->band_words;
-          d.group = sc->entry_off;
-        }
-        d.tile_begin = g.units;
-        d.nstrips = p.nstrips;
-        d.tx = p.tx;
-        if (p.kind < 2) d.group = 1;
-        g.units += (p.kind == 3 ? 1 : d.nstrips) * ((im.crop_h + d.ty - 1) / d.ty);
+      ImgDev& d = descs[k];
+      fill(d, im, p);
+      // aligned base + byte shift (ImgDev::flip bits 8..)
+      const uintptr_t a = reinterpret_cast<uintptr_t>(d.src);
+      d.src = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
+      d.flip |= (int32_t)(a & 3) << 8;
+      d.ty = std::min(g.ty, im.crop_h);
+      if (p.kind == 2) {
+        const DevSched* sc = nullptr;
+        if (int rc = schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
+                                     ScatterShape{p.s, p.dmax, p.p}, &sc))
+          return rc;
+        d.ytab = reinterpret_cast<const float*>(sc->ptr);
+        d.ywidth = sc->band_words;
+        d.group = sc->entry_off;
+      } else {
+        d.group = 1;
       }
-      g.cfg.nunits = g.units;
+      d.tile_begin = g.units;
+      d.nstrips = p.nstrips;
+      d.tx = p.tx;
+      g.units += d.nstrips * ((im.crop_h + d.ty - 1) / d.ty);
     }
-    ImgDev* dev = nullptr;
-    std::unique_lock<std::mutex> hold;
-    Workspace* ws = nullptr;
-    if (int rc = upload_descs(descs, device, stream, &dev, &hold, &ws)) return rc;
-    static const int debug = env_int("MXD_DEBUG");
-    // Several launches: fork them over the caller's stream and the
-    // workspace's helper streams (largest first), join back before return.
-    const int nfork = env_int("MXD_NO_FORK") ? 0 : std::min<int>((int)groups.size() - 1, Workspace::kHelpers);
-    std::vector<int32_t> by_size(groups.size());
-    for (size_t i = 0; i < groups.size(); i++) by_size[i] = (int32_t)i;
-    std::stable_sort(by_size.begin(), by_size.end(),
-                     [&](int32_t a, int32_t b) { return groups[a].units > groups[b].units; });
-    if (nfork > 0) {
-      if (!ws->fork) {
-        MXD_HIP(hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming));
-        for (int h = 0; h < Workspace::kHelpers; h++) {
-          MXD_HIP(hipStreamCreateWithFlags(&ws->helper[h], hipStreamNonBlocking));
-          MXD_HIP(hipEventCreateWithFlags(&ws->join[h], hipEventDisableTiming));
-        }
-      }
-      MXD_HIP(hipEventRecord(ws->fork, reinterpret_cast<hipStream_t>(stream)));
-      for (int h = 0; h < nfork; h++) MXD_HIP(hipStreamWaitEvent(ws->helper[h], ws->fork, 0));
-    }
-    for (size_t k = 0; k < by_size.size(); k++) {
-      const Group& g = groups[by_size[k]];
-      const int lane = nfork > 0 ? (int)(k % (size_t)(nfork + 1)) : 0;
-      void* s = lane == 0 ? stream : reinterpret_cast<void*>(ws->helper[lane - 1]);
-      if (debug)
-        std::fprintf(stderr,
-                     "mxd: launch kind=%d taps=%d s=%d dmax=%d f32=%d imgs=%d units=%d band_rows=%d capacity=%d "
-                     "lane=%d\n",
-                     g.cfg.kind, g.cfg.taps, g.cfg.s, g.cfg.dmax, g.cfg.f32, g.cfg.nimgs, g.cfg.nunits, g.ty,
-                     wave_capacity_cached(g.cfg, device), lane);
-      if (int rc = mxd::launch_wave(g.cfg, dev + g.first, s))
-        return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
-                                        " rc=" + std::to_string(rc));
-    }
-    for (int h = 0; h < nfork; h++) {
-      MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
-      MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
-    }
-    return MXD_OK;
+    g.cfg.nunits = g.units;
   }
 
   // General path (any alignment, any tap count): workgroup tiles, resample.hip.
-  const int32_t vec = aligned16 ? 16 : 1;
   LaunchCfg cfg{};
-  cfg.vec = vec;
-  cfg.channels = channels;
-  cfg.f32 = out_dtype == MXD_F32_DIV255;
-  cfg.nimgs = n;
-  std::vector<ImgDev> descs(n);
   int32_t tiles = 0;
-  for (int32_t i = 0; i < n; i++) {
-    const mxd_image& im = images[i];
-    const DevTable* xt = plans[i].xt;
-    const DevTable* yt = plans[i].yt;
-    const bool flip = im.flip != 0;
-    // Column strips: enough that one strip row's footprint is ~kStripBytes.
-    const int32_t full = strip_chunks(*xt, im.crop_x, im.crop_w, 0, im.crop_w, flip, channels, 1);
-    int32_t nstrips = std::max<int32_t>(1, (full + kStripBytes - 1) / kStripBytes);
-    int32_t tx = (im.crop_w + nstrips - 1) / nstrips;
-    tx = std::min<int32_t>(im.crop_w, (tx + 3) & ~3);
-    nstrips = (im.crop_w + tx - 1) / tx;
-    int32_t max_chunks = 0;
-    for (int32_t s = 0; s < nstrips; s++) {
-      const int32_t ox0 = s * tx, ox1 = std::min(ox0 + tx, im.crop_w);
-      max_chunks = std::max(max_chunks, strip_chunks(*xt, im.crop_x, im.crop_w, ox0, ox1, flip, channels, vec));
+  if (!slow.empty()) {
+    bool aligned16 = true;
+    for (int32_t i : slow) {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
+      aligned16 = aligned16 && (a & 15) == 0;
     }
-    const int32_t vw = (max_chunks * vec + 3) & ~3;
-    const int32_t ty = std::min(kTileRows, im.crop_h);
-    int32_t group = std::max<int32_t>(1, std::min<int32_t>(8, 512 / std::max(1, max_chunks)));
-    group = std::max<int32_t>(1, std::min<int32_t>(group, kLdsBudget / (vw * 4)));
-    group = std::min(group, ty);
-    const int32_t nbands = (im.crop_h + ty - 1) / ty;
-    ImgDev& d = descs[i];
-    fill(d, im, plans[i]);
-    d.tile_begin = tiles;
-    d.nstrips = nstrips;
-    d.ty = ty;
-    d.tx = tx;
-    d.group = group;
-    tiles += nbands * nstrips;
-    cfg.max_tx = std::max(cfg.max_tx, tx);
-    cfg.max_ty = std::max(cfg.max_ty, ty);
-    cfg.max_xw = std::max(cfg.max_xw, xt->padded);
-    cfg.max_yw = std::max(cfg.max_yw, yt->padded);
-    cfg.max_vw = std::max(cfg.max_vw, vw);
-    cfg.max_group = std::max(cfg.max_group, group);
+    const int32_t vec = aligned16 ? 16 : 1;
+    cfg.vec = vec;
+    cfg.channels = channels;
+    cfg.f32 = f32;
+    cfg.nimgs = (int32_t)slow.size();
+    for (size_t k = 0; k < slow.size(); k++) {
+      const int32_t i = slow[k];
+      const mxd_image& im = images[i];
+      const DevTable* xt = plans[i].xt;
+      const DevTable* yt = plans[i].yt;
+      const bool flip = im.flip != 0;
+      // Column strips: enough that one strip row's footprint is ~kStripBytes.
+      const int32_t full = strip_chunks(*xt, im.crop_x, im.crop_w, 0, im.crop_w, flip, channels, 1);
+      int32_t nstrips = std::max<int32_t>(1, (full + kStripBytes - 1) / kStripBytes);
+      int32_t tx = (im.crop_w + nstrips - 1) / nstrips;
+      tx = std::min<int32_t>(im.crop_w, (tx + 3) & ~3);
+      nstrips = (im.crop_w + tx - 1) / tx;
+      int32_t max_chunks = 0;
+      for (int32_t s = 0; s < nstrips; s++) {
+        const int32_t ox0 = s * tx, ox1 = std::min(ox0 + tx, im.crop_w);
+        max_chunks = std::max(max_chunks, strip_chunks(*xt, im.crop_x, im.crop_w, ox0, ox1, flip, channels, vec));
+      }
+      const int32_t vw = (max_chunks * vec + 3) & ~3;
+      const int32_t ty = std::min(kTileRows, im.crop_h);
+      int32_t group = std::max<int32_t>(1, std::min<int32_t>(8, 512 / std::max(1, max_chunks)));
+      group = std::max<int32_t>(1, std::min<int32_t>(group, kLdsBudget / (vw * 4)));
+      group = std::min(group, ty);
+      const int32_t nbands = (im.crop_h + ty - 1) / ty;
+      ImgDev& d = descs[nw + k];
+      fill(d, im, plans[i]);
+      d.tile_begin = tiles;
+      d.nstrips = nstrips;
+      d.ty = ty;
+      d.tx = tx;
+      d.group = group;
+      tiles += nbands * nstrips;
+      cfg.max_tx = std::max(cfg.max_tx, tx);
+      cfg.max_ty = std::max(cfg.max_ty, ty);
+      cfg.max_xw = std::max(cfg.max_xw, xt->padded);
+      cfg.max_yw = std::max(cfg.max_yw, yt->padded);
+      cfg.max_vw = std::max(cfg.max_vw, vw);
+      cfg.max_group = std::max(cfg.max_group, group);
+    }
+    cfg.ntiles = tiles;
+    if (mxd::resample_smem_bytes(cfg) > 160 * 1024) return fail(MXD_ERR_UNSUPPORTED, "mxd: tile does not fit in LDS");
   }
-  cfg.ntiles = tiles;
-  if (mxd::resample_smem_bytes(cfg) > 160 * 1024) return fail(MXD_ERR_UNSUPPORTED, "mxd: tile does not fit in LDS");
+
   ImgDev* dev = nullptr;
   std::unique_lock<std::mutex> hold;
-  if (int rc = upload_descs(descs, device, stream, &dev, &hold)) return rc;
-  if (int rc = mxd::launch_resample(cfg, dev, stream))
-    return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
-                                    " rc=" + std::to_string(rc));
+  Workspace* ws = nullptr;
+  if (int rc = upload_descs(descs, device, stream, &dev, &hold, &ws)) return rc;
+  // Several launches: fork them over the caller's stream and the workspace's
+  // helper streams (largest first), join back before return, so one launch's
+  // tail overlaps the next.
+  struct Launch {
+    int64_t units;
+    int32_t group;  // -1: the general kernel
+  };
+  std::vector<Launch> launches;
+  for (size_t g = 0; g < groups.size(); g++) launches.push_back({groups[g].units, (int32_t)g});
+  if (!slow.empty()) launches.push_back({tiles, -1});
+  std::stable_sort(launches.begin(), launches.end(), [](const Launch& a, const Launch& b) { return a.units > b.units; });
+  const int nfork = std::min<int>((int)launches.size() - 1, Workspace::kHelpers);
+  if (nfork > 0) {
+    if (!ws->fork) {
+      MXD_HIP(hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming));
+      for (int h = 0; h < Workspace::kHelpers; h++) {
+        MXD_HIP(hipStreamCreateWithFlags(&ws->helper[h], hipStreamNonBlocking));
+        MXD_HIP(hipEventCreateWithFlags(&ws->join[h], hipEventDisableTiming));
+      }
+    }
+    MXD_HIP(hipEventRecord(ws->fork, reinterpret_cast<hipStream_t>(stream)));
+    for (int h = 0; h < nfork; h++) MXD_HIP(hipStreamWaitEvent(ws->helper[h], ws->fork, 0));
+  }
+  for (size_t k = 0; k < launches.size(); k++) {
+    const int lane = nfork > 0 ? (int)(k % (size_t)(nfork + 1)) : 0;
+    void* s = lane == 0 ? stream : reinterpret_cast<void*>(ws->helper[lane - 1]);
+    int rc = 0;
+    if (launches[k].group >= 0) {
+      const Group& g = groups[launches[k].group];
+      rc = mxd::launch_wave(g.cfg, dev + g.first, s);
+    } else {
+      rc = mxd::launch_resample(cfg, dev + nw, s);
+    }
+    if (rc)
+      return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
+                                      " rc=" + std::to_string(rc));
+  }
+  for (int h = 0; h < nfork; h++) {
+    MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
+    MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
+  }
   return MXD_OK;
 }
 
@@ -970,6 +929,20 @@ int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t c
 
 int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
   return run_batch(images, n, out_dtype, device, stream);
+}
+
+int mxd_set_kernel_policy(int32_t policy) { return g_policy.exchange(policy); }
+
+int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device, int32_t* info8) {
+  if (!image || !info8) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  if (int rc = validate(*image, 0)) return rc;
+  ImgPlan p;
+  if (int rc = host_tables().get(device, image->src_w, image->resize_w, &p.xt)) return rc;
+  if (int rc = host_tables().get(device, image->src_h, image->resize_h, &p.yt)) return rc;
+  if (!(g_policy.load() & MXD_POLICY_NO_WAVE)) plan_wave(*image, out_dtype == MXD_F32_DIV255, out_dtype, p);
+  const int32_t v[8] = {p.wave ? 1 : 0, p.kind, p.bucket, p.s, p.dmax, p.q, p.nstrips, p.pp};
+  std::memcpy(info8, v, sizeof v);
+  return MXD_OK;
 }
 
 int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps) {

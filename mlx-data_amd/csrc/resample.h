@@ -42,19 +42,22 @@ struct LaunchCfg {
   int32_t max_tx, max_ty, max_xw, max_yw, max_vw, max_group;
 };
 
-// Wave-per-unit fast paths (wave.hip): sources 4-byte aligned, outputs 16-byte
-// (f32) / 4-byte (u8) aligned, every strip's footprint <= wave_row_bytes(),
-// strip_cols*C <= wave_max_outputs(), taps <= 17.  Units are numbered through
-// ImgDev::tile_begin exactly like tiles; ty = band rows, tx = strip columns.
-// kind: 0 = gather, 1 = register ring (ImgDev::ytab is the right-aligned
-// table), 2 = scatter (ImgDev::ytab is the schedule, ywidth its words per band,
-// group the offset of its iteration entries).  taps = horizontal (and, for
-// gather / ring, vertical) tap bucket; s / dmax = scatter shape.
+// Wave-per-unit fast paths (wave.hip): source rows 4-byte aligned (a window
+// may start at any byte: ImgDev::flip bits 8.. hold the base's misalignment),
+// f32 outputs 4-byte aligned, every strip's source window <= wave_window_px()
+// pixels (start aligned to wave_window_align()), strip_cols <= 64 q, taps <=
+// 17.  Units are numbered through ImgDev::tile_begin exactly like tiles; ty =
+// band rows, tx = strip columns.  kind: 0 = gather, 2 = scatter (ImgDev::ytab
+// is the schedule, ywidth its words per band, group the offset of its
+// iteration entries).  taps = horizontal (and, for gather, vertical) tap
+// bucket; s / dmax = scatter shape; q = output pixels per lane; shift = some
+// image of the launch has a misaligned base.
 struct WaveCfg {
   int32_t channels, f32, taps, nimgs, nunits;
-  int32_t mode;  // 0 = product kernel; 1, 2, 9 = timing-only ablations (MXD_WAVE_ABLATE)
   int32_t kind;
   int32_t s, dmax;
+  int32_t q, shift;
+  int32_t p;  // source pixels per lane (wave_default_p, or 8 for wide RGB windows)
 };
 
 // Scatter schedule geometry, shared by the kernel and the host builder:
@@ -69,10 +72,11 @@ constexpr int scatter_block_groups(int s, int dmax) {
 constexpr int scatter_entry_words(int s) { return s <= 2 ? 4 : 8; }  // prefetch row, row, s weights
 
 int wave_taps_bucket(int taps);            // supported padded tap count >= taps, or -1
-int wave_row_floats(int taps, int channels);
-int wave_row_bytes();
-int wave_max_outputs();  // output elements per strip row (4 per lane)
-int wave_band_strips();  // strips one band workgroup (kind 3) covers
+int wave_default_p(int channels);          // source pixels per lane of the gather kernels
+int wave_window_px(int channels, int p);   // source pixels one wave covers per row
+int wave_window_align(int channels);       // window start alignment (pixels)
+int wave_plane_floats(int channels, int p);  // LDS floats per wave
+int wave_lanes();
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
 bool wave_has_kernel(const WaveCfg& cfg);
 // Waves of this configuration the device runs at once (occupancy x CUs), 0 if unknown.

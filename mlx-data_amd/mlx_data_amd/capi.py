@@ -20,7 +20,7 @@ MXD_F32_DIV255 = 1
 EXPORTS = (
     "mxd_abi_version", "mxd_last_error", "mxd_device_count",
     "mxd_resize_smallest_side_dims", "mxd_center_crop_origin", "mxd_axis_taps",
-    "mxd_resize_crop_batch", "mxd_copy_bandwidth",
+    "mxd_resize_crop_batch", "mxd_set_kernel_policy", "mxd_describe_plan", "mxd_copy_bandwidth",
     "mxd_set_device", "mxd_malloc_device", "mxd_free_device", "mxd_malloc_pinned", "mxd_free_pinned",
     "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
     "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
@@ -31,6 +31,10 @@ EXPORTS = (
 
 MXD_AFFINE = 0
 MXD_CHANNEL_REDUCTION = 1
+
+MXD_POLICY_AUTO = 0
+MXD_POLICY_NO_SCATTER = 1
+MXD_POLICY_NO_WAVE = 2
 
 
 class MxdImage(ctypes.Structure):
@@ -145,6 +149,22 @@ def make_images(entries):
 
 def resize_crop_batch(images, n, out_dtype, device=0, stream=None):
     check(lib().mxd_resize_crop_batch(images, n, out_dtype, device, ctypes.c_void_p(stream)))
+
+
+def set_kernel_policy(policy):
+    """Process-wide choice between kernels with identical results; returns the previous policy."""
+    return lib().mxd_set_kernel_policy(int(policy))
+
+
+PLAN_FIELDS = ("wave", "kind", "taps", "s", "dmax", "q", "nstrips", "p")
+
+
+def describe_plan(entry, out_dtype=MXD_U8, device=0):
+    """The kernel mxd_resize_crop_batch picks for one image (host only)."""
+    arr, _ = make_images([dict(entry, src=entry.get("src", 256), dst=entry.get("dst", 256))])
+    info = (ctypes.c_int32 * 8)()
+    check(lib().mxd_describe_plan(arr, out_dtype, device, info))
+    return dict(zip(PLAN_FIELDS, list(info)))
 
 
 def resize_crop_host(images, n, out_dtype, device=0):

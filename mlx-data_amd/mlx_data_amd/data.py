@@ -18,9 +18,10 @@ mirror of the whole batch as one fused GPU launch and writes the stacked
 its own launch.  There is no CPU resize: without a visible GPU the image ops
 raise.
 
-``load_image`` decodes with Pillow (libjpeg-turbo) into host memory, following
-the channel rules of ``core/image/ImageIO.cpp:10-33`` (JPEG -> 3 channels; other
-formats keep 1/2/3 channels, 4 -> 3).
+``load_image`` decodes JPEG natively (``csrc/pipeline/jpeg.cpp``, the
+reference's libjpeg path, ``core/image/ImageJPEG.cpp``); other formats go to a
+Pillow hook that follows the reference's stb_image rules
+(``core/image/ImageSTBI.cpp``: 1/2/3 channels kept, 4 -> 3, 16-bit >> 8).
 """
 import io
 
@@ -34,23 +35,24 @@ __all__ = ["Buffer", "Stream", "buffer_from_vector", "set_state", "set_devices",
 
 
 def _decode(path, data, from_memory, info):
+    """Non-JPEG images (the reference's stb_image fallback, core/image/ImageSTBI.cpp:14-58):
+    channels = min(stbi channels, 3) -- grey 1, grey+alpha 2, RGB 3, RGBA -> RGB;
+    16-bit samples are scaled to 8 bits with >> 8 (stbi__convert_16_to_8); 1-bit
+    images are expanded to 0/255 grey."""
     from PIL import Image
 
     try:
         im = Image.open(io.BytesIO(data.tobytes()) if from_memory else path)
         if info:
             return np.array([im.width, im.height], dtype=np.int64)
-        if im.format == "JPEG":
-            im = im.convert("RGB")
-        elif im.mode in ("L", "RGB"):
-            pass
-        elif im.mode == "LA":
-            pass
-        elif im.mode in ("I;16", "I", "F"):
-            im = im.convert("L")
-        else:
-            im = im.convert("RGB")
-        a = np.asarray(im)
+        if im.mode in ("L", "RGB", "LA"):
+            a = np.asarray(im)
+        elif im.mode in ("I;16", "I;16B", "I;16L", "I"):
+            a = (np.asarray(im).astype(np.int64) >> 8).clip(0, 255).astype(np.uint8)
+        elif im.mode == "1":
+            a = np.asarray(im.convert("L"))
+        else:  # palette, RGBA, CMYK, ...
+            a = np.asarray(im.convert("RGB"))
     except (OSError, ValueError, SyntaxError):
         return None
     if a.ndim == 2:

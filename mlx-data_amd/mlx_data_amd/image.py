@@ -11,6 +11,20 @@ import numpy as np
 from . import capi
 
 
+def _as_image(img):
+    """The reference's checks (core/image/ImageTransform.cpp:17-31 verify_type,
+    core/image/ImageIO.cpp:39-49 verify_image): HWC uint8, 1..4 channels; no
+    silent casts or reshapes."""
+    img = np.asarray(img)
+    if img.dtype != np.uint8:
+        raise TypeError("image must be of type UInt8")
+    if img.ndim != 3:
+        raise ValueError("verifyImage: image must be 3 dimension Array (HWC)")
+    if img.shape[2] == 0 or img.shape[2] > 4:
+        raise ValueError("verifyImage: channels must be 0 <= c <= 4")
+    return np.ascontiguousarray(img)
+
+
 def plan_resize_smallest_side_center_crop(w, h, size, cw, ch):
     """(resize_w, resize_h, crop_x, crop_y) exactly as the reference computes them."""
     tw, th = capi.resize_smallest_side_dims(w, h, size)
@@ -29,9 +43,7 @@ def resize_crop(images, geoms, out_dtype="uint8", device=0):
     outs, entries = [], []
     keep = []
     for img, g in zip(images, geoms):
-        img = np.ascontiguousarray(img, np.uint8)
-        if img.ndim == 2:
-            img = img[:, :, None]
+        img = _as_image(img)
         rw, rh, x, y, cw, ch, flip = g
         out = np.empty((ch, cw, img.shape[2]), np.float32 if f32 else np.uint8)
         keep.append(img)
@@ -56,9 +68,7 @@ def resize_smallest_side_center_crop(images, size, cw, ch, out_dtype="uint8", de
 def _pixmap(images, op, params_of, dims_of, out_c, device):
     entries, outs, keep = [], [], []
     for img in images:
-        img = np.ascontiguousarray(img, np.uint8)
-        if img.ndim == 2:
-            img = img[:, :, None]
+        img = _as_image(img)
         h, w, c = img.shape
         dw, dh = dims_of(w, h)
         out = np.empty((dh, dw, out_c(c)), np.uint8)

@@ -17,7 +17,7 @@ import bench
 r = bench.Ranks()
 assert r.world == 2 and r.dist is not None
 delay = 0.01 * (r.rank + 1)          # rank 1 is the slow one
-wall, local = bench.timed_steps(r, lambda: time.sleep(delay), lambda: None, 5)
+wall, local = bench.timed_steps(r, lambda i: time.sleep(delay), lambda: None, 5)
 line = bench.bench_line("c2", r.world, 256, 5, 1, wall, None, None, None)
 print(json.dumps(dict(rank=r.rank, wall=wall, local=local, line=line)), flush=True)
 r.close()
@@ -55,3 +55,19 @@ def test_two_rank_gloo_timing():
     assert line["config"]["global_batch"] == 512
     assert abs(line["value"] - 2 * 256 * 5 / slow) < 0.1
     assert line["higher_is_better"] is True
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher spawns two rank processes (gloo
+    barrier + max-over-ranks); the line counts both ranks' batches."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "4",
+                        "--simulate", "0.01"], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 512 and line["config"]["per_gpu_batch"] == 256
+    # rank 1 sleeps twice as long: the max over ranks sets the wall time
+    assert line["ms_per_step"] >= 20.0
+    assert abs(line["value"] - 512 * 4 / (line["ms_per_step"] * 4 / 1e3)) / line["value"] < 0.01

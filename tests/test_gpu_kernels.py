@@ -1,9 +1,9 @@
-"""GPU: the wave-kernel kinds of mlx-data_amd/csrc/wave.hip -- band workgroups,
-scatter, register ring, gather -- give bit-identical outputs on the same inputs
-(each sums an output row's taps in the same order from 0), and the default
-choice (scatter) matches the oracle (+-1 per channel, < 0.2 % of channels
-differing).  The kind is chosen through MXD_BAND (opt-in) / MXD_NO_SCATTER /
-MXD_NO_RING, which the C ABI reads on every call."""
+"""GPU: the kernels of the fused stage -- the wave kernels of
+mlx-data_amd/csrc/wave.hip (scatter schedule, gather) and the general tile
+kernel of resample.hip -- give bit-identical outputs on the same inputs (each
+sums an output row's taps in the same order from 0), and the default choice
+matches the oracle (+-1 per channel, < 0.2 % of channels differing).  The
+kernel is chosen through mxd_set_kernel_policy (include/mxd_amd.h)."""
 import numpy as np
 import pytest
 
@@ -12,12 +12,12 @@ from gpu_util import center_geom, compare, oracle_out, run_device, synth
 
 pytestmark = pytest.mark.gpu
 
-SWITCHES = ("MXD_BAND", "MXD_NO_BAND", "MXD_NO_SCATTER", "MXD_NO_RING")
+from mlx_data_amd import capi
+
 KINDS = [
-    ("band", {"MXD_BAND": "1"}),
-    ("default", {}),
-    ("ring", {"MXD_NO_SCATTER": "1"}),
-    ("gather", {"MXD_NO_SCATTER": "1", "MXD_NO_RING": "1"}),
+    ("default", capi.MXD_POLICY_AUTO),
+    ("gather", capi.MXD_POLICY_NO_SCATTER),
+    ("general", capi.MXD_POLICY_NO_WAVE),
 ]
 
 
@@ -41,25 +41,22 @@ def c5():
 CASES = {"c2": c2, "mixed": mixed, "c5": c5}
 
 
-def run_kinds(monkeypatch, imgs, geoms, f32):
+def run_kinds(imgs, geoms, f32):
     outs = {}
-    for name, env in KINDS:
-        for k in SWITCHES:
-            if k in env:
-                monkeypatch.setenv(k, env[k])
-            else:
-                monkeypatch.delenv(k, raising=False)
-        outs[name] = run_device(imgs, geoms, f32=f32)
-    for k in SWITCHES:
-        monkeypatch.delenv(k, raising=False)
+    try:
+        for name, policy in KINDS:
+            capi.set_kernel_policy(policy)
+            outs[name] = run_device(imgs, geoms, f32=f32)
+    finally:
+        capi.set_kernel_policy(capi.MXD_POLICY_AUTO)
     return outs
 
 
 @pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_kernel_kinds_bit_identical(monkeypatch, case, f32):
+def test_kernel_kinds_bit_identical(case, f32):
     imgs, geoms = CASES[case]()
-    outs = run_kinds(monkeypatch, imgs, geoms, f32)
+    outs = run_kinds(imgs, geoms, f32)
     for name, got in outs.items():
         for i, (a, b) in enumerate(zip(outs["gather"], got)):
             assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), (case, name, i)

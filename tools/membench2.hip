@@ -1,0 +1,310 @@
+// tools/membench2.hip -- HBM ceilings on this box (diagnostic, not product).
+//
+//  copy / read / write sweeps over 1 GiB buffers (16 B per lane), grid-stride
+//  and one-chunk-per-block forms, plain and nontemporal; then the C2 access
+//  mix: 256 images of 960 x 3840 B, each reading its 844-row x 2532-B source
+//  footprint and writing 224 rows x 2688 B of f32 output, with one wave per
+//  (image, band) reading whole footprint rows (3 x 1 KiB dwordx4 loads) or
+//  three waves per row (one 1 KiB strip each).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+
+#define CHECK(x)                                                    \
+  do {                                                              \
+    hipError_t e = (x);                                             \
+    if (e != hipSuccess) {                                          \
+      fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e)); \
+      exit(1);                                                      \
+    }                                                               \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+using Rsrc = __amdgpu_buffer_rsrc_t;
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_gs(const f4* __restrict__ a, f4* __restrict__ b, size_t n) {
+  const size_t step = (size_t)gridDim.x * 256 * U;
+  for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i + 256 * (U - 1) < n; i += step) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = NT ? __builtin_nontemporal_load(&a[i + 256 * u]) : a[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (NT) __builtin_nontemporal_store(v[u], &b[i + 256 * u]);
+      else b[i + 256 * u] = v[u];
+    }
+  }
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_flat(const f4* __restrict__ a, f4* __restrict__ b) {
+  const size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+  f4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) v[u] = NT ? __builtin_nontemporal_load(&a[i + 256 * u]) : a[i + 256 * u];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (NT) __builtin_nontemporal_store(v[u], &b[i + 256 * u]);
+    else b[i + 256 * u] = v[u];
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void read_gs(const f4* __restrict__ a, f4* __restrict__ out, size_t n) {
+  const size_t step = (size_t)gridDim.x * 256 * U;
+  float acc = 0.0f;
+  for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i + 256 * (U - 1) < n; i += step) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = a[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  }
+  if (acc == 1234.5f) out[threadIdx.x] = f4{acc, acc, acc, acc};
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void write_gs(f4* __restrict__ b, size_t n) {
+  const size_t step = (size_t)gridDim.x * 256 * U;
+  const float f = (float)threadIdx.x;
+  for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i + 256 * (U - 1) < n; i += step) {
+#pragma unroll
+    for (int u = 0; u < U; u++) b[i + 256 * u] = f4{f, f, f, (float)u};
+  }
+}
+
+// ---- C2 access mix ----
+constexpr int kRows = 960, kStride = 3840, kImgs = 256;
+constexpr int kFy0 = 56, kFy1 = 900, kFb0 = 640, kNeed = 2532;  // footprint rows / bytes
+constexpr int kOutRows = 224, kOutRow = 2688;                      // f32 output row bytes
+constexpr int kNoLoad = 0x7ffffff0;
+
+// One wave per (image, band): NW dwordx4 loads per lane cover NW KiB of each
+// footprint row (whole row: NW = 3), DEPTH rows in flight; every time the
+// running row count crosses an output-row boundary (3.768 rows per output
+// row) the wave stores one output row's share (row bytes / strips).
+template <int NW, int DEPTH>
+__global__ __launch_bounds__(256) void c2_mix(const uint8_t* __restrict__ base, float* __restrict__ out, int nbands,
+                                              int strips, int write) {
+  const int nunits_all = kImgs * nbands * strips;
+  const int lane = threadIdx.x & 63;
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int per_img = nbands * strips;
+  if (unit >= kImgs * per_img) return;
+  const int img = unit / per_img;
+  const int rest = unit - img * per_img;
+  const int band = rest / strips, strip = rest - band * strips;
+  const uint8_t* p = base + (size_t)img * kRows * kStride;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, kRows * kStride, 0x00020000);
+  const int swidth = (kNeed + strips - 1) / strips;
+  int off[NW];
+#pragma unroll
+  for (int j = 0; j < NW; j++) {
+    const int b = 16 * lane + 1024 * j;
+    off[j] = b < swidth && write != 5 ? kFb0 + strip * swidth + b : kNoLoad;
+  }
+  const int oy0 = band * kOutRows / nbands, oy1 = (band + 1) * kOutRows / nbands;
+  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
+  const int orow_share = kOutRow / strips;  // bytes
+  float* o = out + ((size_t)img * kOutRows) * (kOutRow / 4) + strip * (orow_share / 4);
+  u32x4 ring[DEPTH][NW];
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++)
+#pragma unroll
+    for (int j = 0; j < NW; j++)
+      ring[d][j] = __builtin_amdgcn_raw_buffer_load_b128(r, off[j], min(r0 + d, r1 - 1) * kStride, 0);
+  float acc[4] = {0, 0, 0, 0};
+  int oy = oy0;
+  for (int row = r0; row < r1; row += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+#pragma unroll
+      for (int j = 0; j < NW; j++) {
+        acc[0] += (float)(ring[d][j].x & 255);
+        acc[1] += (float)(ring[d][j].y >> 24);
+        acc[2] += (float)(ring[d][j].z & 255);
+        acc[3] += (float)(ring[d][j].w >> 24);
+        ring[d][j] = __builtin_amdgcn_raw_buffer_load_b128(r, off[j], min(row + d + DEPTH, r1 - 1) * kStride, 0);
+      }
+      const int want = (int)((row + d - r0) / 3.768f) + oy0;
+      if (write && want > oy && oy < oy1) {
+        const f4 v = {acc[0], acc[1], acc[2], acc[3]};
+        if (write == 1 || write == 5) {
+          f4* orow = reinterpret_cast<f4*>(o + (size_t)oy * (kOutRow / 4));
+          for (int b = lane; b < orow_share / 16; b += 64) orow[b] = v;
+        } else if (write == 2) {
+          f4* orow = reinterpret_cast<f4*>(out) + ((size_t)(oy - oy0) * nunits_all + unit) * (orow_share / 16);
+          for (int b = lane; b < orow_share / 16; b += 64) orow[b] = v;
+        } else if (write == 3) {
+          f4* orow = reinterpret_cast<f4*>(o + (size_t)oy * (kOutRow / 4));
+          for (int b = lane; b < orow_share / 16; b += 64) __builtin_nontemporal_store(v, &orow[b]);
+        } else if (write == 4 && ((oy - oy0) & 3) == 3) {
+          f4* orow = reinterpret_cast<f4*>(o + (size_t)(oy - 3) * (kOutRow / 4));
+          for (int b = lane; b < 4 * orow_share / 16; b += 64) orow[b] = v;
+        }
+        oy++;
+      }
+    }
+  }
+  if (acc[0] == -1.0f) out[lane] = acc[1];
+}
+
+
+// Kernel-shaped mix: unit = (image, band, strip); the strip reads a window of
+// `wb` bytes (LB bytes per lane: 12 = dwordx3, 16 = dwordx4) at step `step`,
+// the band reads its rows plus `halo` rows; every 3.768 rows it stores one
+// strip-row of `ob` bytes (SB bytes per lane) at out + row*2688 + strip*ob.
+template <int LB, int SB, int DEPTH>
+__global__ __launch_bounds__(256) void c2_kmix(const uint8_t* __restrict__ base, float* __restrict__ out, int nbands,
+                                               int strips, int wb, int step, int ob, int halo, int write) {
+  typedef unsigned uv __attribute__((ext_vector_type(LB / 4)));
+  const int lane = threadIdx.x & 63;
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int per_img = nbands * strips;
+  if (unit >= kImgs * per_img) return;
+  const int img = unit / per_img;
+  const int rest = unit - img * per_img;
+  const int band = rest / strips, strip = rest - band * strips;
+  const uint8_t* p = base + (size_t)img * kRows * kStride;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, kRows * kStride, 0x00020000);
+  const int voff = LB * lane < wb ? kFb0 + strip * step + LB * lane : kNoLoad;
+  const int oy0 = band * kOutRows / nbands, oy1 = (band + 1) * kOutRows / nbands;
+  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + halo);
+  char* o = reinterpret_cast<char*>(out) + (size_t)img * kOutRows * kOutRow + strip * ob;
+  uv ring[DEPTH];
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    if constexpr (LB == 12) ring[d] = __builtin_amdgcn_raw_buffer_load_b96(r, voff, min(r0 + d, r1 - 1) * kStride, 0);
+    else ring[d] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, min(r0 + d, r1 - 1) * kStride, 0);
+  }
+  float acc[4] = {0, 0, 0, 0};
+  int oy = oy0;
+  for (int row = r0; row < r1; row += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      acc[0] += (float)(ring[d].x & 255);
+      acc[1] += (float)(ring[d].y >> 24);
+      acc[2] += (float)(ring[d].z & 255);
+      if constexpr (LB == 12) ring[d] = __builtin_amdgcn_raw_buffer_load_b96(r, voff, min(row + d + DEPTH, r1 - 1) * kStride, 0);
+      else ring[d] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, min(row + d + DEPTH, r1 - 1) * kStride, 0);
+      const int want = (int)((row + d - r0) / 3.768f) + oy0;
+      if (write && want > oy && oy < oy1) {
+        char* orow = o + (size_t)oy * kOutRow;
+        for (int b = lane; b * SB < ob; b += 64) {
+          if constexpr (SB == 12) *reinterpret_cast<f32x3*>(orow + 12 * b) = f32x3{acc[0], acc[1], acc[2]};
+          else *reinterpret_cast<f4*>(orow + 16 * b) = f4{acc[0], acc[1], acc[2], acc[3]};
+        }
+        oy++;
+      }
+    }
+  }
+  if (acc[0] == -1.0f) out[lane] = acc[1];
+}
+
+double timeit(const char* name, double bytes, std::function<void()> f) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  for (int w = 0; w < 3; w++) f();
+  CHECK(hipEventRecord(a));
+  const int iters = 20;
+  for (int i = 0; i < iters; i++) f();
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  CHECK(hipGetLastError());
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms / iters * 1e3;
+  printf("%-46s %9.1f us  %7.1f GB/s\n", name, us, bytes / (us * 1e-6) / 1e9);
+  fflush(stdout);
+  return us;
+}
+
+int main(int argc, char** argv) {
+  const bool only_c2 = argc > 1;
+  const size_t bytes = (size_t)1 << 30, n = bytes / 16;
+  f4 *a, *b;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipMalloc(&b, bytes));
+  CHECK(hipMemset(a, 1, bytes));
+  CHECK(hipMemset(b, 2, bytes));
+  char name[128];
+  for (int k : {2, 4, 8, 16, 32}) {
+    if (only_c2) break;
+    const int g = 256 * k;
+    snprintf(name, sizeof name, "copy gs U=1 blocks=%d", g);
+    timeit(name, 2.0 * bytes, [&] { copy_gs<1, false><<<g, 256>>>(a, b, n); });
+    snprintf(name, sizeof name, "copy gs U=4 blocks=%d", g);
+    timeit(name, 2.0 * bytes, [&] { copy_gs<4, false><<<g, 256>>>(a, b, n); });
+    snprintf(name, sizeof name, "copy gs U=4 nt blocks=%d", g);
+    timeit(name, 2.0 * bytes, [&] { copy_gs<4, true><<<g, 256>>>(a, b, n); });
+  }
+  if (!only_c2) {
+  timeit("copy flat U=1", 2.0 * bytes, [&] { copy_flat<1, false><<<n / 256, 256>>>(a, b); });
+  timeit("copy flat U=4", 2.0 * bytes, [&] { copy_flat<4, false><<<n / 1024, 256>>>(a, b); });
+  timeit("copy flat U=8", 2.0 * bytes, [&] { copy_flat<8, false><<<n / 2048, 256>>>(a, b); });
+  timeit("copy flat U=4 nt", 2.0 * bytes, [&] { copy_flat<4, true><<<n / 1024, 256>>>(a, b); });
+  timeit("hipMemcpyDtoD", 2.0 * bytes, [&] { CHECK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0)); });
+  for (int k : {4, 8, 16}) {
+    snprintf(name, sizeof name, "read gs U=4 blocks=%d", 256 * k);
+    timeit(name, 1.0 * bytes, [&] { read_gs<4><<<256 * k, 256>>>(a, b, n); });
+    snprintf(name, sizeof name, "read gs U=8 blocks=%d", 256 * k);
+    timeit(name, 1.0 * bytes, [&] { read_gs<8><<<256 * k, 256>>>(a, b, n); });
+    snprintf(name, sizeof name, "write gs U=4 blocks=%d", 256 * k);
+    timeit(name, 1.0 * bytes, [&] { write_gs<4><<<256 * k, 256>>>(b, n); });
+  }
+  }
+
+  if (argc > 1 && argv[1][0] == 'k') {
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(a);
+    float* out = reinterpret_cast<float*>(b);
+    const double rd = (double)kImgs * (kFy1 - kFy0) * kNeed, wr = (double)kImgs * kOutRows * kOutRow;
+    struct V { const char* n; int lb, sb, nb, ns, wb, step, ob, halo; };
+    const V vs[] = {
+      {"kernel-like 4x4 x3/x3 768B 672B halo4", 12, 12, 4, 4, 768, 633, 672, 4},
+      {"4x4 x3 loads, 672B x4-less? (x3) halo0", 12, 12, 4, 4, 768, 633, 672, 0},
+      {"4x4 window 633B (no overlap)", 12, 12, 4, 4, 633, 633, 672, 4},
+      {"4x4 x4 loads 768B", 16, 12, 4, 4, 768, 633, 672, 4},
+      {"4x4 stores x4 672B", 12, 16, 4, 4, 768, 633, 672, 4},
+      {"3x4 strips 896B out, 1KiB window", 16, 16, 4, 3, 1024, 844, 896, 4},
+      {"3x4 strips 896B out, 844B window", 16, 16, 4, 3, 844, 844, 896, 0},
+      {"4x8 bands", 12, 12, 8, 4, 768, 633, 672, 4},
+      {"4x2 bands", 12, 12, 2, 4, 768, 633, 672, 4},
+    };
+    for (const V& v : vs) {
+      for (int write : {0, 1}) {
+        const int units = kImgs * v.nb * v.ns;
+        snprintf(name, sizeof name, "%s w=%d", v.n, write);
+        auto go = [&] {
+          if (v.lb == 12 && v.sb == 12) c2_kmix<12, 12, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
+          else if (v.lb == 16 && v.sb == 12) c2_kmix<16, 12, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
+          else if (v.lb == 12 && v.sb == 16) c2_kmix<12, 16, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
+          else c2_kmix<16, 16, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
+        };
+        timeit(name, rd + write * wr, go);
+      }
+    }
+    return 0;
+  }
+  // C2 mix: sources in `a` (256 x 3.69 MB = 944 MB), outputs in `b`.
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(a);
+  float* out = reinterpret_cast<float*>(b);
+  const double rd = (double)kImgs * (kFy1 - kFy0) * kNeed, wr = (double)kImgs * kOutRows * kOutRow;
+  const char* wname[] = {"none", "nhwc", "interleaved", "nt", "burst4", "write-only"};
+  for (int write : {0, 1, 2, 3, 4, 5}) {
+    for (int nb : {4, 8}) {
+      const int units = kImgs * nb;
+      const double by = (write == 5 ? 0 : rd) + (write ? wr : 0);
+      snprintf(name, sizeof name, "c2 row-wave nb=%d d=8 %s", nb, wname[write]);
+      timeit(name, by, [&] { c2_mix<3, 8><<<(units + 3) / 4, 256>>>(src, out, nb, 1, write); });
+      snprintf(name, sizeof name, "c2 strip-wave nb=%d d=8 %s", nb, wname[write]);
+      timeit(name, by, [&] { c2_mix<1, 8><<<(units * 3 + 3) / 4, 256>>>(src, out, nb, 3, write); });
+    }
+  }
+  return 0;
+}
