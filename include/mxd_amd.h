@@ -152,6 +152,28 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop);
  * ops use when samples live in host memory (mlx-data's default). */
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device);
 
+/* ---- JPEG decode (load_image's producer) ---------------
+ *
+ *   core::image::load_jpeg(contents)         mlx/data/core/image/ImageJPEG.cpp:99-146,197-232
+ *   op::LoadImage::apply_key                 mlx/data/op/LoadImage.cpp:23-48
+ *
+ * A from-scratch decoder with libjpeg's default output: ISLOW inverse DCT,
+ * fancy chroma upsampling, YCbCr -> RGB; the result is always H x W x 3
+ * (grey replicated, CMYK: its first three channels).  Host only. */
+
+/* Nonzero when the bytes start with the reference's JPEG signature FF D8 FF. */
+int mxd_is_jpeg(const uint8_t* data, size_t size);
+
+/* Image size and component count from the frame header. */
+int mxd_jpeg_info(const uint8_t* data, size_t size, int32_t* width, int32_t* height, int32_t* components);
+
+/* Decodes into dst: height rows of width*3 bytes, dst_stride bytes apart (any
+ * host memory, e.g. pinned staging from mxd_malloc_pinned).  width/height
+ * must be mxd_jpeg_info's.  MXD_ERR_INVALID with libjpeg's message on corrupt
+ * or unsupported data. */
+int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, int32_t width,
+                    int32_t height);
+
 /* ---- pixel maps: rotate / affine and channel reduction --
  *
  *   core::image::affine(img, mx, crop)       mlx/data/core/image/ImageTransform.cpp:75-110

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "mxd_amd.h"
+#include "jpeg.h"
 #include "pixmap.h"
 #include "resample.h"
 #include "taps.h"
@@ -1164,6 +1165,29 @@ int mxd_channel_reduction_preset(const char* preset, float* params4) {
       return MXD_OK;
     }
   return fail(MXD_ERR_INVALID, std::string("ImageChannelReduction: unable to find preset ") + preset);
+}
+
+int mxd_is_jpeg(const uint8_t* data, size_t size) { return data && mxd::jpeg::is_jpeg(data, size) ? 1 : 0; }
+
+int mxd_jpeg_info(const uint8_t* data, size_t size, int32_t* width, int32_t* height, int32_t* components) {
+  if (!data || !width || !height || !components) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  int w = 0, h = 0, c = 0;
+  std::string err;
+  if (!mxd::jpeg::info(data, size, &w, &h, &c, &err)) return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
+  *width = w;
+  *height = h;
+  *components = c;
+  return MXD_OK;
+}
+
+int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, int32_t width,
+                    int32_t height) {
+  if (!data || !dst) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  if (dst_stride < (int64_t)width * 3) return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than a row");
+  std::string err;
+  if (!mxd::jpeg::decode(data, size, dst, dst_stride, width, height, &err))
+    return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
+  return MXD_OK;
 }
 
 int mxd_pixmap_batch(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, void* stream) {

@@ -1,0 +1,1002 @@
+// jpeg.cpp -- from-scratch JPEG decoder for load_image.
+//
+// The reference decodes with libjpeg(-turbo) defaults and always hands back
+// H x W x 3 (core/image/ImageJPEG.cpp:99-146): 3 components -> RGB, 1 -> grey
+// replicated, 4 -> the first three channels of libjpeg's CMYK output.  The
+// libjpeg defaults that shape the pixels, restated here (file names are
+// libjpeg-turbo's):
+//   * entropy decoding: Huffman, baseline / extended sequential (SOF0, SOF1)
+//     and progressive (SOF2) with successive approximation (jdhuff.c,
+//     jdphuff.c), restart markers; after data runs out (a marker where entropy
+//     bits were needed) the rest of the restart interval decodes as zeros
+//     (uniform grey), as jdhuff.c does for "insufficient data";
+//   * dequantize + inverse DCT: JDCT_ISLOW, 13-bit fixed point, two passes with
+//     PASS1_BITS = 2 (jidctint.c), outputs through the 1024-entry IDCT range
+//     limit table (jdmaster.c prepare_range_limit_table);
+//   * chroma upsampling: "fancy" triangle upsampling h2v1 / h1v2 / h2v2
+//     (jdsample.c) with edge columns special-cased and the rows above the
+//     first / below the last real row replicated (jdmainct.c context rows);
+//     plain replication for other integral factors;
+//   * colour: YCbCr -> RGB with 16-bit fixed-point tables (jdcolor.c); YCCK ->
+//     CMYK; colour space from JFIF / Adobe markers / component ids
+//     (jdapimin.c default_decompress_parms).
+// Arithmetic coding, 12-bit and lossless JPEGs are rejected (the reference's
+// 8-bit libjpeg API rejects or does not produce them either).
+#include "jpeg.h"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace mxd {
+namespace jpeg {
+namespace {
+
+// Zig-zag -> natural order, with 16 extra entries so a corrupt run past 63
+// lands on 63 (jutils.c jpeg_natural_order).
+const int kNatural[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
+                          40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
+                          29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
+                          47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+struct Error {
+  std::string msg;
+};
+
+[[noreturn]] void fail(const std::string& m) { throw Error{m}; }
+
+std::string hex2(int v) {
+  static const char* d = "0123456789abcdef";
+  return std::string("0x") + d[(v >> 4) & 15] + d[v & 15];
+}
+
+// SOF markers other than 0xC0-0xC2: arithmetic coding (0xC9-0xCB, 0xCD-0xCF)
+// and lossless / hierarchical processes are not decoded here.
+[[noreturn]] void unsupported_sof(int m) {
+  if ((m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) fail("Sorry, arithmetic coding is not supported");
+  fail("Unsupported JPEG process: SOF type " + hex2(m));
+}
+
+// ---------------------------------------------------------------- Huffman
+constexpr int kLook = 9;
+
+struct Huff {
+  bool present = false;
+  uint16_t look[1 << kLook];  // (length << 8) | symbol, 0 = longer code
+  int32_t maxcode[18];
+  int32_t valoffset[18];
+  uint8_t vals[256];
+};
+
+// jdhuff.c jpeg_make_d_derived_tbl
+void build_huff(Huff& h, const uint8_t* bits /* [17], bits[0] unused */, const uint8_t* vals, int nvals) {
+  int32_t size[257], code[257];
+  int p = 0;
+  for (int l = 1; l <= 16; l++)
+    for (int i = 0; i < bits[l]; i++) {
+      if (p >= 256) fail("Bogus Huffman table definition");
+      size[p++] = l;
+    }
+  size[p] = 0;
+  const int n = p;
+  if (n != nvals) fail("Bogus Huffman table definition");
+  int32_t c = 0;
+  int si = size[0];
+  p = 0;
+  while (size[p]) {
+    while (size[p] == si) code[p++] = c++;
+    if (c >= (1 << si)) fail("Bogus Huffman table definition");
+    c <<= 1;
+    si++;
+  }
+  p = 0;
+  for (int l = 1; l <= 16; l++) {
+    if (bits[l]) {
+      h.valoffset[l] = p - code[p];
+      p += bits[l];
+      h.maxcode[l] = code[p - 1];
+    } else {
+      h.maxcode[l] = -1;
+    }
+  }
+  h.maxcode[17] = 0xFFFFF;
+  std::memset(h.look, 0, sizeof h.look);
+  p = 0;
+  for (int l = 1; l <= kLook; l++)
+    for (int i = 1; i <= bits[l]; i++, p++) {
+      const int lookbits = code[p] << (kLook - l);
+      for (int ctr = 1 << (kLook - l); ctr > 0; ctr--) h.look[lookbits + ctr - 1] = (uint16_t)((l << 8) | vals[p]);
+    }
+  std::memcpy(h.vals, vals, n);
+  h.present = true;
+}
+
+// Entropy-coded segment reader: stops at a marker; bits needed past it are
+// zeros and set `insufficient` (jdhuff.c jpeg_fill_bit_buffer).
+struct Bits {
+  const uint8_t* p = nullptr;
+  const uint8_t* end = nullptr;
+  uint64_t buf = 0;
+  int cnt = 0;
+  bool at_marker = false;
+  bool insufficient = false;
+
+  void fill() {
+    while (cnt <= 56) {
+      if (at_marker || p >= end) return;
+      const uint8_t b = *p;
+      if (b == 0xFF) {
+        if (p + 1 >= end) {
+          at_marker = true;
+          return;
+        }
+        const uint8_t b2 = p[1];
+        if (b2 == 0x00) {
+          p += 2;
+        } else if (b2 == 0xFF) {
+          p++;  // fill byte
+          continue;
+        } else {
+          at_marker = true;
+          return;
+        }
+      } else {
+        p++;
+      }
+      buf |= (uint64_t)b << (56 - cnt);
+      cnt += 8;
+    }
+  }
+  int peek(int n) const { return (int)(buf >> (64 - n)); }
+  void skip(int n) {
+    buf <<= n;
+    cnt -= n;
+  }
+  int get(int n) {
+    if (n == 0) return 0;
+    if (cnt < n) fill();
+    const int v = peek(n);
+    consume(n);
+    return v;
+  }
+  // Consumes n bits; bits past the end of the segment are zeros and mark the
+  // data insufficient (only when they are actually used).
+  void consume(int n) {
+    if (n > cnt) {
+      insufficient = true;
+      cnt = 64;
+    }
+    skip(n);
+  }
+  int decode(const Huff& h) {
+    if (cnt < 16) fill();
+    const int look = peek(kLook);
+    const int e = h.look[look];
+    if (e) {
+      consume(e >> 8);
+      return e & 0xff;
+    }
+    int l = kLook + 1;
+    int32_t code = peek(l);
+    while (code > h.maxcode[l]) {
+      l++;
+      if (l > 16) {
+        // jdhuff.c jpeg_huff_decode: corrupt data, return a zero
+        consume(16);
+        return 0;
+      }
+      code = peek(l);
+    }
+    consume(l);
+    return h.vals[(code + h.valoffset[l]) & 0xff];
+  }
+  // Next marker from p: p at its 0xFF, returns its code; 0xD9 (EOI) at the
+  // end of the data, as libjpeg's sources insert a fake EOI there.
+  int find_marker() {
+    for (;;) {
+      while (p < end && *p != 0xFF) p++;
+      if (p + 1 >= end) {
+        p = end;
+        return 0xD9;
+      }
+      if (p[1] != 0x00 && p[1] != 0xFF) return p[1];
+      p += p[1] == 0x00 ? 2 : 1;
+    }
+  }
+  // End of a restart interval (jdhuff.c process_restart, jdmarker.c
+  // read_restart_marker + jpeg_resync_to_restart): drop the buffered bits,
+  // expect RST<expected>.  The wanted marker (or one too far off to place) is
+  // consumed and the out-of-data flag cleared; one of the next two markers or
+  // a non-RST marker is left in place (the next segment is empty, and the
+  // flag stays as it was); an older RST or a non-marker is skipped.
+  void restart(int expected) {
+    buf = 0;
+    cnt = 0;
+    for (;;) {
+      const int m = p < end && at_marker ? p[1] : find_marker();
+      at_marker = true;
+      int action;
+      if (m < 0xC0) action = 2;
+      else if (m < 0xD0 || m > 0xD7) action = 3;
+      else if (m == 0xD0 + ((expected + 1) & 7) || m == 0xD0 + ((expected + 2) & 7)) action = 3;
+      else if (m == 0xD0 + ((expected - 1) & 7) || m == 0xD0 + ((expected - 2) & 7)) action = 2;
+      else action = 1;
+      if (action == 1) {
+        p += 2;
+        at_marker = false;
+        insufficient = false;
+        return;
+      }
+      if (action == 3) return;
+      p += 2;
+      at_marker = false;
+    }
+  }
+};
+
+inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v + ((-1) << s) + 1 : v; }
+
+// ---------------------------------------------------------------- IDCT
+constexpr int kConstBits = 13;
+constexpr int kPass1Bits = 2;
+constexpr int32_t FIX_0_298631336 = 2446, FIX_0_390180644 = 3196, FIX_0_541196100 = 4433, FIX_0_765366865 = 6270,
+                  FIX_0_899976223 = 7373, FIX_1_175875602 = 9633, FIX_1_501321110 = 12299,
+                  FIX_1_847759065 = 15137, FIX_1_961570560 = 16069, FIX_2_053119869 = 16819,
+                  FIX_2_562915447 = 20995, FIX_3_072711026 = 25172;
+
+using JLONG = int64_t;  // libjpeg-turbo's JLONG (long on LP64)
+
+inline int32_t descale(JLONG x, int n) { return (int32_t)((x + ((JLONG)1 << (n - 1))) >> n); }
+
+struct RangeLimit {
+  uint8_t idct[1024];  // jdmaster.c post-IDCT table, indexed by (x & 1023)
+  RangeLimit() {
+    for (int i = 0; i < 1024; i++) {
+      if (i < 128) idct[i] = (uint8_t)(i + 128);
+      else if (i < 512) idct[i] = 255;
+      else if (i < 896) idct[i] = 0;
+      else idct[i] = (uint8_t)(i - 896);
+    }
+  }
+};
+const RangeLimit kRange;
+
+// jidctint.c jpeg_idct_islow: dequantize + 8x8 inverse DCT into out (stride).
+void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) {
+  int32_t ws[64];  // (int) workspace of pass 1
+  for (int c = 0; c < 8; c++) {
+    const int16_t* ip = in + c;
+    const uint16_t* qp = q + c;
+    int32_t* wp = ws + c;
+    if (ip[8] == 0 && ip[16] == 0 && ip[24] == 0 && ip[32] == 0 && ip[40] == 0 && ip[48] == 0 && ip[56] == 0) {
+      const int32_t dc = (JLONG)ip[0] * qp[0] * (1 << kPass1Bits);
+      for (int r = 0; r < 8; r++) wp[8 * r] = dc;
+      continue;
+    }
+    JLONG z2 = (JLONG)ip[16] * qp[16], z3 = (JLONG)ip[48] * qp[48];
+    JLONG z1 = (z2 + z3) * FIX_0_541196100;
+    JLONG tmp2 = z1 + z3 * -FIX_1_847759065;
+    JLONG tmp3 = z1 + z2 * FIX_0_765366865;
+    z2 = (JLONG)ip[0] * qp[0];
+    z3 = (JLONG)ip[32] * qp[32];
+    JLONG tmp0 = (z2 + z3) * (1 << kConstBits);
+    JLONG tmp1 = (z2 - z3) * (1 << kConstBits);
+    const JLONG tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = (JLONG)ip[56] * qp[56];
+    tmp1 = (JLONG)ip[40] * qp[40];
+    tmp2 = (JLONG)ip[24] * qp[24];
+    tmp3 = (JLONG)ip[8] * qp[8];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    JLONG z4 = tmp1 + tmp3;
+    const JLONG z5 = (z3 + z4) * FIX_1_175875602;
+    tmp0 *= FIX_0_298631336;
+    tmp1 *= FIX_2_053119869;
+    tmp2 *= FIX_3_072711026;
+    tmp3 *= FIX_1_501321110;
+    z1 *= -FIX_0_899976223;
+    z2 *= -FIX_2_562915447;
+    z3 *= -FIX_1_961570560;
+    z4 *= -FIX_0_390180644;
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    constexpr int s = kConstBits - kPass1Bits;
+    wp[0] = descale(tmp10 + tmp3, s);
+    wp[56] = descale(tmp10 - tmp3, s);
+    wp[8] = descale(tmp11 + tmp2, s);
+    wp[48] = descale(tmp11 - tmp2, s);
+    wp[16] = descale(tmp12 + tmp1, s);
+    wp[40] = descale(tmp12 - tmp1, s);
+    wp[24] = descale(tmp13 + tmp0, s);
+    wp[32] = descale(tmp13 - tmp0, s);
+  }
+  const uint8_t* rl = kRange.idct;
+  for (int r = 0; r < 8; r++) {
+    const int32_t* wp = ws + 8 * r;
+    uint8_t* op = out + (size_t)r * stride;
+    if (wp[1] == 0 && wp[2] == 0 && wp[3] == 0 && wp[4] == 0 && wp[5] == 0 && wp[6] == 0 && wp[7] == 0) {
+      const uint8_t v = rl[descale(wp[0], kPass1Bits + 3) & 1023];
+      for (int c = 0; c < 8; c++) op[c] = v;
+      continue;
+    }
+    JLONG z2 = wp[2], z3 = wp[6];
+    JLONG z1 = (z2 + z3) * FIX_0_541196100;
+    JLONG tmp2 = z1 + z3 * -FIX_1_847759065;
+    JLONG tmp3 = z1 + z2 * FIX_0_765366865;
+    JLONG tmp0 = ((JLONG)wp[0] + wp[4]) * (1 << kConstBits);
+    JLONG tmp1 = ((JLONG)wp[0] - wp[4]) * (1 << kConstBits);
+    const JLONG tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = wp[7];
+    tmp1 = wp[5];
+    tmp2 = wp[3];
+    tmp3 = wp[1];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    JLONG z4 = tmp1 + tmp3;
+    const JLONG z5 = (z3 + z4) * FIX_1_175875602;
+    tmp0 *= FIX_0_298631336;
+    tmp1 *= FIX_2_053119869;
+    tmp2 *= FIX_3_072711026;
+    tmp3 *= FIX_1_501321110;
+    z1 *= -FIX_0_899976223;
+    z2 *= -FIX_2_562915447;
+    z3 *= -FIX_1_961570560;
+    z4 *= -FIX_0_390180644;
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    constexpr int s = kConstBits + kPass1Bits + 3;
+    op[0] = rl[descale(tmp10 + tmp3, s) & 1023];
+    op[7] = rl[descale(tmp10 - tmp3, s) & 1023];
+    op[1] = rl[descale(tmp11 + tmp2, s) & 1023];
+    op[6] = rl[descale(tmp11 - tmp2, s) & 1023];
+    op[2] = rl[descale(tmp12 + tmp1, s) & 1023];
+    op[5] = rl[descale(tmp12 - tmp1, s) & 1023];
+    op[3] = rl[descale(tmp13 + tmp0, s) & 1023];
+    op[4] = rl[descale(tmp13 - tmp0, s) & 1023];
+  }
+}
+
+// ---------------------------------------------------------------- colour
+struct ColorTables {
+  int cr_r[256], cb_b[256];
+  int32_t cr_g[256], cb_g[256];
+  ColorTables() {
+    constexpr int kScale = 16;
+    constexpr int32_t kHalf = (int32_t)1 << (kScale - 1);
+    auto fix = [](double x) { return (int32_t)(x * (1 << kScale) + 0.5); };
+    for (int i = 0; i < 256; i++) {
+      const int32_t x = i - 128;
+      cr_r[i] = (int)((fix(1.40200) * x + kHalf) >> kScale);
+      cb_b[i] = (int)((fix(1.77200) * x + kHalf) >> kScale);
+      cr_g[i] = -fix(0.71414) * x;
+      cb_g[i] = -fix(0.34414) * x + kHalf;
+    }
+  }
+};
+const ColorTables kColor;
+
+inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+// ---------------------------------------------------------------- decoder
+struct Component {
+  int id = 0, h = 1, v = 1, tq = 0;
+  int dc_tbl = 0, ac_tbl = 0;
+  int dw = 0, dh = 0;          // downsampled width / height (samples)
+  int bw = 0, bh = 0;          // blocks per row / column in the MCU-padded grid
+  int wib = 0, hib = 0;        // width / height in blocks of the component proper
+  std::vector<int16_t> coef;   // bw*bh blocks of 64 (progressive / deferred IDCT)
+  std::vector<uint8_t> plane;  // bw*8 x bh*8 samples
+  int dc_pred = 0;
+  int coef_bits_known = 0;     // progressive: set when any DC scan seen
+};
+
+struct Decoder {
+  const uint8_t* data;
+  size_t size;
+  size_t pos = 0;
+  int width = 0, height = 0, ncomp = 0;
+  bool progressive = false, baseline_seen = false;
+  bool jfif = false, adobe = false;
+  int adobe_transform = -1;
+  int restart_interval = 0;
+  int max_h = 1, max_v = 1, mcux = 0, mcuy = 0;
+  uint16_t qt[4][64];
+  bool qt_present[4] = {false, false, false, false};
+  Huff dc[4], ac[4];
+  Component comp[4];
+  bool frame = false, any_scan = false;
+  int eobrun = 0;
+
+  Decoder(const uint8_t* d, size_t n) : data(d), size(n) {}
+
+  int u8() {
+    if (pos >= size) fail("Premature end of JPEG file");
+    return data[pos++];
+  }
+  int u16() {
+    const int a = u8();
+    return (a << 8) | u8();
+  }
+
+  // Next marker code (after 0xFF fill bytes), skipping garbage like libjpeg.
+  int next_marker() {
+    for (;;) {
+      while (pos < size && data[pos] != 0xFF) pos++;
+      if (pos >= size) return -1;
+      while (pos < size && data[pos] == 0xFF) pos++;
+      if (pos >= size) return -1;
+      const int m = data[pos++];
+      if (m != 0) return m;
+    }
+  }
+
+  void read_dqt() {
+    int len = u16() - 2;
+    while (len > 0) {
+      const int pq = u8();
+      const int t = pq & 15, prec = pq >> 4;
+      if (t > 3) fail("Bogus DQT index");
+      for (int i = 0; i < 64; i++) qt[t][kNatural[i]] = (uint16_t)(prec ? u16() : u8());
+      qt_present[t] = true;
+      len -= 1 + 64 * (prec ? 2 : 1);
+    }
+    if (len < 0) fail("Bogus marker length");
+  }
+
+  void read_dht() {
+    int len = u16() - 2;
+    while (len > 16) {
+      const int tc = u8();
+      uint8_t bits[17] = {0};
+      int count = 0;
+      for (int i = 1; i <= 16; i++) {
+        bits[i] = (uint8_t)u8();
+        count += bits[i];
+      }
+      len -= 17;
+      if (count > 256 || count > len) fail("Bogus Huffman table definition");
+      uint8_t vals[256];
+      for (int i = 0; i < count; i++) vals[i] = (uint8_t)u8();
+      len -= count;
+      const int cls = tc >> 4, idx = tc & 15;
+      if (idx > 3) fail("Bogus DHT index");
+      build_huff(cls ? ac[idx] : dc[idx], bits, vals, count);
+    }
+    if (len != 0) fail("Bogus marker length");
+  }
+
+  void read_sof(int marker) {
+    if (frame) fail("Invalid JPEG file structure: two SOF markers");
+    const int len = u16();
+    const int prec = u8();
+    height = u16();
+    width = u16();
+    ncomp = u8();
+    if (prec != 8) fail("Unsupported JPEG data precision " + std::to_string(prec));
+    if (width <= 0 || height <= 0 || ncomp <= 0 || ncomp > 4) fail("Empty JPEG image (DNL not supported)");
+    if (len != 8 + 3 * ncomp) fail("Bogus marker length");
+    progressive = marker == 0xC2;
+    for (int i = 0; i < ncomp; i++) {
+      Component& c = comp[i];
+      c.id = u8();
+      const int hv = u8();
+      c.h = hv >> 4;
+      c.v = hv & 15;
+      c.tq = u8();
+      if (c.h < 1 || c.h > 4 || c.v < 1 || c.v > 4 || c.tq > 3) fail("Bogus sampling factors");
+      max_h = std::max(max_h, c.h);
+      max_v = std::max(max_v, c.v);
+    }
+    mcux = (width + 8 * max_h - 1) / (8 * max_h);
+    mcuy = (height + 8 * max_v - 1) / (8 * max_v);
+    for (int i = 0; i < ncomp; i++) {
+      Component& c = comp[i];
+      c.dw = (int)(((int64_t)width * c.h + max_h - 1) / max_h);
+      c.dh = (int)(((int64_t)height * c.v + max_v - 1) / max_v);
+      c.wib = (c.dw + 7) / 8;
+      c.hib = (c.dh + 7) / 8;
+      c.bw = mcux * c.h;
+      c.bh = mcuy * c.v;
+      c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
+      if (progressive) c.coef.assign((size_t)c.bw * c.bh * 64, 0);
+    }
+    frame = true;
+  }
+
+  void read_app(int marker) {
+    const int len = u16();
+    if (len < 2 || pos + len - 2 > size) fail("Bogus marker length");
+    const uint8_t* d = data + pos;
+    const int n = len - 2;
+    if (marker == 0xE0 && n >= 5 && std::memcmp(d, "JFIF\0", 5) == 0) jfif = true;
+    if (marker == 0xEE && n >= 12 && std::memcmp(d, "Adobe", 5) == 0) {
+      adobe = true;
+      adobe_transform = d[11];
+    }
+    pos += n;
+  }
+
+  void skip_segment() {
+    const int len = u16();
+    if (len < 2) fail("Bogus marker length");
+    pos += len - 2;
+    if (pos > size) pos = size;
+  }
+
+  const uint16_t* quant(const Component& c) const {
+    if (!qt_present[c.tq]) fail("Quantization table 0x0" + std::to_string(c.tq) + " was not defined");
+    return qt[c.tq];
+  }
+
+  // ---- scans
+  void read_sos() {
+    if (!frame) fail("Invalid JPEG file structure: SOS before SOF");
+    const int len = u16();
+    const int ns = u8();
+    if (ns < 1 || ns > 4 || len != 6 + 2 * ns) fail("Bogus marker length");
+    Component* sc[4];
+    for (int i = 0; i < ns; i++) {
+      const int id = u8(), t = u8();
+      Component* c = nullptr;
+      for (int k = 0; k < ncomp; k++)
+        if (comp[k].id == id && !c) c = &comp[k];
+      if (!c) fail("Invalid component ID " + std::to_string(id) + " in SOS");
+      c->dc_tbl = t >> 4;
+      c->ac_tbl = t & 15;
+      sc[i] = c;
+    }
+    const int ss = u8(), se = u8(), a = u8();
+    const int ah = a >> 4, al = a & 15;
+    if (progressive) {
+      if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || ah > 13 || al > 13)
+        fail("Invalid progressive parameters");
+    } else if (ss != 0 || se != 63 || ah != 0 || al != 0) {
+      // libjpeg only warns here; sequential decoding ignores the fields
+    }
+    any_scan = true;
+    Bits bits;
+    bits.p = data + pos;
+    bits.end = data + size;
+    for (int i = 0; i < ns; i++) sc[i]->dc_pred = 0;
+    eobrun = 0;
+    decode_scan(bits, sc, ns, ss, se, ah, al);
+    // resume marker parsing where the entropy data ended
+    pos = (size_t)(bits.p - data);
+  }
+
+  template <class F>
+  void for_each_mcu(Bits& bits, Component** sc, int ns, F&& decode_block) {
+    int restarts_left = restart_interval, next_rst = 0;
+    auto restart_check = [&]() {
+      if (restart_interval) {
+        if (restarts_left == 0) {
+          bits.restart(next_rst);
+          next_rst = (next_rst + 1) & 7;
+          for (int i = 0; i < ns; i++) sc[i]->dc_pred = 0;
+          eobrun = 0;
+          restarts_left = restart_interval;
+        }
+        restarts_left--;
+      }
+    };
+    if (ns == 1) {
+      // non-interleaved: MCU = one block of the component proper
+      Component& c = *sc[0];
+      for (int by = 0; by < c.hib; by++)
+        for (int bx = 0; bx < c.wib; bx++) {
+          restart_check();
+          decode_block(c, bx, by, bits.insufficient);
+        }
+    } else {
+      for (int my = 0; my < mcuy; my++)
+        for (int mx = 0; mx < mcux; mx++) {
+          restart_check();
+          const bool skip = bits.insufficient;
+          for (int i = 0; i < ns; i++) {
+            Component& c = *sc[i];
+            for (int v = 0; v < c.v; v++)
+              for (int h = 0; h < c.h; h++) decode_block(c, mx * c.h + h, my * c.v + v, skip);
+          }
+        }
+    }
+  }
+
+  void decode_scan(Bits& bits, Component** sc, int ns, int ss, int se, int ah, int al) {
+    if (!progressive) {
+      for (int i = 0; i < ns; i++) {
+        if (!dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present) fail("Huffman table was not defined");
+        quant(*sc[i]);
+      }
+      int16_t blk[64];
+      for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
+        std::memset(blk, 0, sizeof blk);
+        if (!skip) {
+          const Huff& hd = dc[c.dc_tbl];
+          const Huff& ha = ac[c.ac_tbl];
+          int s = bits.decode(hd);
+          if (s) s = extend(bits.get(s), s);
+          s += c.dc_pred;
+          c.dc_pred = s;
+          blk[0] = (int16_t)s;
+          for (int k = 1; k < 64; k++) {
+            int rs = bits.decode(ha);
+            const int r = rs >> 4;
+            s = rs & 15;
+            if (s) {
+              k += r;
+              blk[kNatural[k]] = (int16_t)extend(bits.get(s), s);
+            } else {
+              if (r != 15) break;
+              k += 15;
+            }
+          }
+        }
+        idct_islow(blk, quant(c), c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
+      });
+      return;
+    }
+    // progressive (jdphuff.c)
+    if (ss == 0) {
+      if (ah == 0)
+        for (int i = 0; i < ns; i++)
+          if (!dc[sc[i]->dc_tbl].present) fail("Huffman table was not defined");
+      for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
+        int16_t* blk = c.coef.data() + ((size_t)by * c.bw + bx) * 64;
+        if (ah == 0) {
+          if (skip) return;
+          int s = bits.decode(dc[c.dc_tbl]);
+          if (s) s = extend(bits.get(s), s);
+          s += c.dc_pred;
+          c.dc_pred = s;
+          blk[0] = (int16_t)(s * (1 << al));
+        } else if (bits.get(1)) {
+          blk[0] |= (int16_t)(1 << al);
+        }
+      });
+      return;
+    }
+    Component& c0 = *sc[0];
+    if (!ac[c0.ac_tbl].present) fail("Huffman table was not defined");
+    const Huff& ha = ac[c0.ac_tbl];
+    if (ah == 0) {
+      for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
+        if (skip) return;
+        int16_t* blk = c.coef.data() + ((size_t)by * c.bw + bx) * 64;
+        if (eobrun > 0) {
+          eobrun--;
+          return;
+        }
+        for (int k = ss; k <= se; k++) {
+          const int rs = bits.decode(ha);
+          int r = rs >> 4;
+          const int s = rs & 15;
+          if (s) {
+            k += r;
+            blk[kNatural[k]] = (int16_t)(extend(bits.get(s), s) * (1 << al));
+          } else if (r == 15) {
+            k += 15;
+          } else {
+            eobrun = 1 << r;
+            if (r) eobrun += bits.get(r);
+            eobrun--;
+            break;
+          }
+        }
+      });
+      return;
+    }
+    const int p1 = 1 << al, m1 = -1 * (1 << al);
+    for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
+      if (skip) return;
+      int16_t* blk = c.coef.data() + ((size_t)by * c.bw + bx) * 64;
+      int k = ss;
+      if (eobrun == 0) {
+        for (; k <= se; k++) {
+          const int rs = bits.decode(ha);
+          int r = rs >> 4;
+          int s = rs & 15;
+          if (s) {
+            s = bits.get(1) ? p1 : m1;
+          } else if (r != 15) {
+            eobrun = 1 << r;
+            if (r) eobrun += bits.get(r);
+            break;
+          }
+          do {
+            int16_t& co = blk[kNatural[k]];
+            if (co != 0) {
+              if (bits.get(1) && (co & p1) == 0) co = (int16_t)(co >= 0 ? co + p1 : co + m1);
+            } else {
+              if (--r < 0) break;
+            }
+            k++;
+          } while (k <= se);
+          if (s) blk[kNatural[k]] = (int16_t)s;
+        }
+      }
+      if (eobrun > 0) {
+        for (; k <= se; k++) {
+          int16_t& co = blk[kNatural[k]];
+          if (co != 0 && bits.get(1) && (co & p1) == 0) co = (int16_t)(co >= 0 ? co + p1 : co + m1);
+        }
+        eobrun--;
+      }
+    });
+  }
+
+  void parse() {
+    if (size < 3 || data[0] != 0xFF || data[1] != 0xD8) fail("Not a JPEG file");
+    pos = 2;
+    for (;;) {
+      const int m = next_marker();
+      if (m < 0) {
+        if (!any_scan) fail("Premature end of JPEG file");
+        return;  // libjpeg warns and finishes with what it has
+      }
+      switch (m) {
+        case 0xC0:
+        case 0xC1:
+        case 0xC2:
+          read_sof(m);
+          break;
+        case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE:
+        case 0xCF:
+          unsupported_sof(m);
+        case 0xC4:
+          read_dht();
+          break;
+        case 0xCC:
+          fail("Sorry, arithmetic coding is not supported");
+        case 0xDB:
+          read_dqt();
+          break;
+        case 0xDD:
+          if (u16() != 4) fail("Bogus marker length");
+          restart_interval = u16();
+          break;
+        case 0xDA:
+          read_sos();
+          break;
+        case 0xD9:
+          if (!any_scan) fail("Premature end of JPEG file");
+          return;
+        case 0xD8:
+          fail("Invalid JPEG file structure: two SOI markers");
+        default:
+          if (m >= 0xD0 && m <= 0xD7) break;  // stray RST
+          if (m >= 0xE0 && m <= 0xEF) read_app(m);
+          else skip_segment();
+      }
+    }
+  }
+
+  int color_space() const;  // 0 grey, 1 YCbCr, 2 RGB, 3 CMYK, 4 YCCK
+
+  // Component c upsampled to full size, rows [0, height), cols [0, width).
+  void upsample(const Component& c, std::vector<uint8_t>& out) const {
+    const int W = width, H = height;
+    out.resize((size_t)W * H);
+    const int stride = c.bw * 8;
+    const uint8_t* pl = c.plane.data();
+    const int hx = max_h / c.h, vx = max_v / c.v;
+    const bool h2 = c.h * 2 == max_h, v2 = c.v * 2 == max_v;
+    auto row = [&](int y) { return pl + (size_t)std::min(std::max(y, 0), c.dh - 1) * stride; };
+    if (c.h == max_h && c.v == max_v) {
+      for (int y = 0; y < H; y++) std::memcpy(out.data() + (size_t)y * W, pl + (size_t)y * stride, W);
+      return;
+    }
+    std::vector<uint8_t> tmp(2 * (size_t)c.dw + 2);
+    if (h2 && c.v == max_v) {
+      // jdsample.c h2v1_fancy_upsample (or h2v1_upsample when dw <= 2)
+      for (int y = 0; y < H; y++) {
+        const uint8_t* in = pl + (size_t)y * stride;
+        uint8_t* o = tmp.data();
+        if (c.dw > 2) {
+          int v = in[0];
+          o[0] = (uint8_t)v;
+          o[1] = (uint8_t)((v * 3 + in[1] + 2) >> 2);
+          for (int x = 1; x < c.dw - 1; x++) {
+            v = in[x] * 3;
+            o[2 * x] = (uint8_t)((v + in[x - 1] + 1) >> 2);
+            o[2 * x + 1] = (uint8_t)((v + in[x + 1] + 2) >> 2);
+          }
+          v = in[c.dw - 1];
+          o[2 * c.dw - 2] = (uint8_t)((v * 3 + in[c.dw - 2] + 1) >> 2);
+          o[2 * c.dw - 1] = (uint8_t)v;
+        } else {
+          for (int x = 0; x < c.dw; x++) o[2 * x] = o[2 * x + 1] = in[x];
+        }
+        std::memcpy(out.data() + (size_t)y * W, o, W);
+      }
+      return;
+    }
+    if (c.h == max_h && v2) {
+      // jdsample.c h1v2_fancy_upsample
+      for (int y = 0; y < H; y++) {
+        const int iy = y >> 1;
+        const bool below = y & 1;
+        const uint8_t* in0 = row(iy);
+        const uint8_t* in1 = row(below ? iy + 1 : iy - 1);
+        const int bias = below ? 2 : 1;
+        uint8_t* o = out.data() + (size_t)y * W;
+        for (int x = 0; x < W; x++) o[x] = (uint8_t)((in0[x] * 3 + in1[x] + bias) >> 2);
+      }
+      return;
+    }
+    if (h2 && v2 && c.dw > 2) {
+      // jdsample.c h2v2_fancy_upsample
+      for (int y = 0; y < H; y++) {
+        const int iy = y >> 1;
+        const bool below = y & 1;
+        const uint8_t* in0 = row(iy);
+        const uint8_t* in1 = row(below ? iy + 1 : iy - 1);
+        uint8_t* o = tmp.data();
+        int thiscol = in0[0] * 3 + in1[0];
+        int nextcol = in0[1] * 3 + in1[1];
+        o[0] = (uint8_t)((thiscol * 4 + 8) >> 4);
+        o[1] = (uint8_t)((thiscol * 3 + nextcol + 7) >> 4);
+        int lastcol = thiscol;
+        thiscol = nextcol;
+        for (int x = 1; x < c.dw - 1; x++) {
+          nextcol = in0[x + 1] * 3 + in1[x + 1];
+          o[2 * x] = (uint8_t)((thiscol * 3 + lastcol + 8) >> 4);
+          o[2 * x + 1] = (uint8_t)((thiscol * 3 + nextcol + 7) >> 4);
+          lastcol = thiscol;
+          thiscol = nextcol;
+        }
+        o[2 * c.dw - 2] = (uint8_t)((thiscol * 3 + lastcol + 8) >> 4);
+        o[2 * c.dw - 1] = (uint8_t)((thiscol * 4 + 7) >> 4);
+        std::memcpy(out.data() + (size_t)y * W, o, W);
+      }
+      return;
+    }
+    if (max_h % c.h != 0 || max_v % c.v != 0) fail("Fractional sampling not implemented yet");
+    // int_upsample / h2v1_upsample / h2v2_upsample: replication.  Source rows
+    // come from the padded plane (not clamped), like the row groups libjpeg
+    // replicates.
+    for (int y = 0; y < H; y++) {
+      const uint8_t* in = pl + (size_t)(y / vx) * stride;
+      uint8_t* o = out.data() + (size_t)y * W;
+      for (int x = 0; x < W; x++) o[x] = in[x / hx];
+    }
+  }
+
+  void output(uint8_t* dst, int64_t dst_stride) {
+    if (progressive)
+      for (int i = 0; i < ncomp; i++) {
+        Component& c = comp[i];
+        const uint16_t* q = quant(c);
+        for (int by = 0; by < c.bh; by++)
+          for (int bx = 0; bx < c.bw; bx++)
+            idct_islow(c.coef.data() + ((size_t)by * c.bw + bx) * 64, q,
+                       c.plane.data() + (size_t)by * 8 * c.bw * 8 + (size_t)bx * 8, c.bw * 8);
+      }
+    const int cs = color_space();
+    const int W = width, H = height;
+    if (ncomp == 1) {
+      const Component& c = comp[0];
+      for (int y = 0; y < H; y++) {
+        const uint8_t* in = c.plane.data() + (size_t)y * c.bw * 8;
+        uint8_t* o = dst + (size_t)y * dst_stride;
+        for (int x = 0; x < W; x++) o[3 * x] = o[3 * x + 1] = o[3 * x + 2] = in[x];
+      }
+      return;
+    }
+    std::vector<uint8_t> up[4];
+    const int nuse = ncomp == 4 && cs == 3 ? 3 : ncomp;  // CMYK: K is dropped by the caller
+    for (int i = 0; i < nuse; i++) upsample(comp[i], up[i]);
+    for (int y = 0; y < H; y++) {
+      const uint8_t* a = up[0].data() + (size_t)y * W;
+      const uint8_t* b = up[1].data() + (size_t)y * W;
+      const uint8_t* c = up[2].data() + (size_t)y * W;
+      uint8_t* o = dst + (size_t)y * dst_stride;
+      if (cs == 1 || cs == 4) {
+        // ycc_rgb_convert; YCCK -> CMYK inverts the converted RGB
+        for (int x = 0; x < W; x++) {
+          const int Y = a[x], cb = b[x], cr = c[x];
+          const int r = Y + kColor.cr_r[cr];
+          const int g = Y + (int)((kColor.cb_g[cb] + kColor.cr_g[cr]) >> 16);
+          const int bl = Y + kColor.cb_b[cb];
+          if (cs == 1) {
+            o[3 * x] = clamp255(r);
+            o[3 * x + 1] = clamp255(g);
+            o[3 * x + 2] = clamp255(bl);
+          } else {
+            o[3 * x] = clamp255(255 - r);
+            o[3 * x + 1] = clamp255(255 - g);
+            o[3 * x + 2] = clamp255(255 - bl);
+          }
+        }
+      } else {
+        for (int x = 0; x < W; x++) {
+          o[3 * x] = a[x];
+          o[3 * x + 1] = b[x];
+          o[3 * x + 2] = c[x];
+        }
+      }
+    }
+  }
+};
+
+// jdapimin.c default_decompress_parms
+int Decoder::color_space() const {
+  if (ncomp == 1) return 0;
+  if (ncomp == 3) {
+    if (jfif) return 1;
+    if (adobe) return adobe_transform == 0 ? 2 : 1;
+    if (comp[0].id == 1 && comp[1].id == 2 && comp[2].id == 3) return 1;
+    if (comp[0].id == 82 && comp[1].id == 71 && comp[2].id == 66) return 2;
+    return 1;
+  }
+  if (ncomp == 4) {
+    if (adobe) return adobe_transform == 0 ? 3 : 4;
+    return 3;
+  }
+  return -1;
+}
+
+}  // namespace
+
+bool is_jpeg(const uint8_t* data, size_t size) {
+  return size >= 3 && data[0] == 0xFF && data[1] == 0xD8 && data[2] == 0xFF;
+}
+
+bool info(const uint8_t* data, size_t size, int* width, int* height, int* components, std::string* err) {
+  try {
+    Decoder d(data, size);
+    if (!is_jpeg(data, size)) fail("Not a JPEG file");
+    d.pos = 2;
+    for (;;) {
+      const int m = d.next_marker();
+      if (m < 0) fail("Premature end of JPEG file");
+      if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+        d.read_sof(m);
+        break;
+      }
+      if (m == 0xD9 || m == 0xDA) fail("Invalid JPEG file structure: SOS before SOF");
+      if (m >= 0xD0 && m <= 0xD7) continue;
+      if ((m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) unsupported_sof(m);
+      d.skip_segment();
+    }
+    *width = d.width;
+    *height = d.height;
+    *components = d.ncomp;
+    return true;
+  } catch (const Error& e) {
+    if (err) *err = e.msg;
+    return false;
+  }
+}
+
+bool decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, int width, int height,
+            std::string* err) {
+  try {
+    Decoder d(data, size);
+    d.parse();
+    if (!d.frame) fail("Invalid JPEG file structure: missing SOF marker");
+    if (d.width != width || d.height != height) fail("mxd: output buffer does not match the image size");
+    if (d.ncomp == 2 || d.color_space() < 0) fail("unhandled format");
+    d.output(dst, dst_stride);
+    return true;
+  } catch (const Error& e) {
+    if (err) *err = e.msg;
+    return false;
+  } catch (const std::bad_alloc&) {
+    if (err) *err = "Insufficient memory";
+    return false;
+  }
+}
+
+}  // namespace jpeg
+}  // namespace mxd

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -523,7 +524,30 @@ LoadImage::LoadImage(std::string ikey, std::string prefix, bool info, std::strin
       format_(std::move(format)),
       from_memory_(from_memory) {}
 
-// op/LoadImage.cpp:23-48
+namespace {
+// The whole file (the reference's check_signature fopen failure message).
+std::vector<uint8_t> read_file(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+  std::vector<uint8_t> data;
+  uint8_t chunk[1 << 16];
+  size_t n;
+  while ((n = std::fread(chunk, 1, sizeof chunk, f)) > 0) data.insert(data.end(), chunk, chunk + n);
+  std::fclose(f);
+  return data;
+}
+
+// libjpeg's message without the C ABI's "load_jpeg: " prefix.
+std::string jpeg_error() {
+  std::string m = mxd_last_error();
+  const std::string pre = "load_jpeg: ";
+  return m.compare(0, pre.size(), pre) == 0 ? m.substr(pre.size()) : m;
+}
+}  // namespace
+
+// op/LoadImage.cpp:23-48 -> core/image/ImageIO.cpp:10-24: JPEG (signature
+// FF D8 FF) through the native decoder (ImageJPEG.cpp:99-232 semantics),
+// anything else through the installed stb_image-rules hook.
 std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) const {
   std::string path;
   if (!from_memory_) {
@@ -533,6 +557,37 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
     if (!filename.empty() && filename[0] == '/') path = filename;  // std::filesystem::path operator/
     else if (!path.empty()) path = (path.back() == '/' ? path : path + "/") + filename;
     else path = filename;
+  }
+  std::vector<uint8_t> file;
+  const uint8_t* bytes = nullptr;
+  size_t nbytes = 0;
+  if (from_memory_) {
+    bytes = static_cast<const uint8_t*>(x->data());
+    nbytes = (size_t)x->nbytes();
+  } else {
+    file = read_file(path);
+    bytes = file.data();
+    nbytes = file.size();
+  }
+  const std::string where = from_memory_ ? std::string("from memory") : "<" + path + ">";
+  if (mxd_is_jpeg(bytes, nbytes)) {
+    int32_t w = 0, h = 0, c = 0;
+    const bool ok = mxd_jpeg_info(bytes, nbytes, &w, &h, &c) == MXD_OK;
+    if (info_) {
+      // stbi_info: (w, h), zeros when the header cannot be read
+      auto out = std::make_shared<Array>(DType::Int64, std::vector<int64_t>{2});
+      static_cast<int64_t*>(out->data())[0] = ok ? w : 0;
+      static_cast<int64_t*>(out->data())[1] = ok ? h : 0;
+      return out;
+    }
+    if (!ok) throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
+    auto out = std::make_shared<Array>(DType::UInt8, std::vector<int64_t>{h, w, 3}, alloc_bytes((int64_t)h * w * 3));
+    if (mxd_jpeg_decode(bytes, nbytes, static_cast<uint8_t*>(out->data()), (int64_t)w * 3, w, h) != MXD_OK) {
+      const std::string e = jpeg_error();
+      throw std::runtime_error("load_jpeg: could not load " + where + " (" +
+                               (e == "unhandled format" ? e : e) + ")");
+    }
+    return out;
   }
   ImageDecoder dec;
   {

@@ -27,6 +27,7 @@ EXPORTS = (
     "mxd_event_create", "mxd_event_destroy", "mxd_event_record", "mxd_event_synchronize", "mxd_event_elapsed_ms",
     "mxd_resize_crop_host",
     "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
+    "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
 )
 
 MXD_AFFINE = 0
@@ -169,6 +170,25 @@ def describe_plan(entry, out_dtype=MXD_U8, device=0):
 
 def resize_crop_host(images, n, out_dtype, device=0):
     check(lib().mxd_resize_crop_host(images, n, out_dtype, device))
+
+
+def jpeg_info(data):
+    """(width, height, components) of a JPEG (bytes / uint8 array)."""
+    buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
+    w, h, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    check(lib().mxd_jpeg_info(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes), ctypes.byref(w),
+                              ctypes.byref(h), ctypes.byref(c)))
+    return w.value, h.value, c.value
+
+
+def jpeg_decode(data):
+    """The native decoder: (H, W, 3) uint8, libjpeg ISLOW + fancy upsampling output."""
+    buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
+    w, h, _ = jpeg_info(buf)
+    out = np.empty((h, w, 3), np.uint8)
+    check(lib().mxd_jpeg_decode(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes),
+                                out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(w * 3), w, h))
+    return out
 
 
 def rotate_geometry(w, h, angle, crop=False):

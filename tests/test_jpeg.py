@@ -1,0 +1,111 @@
+"""The native JPEG decoder behind load_image (SURVEY.md §8f row f1;
+mlx-data_amd/csrc/jpeg.cpp) against libjpeg-turbo, which the reference links
+(core/image/ImageJPEG.cpp:99-146, libjpeg defaults: ISLOW IDCT, fancy
+upsampling, RGB out, grey replicated, CMYK -> first three raw channels).
+
+Pinned two ways: the committed fixtures (tests/golden/jpeg.npz, encoded and
+decoded by Pillow's bundled libjpeg-turbo; generator make_jpeg_golden.py) and,
+on hosts with Pillow, a seeded sweep decoded live by Pillow.  Bit-exact
+everywhere.  Not reproduced: libjpeg's block smoothing of progressive files
+whose later scans are missing (truncated progressive data)."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from mlx_data_amd import capi
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "jpeg.npz"))
+CASES = sorted(k[:-4] for k in GOLD.files if k.endswith("_jpg"))
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fixture_bit_exact(case):
+    data = GOLD[f"{case}_jpg"]
+    want = GOLD[f"{case}_rgb"]
+    got = capi.jpeg_decode(data)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want), (case, int(np.abs(got.astype(int) - want.astype(int)).max()))
+
+
+def test_info_and_signature():
+    data = GOLD["sub2_prog0_jpg"]
+    w, h, c = capi.jpeg_info(data)
+    assert (h, w, c) == (*GOLD["sub2_prog0_rgb"].shape[:2], 3)
+    assert capi.jpeg_info(GOLD["grey_jpg"])[2] == 1
+    assert capi.jpeg_info(GOLD["cmyk_jpg"])[2] == 4
+    assert capi.lib().mxd_is_jpeg(bytes(data[:3]), 3) == 1
+    assert capi.lib().mxd_is_jpeg(b"\x89PNG", 4) == 0
+
+
+def _smooth(rng, h, w, c):
+    x = np.linspace(0, 6, w)[None, :, None]
+    y = np.linspace(0, 4, h)[:, None, None]
+    base = (np.sin(x * 1.3 + y * 0.7) + np.cos(y * 2.1 - x * 0.4)) * 60 + 128
+    return np.clip(base + rng.normal(0, 25, (h, w, c)) + np.arange(c)[None, None, :] * 20, 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_live_pillow_sweep(seed):
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(seed)
+    for _ in range(6):
+        h, w = int(rng.integers(1, 140)), int(rng.integers(1, 140))
+        grey = rng.random() < 0.2
+        a = _smooth(rng, h, w, 1 if grey else 3)
+        kw = dict(quality=int(rng.integers(5, 101)), progressive=bool(rng.random() < 0.5),
+                  optimize=bool(rng.random() < 0.5))
+        if not grey:
+            kw["subsampling"] = int(rng.integers(0, 3))
+        if rng.random() < 0.3:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 6))
+        b = io.BytesIO()
+        Image.fromarray(a[:, :, 0] if grey else a).save(b, "JPEG", **kw)
+        data = b.getvalue()
+        want = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+        assert np.array_equal(capi.jpeg_decode(data), want), (h, w, kw)
+
+
+def _segment(marker, payload):
+    return bytes([0xFF, marker]) + (len(payload) + 2).to_bytes(2, "big") + payload
+
+
+def test_errors_carry_libjpeg_messages():
+    with pytest.raises(capi.MxdError, match="Not a JPEG file"):
+        capi.jpeg_info(b"\x89PNG\r\n\x1a\n" + bytes(32))
+    # arithmetic-coded frame (SOF9)
+    sof9 = b"\xff\xd8" + _segment(0xC9, bytes([8, 0, 8, 0, 8, 1, 1, 0x11, 0]))
+    with pytest.raises(capi.MxdError, match="arithmetic"):
+        capi.jpeg_info(sof9)
+    # 12-bit precision
+    sof1_12 = b"\xff\xd8" + _segment(0xC1, bytes([12, 0, 8, 0, 8, 1, 1, 0x11, 0]))
+    with pytest.raises(capi.MxdError, match="precision"):
+        capi.jpeg_info(sof1_12)
+    # header cut inside the frame
+    data = bytes(GOLD["sub2_prog0_jpg"])
+    sof = data.index(b"\xff\xc0")
+    with pytest.raises(capi.MxdError):
+        capi.jpeg_info(data[:sof + 6])
+
+
+def test_load_image_uses_native_decoder(tmp_path):
+    """load_image on JPEG bytes (from_memory) and files: the fixture pixels, in
+    the reference's (H, W, 3) layout; info=True gives (w, h)."""
+    from mlx_data_amd import data as dx
+
+    raw = GOLD["caltech_300x200_jpg"]
+    want = GOLD["caltech_300x200_rgb"]
+    (tmp_path / "x.jpg").write_bytes(raw.tobytes())
+    b = dx.buffer_from_vector([dict(f=b"x.jpg", m=raw)])
+    s = b.load_image("f", prefix=str(tmp_path), output_key="img").load_image("m", from_memory=True)[0]
+    assert np.array_equal(s["img"], want) and np.array_equal(s["m"], want)
+    info = b.load_image("f", prefix=str(tmp_path), info=True)[0]["f"]
+    assert info.tolist() == [want.shape[1], want.shape[0]]
+    grey = dx.buffer_from_vector([dict(m=GOLD["grey_jpg"])]).load_image("m", from_memory=True)[0]["m"]
+    assert np.array_equal(grey, GOLD["grey_rgb"]) and grey.shape[2] == 3
+    bad = np.frombuffer(bytes(raw[:200]) + b"\xff\xd9", np.uint8)
+    bad = np.concatenate([bad[:2], np.frombuffer(b"\xff\xc9\x00\x0b\x08\x00\x08\x00\x08\x01\x01\x11\x00", np.uint8),
+                          bad[2:]])
+    with pytest.raises(RuntimeError, match=r"load_jpeg: could not load from memory \(.*arithmetic"):
+        dx.buffer_from_vector([dict(m=bad)]).load_image("m", from_memory=True)[0]

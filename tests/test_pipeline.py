@@ -226,7 +226,8 @@ def test_load_image(tmp_path):
     raw = (tmp_path / "a.jpg").read_bytes()
     m = dx.buffer_from_vector([dict(f=np.frombuffer(raw, np.uint8))]).load_image("f", from_memory=True)
     assert np.array_equal(m[0]["f"], expect)
-    with pytest.raises(RuntimeError, match=r"LoadImage: unable to load image <.*missing.jpg>"):
+    # core/image/ImageJPEG.cpp:77-80 (check_signature's fopen) names the path
+    with pytest.raises(RuntimeError, match=r"load_jpeg: could not load <.*missing.jpg>"):
         dx.buffer_from_vector([dict(f=b"missing.jpg")]).load_image("f", prefix=str(tmp_path))[0]
     with pytest.raises(RuntimeError, match=r"char array \(int8\) expected"):
         dx.buffer_from_vector([dict(f=np.zeros(3, np.uint8))]).load_image("f")[0]
