@@ -318,6 +318,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-copy", action="store_true")
+    # kernel policy (include/mxd_amd.h mxd_policy; tuning measurements only)
+    ap.add_argument("--policy", type=int, default=0, help=argparse.SUPPRESS)
+    # input/output sets that alternate step by step (1 = every step re-reads the same batch)
+    ap.add_argument("--sets", type=int, default=2, help=argparse.SUPPRESS)
     # timing plumbing without a GPU (tests/test_bench_dist.py): each step sleeps
     ap.add_argument("--simulate", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -342,6 +346,8 @@ def main():
     ranks = Ranks()
     dev = int(os.environ.get("MXD_BENCH_DEVICE", ranks.local))  # rehearsal: several ranks on one GPU
     capi.check(capi.lib().mxd_set_device(dev))
+    if args.policy:
+        capi.set_kernel_policy(args.policy)
     sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank)
     elem = 4 if f32 else 1
 
@@ -367,7 +373,7 @@ def main():
     L = capi.lib()
     hs = ctypes.c_void_p(stream.handle)
     sets = []
-    for _ in range(2):
+    for _ in range(max(1, args.sets)):
         src = capi.DeviceBuffer(total, dev)
         dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
         src.upload(host, stream=stream)
@@ -379,7 +385,7 @@ def main():
         sets.append((src, dst, imgs, n))
 
     def step(i):
-        _, _, imgs, n = sets[i & 1]
+        _, _, imgs, n = sets[i % len(sets)]
         capi.check(L.mxd_resize_crop_batch(imgs, n, mode, dev, hs))
 
     for i in range(args.warmup):

@@ -109,8 +109,9 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
  * bit-identical results (for tests and tuning; default 0 = automatic choice).
  * MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
  * of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
- * general workgroup-tile kernel.  Returns the previous policy. */
-enum mxd_policy { MXD_POLICY_AUTO = 0, MXD_POLICY_NO_SCATTER = 1, MXD_POLICY_NO_WAVE = 2 };
+ * general workgroup-tile kernel; MXD_POLICY_NARROW: wave kernels keep the
+ * narrow per-lane window (no wide RGB strips).  Returns the previous policy. */
+enum mxd_policy { MXD_POLICY_AUTO = 0, MXD_POLICY_NO_SCATTER = 1, MXD_POLICY_NO_WAVE = 2, MXD_POLICY_NARROW = 4 };
 int mxd_set_kernel_policy(int32_t policy);
 
 /* The kernel mxd_resize_crop_batch would run for one image on `device`
@@ -146,11 +147,18 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop);
 
 /* ---- host-resident convenience path ------------------------------------ */
 
-/* Host image in, host result out: pinned staging, H2D, fused kernel, D2H on
- * the calling thread's per-device stream; synchronous.  `images[i].src` and
- * `images[i].dst` are HOST pointers here.  This is the path the C++ pipeline
- * ops use when samples live in host memory (mlx-data's default). */
+/* Host image in, host result out; synchronous.  `images[i].src` and
+ * `images[i].dst` are HOST pointers here.  Only each image's source footprint
+ * (the rows and columns its crop window's taps touch) is staged into pinned
+ * memory and copied to the device; the batch runs in chunks whose host
+ * staging, H2D, kernel, D2H and copy-out overlap across two streams.  Calls
+ * borrow one of a bounded number of per-device contexts (threads beyond that
+ * wait), so pinned and device memory stay bounded.  This is the path the C++
+ * pipeline ops use when samples live in host memory (mlx-data's default). */
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device);
+
+/* Frees the pinned and device buffers of idle host-path contexts. */
+int mxd_release_host_buffers(void);
 
 /* ---- JPEG decode (load_image's producer) ---------------
  *

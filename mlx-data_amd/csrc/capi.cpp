@@ -7,10 +7,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -128,11 +130,20 @@ TableCache& host_tables() {
 // the ImgDev array.  Re-uploads are skipped when the batch is unchanged.
 struct Workspace {
   std::mutex mu;
-  ImgDev* host = nullptr;  // pinned
-  ImgDev* dev = nullptr;
-  size_t cap = 0;
-  size_t count = 0;
-  hipEvent_t copied = nullptr;
+  // Descriptor slots: each launch reads its descriptors from one slot's
+  // device copy; a new batch takes the next slot, whose host staging is
+  // refilled once the launch that last used it has finished.  The upload runs
+  // on a copy stream while the previous launch computes, and the launch waits
+  // for it, so consecutive batches never serialize behind an H2D copy.
+  static constexpr int kSlots = 4;
+  struct Slot {
+    ImgDev* host = nullptr;  // pinned
+    ImgDev* dev = nullptr;
+    size_t cap = 0, count = 0;
+    hipEvent_t copied = nullptr, used = nullptr;
+  } slot[kSlots];
+  int cur = -1;
+  hipStream_t copy = nullptr;
   // Fork/join helpers: the launches of a mixed batch (one per kernel shape)
   // run concurrently on these streams, so one launch's tail overlaps the
   // next instead of idling the CUs between serialized launches.
@@ -206,29 +217,44 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t n = descs.size();
   const size_t bytes = sizeof(ImgDev) * n;
-  const bool same = ws->count == n && ws->host && std::memcmp(ws->host, descs.data(), bytes) == 0;
-  if (!same) {
-    if (ws->copied) MXD_HIP(hipEventSynchronize(ws->copied));  // staging no longer read
-    if (n > ws->cap) {
-      if (ws->dev) {
-        MXD_HIP(hipStreamSynchronize(s));
-        MXD_HIP(hipFree(ws->dev));
-        MXD_HIP(hipHostFree(ws->host));
-        ws->dev = nullptr;
-        ws->host = nullptr;
-      }
-      const size_t cap = std::max<size_t>(n, 64);
-      MXD_HIP(hipMalloc(reinterpret_cast<void**>(&ws->dev), sizeof(ImgDev) * cap));
-      MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws->host), sizeof(ImgDev) * cap, hipHostMallocDefault));
-      ws->cap = cap;
+  if (ws->cur >= 0) {
+    Workspace::Slot& c = ws->slot[ws->cur];
+    if (c.count == n && std::memcmp(c.host, descs.data(), bytes) == 0) {  // same batch again
+      *dev_out = c.dev;
+      return MXD_OK;
     }
-    if (!ws->copied) MXD_HIP(hipEventCreateWithFlags(&ws->copied, hipEventDisableTiming));
-    std::memcpy(ws->host, descs.data(), bytes);
-    MXD_HIP(hipMemcpyAsync(ws->dev, ws->host, bytes, hipMemcpyHostToDevice, s));
-    MXD_HIP(hipEventRecord(ws->copied, s));
-    ws->count = n;
   }
-  *dev_out = ws->dev;
+  if (!ws->copy) MXD_HIP(hipStreamCreateWithFlags(&ws->copy, hipStreamNonBlocking));
+  ws->cur = (ws->cur + 1) % Workspace::kSlots;
+  Workspace::Slot& c = ws->slot[ws->cur];
+  if (!c.copied) {
+    MXD_HIP(hipEventCreateWithFlags(&c.copied, hipEventDisableTiming));
+    MXD_HIP(hipEventCreateWithFlags(&c.used, hipEventDisableTiming));
+  } else {
+    MXD_HIP(hipEventSynchronize(c.used));  // the launch that last read this slot is done
+  }
+  if (n > c.cap) {
+    if (c.dev) MXD_HIP(hipFree(c.dev));
+    if (c.host) MXD_HIP(hipHostFree(c.host));
+    c.dev = nullptr;
+    c.host = nullptr;
+    const size_t cap = std::max<size_t>(n, 64);
+    MXD_HIP(hipMalloc(reinterpret_cast<void**>(&c.dev), sizeof(ImgDev) * cap));
+    MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&c.host), sizeof(ImgDev) * cap, hipHostMallocDefault));
+    c.cap = cap;
+  }
+  std::memcpy(c.host, descs.data(), bytes);
+  c.count = n;
+  MXD_HIP(hipMemcpyAsync(c.dev, c.host, bytes, hipMemcpyHostToDevice, ws->copy));
+  MXD_HIP(hipEventRecord(c.copied, ws->copy));
+  MXD_HIP(hipStreamWaitEvent(s, c.copied, 0));
+  *dev_out = c.dev;
+  return MXD_OK;
+}
+
+// After the launches of a batch: the slot is free again once they finish.
+int release_descs(Workspace* ws, void* stream) {
+  MXD_HIP(hipEventRecord(ws->slot[ws->cur].used, reinterpret_cast<hipStream_t>(stream)));
   return MXD_OK;
 }
 
@@ -425,6 +451,9 @@ bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t pp, int32_t* n
 // stays <= kMaxBand, then the smallest band height whose unit count fits them.
 int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_t capacity) {
   constexpr int32_t kMinBand = 8, kMaxBand = 64;
+#ifdef MXD_TUNING_ENV  // tuning builds only (tools/ablate8.sh): never read by the product library
+  if (const char* e = std::getenv("MXD_BAND_ROWS")) return std::max(1, std::atoi(e));
+#endif
   int64_t rows = 0;
   int32_t max_h = 1;
   for (auto& s : strips) {
@@ -460,26 +489,38 @@ int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
   return c;
 }
 
-// The wave path reads through the 4-byte aligned address below `src` and
-// shifts its column bytes by the remainder (a source window at any x, e.g.
-// random_area_crop); rows must stay 4-byte aligned.  f32 outputs are stored
-// per pixel (4-byte aligned), u8 outputs per byte.
-bool wave_layout_ok(const mxd_image& im, int32_t out_dtype) {
+// Where an image's source bytes live: the whole image at mxd_image::src, or
+// (host path) only its staged footprint: `rows` rows from source row y0 and
+// columns from source pixel x0 at base, `stride` bytes apart.
+struct Stored {
+  const uint8_t* base;
+  int64_t stride;
+  int32_t x0, y0, rows;
+};
+
+Stored whole(const mxd_image& im) { return Stored{im.src, im.src_stride, 0, 0, im.src_h}; }
+
+// The wave path reads through the 4-byte aligned address below the stored
+// base and shifts its column bytes by the remainder (a source window at any
+// x, e.g. random_area_crop); rows must stay 4-byte aligned.  f32 outputs are
+// stored per pixel (4-byte aligned), u8 outputs per byte.
+bool wave_layout_ok(const mxd_image& im, const Stored& st, int32_t out_dtype) {
   const uintptr_t o = reinterpret_cast<uintptr_t>(im.dst) | (uintptr_t)im.dst_stride;
-  return im.channels <= 3 && (im.src_stride & 3) == 0 && (out_dtype != MXD_F32_DIV255 || (o & 3) == 0) &&
-         (int64_t)(reinterpret_cast<uintptr_t>(im.src) & 3) + (int64_t)im.src_w * im.channels <= im.src_stride &&
-         im.src_stride * (int64_t)im.src_h < ((int64_t)1 << 31);
+  const int64_t row = (int64_t)(im.src_w - st.x0) * im.channels;
+  return im.channels <= 3 && (st.stride & 3) == 0 && (out_dtype != MXD_F32_DIV255 || (o & 3) == 0) &&
+         (int64_t)(reinterpret_cast<uintptr_t>(st.base) & 3) + std::min(row, st.stride) <= st.stride &&
+         st.stride * (int64_t)st.rows < ((int64_t)1 << 31);
 }
 
 // Chooses the wave kernel of one image (p.wave = false: the general kernel):
 // over the lane widths available for its channel count, the one that cuts
 // the crop into the fewest strips (narrow strips read more halo and more,
 // shorter row pieces), then the narrower lane width.
-void plan_wave(const mxd_image& im, int32_t f32, int32_t out_dtype, ImgPlan& p) {
+void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_dtype, ImgPlan& p) {
   p.wave = false;
-  if (!wave_layout_ok(im, out_dtype)) return;
+  if (!wave_layout_ok(im, st, out_dtype)) return;
   const int32_t c = im.channels;
-  const int32_t shift = (reinterpret_cast<uintptr_t>(im.src) & 3) != 0 ? 1 : 0;
+  const int32_t shift = (reinterpret_cast<uintptr_t>(st.base) & 3) != 0 ? 1 : 0;
   // Scatter when the vertical axis downsamples into a shape with a kernel,
   // else gather.
   const ScatterShape sh =
@@ -487,7 +528,7 @@ void plan_wave(const mxd_image& im, int32_t f32, int32_t out_dtype, ImgPlan& p) 
   const int32_t xb = mxd::wave_taps_bucket(p.xt->width);
   const int32_t gb = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
   const int32_t dp = mxd::wave_default_p(c);
-  const int32_t widths[2] = {dp, c == 3 ? 8 : dp};
+  const int32_t widths[2] = {dp, c == 3 && !(g_policy.load() & MXD_POLICY_NARROW) ? 8 : dp};
   for (int32_t pp : widths) {
     if (p.wave && pp == p.pp) continue;
     int32_t ns = 0, tx = 0, q = 0;
@@ -517,7 +558,8 @@ void plan_wave(const mxd_image& im, int32_t f32, int32_t out_dtype, ImgPlan& p) 
   }
 }
 
-int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream) {
+int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream,
+              const Stored* stored = nullptr) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
   if (n == 0) return MXD_OK;
@@ -539,16 +581,20 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     ImgPlan& p = plans[i];
     if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
     if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
-    if (!no_wave) plan_wave(im, f32, out_dtype, p);
+    if (!no_wave) plan_wave(im, stored ? stored[i] : whole(im), f32, out_dtype, p);
     if (!p.wave) slow.push_back(i);
   }
   DeviceGuard guard(device);
-  auto fill = [&](ImgDev& d, const mxd_image& im, const ImgPlan& p) {
+  auto fill = [&](ImgDev& d, int32_t i, const ImgPlan& p) {
+    const mxd_image& im = images[i];
+    const Stored st = stored ? stored[i] : whole(im);
     d = ImgDev{};
-    d.src = im.src;
-    d.src_stride = im.src_stride;
+    d.src = st.base;
+    d.src_stride = st.stride;
     d.src_w = im.src_w;
-    d.src_h = im.src_h;
+    d.src_h = st.rows;
+    d.src_x0 = st.x0;
+    d.src_y0 = st.y0;
     d.dst = im.dst;
     d.dst_stride = im.dst_stride;
     d.xwidth = p.xt->padded;
@@ -595,7 +641,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const mxd_image& im = images[i];
       const ImgPlan& p = plans[i];
       ImgDev& d = descs[k];
-      fill(d, im, p);
+      fill(d, i, p);
       // aligned base + byte shift (ImgDev::flip bits 8..)
       const uintptr_t a = reinterpret_cast<uintptr_t>(d.src);
       d.src = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
@@ -624,9 +670,17 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   LaunchCfg cfg{};
   int32_t tiles = 0;
   if (!slow.empty()) {
+    // The tile kernel addresses rows from the image's row 0: a staged
+    // footprint is reached through the (never dereferenced) address its
+    // row 0 would have; the kernel only reads footprint rows and columns.
+    auto base0 = [&](int32_t i) {
+      const Stored st = stored ? stored[i] : whole(images[i]);
+      return st.base - (int64_t)st.y0 * st.stride - (int64_t)st.x0 * images[i].channels;
+    };
     bool aligned16 = true;
     for (int32_t i : slow) {
-      const uintptr_t a = reinterpret_cast<uintptr_t>(images[i].src) | (uintptr_t)images[i].src_stride;
+      const Stored st = stored ? stored[i] : whole(images[i]);
+      const uintptr_t a = reinterpret_cast<uintptr_t>(base0(i)) | (uintptr_t)st.stride;
       aligned16 = aligned16 && (a & 15) == 0;
     }
     const int32_t vec = aligned16 ? 16 : 1;
@@ -658,7 +712,10 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       group = std::min(group, ty);
       const int32_t nbands = (im.crop_h + ty - 1) / ty;
       ImgDev& d = descs[nw + k];
-      fill(d, im, plans[i]);
+      fill(d, i, plans[i]);
+      d.src = base0(i);
+      d.src_h = im.src_h;
+      d.src_x0 = d.src_y0 = 0;
       d.tile_begin = tiles;
       d.nstrips = nstrips;
       d.ty = ty;
@@ -721,7 +778,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
     MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
   }
-  return MXD_OK;
+  return release_descs(ws, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -842,9 +899,15 @@ int run_pixmap(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, 
 }
 
 // ---------------------------------------------------------------------------
-// Host-resident path: per-(thread, device) stream + growable buffers.
-struct HostCtx {
+// Host-resident path.  Each call borrows a context from its device's pool
+// (at most kCtxPerDevice, so pinned / device memory is bounded no matter how
+// many threads call), and runs the batch in chunks over the context's two
+// slots: while the GPU copies in, computes and copies out chunk k on one
+// slot's stream, the calling thread stages chunk k+1 into the other slot's
+// pinned buffer and copies chunk k-1's results out.
+struct Slot {
   hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
   uint8_t* pin_in = nullptr;
   size_t pin_in_cap = 0;
   uint8_t* pin_out = nullptr;
@@ -855,11 +918,16 @@ struct HostCtx {
   size_t dev_out_cap = 0;
 };
 
+struct HostCtx {
+  Slot slot[2];
+};
+
 int grow_pinned(uint8_t** p, size_t* cap, size_t need) {
   if (need <= *cap) return MXD_OK;
   if (*p) MXD_HIP(hipHostFree(*p));
   *p = nullptr;
-  const size_t c = std::max(need, *cap * 2);
+  *cap = 0;
+  const size_t c = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
   MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(p), c, hipHostMallocDefault));
   *cap = c;
   return MXD_OK;
@@ -869,15 +937,94 @@ int grow_device(uint8_t** p, size_t* cap, size_t need) {
   if (need <= *cap) return MXD_OK;
   if (*p) MXD_HIP(hipFree(*p));
   *p = nullptr;
-  const size_t c = std::max(need, *cap * 2);
+  *cap = 0;
+  const size_t c = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
   MXD_HIP(hipMalloc(reinterpret_cast<void**>(p), c));
   *cap = c;
   return MXD_OK;
 }
 
-HostCtx& host_ctx(int32_t device) {
-  thread_local std::map<int32_t, HostCtx> ctx;
-  return ctx[device];
+void free_slot_buffers(Slot& s) {
+  if (s.pin_in) (void)hipHostFree(s.pin_in);
+  if (s.pin_out) (void)hipHostFree(s.pin_out);
+  if (s.dev_in) (void)hipFree(s.dev_in);
+  if (s.dev_out) (void)hipFree(s.dev_out);
+  s.pin_in = s.pin_out = s.dev_in = s.dev_out = nullptr;
+  s.pin_in_cap = s.pin_out_cap = s.dev_in_cap = s.dev_out_cap = 0;
+}
+
+constexpr int kCtxPerDevice = 4;
+
+class HostPool {
+ public:
+  HostCtx* acquire(int32_t device) {
+    std::unique_lock<std::mutex> lk(mu_);
+    Dev& d = devs_[device];
+    cv_.wait(lk, [&] { return !d.idle.empty() || (int)d.all.size() < kCtxPerDevice; });
+    if (!d.idle.empty()) {
+      HostCtx* c = d.idle.back();
+      d.idle.pop_back();
+      return c;
+    }
+    d.all.push_back(std::make_unique<HostCtx>());
+    return d.all.back().get();
+  }
+  void release(int32_t device, HostCtx* c) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      devs_[device].idle.push_back(c);
+    }
+    cv_.notify_one();
+  }
+  // Frees the buffers of every idle context (streams stay).
+  void trim() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& kv : devs_) {
+      DeviceGuard g(kv.first);
+      for (HostCtx* c : kv.second.idle)
+        for (Slot& s : c->slot) free_slot_buffers(s);
+    }
+  }
+
+ private:
+  struct Dev {
+    std::vector<std::unique_ptr<HostCtx>> all;
+    std::vector<HostCtx*> idle;
+  };
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int32_t, Dev> devs_;
+};
+
+HostPool& host_pool() {
+  static HostPool* p = new HostPool();
+  return *p;
+}
+
+// Borrowed context, returned to the pool on scope exit.
+struct CtxLease {
+  int32_t device;
+  HostCtx* ctx;
+  explicit CtxLease(int32_t d) : device(d), ctx(host_pool().acquire(d)) {}
+  ~CtxLease() { host_pool().release(device, ctx); }
+};
+
+int init_slot(Slot& s) {
+  if (!s.stream) MXD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  if (!s.done) MXD_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  return MXD_OK;
+}
+
+// Source footprint of an image's crop window (rows [y_lo, y_hi], pixels
+// [x_lo, x_hi]): taps are monotone, so the window's ends bound it.
+void footprint(const DevTable& xt, const DevTable& yt, const mxd_image& im, int32_t* x_lo, int32_t* x_hi,
+               int32_t* y_lo, int32_t* y_hi) {
+  const int32_t xa = im.crop_x, xb = im.crop_x + im.crop_w - 1;
+  const int32_t ya = im.crop_y, yb = im.crop_y + im.crop_h - 1;
+  *x_lo = xt.first[xa];
+  *x_hi = xt.first[xb] + xt.count[xb] - 1;
+  *y_lo = yt.first[ya];
+  *y_hi = yt.first[yb] + yt.count[yb] - 1;
 }
 
 }  // namespace
@@ -940,7 +1087,7 @@ int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device,
   ImgPlan p;
   if (int rc = host_tables().get(device, image->src_w, image->resize_w, &p.xt)) return rc;
   if (int rc = host_tables().get(device, image->src_h, image->resize_h, &p.yt)) return rc;
-  if (!(g_policy.load() & MXD_POLICY_NO_WAVE)) plan_wave(*image, out_dtype == MXD_F32_DIV255, out_dtype, p);
+  if (!(g_policy.load() & MXD_POLICY_NO_WAVE)) plan_wave(*image, whole(*image), out_dtype == MXD_F32_DIV255, out_dtype, p);
   const int32_t v[8] = {p.wave ? 1 : 0, p.kind, p.bucket, p.s, p.dmax, p.q, p.nstrips, p.pp};
   std::memcpy(info8, v, sizeof v);
   return MXD_OK;
@@ -1075,51 +1222,121 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop) {
 
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
   if (n == 0) return MXD_OK;
   const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
   for (int32_t i = 0; i < n; i++)
     if (int rc = validate(images[i], i)) return rc;
   DeviceGuard g(device);
-  HostCtx& ctx = host_ctx(device);
-  if (!ctx.stream) MXD_HIP(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
-  // Pack every source with a 16-byte aligned pitch so the vector path applies.
-  std::vector<size_t> in_off(n), out_off(n);
-  std::vector<int64_t> pitch(n);
-  size_t in_bytes = 0, out_bytes = 0;
+  // Per image: the staged footprint (columns from x0, 16-byte aligned so both
+  // kernel families read it as they would the whole image) and its offsets.
+  struct Stage {
+    int32_t x0, y0, rows;
+    int64_t pitch, copy, in_off, out_off, out_row;
+  };
+  std::vector<Stage> st(n);
   for (int32_t i = 0; i < n; i++) {
     const mxd_image& im = images[i];
-    pitch[i] = ((int64_t)im.src_w * im.channels + 15) & ~(int64_t)15;
-    in_off[i] = in_bytes;
-    in_bytes += ((size_t)pitch[i] * im.src_h + 255) & ~(size_t)255;
-    out_off[i] = out_bytes;
-    out_bytes += ((size_t)im.crop_w * im.channels * elem * im.crop_h + 255) & ~(size_t)255;
+    const DevTable *xt = nullptr, *yt = nullptr;
+    if (int rc = tables().get(device, im.src_w, im.resize_w, &xt)) return rc;
+    if (int rc = tables().get(device, im.src_h, im.resize_h, &yt)) return rc;
+    int32_t xl, xh, yl, yh;
+    footprint(*xt, *yt, im, &xl, &xh, &yl, &yh);
+    const int32_t c = im.channels;
+    const int32_t m = 16 / std::gcd(c, 16);  // x0 * c is a multiple of 16
+    Stage& s = st[i];
+    s.x0 = xl - xl % m;
+    s.y0 = yl;
+    s.rows = yh - yl + 1;
+    const int64_t want = (int64_t)(xh + 1 - s.x0) * c + 32;  // + the kernels' read-ahead inside a row
+    s.copy = std::min<int64_t>((int64_t)(im.src_w - s.x0) * c, want);
+    s.pitch = (want + 15) & ~(int64_t)15;
+    s.out_row = (int64_t)im.crop_w * c * elem;
   }
-  if (int rc = grow_pinned(&ctx.pin_in, &ctx.pin_in_cap, in_bytes)) return rc;
-  if (int rc = grow_pinned(&ctx.pin_out, &ctx.pin_out_cap, out_bytes)) return rc;
-  if (int rc = grow_device(&ctx.dev_in, &ctx.dev_in_cap, in_bytes)) return rc;
-  if (int rc = grow_device(&ctx.dev_out, &ctx.dev_out_cap, out_bytes)) return rc;
-  std::vector<mxd_image> dev_imgs(images, images + n);
-  for (int32_t i = 0; i < n; i++) {
-    const mxd_image& im = images[i];
-    const size_t row = (size_t)im.src_w * im.channels;
-    uint8_t* stage = ctx.pin_in + in_off[i];
-    for (int32_t r = 0; r < im.src_h; r++) std::memcpy(stage + (size_t)r * pitch[i], im.src + (size_t)r * im.src_stride, row);
-    dev_imgs[i].src = ctx.dev_in + in_off[i];
-    dev_imgs[i].src_stride = pitch[i];
-    dev_imgs[i].dst = ctx.dev_out + out_off[i];
-    dev_imgs[i].dst_stride = (int64_t)im.crop_w * im.channels * elem;
+  // Chunks of about kChunk staged bytes (at least one image each).
+  constexpr int64_t kChunk = 24 << 20;
+  std::vector<std::pair<int32_t, int32_t>> chunks;  // [first, end)
+  for (int32_t i = 0; i < n;) {
+    int32_t j = i;
+    int64_t bytes = 0;
+    while (j < n && (j == i || bytes + st[j].pitch * st[j].rows <= kChunk)) {
+      bytes += st[j].pitch * st[j].rows;
+      j++;
+    }
+    chunks.push_back({i, j});
+    i = j;
   }
-  MXD_HIP(hipMemcpyAsync(ctx.dev_in, ctx.pin_in, in_bytes, hipMemcpyHostToDevice, ctx.stream));
-  if (int rc = run_batch(dev_imgs.data(), n, out_dtype, device, ctx.stream)) return rc;
-  MXD_HIP(hipMemcpyAsync(ctx.pin_out, ctx.dev_out, out_bytes, hipMemcpyDeviceToHost, ctx.stream));
-  MXD_HIP(hipStreamSynchronize(ctx.stream));
-  for (int32_t i = 0; i < n; i++) {
-    const mxd_image& im = images[i];
-    const size_t row = (size_t)im.crop_w * im.channels * elem;
-    uint8_t* d = static_cast<uint8_t*>(im.dst);
-    const uint8_t* s = ctx.pin_out + out_off[i];
-    for (int32_t r = 0; r < im.crop_h; r++) std::memcpy(d + (size_t)r * im.dst_stride, s + r * row, row);
+  CtxLease lease(device);
+  HostCtx& ctx = *lease.ctx;
+  for (Slot& sl : ctx.slot)
+    if (int rc = init_slot(sl)) return rc;
+  int pending[2] = {-1, -1};  // chunk in flight on each slot
+  auto copy_out = [&](int k) -> int {
+    Slot& sl = ctx.slot[k & 1];
+    MXD_HIP(hipEventSynchronize(sl.done));
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+      const mxd_image& im = images[i];
+      uint8_t* d = static_cast<uint8_t*>(im.dst);
+      const uint8_t* src = sl.pin_out + st[i].out_off;
+      if (im.dst_stride == st[i].out_row) {
+        std::memcpy(d, src, (size_t)st[i].out_row * im.crop_h);
+      } else {
+        for (int32_t r = 0; r < im.crop_h; r++)
+          std::memcpy(d + (size_t)r * im.dst_stride, src + (size_t)r * st[i].out_row, st[i].out_row);
+      }
+    }
+    pending[k & 1] = -1;
+    return MXD_OK;
+  };
+  for (int k = 0; k < (int)chunks.size(); k++) {
+    Slot& sl = ctx.slot[k & 1];
+    if (pending[k & 1] >= 0)
+      if (int rc = copy_out(pending[k & 1])) return rc;
+    int64_t in_bytes = 0, out_bytes = 0;
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+      st[i].in_off = in_bytes;
+      in_bytes += (st[i].pitch * st[i].rows + 255) & ~(int64_t)255;
+      st[i].out_off = out_bytes;
+      out_bytes += (st[i].out_row * images[i].crop_h + 255) & ~(int64_t)255;
+    }
+    if (int rc = grow_pinned(&sl.pin_in, &sl.pin_in_cap, in_bytes)) return rc;
+    if (int rc = grow_pinned(&sl.pin_out, &sl.pin_out_cap, out_bytes)) return rc;
+    if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, in_bytes)) return rc;
+    if (int rc = grow_device(&sl.dev_out, &sl.dev_out_cap, out_bytes)) return rc;
+    const int32_t cn = chunks[k].second - chunks[k].first;
+    std::vector<mxd_image> dev_imgs(images + chunks[k].first, images + chunks[k].second);
+    std::vector<Stored> where(cn);
+    for (int32_t j = 0; j < cn; j++) {
+      const int32_t i = chunks[k].first + j;
+      const mxd_image& im = images[i];
+      const Stage& s = st[i];
+      uint8_t* stage = sl.pin_in + s.in_off;
+      const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
+      for (int32_t r = 0; r < s.rows; r++) std::memcpy(stage + r * s.pitch, from + (int64_t)r * im.src_stride, s.copy);
+      where[j] = Stored{sl.dev_in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
+      dev_imgs[j].src = sl.dev_in + s.in_off;  // checked by validate() only; `where` says what is stored
+      dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
+      dev_imgs[j].dst = sl.dev_out + s.out_off;
+      dev_imgs[j].dst_stride = s.out_row;
+    }
+    MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_bytes, hipMemcpyHostToDevice, sl.stream));
+    if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
+    MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_bytes, hipMemcpyDeviceToHost, sl.stream));
+    MXD_HIP(hipEventRecord(sl.done, sl.stream));
+    pending[k & 1] = k;
+    // results of the previous chunk, while this one runs
+    const int prev = pending[(k + 1) & 1];
+    if (prev >= 0)
+      if (int rc = copy_out(prev)) return rc;
   }
+  for (int k = 0; k < 2; k++)
+    if (pending[k] >= 0)
+      if (int rc = copy_out(pending[k])) return rc;
+  return MXD_OK;
+}
+
+int mxd_release_host_buffers(void) {
+  host_pool().trim();
   return MXD_OK;
 }
 
@@ -1200,8 +1417,9 @@ int mxd_pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t dev
   for (int32_t i = 0; i < n; i++)
     if (int rc = pix_validate(images[i], op, i)) return rc;
   DeviceGuard g(device);
-  HostCtx& ctx = host_ctx(device);
-  if (!ctx.stream) MXD_HIP(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+  CtxLease lease(device);
+  Slot& ctx = lease.ctx->slot[0];
+  if (int rc = init_slot(ctx)) return rc;
   std::vector<size_t> in_off(n), out_off(n);
   std::vector<int64_t> in_pitch(n), out_pitch(n);
   size_t in_bytes = 0, out_bytes = 0;

@@ -29,9 +29,10 @@ struct ImgDev {
                  // source window past the 4-byte aligned `src` (0..3)
   int32_t tile_begin;
   int32_t nstrips, ty, tx, group;
-  int32_t src_w, src_h;
+  int32_t src_w, src_h;  // src_h: rows stored at src (the whole image, or a staged footprint)
+  int32_t src_x0, src_y0;  // source pixel at src (0, 0 unless only a footprint is stored)
 };
-static_assert(sizeof(ImgDev) == 96, "ImgDev layout");
+static_assert(sizeof(ImgDev) == 104, "ImgDev layout");
 
 struct LaunchCfg {
   int32_t vec;        // bytes per thread per source row: 16 (16-byte aligned rows) or 1

@@ -74,6 +74,12 @@ constexpr int kLanes = 64;
 #ifndef MXD_MIN_WAVES_WIDE
 #define MXD_MIN_WAVES_WIDE 2
 #endif
+// Tuning build (-DMXD_SYNC_STRIPS=1): when a workgroup's four waves are the
+// four strips of one band, an s_barrier after every group keeps them loading
+// the same source rows at the same time.
+#ifndef MXD_SYNC_STRIPS
+#define MXD_SYNC_STRIPS 0
+#endif
 constexpr int kPad = 32;  // floats after each plane: padded taps read zeros there
 
 #define GLOBAL_PTR(T, p) ((__attribute__((address_space(1))) T*)(p))
@@ -172,22 +178,26 @@ __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_
 // records: every load through it returns zeros without a memory request).
 // SHIFT: the window starts `sh` bytes past a 4-byte boundary (a source window
 // at any x); one more dword is loaded and the bytes are realigned.
+// Row offsets go into the VGPR offset (r - y0) * stride + lane offset, which
+// the buffer range check covers (the scalar offset is not checked): rows
+// outside the stored region read zeros, never other memory.
 template <class L, bool SHIFT>
 struct Src {
   Rsrc live, dead;
-  int stride, voff, sh;
+  int stride, voff, sh, y0;
 
   __device__ __forceinline__ Raw<L::ND> load(int r) const {
     constexpr int ND = L::ND;
     const bool ok = r >= 0 && !(MXD_ABLATE & 1);
     const Rsrc rs = ok ? live : dead;
-    const int soff = ok ? r * stride : 0;
+    // unsigned: a row above the region wraps to a huge (out-of-range) offset
+    const int off = (int)((uint32_t)voff + (ok ? (uint32_t)((r - y0) * stride) : 0u));
     Raw<ND> x;
     if constexpr (!SHIFT) {
-      load_dwords<ND>(rs, voff, soff, x.d);
+      load_dwords<ND>(rs, off, 0, x.d);
     } else {
       uint32_t w[ND + 1];
-      load_dwords<ND + 1>(rs, voff, soff, w);
+      load_dwords<ND + 1>(rs, off, 0, w);
 #pragma unroll
       for (int j = 0; j < ND; j++) x.d[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
     }
@@ -336,7 +346,8 @@ struct HStrip {
 // Runs a band's scatter schedule (see the top of the file); on_row(acc, y) is
 // called with the V sums of every completed output row y.
 template <class L, int S, int DMAX, bool SHIFT, class OnRow>
-__device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const Src<L, SHIFT>& src, OnRow&& on_row) {
+__device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const Src<L, SHIFT>& src, OnRow&& on_row,
+                                             bool sync = false) {
   constexpr int C = L::C;
   constexpr int R = scatter_ring_slots(DMAX);
   constexpr int LA = R - 1;  // iterations loaded ahead
@@ -386,6 +397,8 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
       const int y = gout[gb + gi];
       if (y >= 0) on_row(acc[gi % S], y);
       zero_planes<C, P>(acc[gi % S]);
+      if constexpr (MXD_SYNC_STRIPS != 0)
+        if (sync) __builtin_amdgcn_s_barrier();
     });
   }
 }
@@ -438,7 +451,9 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
     src.live = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, stride * rows, 0x00020000);
     src.dead = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0, 0x00020000);
     src.stride = stride;
-    const int fbyte = wp0 * C + shift;  // window start, bytes past the 4-byte aligned base
+    src.y0 = __builtin_amdgcn_readfirstlane(im.src_y0);
+    // window start, bytes past the 4-byte aligned base of the stored region
+    const int fbyte = (wp0 - __builtin_amdgcn_readfirstlane(im.src_x0)) * C + shift;
     src.sh = fbyte & 3;
     src.voff = P * lane < npx ? (fbyte & ~3) + L::LB * lane : kNoLoad;
   }
@@ -504,7 +519,8 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row);
+    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row,
+                                    nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0);
   }
 }
 

@@ -25,7 +25,7 @@ EXPORTS = (
     "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
     "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
     "mxd_event_create", "mxd_event_destroy", "mxd_event_record", "mxd_event_synchronize", "mxd_event_elapsed_ms",
-    "mxd_resize_crop_host",
+    "mxd_resize_crop_host", "mxd_release_host_buffers",
     "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
 )
@@ -36,6 +36,7 @@ MXD_CHANNEL_REDUCTION = 1
 MXD_POLICY_AUTO = 0
 MXD_POLICY_NO_SCATTER = 1
 MXD_POLICY_NO_WAVE = 2
+MXD_POLICY_NARROW = 4
 
 
 class MxdImage(ctypes.Structure):

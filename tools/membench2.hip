@@ -206,14 +206,98 @@ __global__ __launch_bounds__(256) void c2_kmix(const uint8_t* __restrict__ base,
   if (acc[0] == -1.0f) out[lane] = acc[1];
 }
 
+int g_iter = 0;  // launches alternate source / output buffers on g_iter's parity
+
+
+// Workgroup = (image, band): wave w reads strip w's window (LB bytes per lane,
+// strips x wb bytes at step `step`); every K output rows the workgroup writes
+// the K full output rows (K x 2688 B, contiguous) with 16 B per lane, between
+// two barriers (the K-row burst a workgroup-staged kernel would produce).
+template <int K, int DEPTH>
+__global__ __launch_bounds__(256) void c2_wgmix(const uint8_t* __restrict__ base, float* __restrict__ out, int nbands,
+                                                int wb, int step, int halo, int write) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int unit = blockIdx.x;
+  if (unit >= kImgs * nbands) return;
+  const int img = unit / nbands, band = unit - img * nbands;
+  const uint8_t* p = base + (size_t)img * kRows * kStride;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, kRows * kStride, 0x00020000);
+  const int voff = 12 * lane < wb ? kFb0 + wave * step + 12 * lane : kNoLoad;
+  const int oy0 = band * kOutRows / nbands, oy1 = (band + 1) * kOutRows / nbands;
+  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + halo);
+  char* o = reinterpret_cast<char*>(out) + (size_t)img * kOutRows * kOutRow;
+  typedef unsigned uv __attribute__((ext_vector_type(3)));
+  uv ring[DEPTH];
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) ring[d] = __builtin_amdgcn_raw_buffer_load_b96(r, voff, min(r0 + d, r1 - 1) * kStride, 0);
+  float acc[4] = {0, 0, 0, 0};
+  int oy = oy0, pend = 0;
+  for (int row = r0; row < r1; row += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      acc[0] += (float)(ring[d].x & 255);
+      acc[1] += (float)(ring[d].y >> 24);
+      acc[2] += (float)(ring[d].z & 255);
+      ring[d] = __builtin_amdgcn_raw_buffer_load_b96(r, voff, min(row + d + DEPTH, r1 - 1) * kStride, 0);
+      const int want = (int)((row + d - r0) / 3.768f) + oy0;
+      if (want > oy && oy < oy1) {
+        oy++;
+        if (++pend == K || oy == oy1) {
+          if (write) {
+            __syncthreads();
+            f4* dst = reinterpret_cast<f4*>(o + (size_t)(oy - pend) * kOutRow);
+            for (int b = threadIdx.x; b < pend * kOutRow / 16; b += 256) dst[b] = f4{acc[0], acc[1], acc[2], acc[3]};
+            __syncthreads();
+          }
+          pend = 0;
+        }
+      }
+    }
+  }
+  if (acc[0] == -1.0f) out[lane] = acc[1];
+}
+
+int g_iter_dummy;
+
+// DRAM mix probes (one workgroup per chunk of consecutive "rows"):
+//   mode 0: read `rb` bytes of each of `nrows` rows spaced `rstride` apart,
+//           write 2688 B to a sequential output every `ratio` rows.
+template <int U>
+__global__ __launch_bounds__(256) void mixprobe(const uint8_t* __restrict__ base, f4* __restrict__ out, int nrows,
+                                                int rstride, int rb, float ratio, int rows_per_block, int write) {
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, nrows);
+  float acc = 0.0f;
+  int wrote = (int)(r0 / ratio);
+  for (int r = r0; r < r1; r += U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int rr = min(r + u, nrows - 1);
+      const int off = 16 * threadIdx.x;
+      v[u] = off < rb ? *reinterpret_cast<const u32x4*>(base + (size_t)rr * rstride + off) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) acc += (float)(v[u].x & 255) + (float)(v[u].w >> 24);
+    const int want = (int)((r + U) / ratio);
+    if (write) {
+      for (; wrote < want; wrote++) {
+        f4* o = out + (size_t)wrote * (2688 / 16);
+        if (threadIdx.x < 2688 / 16) o[threadIdx.x] = f4{acc, acc, acc, acc};
+      }
+    }
+  }
+  if (acc == -1.0f) out[0] = f4{acc, acc, acc, acc};
+}
+
 double timeit(const char* name, double bytes, std::function<void()> f) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  for (int w = 0; w < 3; w++) f();
+  for (int w = 0; w < 3; w++, g_iter++) f();
   CHECK(hipEventRecord(a));
   const int iters = 20;
-  for (int i = 0; i < iters; i++) f();
+  for (int i = 0; i < iters; i++, g_iter++) f();
   CHECK(hipEventRecord(b));
   CHECK(hipEventSynchronize(b));
   CHECK(hipGetLastError());
@@ -260,12 +344,43 @@ int main(int argc, char** argv) {
   }
   }
 
+  if (argc > 1 && argv[1][0] == 'm') {
+    uint8_t* src2;
+    f4* out2;
+    CHECK(hipMalloc(&src2, bytes));
+    CHECK(hipMalloc(&out2, bytes));
+    const uint8_t* srcs[2] = {reinterpret_cast<const uint8_t*>(a), src2};
+    f4* outs[2] = {b, out2};
+    const int nrows = 256 * 844;  // C2 footprint rows
+    struct V { const char* n; int rstride, rb; };
+    const V vs[] = {{"contiguous 2560B rows", 2560, 2560}, {"2560B of 3840B rows", 3840, 2560},
+                    {"full 3840B rows", 3840, 3840}};
+    for (const V& v : vs)
+      for (int write : {0, 1})
+        for (int rpb : {16, 64}) {
+          snprintf(name, sizeof name, "%s rows/block=%d write=%d", v.n, rpb, write);
+          const double by = (double)nrows * v.rb + write * (double)nrows / 3.768 * 2688;
+          timeit(name, by, [&] {
+            mixprobe<4><<<(nrows + rpb - 1) / rpb, 256>>>(srcs[g_iter & 1], outs[g_iter & 1], nrows, v.rstride, v.rb,
+                                                          3.768f, rpb, write);
+          });
+        }
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'k') {
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(a);
-    float* out = reinterpret_cast<float*>(b);
+    // two source sets and two output sets, alternating (no Infinity Cache reuse between launches)
+    uint8_t *src2;
+    float* out2;
+    CHECK(hipMalloc(&src2, bytes));
+    CHECK(hipMalloc(&out2, bytes));
+    CHECK(hipMemset(src2, 3, bytes));
+    const uint8_t* srcs[2] = {reinterpret_cast<const uint8_t*>(a), src2};
+    float* outs[2] = {reinterpret_cast<float*>(b), out2};
     const double rd = (double)kImgs * (kFy1 - kFy0) * kNeed, wr = (double)kImgs * kOutRows * kOutRow;
     struct V { const char* n; int lb, sb, nb, ns, wb, step, ob, halo; };
     const V vs[] = {
+      {"1 strip (whole 2532B rows) x4 bands", 16, 16, 4, 1, 2532, 0, 2688, 4},
+      {"2 strips 1266B x4 bands", 16, 16, 4, 2, 1280, 1266, 1344, 4},
       {"kernel-like 4x4 x3/x3 768B 672B halo4", 12, 12, 4, 4, 768, 633, 672, 4},
       {"4x4 x3 loads, 672B x4-less? (x3) halo0", 12, 12, 4, 4, 768, 633, 672, 0},
       {"4x4 window 633B (no overlap)", 12, 12, 4, 4, 633, 633, 672, 4},
@@ -276,11 +391,28 @@ int main(int argc, char** argv) {
       {"4x8 bands", 12, 12, 8, 4, 768, 633, 672, 4},
       {"4x2 bands", 12, 12, 2, 4, 768, 633, 672, 4},
     };
+    for (int k : {1, 4, 8, 16}) {
+      for (int nb : {4, 8}) {
+        snprintf(name, sizeof name, "wg burst K=%d nb=%d (4 strips, full-row writes)", k, nb);
+        auto go = [&] {
+          const uint8_t* src = srcs[g_iter & 1];
+          float* out = outs[g_iter & 1];
+          if (k == 1) c2_wgmix<1, 8><<<kImgs * nb, 256>>>(src, out, nb, 768, 633, 4, 1);
+          if (k == 4) c2_wgmix<4, 8><<<kImgs * nb, 256>>>(src, out, nb, 768, 633, 4, 1);
+          if (k == 8) c2_wgmix<8, 8><<<kImgs * nb, 256>>>(src, out, nb, 768, 633, 4, 1);
+          if (k == 16) c2_wgmix<16, 8><<<kImgs * nb, 256>>>(src, out, nb, 768, 633, 4, 1);
+        };
+        timeit(name, rd + wr, go);
+      }
+    }
     for (const V& v : vs) {
+      if (v.wb > 1024) continue;
       for (int write : {0, 1}) {
         const int units = kImgs * v.nb * v.ns;
         snprintf(name, sizeof name, "%s w=%d", v.n, write);
         auto go = [&] {
+          const uint8_t* src = srcs[g_iter & 1];
+          float* out = outs[g_iter & 1];
           if (v.lb == 12 && v.sb == 12) c2_kmix<12, 12, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
           else if (v.lb == 16 && v.sb == 12) c2_kmix<16, 12, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
           else if (v.lb == 12 && v.sb == 16) c2_kmix<12, 16, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
