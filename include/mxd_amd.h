@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MXD_ABI_VERSION 1
+#define MXD_ABI_VERSION 2
 
 enum mxd_status {
   MXD_OK = 0,
@@ -64,6 +64,12 @@ enum mxd_dtype {
  *   flip         nonzero: mirror the cropped result horizontally (core::image::hflip)
  *   dst          device pointer to row 0 of the output image
  *   dst_stride   bytes between output rows
+ *   rgba_weighted  4 channels only: nonzero = the resample is stbir's STBIR_RGBA
+ *                (colours weighted by alpha while filtering), as
+ *                core::image::resize does for c = 4 (ImageTransform.cpp:49-58);
+ *                zero = channels filtered independently, which an identity
+ *                resize turns into the exact copy a pure crop / flip is
+ *                (array::sub / hflip never call stbir)
  */
 typedef struct mxd_image {
   const uint8_t* src;
@@ -74,6 +80,8 @@ typedef struct mxd_image {
   int32_t flip;
   void* dst;
   int64_t dst_stride;
+  int32_t rgba_weighted;
+  int32_t reserved;
 } mxd_image;
 
 /* ---- library / errors ------------------------------------------------- */

@@ -194,8 +194,6 @@ int validate(const mxd_image& im, int32_t i) {
     return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
   if (im.channels <= 0 || im.channels > 4)
     return fail(MXD_ERR_INVALID, "verifyImage: channels must be 0 <= c <= 4" + at);
-  if (im.channels == 4)
-    return fail(MXD_ERR_UNSUPPORTED, "mxd: 4-channel (STBIR_RGBA alpha-weighted) resize not supported" + at);
   if (im.resize_w <= 0 || im.resize_h <= 0 || im.crop_w <= 0 || im.crop_h <= 0)
     return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
   if (im.crop_x < 0 || im.crop_y < 0 || im.crop_x >= im.resize_w || im.crop_y >= im.resize_h)
@@ -572,6 +570,22 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (images[i].dst_stride < (int64_t)images[i].crop_w * channels * elem)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
   }
+  if (channels == 4) {
+    // one alpha mode per general-kernel launch: split a mixed batch
+    int32_t nw = 0;
+    for (int32_t i = 0; i < n; i++) nw += images[i].rgba_weighted ? 1 : 0;
+    if (nw > 0 && nw < n) {
+      std::vector<mxd_image> a, b;
+      std::vector<Stored> sa, sb;
+      for (int32_t i = 0; i < n; i++) {
+        (images[i].rgba_weighted ? a : b).push_back(images[i]);
+        if (stored) (images[i].rgba_weighted ? sa : sb).push_back(stored[i]);
+      }
+      if (int rc = run_batch(a.data(), (int32_t)a.size(), out_dtype, device, stream, stored ? sa.data() : nullptr))
+        return rc;
+      return run_batch(b.data(), (int32_t)b.size(), out_dtype, device, stream, stored ? sb.data() : nullptr);
+    }
+  }
   const int32_t f32 = out_dtype == MXD_F32_DIV255 ? 1 : 0;
   const bool no_wave = (g_policy.load() & MXD_POLICY_NO_WAVE) != 0;
   std::vector<ImgPlan> plans(n);
@@ -686,6 +700,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const int32_t vec = aligned16 ? 16 : 1;
     cfg.vec = vec;
     cfg.channels = channels;
+    cfg.alpha = channels == 4 && images[slow[0]].rgba_weighted ? 1 : 0;
     cfg.f32 = f32;
     cfg.nimgs = (int32_t)slow.size();
     for (size_t k = 0; k < slow.size(); k++) {

@@ -82,6 +82,7 @@ mxd_image plan_desc(const ImagePlan& p, void* dst, int64_t dst_stride) {
   d.crop_w = (int32_t)p.crop_w;
   d.crop_h = (int32_t)p.crop_h;
   d.flip = p.flip ? 1 : 0;
+  d.rgba_weighted = p.resampled && c == 4 ? 1 : 0;
   d.dst = dst;
   d.dst_stride = dst_stride;
   return d;
@@ -214,7 +215,10 @@ std::shared_ptr<Array> make(const ImagePlan& p) { return std::make_shared<Array>
 std::shared_ptr<Array> plan_resize(const std::shared_ptr<Array>& img, int64_t dw, int64_t dh) {
   verify_dimensions(dw, dh, img->shape(2));
   ImagePlan p = view(img);
-  const bool identity_so_far = p.resize_w == p.sw && p.resize_h == p.sh && !p.flip;
+  // (an alpha-weighted same-size resize is not the identity: it zeroes the
+  // colour of transparent pixels, so it runs before the next one)
+  const bool identity_so_far =
+      p.resize_w == p.sw && p.resize_h == p.sh && !p.flip && !(p.resampled && p.channels() == 4);
   if (identity_so_far) {
     // crop-then-resize: the crop becomes the source window.
     p.sx += p.crop_x;
@@ -231,8 +235,7 @@ std::shared_ptr<Array> plan_resize(const std::shared_ptr<Array>& img, int64_t dw
   p.resize_h = p.crop_h = dh;
   p.crop_x = p.crop_y = 0;
   p.flip = false;
-  if (p.src->shape(2) == 4)
-    throw std::runtime_error("mxd: 4-channel (STBIR_RGBA alpha-weighted) resize not supported");
+  p.resampled = true;
   return make(p);
 }
 

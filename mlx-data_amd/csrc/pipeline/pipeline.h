@@ -50,6 +50,9 @@ struct ImagePlan {
   int64_t resize_w = 0, resize_h = 0;
   int64_t crop_x = 0, crop_y = 0, crop_w = 0, crop_h = 0;
   bool flip = false;
+  // Went through core::image::resize (stbir): 4-channel images are then
+  // alpha-weighted (STBIR_RGBA); crops and mirrors alone never are.
+  bool resampled = false;
   int64_t channels() const;
 };
 

@@ -36,7 +36,8 @@ static_assert(sizeof(ImgDev) == 104, "ImgDev layout");
 
 struct LaunchCfg {
   int32_t vec;        // bytes per thread per source row: 16 (16-byte aligned rows) or 1
-  int32_t channels;   // 1..3
+  int32_t channels;   // 1..4
+  int32_t alpha;      // channels == 4: STBIR_RGBA alpha weighting
   int32_t f32;        // output f32 /255
   int32_t nimgs;
   int32_t ntiles;

@@ -18,6 +18,11 @@
 //            rounds like stbir's encode (trunc(v+0.5) clamped), and writes u8
 //            or the exact f32 q/255.0f with 16-byte (f32) / 4-byte (u8) stores.
 // Arithmetic is in byte units (v = sum w*p), f32 accumulation with FMA.
+// 4 channels with ALPHA (stb_image_resize2's STBIR_RGBA, the layout
+// core::image::resize passes for c = 4, ImageTransform.cpp:49-58): colours are
+// weighted by alpha (p * a / 255) before both passes and divided by the
+// filtered alpha (times 255) after them, unless that alpha is below
+// stbir's tiny threshold; alpha itself is filtered as is.
 // Workgroup ids are remapped so that tiles of the same image run on the same
 // XCD (blocks b, b+8, ... share an XCD): the vertical halo of adjacent bands
 // then hits that XCD's L2.
@@ -49,35 +54,46 @@ __device__ __forceinline__ float encode(float v) {
   return truncf(fminf(fmaxf(v + 0.5f, 0.0f), 255.0f));
 }
 
-template <int VEC>
+constexpr float kInv255 = 1.0f / 255.0f;
+// stbir's "small float" below which a filtered alpha counts as zero (colours
+// then stay premultiplied, i.e. ~0): 1 / 2^120.
+constexpr float kTinyAlpha = 7.52316384526264e-37f;
+
+// ALPHA: the chunk holds whole RGBA pixels (16-byte chunks of a 4-channel row
+// start on a pixel); colours enter premultiplied.
+template <int VEC, bool ALPHA>
 struct Chunk;
 
-template <>
-struct Chunk<16> {
+template <bool ALPHA>
+struct Chunk<16, ALPHA> {
   uint4 v;
   __device__ __forceinline__ void load(const uint8_t* p) { v = *reinterpret_cast<const uint4*>(p); }
   __device__ __forceinline__ void fma_into(float* acc, float w) const {
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      acc[4 * i + 0] = __builtin_fmaf(w, (float)(d[i] & 0xffu), acc[4 * i + 0]);
-      acc[4 * i + 1] = __builtin_fmaf(w, (float)((d[i] >> 8) & 0xffu), acc[4 * i + 1]);
-      acc[4 * i + 2] = __builtin_fmaf(w, (float)((d[i] >> 16) & 0xffu), acc[4 * i + 2]);
-      acc[4 * i + 3] = __builtin_fmaf(w, (float)(d[i] >> 24), acc[4 * i + 3]);
+      const float a = (float)(d[i] >> 24);
+      const float m = ALPHA ? a * kInv255 : 1.0f;
+      acc[4 * i + 0] = __builtin_fmaf(w, (float)(d[i] & 0xffu) * m, acc[4 * i + 0]);
+      acc[4 * i + 1] = __builtin_fmaf(w, (float)((d[i] >> 8) & 0xffu) * m, acc[4 * i + 1]);
+      acc[4 * i + 2] = __builtin_fmaf(w, (float)((d[i] >> 16) & 0xffu) * m, acc[4 * i + 2]);
+      acc[4 * i + 3] = __builtin_fmaf(w, a, acc[4 * i + 3]);
     }
   }
 };
 
-template <>
-struct Chunk<1> {
-  uint32_t v;
-  __device__ __forceinline__ void load(const uint8_t* p) { v = *p; }
-  __device__ __forceinline__ void fma_into(float* acc, float w) const {
-    acc[0] = __builtin_fmaf(w, (float)v, acc[0]);
+// One byte; ALPHA: byte `c` of an RGBA pixel, its alpha 3 - c bytes on.
+template <bool ALPHA>
+struct Chunk<1, ALPHA> {
+  float v;
+  __device__ __forceinline__ void load(const uint8_t* p, int c = 3) {
+    v = (float)*p;
+    if (ALPHA && c < 3) v *= (float)p[3 - c] * kInv255;
   }
+  __device__ __forceinline__ void fma_into(float* acc, float w) const { acc[0] = __builtin_fmaf(w, v, acc[0]); }
 };
 
-template <int VEC, int C, bool F32>
+template <int VEC, int C, bool F32, bool ALPHA>
 __global__ __launch_bounds__(kThreads) void resample_tiles(const ImgDev* __restrict__ imgs, int nimgs, int vw,
                                                            int xs, int ys, int x_off, int y_off) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -165,21 +181,30 @@ __global__ __launch_bounds__(kThreads) void resample_tiles(const ImgDev* __restr
 #pragma unroll
       for (int i = 0; i < VEC; i++) acc[i] = 0.0f;
       int k = 0;
-      for (; k + 4 <= nt; k += 4) {
-        Chunk<VEC> c0, c1, c2, c3;
-        c0.load(p + (k + 0) * sstride);
-        c1.load(p + (k + 1) * sstride);
-        c2.load(p + (k + 2) * sstride);
-        c3.load(p + (k + 3) * sstride);
-        c0.fma_into(acc, yi[kTapHeader + k + 0]);
-        c1.fma_into(acc, yi[kTapHeader + k + 1]);
-        c2.fma_into(acc, yi[kTapHeader + k + 2]);
-        c3.fma_into(acc, yi[kTapHeader + k + 3]);
-      }
-      for (; k < nt; k++) {
-        Chunk<VEC> c0;
-        c0.load(p + k * sstride);
-        c0.fma_into(acc, yi[kTapHeader + k]);
+      if constexpr (VEC == 1) {
+        const int c = (tile.fb0 + ch) % C;  // fb0 starts a pixel
+        for (; k < nt; k++) {
+          Chunk<1, ALPHA> c0;
+          c0.load(p + k * sstride, c);
+          c0.fma_into(acc, yi[kTapHeader + k]);
+        }
+      } else {
+        for (; k + 4 <= nt; k += 4) {
+          Chunk<VEC, ALPHA> c0, c1, c2, c3;
+          c0.load(p + (k + 0) * sstride);
+          c1.load(p + (k + 1) * sstride);
+          c2.load(p + (k + 2) * sstride);
+          c3.load(p + (k + 3) * sstride);
+          c0.fma_into(acc, yi[kTapHeader + k + 0]);
+          c1.fma_into(acc, yi[kTapHeader + k + 1]);
+          c2.fma_into(acc, yi[kTapHeader + k + 2]);
+          c3.fma_into(acc, yi[kTapHeader + k + 3]);
+        }
+        for (; k < nt; k++) {
+          Chunk<VEC, ALPHA> c0;
+          c0.load(p + k * sstride);
+          c0.fma_into(acc, yi[kTapHeader + k]);
+        }
       }
       float* dstv = vbuf + g * vw + ch * VEC;
       if constexpr (VEC % 4 == 0) {
@@ -211,8 +236,18 @@ __global__ __launch_bounds__(kThreads) void resample_tiles(const ImgDev* __restr
           const int nt = __float_as_int(xi[1]);
           for (int k = 0; k < nt; k++) s = __builtin_fmaf(xi[kTapHeader + k], vr[base + k * C], s);
         }
-        res[j] = encode(s);
+        res[j] = s;
       }
+      if constexpr (ALPHA) {
+        // the thread's 4 elements are one RGBA pixel (tiles start on a pixel)
+        if (res[3] * kInv255 >= kTinyAlpha) {
+          const float ia = 255.0f / res[3];
+#pragma unroll
+          for (int j = 0; j < 3; j++) res[j] *= ia;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) res[j] = encode(res[j]);
       const int64_t row = (int64_t)(oy + g) * im.dst_stride;
       const int o0 = tile.ox0 * C + 4 * q;
       if constexpr (F32) {
@@ -241,8 +276,15 @@ __global__ __launch_bounds__(kThreads) void resample_tiles(const ImgDev* __restr
 
 template <int VEC, int C, bool F32>
 int launch_t(const LaunchCfg& cfg, const ImgDev* imgs, int vw, int xs, int ys, int x_off, int y_off, hipStream_t s) {
-  hipLaunchKernelGGL((resample_tiles<VEC, C, F32>), dim3(cfg.ntiles), dim3(kThreads), resample_smem_bytes(cfg), s,
-                     imgs, cfg.nimgs, vw, xs, ys, x_off, y_off);
+  if constexpr (C == 4) {
+    if (cfg.alpha) {
+      hipLaunchKernelGGL((resample_tiles<VEC, C, F32, true>), dim3(cfg.ntiles), dim3(kThreads),
+                         resample_smem_bytes(cfg), s, imgs, cfg.nimgs, vw, xs, ys, x_off, y_off);
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+  }
+  hipLaunchKernelGGL((resample_tiles<VEC, C, F32, false>), dim3(cfg.ntiles), dim3(kThreads), resample_smem_bytes(cfg),
+                     s, imgs, cfg.nimgs, vw, xs, ys, x_off, y_off);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -255,6 +297,8 @@ int launch_v(const LaunchCfg& cfg, const ImgDev* i, int vw, int xs, int ys, int 
     case 5: return launch_t<VEC, 2, true>(cfg, i, vw, xs, ys, xo, yo, s);
     case 6: return launch_t<VEC, 3, false>(cfg, i, vw, xs, ys, xo, yo, s);
     case 7: return launch_t<VEC, 3, true>(cfg, i, vw, xs, ys, xo, yo, s);
+    case 8: return launch_t<VEC, 4, false>(cfg, i, vw, xs, ys, xo, yo, s);
+    case 9: return launch_t<VEC, 4, true>(cfg, i, vw, xs, ys, xo, yo, s);
     default: return -2;
   }
 }

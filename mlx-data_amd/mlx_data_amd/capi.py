@@ -57,6 +57,8 @@ class MxdImage(ctypes.Structure):
         ("flip", ctypes.c_int32),
         ("dst", ctypes.c_void_p),
         ("dst_stride", ctypes.c_int64),
+        ("rgba_weighted", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

@@ -65,12 +65,14 @@ def axis_coeffs(in_size, out_size):
     return n0, n1, w
 
 
-def resize(img, dw, dh):
-    """stbir_resize_uint8_linear restated: (H, W, C) u8 -> (dh, dw, C) u8."""
+def resize(img, dw, dh, rgba_weighted=None):
+    """stbir_resize_uint8_linear restated: (H, W, C) u8 -> (dh, dw, C) u8.
+    C = 4 is alpha-weighted (STBIR_RGBA) unless rgba_weighted=False."""
     img = np.ascontiguousarray(img, np.uint8)
     h, w, c = img.shape
     out = np.zeros((dh, dw, c), np.uint8)
-    if lib().orc_resize_u8(_ptr(img), w, h, c, _ptr(out), dw, dh):
+    weighted = (c == 4) if rgba_weighted is None else bool(rgba_weighted)
+    if lib().orc_resize_u8_layout(_ptr(img), w, h, c, _ptr(out), dw, dh, int(weighted)):
         raise ValueError("orc_resize_u8 failed")
     return out
 

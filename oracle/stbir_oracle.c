@@ -255,11 +255,17 @@ int orc_resize_smallest_side_dims(int64_t w, int64_t h, int64_t size, int64_t* t
 
 /*
  * stbir_resize_uint8_linear restated (triangle filter, clamp edges, packed
- * strides).  channels 1..3 (c=4 is STBIR_RGBA alpha-weighted: not restated).
- * Horizontal pass first into an f32 intermediate, then vertical.
+ * strides).  channels 1..4; with rgba_weighted (c = 4, the STBIR_RGBA layout
+ * core::image::resize passes, ImageTransform.cpp:49-58) colours are
+ * multiplied by their alpha after decode and divided by the filtered alpha
+ * before encode (left as they are when that alpha is below stbir's tiny
+ * float) -- SURVEY.md Appendix A item 9, a restatement (stb is absent):
+ * parity unpinned.  Horizontal pass first into an f32 intermediate, then
+ * vertical.
  */
-int orc_resize_u8(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw, int dh) {
-  if (w <= 0 || h <= 0 || dw <= 0 || dh <= 0 || c < 1 || c > 3) return -1;
+int orc_resize_u8_layout(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw, int dh, int rgba_weighted) {
+  if (w <= 0 || h <= 0 || dw <= 0 || dh <= 0 || c < 1 || c > 4) return -1;
+  const int alpha = c == 4 && rgba_weighted;
   const int cwx = orc_axis_width(w, dw), cwy = orc_axis_width(h, dh);
   int* x0 = (int*)malloc(sizeof(int) * (size_t)dw * 2);
   int* y0 = (int*)malloc(sizeof(int) * (size_t)dh * 2);
@@ -276,6 +282,9 @@ int orc_resize_u8(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw,
   for (int r = 0; r < h; r++) {
     const uint8_t* s = src + (size_t)r * w * c;
     for (int i = 0; i < w * c; i++) dec[i] = (float)s[i] * inv255;
+    if (alpha)
+      for (int i = 0; i < w; i++)
+        for (int k = 0; k < 3; k++) dec[4 * i + k] *= dec[4 * i + 3];
     float* hr = hbuf + (size_t)r * dw * c;
     for (int ox = 0; ox < dw; ox++) {
       const int a = x0[ox], b = x0[dw + ox];
@@ -295,6 +304,14 @@ int orc_resize_u8(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw,
       for (int k = 1; k <= b - a; k++) acc = acc + cf[k] * hbuf[(size_t)(a + k) * dw * c + i];
       vrow[i] = acc;
     }
+    if (alpha)
+      for (int i = 0; i < dw; i++) {
+        const float a = vrow[4 * i + 3];
+        if (a >= 7.52316384526264e-37f) { /* stbir's small float, 1 / 2^120 */
+          const float ia = 1.0f / a;
+          for (int k = 0; k < 3; k++) vrow[4 * i + k] *= ia;
+        }
+      }
     uint8_t* d = dst + (size_t)oy * dw * c;
     for (int i = 0; i < dw * c; i++) {
       float f = vrow[i] * 255.0f + 0.5f;
@@ -313,6 +330,10 @@ out:
   free(hbuf);
   free(vrow);
   return rc;
+}
+
+int orc_resize_u8(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw, int dh) {
+  return orc_resize_u8_layout(src, w, h, c, dst, dw, dh, c == 4);
 }
 
 /* ImageCenterCrop::apply_image offsets (integer floor). */

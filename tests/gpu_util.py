@@ -6,7 +6,7 @@ import oracle as O
 from mlx_data_amd import capi
 
 
-def run_device(images, geoms, f32=False, src_align=16, dst_pad=0, device=0):
+def run_device(images, geoms, f32=False, src_align=16, dst_pad=0, device=0, rgba_weighted=0):
     """images: list of (H, W, C) uint8; geoms: (rw, rh, cx, cy, cw, ch, flip).
 
     Sources are packed into one device buffer with row pitch rounded up to
@@ -36,7 +36,7 @@ def run_device(images, geoms, f32=False, src_align=16, dst_pad=0, device=0):
         dsts.append((d, dpitch))
         entries.append(dict(src=src.ptr + o, src_stride=p, src_w=img.shape[1], src_h=img.shape[0], channels=c,
                             resize_w=rw, resize_h=rh, crop_x=cx, crop_y=cy, crop_w=cw, crop_h=ch, flip=int(flip),
-                            dst=d.ptr, dst_stride=dpitch))
+                            dst=d.ptr, dst_stride=dpitch, rgba_weighted=int(rgba_weighted)))
     arr, n = capi.make_images(entries)
     capi.resize_crop_batch(arr, n, capi.MXD_F32_DIV255 if f32 else capi.MXD_U8, device, None)
     for (d, dpitch), g, img in zip(dsts, geoms, images):
@@ -50,9 +50,9 @@ def run_device(images, geoms, f32=False, src_align=16, dst_pad=0, device=0):
     return douts
 
 
-def oracle_out(img, g):
+def oracle_out(img, g, rgba_weighted=None):
     rw, rh, cx, cy, cw, ch, flip = g
-    r = O.resize(img, rw, rh)
+    r = O.resize(img, rw, rh, rgba_weighted)
     out = O.crop(r, cx, cy, cw, ch)
     return O.hflip(out) if flip else out
 

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(capi.EXPORTS) == syms
-    assert L.mxd_abi_version() == 1
+    assert L.mxd_abi_version() == 2
 
 
 @pytest.mark.parametrize("w,h,size", [(1280, 960, 256), (375, 500, 256), (500, 375, 256), (300, 200, 256),
@@ -89,8 +89,10 @@ def test_batch_validation_rejects_before_touching_the_device(kw, msg):
         capi.resize_crop_batch(arr, n, capi.MXD_U8)
 
 
-def test_rgba_is_reported_unsupported_not_wrong():
-    arr, n = _one(channels=4, src_stride=400, dst_stride=200)
-    with pytest.raises(capi.MxdError) as e:
+def test_channel_count_checked_like_verify_image():
+    """1..4 channels (4 = STBIR_RGBA, tests/test_gpu_rgba.py); 5 is rejected
+    with core/image/ImageIO.cpp:45-47's message before any device work."""
+    arr, n = _one(channels=5, src_stride=500, dst_stride=250)
+    with pytest.raises(capi.MxdError, match="channels must be 0 <= c <= 4") as e:
         capi.resize_crop_batch(arr, n, capi.MXD_U8)
-    assert e.value.code == 2
+    assert e.value.code == 1
