@@ -39,6 +39,19 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// Every entry point that takes a device ordinal refuses one that does not
+// exist (DeviceGuard would otherwise leave the work on the current device).
+int check_device(int32_t device) {
+  static const int count = [] {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+  }();
+  if (device < 0 || device >= count)
+    return fail(MXD_ERR_INVALID, "mxd: invalid device " + std::to_string(device) + " (" + std::to_string(count) +
+                                     " visible)");
+  return MXD_OK;
+}
+
 #define MXD_HIP(expr)                                                                                    \
   do {                                                                                                   \
     hipError_t e_ = (expr);                                                                              \
@@ -563,12 +576,29 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   if (n == 0) return MXD_OK;
   const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
   const int32_t channels = images[0].channels;
+  bool mixed = false;
   for (int32_t i = 0; i < n; i++) {
     if (int rc = validate(images[i], i)) return rc;
-    if (images[i].channels != channels)
-      return fail(MXD_ERR_INVALID, "mxd: all images of a batch must have the same channel count");
-    if (images[i].dst_stride < (int64_t)images[i].crop_w * channels * elem)
+    mixed = mixed || images[i].channels != channels;
+    if (images[i].dst_stride < (int64_t)images[i].crop_w * images[i].channels * elem)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+  }
+  if (int rc = check_device(device)) return rc;
+  if (mixed) {
+    // one channel count per launch: one sub-batch per count, in order
+    for (int32_t c = 1; c <= 4; c++) {
+      std::vector<mxd_image> sub;
+      std::vector<Stored> ssub;
+      for (int32_t i = 0; i < n; i++)
+        if (images[i].channels == c) {
+          sub.push_back(images[i]);
+          if (stored) ssub.push_back(stored[i]);
+        }
+      if (!sub.empty())
+        if (int rc = run_batch(sub.data(), (int32_t)sub.size(), out_dtype, device, stream, stored ? ssub.data() : nullptr))
+          return rc;
+    }
+    return MXD_OK;
   }
   if (channels == 4) {
     // one alpha mode per general-kernel launch: split a mixed batch
@@ -1050,6 +1080,7 @@ int mxd_abi_version(void) { return MXD_ABI_VERSION; }
 
 const char* mxd_last_error(void) { return g_error.c_str(); }
 
+
 int mxd_device_count(int* count) {
   if (!count) return fail(MXD_ERR_INVALID, "mxd: null count");
   MXD_HIP(hipGetDeviceCount(count));
@@ -1110,6 +1141,7 @@ int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device,
 
 int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps) {
   if (!gbps || bytes < 16 || iters <= 0) return fail(MXD_ERR_INVALID, "mxd: bad copy_bandwidth arguments");
+  if (int rc = check_device(device)) return rc;
   DeviceGuard g(device);
   void *a = nullptr, *b = nullptr;
   hipStream_t s = nullptr;
@@ -1137,11 +1169,13 @@ int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps)
 }
 
 int mxd_set_device(int32_t device) {
+  if (int rc = check_device(device)) return rc;
   MXD_HIP(hipSetDevice(device));
   return MXD_OK;
 }
 
 int mxd_malloc_device(void** ptr, size_t bytes, int32_t device) {
+  if (int rc = check_device(device)) return rc;
   if (!ptr) return fail(MXD_ERR_INVALID, "mxd: null ptr");
   DeviceGuard g(device);
   MXD_HIP(hipMalloc(ptr, bytes));
@@ -1149,6 +1183,7 @@ int mxd_malloc_device(void** ptr, size_t bytes, int32_t device) {
 }
 
 int mxd_free_device(void* ptr, int32_t device) {
+  if (int rc = check_device(device)) return rc;
   DeviceGuard g(device);
   MXD_HIP(hipFree(ptr));
   return MXD_OK;
@@ -1188,6 +1223,7 @@ int mxd_memset_async(void* dst, int value, size_t bytes, void* stream) {
 }
 
 int mxd_stream_create(int32_t device, void** stream) {
+  if (int rc = check_device(device)) return rc;
   if (!stream) return fail(MXD_ERR_INVALID, "mxd: null stream");
   DeviceGuard g(device);
   hipStream_t s = nullptr;
@@ -1242,6 +1278,7 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
   const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
   for (int32_t i = 0; i < n; i++)
     if (int rc = validate(images[i], i)) return rc;
+  if (int rc = check_device(device)) return rc;
   DeviceGuard g(device);
   // Per image: the staged footprint (columns from x0, 16-byte aligned so both
   // kernel families read it as they would the whole image) and its offsets.
@@ -1423,6 +1460,11 @@ int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_
 }
 
 int mxd_pixmap_batch(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device, void* stream) {
+  if (n > 0 && images)
+    for (int32_t i = 0; i < n; i++)
+      if (int rc = pix_validate(images[i], op, i)) return rc;
+  if (n > 0)
+    if (int rc = check_device(device)) return rc;
   return run_pixmap(images, n, op, device, stream);
 }
 
@@ -1431,6 +1473,7 @@ int mxd_pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t dev
   if (n == 0) return MXD_OK;
   for (int32_t i = 0; i < n; i++)
     if (int rc = pix_validate(images[i], op, i)) return rc;
+  if (int rc = check_device(device)) return rc;
   DeviceGuard g(device);
   CtxLease lease(device);
   Slot& ctx = lease.ctx->slot[0];

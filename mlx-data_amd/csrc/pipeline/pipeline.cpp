@@ -88,10 +88,35 @@ mxd_image plan_desc(const ImagePlan& p, void* dst, int64_t dst_stride) {
   return d;
 }
 
-void run_host(const std::vector<mxd_image>& descs) {
+// Runs the descriptors (one fused launch per device).  Several devices:
+// contiguous slices [k n / D, (k + 1) n / D), slice 0 on the calling thread,
+// the others on their own threads; the first failing slice's message wins.
+void run_host(const std::vector<mxd_image>& descs, int32_t dtype) {
   if (descs.empty()) return;
-  check(mxd_resize_crop_host(descs.data(), (int32_t)descs.size(), MXD_U8, next_device()));
+  const std::vector<int> devs = devices();
+  if (devs.empty()) throw std::runtime_error("mxd: no HIP device visible (the image path runs only on the GPU)");
+  const size_t n = descs.size();
+  const size_t k = std::min(devs.size(), n);
+  const uint64_t first = g_rr.fetch_add(k);
+  if (k == 1) {
+    check(mxd_resize_crop_host(descs.data(), (int32_t)n, dtype, devs[first % devs.size()]));
+    return;
+  }
+  std::vector<std::string> err(k);
+  auto slice = [&](size_t s) {
+    const size_t b = s * n / k, e = (s + 1) * n / k;
+    if (mxd_resize_crop_host(descs.data() + b, (int32_t)(e - b), dtype, devs[(first + s) % devs.size()]) != MXD_OK)
+      err[s] = mxd_last_error();  // thread-local: read on the failing thread
+  };
+  std::vector<std::thread> workers;
+  for (size_t s = 1; s < k; s++) workers.emplace_back(slice, s);
+  slice(0);
+  for (auto& w : workers) w.join();
+  for (const auto& e : err)
+    if (!e.empty()) throw std::runtime_error(e);
 }
+
+int32_t out_dtype(DType t) { return t == DType::Float ? MXD_F32_DIV255 : MXD_U8; }
 
 }  // namespace
 
@@ -110,7 +135,9 @@ Array::Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data)
     : type_(type), shape_(std::move(shape)), data_(std::move(data)) {}
 
 Array::Array(std::shared_ptr<const ImagePlan> plan)
-    : type_(DType::UInt8), shape_({plan->crop_h, plan->crop_w, plan->channels()}), plan_(std::move(plan)) {}
+    : type_(plan->f32 ? DType::Float : DType::UInt8),
+      shape_({plan->crop_h, plan->crop_w, plan->channels()}),
+      plan_(std::move(plan)) {}
 
 int64_t Array::shape(int d) const {
   if (d < 0) d += ndim();
@@ -129,8 +156,8 @@ void* Array::data() const {
   std::lock_guard<std::mutex> lk(mu_);
   if (!data_ && plan_) {
     auto buf = alloc_bytes(nbytes());
-    const int64_t row = shape_[1] * shape_[2];
-    run_host({plan_desc(*plan_, buf.get(), row)});
+    const int64_t row = shape_[1] * shape_[2] * itemsize(type_);
+    run_host({plan_desc(*plan_, buf.get(), row)}, out_dtype(type_));
     data_ = buf;
   }
   return data_.get();
@@ -194,8 +221,8 @@ namespace {
 // The image (H, W, C) as a plan: a pending one as is, a materialised one as
 // the identity plan over all of it.
 ImagePlan view(const std::shared_ptr<Array>& img) {
-  if (img->plan() && img->pending()) return *img->plan();
   if (img->type() != DType::UInt8) throw std::invalid_argument("image must be of type UInt8");
+  if (img->plan() && img->pending()) return *img->plan();
   ImagePlan p;
   p.src = img;
   p.sw = p.resize_w = p.crop_w = img->shape(1);
@@ -292,17 +319,18 @@ std::shared_ptr<Array> stack_frames(const std::vector<std::shared_ptr<Array>>& f
     if (f->shape(0) != h || f->shape(1) != w)
       throw std::runtime_error("applyVideo: frame size inconsistent during transform");
   auto out = std::make_shared<Array>(f0->type(), std::vector<int64_t>{(int64_t)frames.size(), h, w, c});
-  const int64_t bytes = h * w * c * itemsize(f0->type());
+  const int64_t isz = itemsize(f0->type()), bytes = h * w * c * isz;
   auto* dst = static_cast<uint8_t*>(out->data());
   std::vector<mxd_image> descs;
   for (size_t i = 0; i < frames.size(); i++) {
     const auto& f = frames[i];
+    if (f->type() != f0->type()) throw std::runtime_error("applyVideo: frame type inconsistent during transform");
     if (f->plan() && f->pending())
-      descs.push_back(plan_desc(*f->plan(), dst + i * bytes, w * c));
+      descs.push_back(plan_desc(*f->plan(), dst + i * bytes, w * c * isz));
     else
       std::memcpy(dst + i * bytes, f->data(), bytes);
   }
-  run_host(descs);  // every pending frame in one launch
+  run_host(descs, out_dtype(f0->type()));  // every pending frame in one launch
   return out;
 }
 
@@ -387,6 +415,13 @@ std::shared_ptr<Array> ImageRandomHFlip::apply_image(const std::shared_ptr<Array
     return make(p);
   }
   return img;
+}
+
+std::shared_ptr<Array> ImageToFloat::apply_image(const std::shared_ptr<Array>& img) const {
+  verify_dimensions(img->shape(1), img->shape(0), img->shape(2));
+  ImagePlan p = view(img);
+  p.f32 = true;
+  return make(p);
 }
 
 namespace {
@@ -716,16 +751,18 @@ std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& a
   std::vector<mxd_image> launch;
   int64_t off = 0;
   for (const auto& a : arrs) {
-    // Pending uint8 HWC images in the default stacking layout go to the
-    // fused kernel, which writes rows straight into the batch.
-    if (!has_dim && a->pending() && nd == 3) {
-      launch.push_back(plan_desc(*a->plan(), base + off, stride[0]));
+    // Pending HWC images in the default stacking layout whose pixels fill
+    // the batch's pixel slots (same channel count) go to the fused kernel,
+    // which writes rows straight into the batch; the rest (and a channel
+    // count the batch pads) are materialised and copied.
+    if (!has_dim && a->pending() && nd == 3 && a->shape(2) == bshape[3]) {
+      launch.push_back(plan_desc(*a->plan(), base + off * isz, stride[0] * isz));
     } else {
       copy_to_strided(base, off, static_cast<const uint8_t*>(a->data()), a->shape(), stride, isz);
     }
     off += has_dim ? item * a->shape(dim) : item;
   }
-  run_host(launch);
+  run_host(launch, out_dtype(type));
   return res;
 }
 

@@ -53,6 +53,9 @@ struct ImagePlan {
   // Went through core::image::resize (stbir): 4-channel images are then
   // alpha-weighted (STBIR_RGBA); crops and mirrors alone never are.
   bool resampled = false;
+  // image_to_float: the kernel writes float32 q / 255 (MXD_F32_DIV255)
+  // instead of the uint8 q; the array's type is then Float.
+  bool f32 = false;
   int64_t channels() const;
 };
 
@@ -85,8 +88,11 @@ using Sample = std::unordered_map<std::string, std::shared_ptr<Array>>;
 
 std::shared_ptr<Array> check_key(const Sample& s, const std::string& key);
 
-// Devices the fused kernel may use (default: all visible).  Batches are
-// spread over them round-robin.
+// Devices the fused kernel may use (default: all visible).  With several,
+// one batch is split into contiguous slices, one per device, each launched
+// from its own host thread (the reference's shard / partition analogue,
+// op/Shard.cpp:11-20, stream/Partition.cpp:23-35); outputs land at the same
+// offsets, so the batch is identical to a single-device one.
 void set_devices(const std::vector<int>& devices);
 std::vector<int> devices();
 
@@ -191,6 +197,20 @@ class ImageRandomHFlip : public ImageOp {
 
  private:
   float prob_;
+};
+
+// Fused normalize: the reference's post-batch
+// `key_transform(key, lambda x: x.astype("float32") / 255)`
+// (benchmarks/comparative/caltech101/mlx_data.py:34,46) as an image op ahead
+// of batch.  A pending image (resize / crop / mirror not run yet) only
+// records it, so batch writes the float32 tensor from the same launch; a
+// materialised uint8 image is converted by one identity launch.  Values are
+// exactly float(q) / 255.0f.  UInt8 input only ("image must be of type
+// UInt8", core/image/ImageTransform.cpp:17-21).
+class ImageToFloat : public ImageOp {
+ public:
+  ImageToFloat(std::string ikey, std::string okey) : ImageOp(std::move(ikey), std::move(okey)) {}
+  std::shared_ptr<Array> apply_image(const std::shared_ptr<Array>& img) const override;
 };
 
 // op/ImageTransform.h:139-152 ImageRotate: nearest-pixel rotation about the

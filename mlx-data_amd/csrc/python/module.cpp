@@ -88,6 +88,22 @@ std::shared_ptr<Array> to_array(py::handle obj) {
   }
   if (py::isinstance<py::str>(obj))
     throw std::invalid_argument("[to_array] Cannot convert strings to arrays. Please encode them as bytes first.");
+  // A Python buffer (bytearray, array.array, memoryview ...) is copied: it
+  // may be mutable and is not ours to alias (wrap.cpp:159-163, to_array(py::buffer)).
+  if (py::isinstance<py::buffer>(obj)) {
+    py::buffer_info info = obj.cast<py::buffer>().request();
+    int64_t expect = info.itemsize;
+    bool contiguous = true;
+    for (int d = info.ndim - 1; d >= 0; d--) {
+      if (info.shape[d] > 1 && info.strides[d] != expect) contiguous = false;
+      expect *= info.shape[d];
+    }
+    if (!contiguous) throw std::invalid_argument("[to_array] Contiguous buffer expected -- maybe cast to np.array");
+    py::array a = py::array::ensure(obj);
+    if (!a) throw std::invalid_argument("[to_array] Unsupported buffer type '" + info.format + "'");
+    return from_numpy(a.attr("copy")().cast<py::array>());
+  }
+  // Anything else with the array interface (wrap.cpp:165-175).
   try {
     return from_numpy(py::array::ensure(obj));
   } catch (const std::exception&) {
@@ -225,7 +241,13 @@ void dataset_ops(py::class_<D, std::shared_ptr<D>>& cls, Wrap wrap) {
           [wrap](const Self& self, const std::string& key, const std::string& preset, const std::string& output_key) {
             return wrap(self, std::make_shared<ImageChannelReduction>(key, preset, output_key));
           },
-          py::arg("key"), py::arg("preset") = "default", py::arg("output_key") = "");
+          py::arg("key"), py::arg("preset") = "default", py::arg("output_key") = "")
+      .def(
+          "image_to_float",
+          [wrap](const Self& self, const std::string& key, const std::string& output_key) {
+            return wrap(self, std::make_shared<ImageToFloat>(key, output_key));
+          },
+          py::arg("key"), py::arg("output_key") = "");
 }
 
 using PadMap = std::unordered_map<std::string, double>;

@@ -14,9 +14,13 @@ Same names, keyword arguments and error behaviour as mlx-data 0.2.0
 
 The image ops only record geometry; ``batch`` runs the resize, crop and
 mirror of the whole batch as one fused GPU launch and writes the stacked
-(B, H, W, C) uint8 tensor.  Reading an unbatched image materialises it with
-its own launch.  There is no CPU resize: without a visible GPU the image ops
-raise.
+(B, H, W, C) uint8 tensor.  ``image_to_float(key)`` before ``batch`` (this
+build's one addition to the surface) replaces the trailing
+``key_transform(..., lambda x: x.astype("float32") / 255)``: the same launch
+then writes the float32 batch, bit-identical to that lambda.  With several
+devices (``set_devices``) one batch is split into contiguous slices, one per
+device.  Reading an unbatched image materialises it with its own launch.
+There is no CPU resize: without a visible GPU the image ops raise.
 
 ``load_image`` decodes JPEG natively (``csrc/pipeline/jpeg.cpp``, the
 reference's libjpeg path, ``core/image/ImageJPEG.cpp``); other formats go to a
@@ -68,7 +72,7 @@ def _add_if_variants(cls):
     unchanged (``Dataset::*_if``, ``Dataset.cpp``)."""
     for name in ("key_transform", "load_image", "image_resize_smallest_side", "image_resize",
                  "image_center_crop", "image_random_crop", "image_random_h_flip", "image_random_area_crop",
-                 "image_rotate", "image_channel_reduction"):
+                 "image_rotate", "image_channel_reduction", "image_to_float"):
         def op_if(self, cond, *args, _name=name, **kwargs):
             return getattr(self, _name)(*args, **kwargs) if cond else self
 

@@ -50,3 +50,16 @@ def test_passing_python_objects():
     assert 1 == b[0]["a"]
     assert np.all(y == b[0]["d"])
     assert np.all(x == b[0]["e"])
+    # numpy inputs are taken without a copy ...
+    y[0] = 0
+    assert np.all(y == b[0]["d"])
+    # ... and Python buffers by copy (python/tests/test_buffer.py:71-77)
+    x[0] = 0
+    assert 10 == b[0]["e"][0]
+
+
+def test_non_contiguous_buffer_rejected():
+    """wrap.cpp:27-41: a strided buffer is refused with the reference's message."""
+    m = memoryview(np.arange(16, dtype=np.uint8).reshape(4, 4)[:, ::2])
+    with pytest.raises(ValueError, match="Contiguous buffer expected"):
+        dx.buffer_from_vector([{"a": m}])
