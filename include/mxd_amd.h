@@ -165,6 +165,19 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop);
  * pipeline ops use when samples live in host memory (mlx-data's default). */
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device);
 
+/* Host image in, DEVICE result out (the device-resident
+ * batch): as mxd_resize_crop_host, but `images[i].dst` are device pointers on
+ * `device` (e.g. one (B, H, W, C) batch tensor) that the kernel writes
+ * directly -- no D2H, no host copy-out.  Returns once the results are
+ * complete on the device, so any stream (or another library sharing this HIP
+ * runtime) may read them.  Replaces, for device consumers, the host batch of
+ * stream/Batch.cpp:25-39 -> core/Utils.cpp:209-252 (merge_batch). */
+int mxd_resize_crop_to_device(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device);
+
+/* Synchronous copies for device-resident batches (fill, read back). */
+int mxd_memcpy_h2d(void* dst, const void* src, size_t bytes, int32_t device);
+int mxd_memcpy_d2h(void* dst, const void* src, size_t bytes, int32_t device);
+
 /* Frees the pinned and device buffers of idle host-path contexts. */
 int mxd_release_host_buffers(void);
 

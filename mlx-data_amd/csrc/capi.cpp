@@ -1271,7 +1271,39 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop) {
   return MXD_OK;
 }
 
+namespace {
+int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device);
+}  // namespace
+
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device) {
+  return host_path(images, n, out_dtype, device, false);
+}
+
+int mxd_resize_crop_to_device(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device) {
+  return host_path(images, n, out_dtype, device, true);
+}
+
+int mxd_memcpy_h2d(void* dst, const void* src, size_t bytes, int32_t device) {
+  if (!dst || !src) return fail(MXD_ERR_INVALID, "mxd: null pointer");
+  if (int rc = check_device(device)) return rc;
+  DeviceGuard g(device);
+  MXD_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return MXD_OK;
+}
+
+int mxd_memcpy_d2h(void* dst, const void* src, size_t bytes, int32_t device) {
+  if (!dst || !src) return fail(MXD_ERR_INVALID, "mxd: null pointer");
+  if (int rc = check_device(device)) return rc;
+  DeviceGuard g(device);
+  MXD_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return MXD_OK;
+}
+
+namespace {
+// The host path: host sources (footprints staged through pinned memory),
+// results to host (dst_device false: D2H + copy-out) or straight into device
+// destinations (dst_device true).
+int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
   if (n == 0) return MXD_OK;
@@ -1326,6 +1358,8 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
   auto copy_out = [&](int k) -> int {
     Slot& sl = ctx.slot[k & 1];
     MXD_HIP(hipEventSynchronize(sl.done));
+    pending[k & 1] = -1;
+    if (dst_device) return MXD_OK;  // the kernel wrote the destinations
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
       const mxd_image& im = images[i];
       uint8_t* d = static_cast<uint8_t*>(im.dst);
@@ -1337,7 +1371,6 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
           std::memcpy(d + (size_t)r * im.dst_stride, src + (size_t)r * st[i].out_row, st[i].out_row);
       }
     }
-    pending[k & 1] = -1;
     return MXD_OK;
   };
   for (int k = 0; k < (int)chunks.size(); k++) {
@@ -1352,9 +1385,11 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
       out_bytes += (st[i].out_row * images[i].crop_h + 255) & ~(int64_t)255;
     }
     if (int rc = grow_pinned(&sl.pin_in, &sl.pin_in_cap, in_bytes)) return rc;
-    if (int rc = grow_pinned(&sl.pin_out, &sl.pin_out_cap, out_bytes)) return rc;
     if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, in_bytes)) return rc;
-    if (int rc = grow_device(&sl.dev_out, &sl.dev_out_cap, out_bytes)) return rc;
+    if (!dst_device) {
+      if (int rc = grow_pinned(&sl.pin_out, &sl.pin_out_cap, out_bytes)) return rc;
+      if (int rc = grow_device(&sl.dev_out, &sl.dev_out_cap, out_bytes)) return rc;
+    }
     const int32_t cn = chunks[k].second - chunks[k].first;
     std::vector<mxd_image> dev_imgs(images + chunks[k].first, images + chunks[k].second);
     std::vector<Stored> where(cn);
@@ -1368,12 +1403,14 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
       where[j] = Stored{sl.dev_in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
       dev_imgs[j].src = sl.dev_in + s.in_off;  // checked by validate() only; `where` says what is stored
       dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
-      dev_imgs[j].dst = sl.dev_out + s.out_off;
-      dev_imgs[j].dst_stride = s.out_row;
+      if (!dst_device) {
+        dev_imgs[j].dst = sl.dev_out + s.out_off;
+        dev_imgs[j].dst_stride = s.out_row;
+      }
     }
     MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_bytes, hipMemcpyHostToDevice, sl.stream));
     if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
-    MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_bytes, hipMemcpyDeviceToHost, sl.stream));
+    if (!dst_device) MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_bytes, hipMemcpyDeviceToHost, sl.stream));
     MXD_HIP(hipEventRecord(sl.done, sl.stream));
     pending[k & 1] = k;
     // results of the previous chunk, while this one runs
@@ -1386,6 +1423,7 @@ int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, 
       if (int rc = copy_out(pending[k])) return rc;
   return MXD_OK;
 }
+}  // namespace
 
 int mxd_release_host_buffers(void) {
   host_pool().trim();

@@ -134,6 +134,9 @@ Array::Array(DType type, std::vector<int64_t> shape) : type_(type), shape_(std::
 Array::Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data)
     : type_(type), shape_(std::move(shape)), data_(std::move(data)) {}
 
+Array::Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data, int device)
+    : type_(type), shape_(std::move(shape)), data_(std::move(data)), device_(device) {}
+
 Array::Array(std::shared_ptr<const ImagePlan> plan)
     : type_(plan->f32 ? DType::Float : DType::UInt8),
       shape_({plan->crop_h, plan->crop_w, plan->channels()}),
@@ -295,6 +298,7 @@ std::shared_ptr<Array> plan_crop(const std::shared_ptr<Array>& img, int64_t x, i
 
 // op/ImageTransform.cpp:22-31 + core/image/ImageIO.cpp:39-49 + core/video/Video.cpp:69-79
 std::shared_ptr<Array> ImageOp::apply_key(const std::shared_ptr<Array>& x) const {
+  if (x->device() >= 0) throw std::runtime_error("image: device-resident array (batch(..., device=)) expected on host");
   if (x->ndim() == 4) {
     if (x->shape(3) == 0 || x->shape(3) > 4) throw std::runtime_error("verifyVideo: channels must be 0 <= c <= 4");
     return apply_video(x);
@@ -587,6 +591,7 @@ std::string jpeg_error() {
 // FF D8 FF) through the native decoder (ImageJPEG.cpp:99-232 semantics),
 // anything else through the installed stb_image-rules hook.
 std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) const {
+  if (x->device() >= 0) throw std::runtime_error("LoadImage: device-resident array expected on host");
   std::string path;
   if (!from_memory_) {
     if (x->type() != DType::Int8) throw std::runtime_error("LoadImage: char array (int8) expected");
@@ -686,10 +691,41 @@ void fill(Array& a, double v) {
 
 }  // namespace
 
+namespace {
+// batch_arrays into device memory.  The fused case -- every array a pending
+// image filling the batch's pixel slots, nothing to pad -- has the kernel
+// write the batch in place; otherwise the host batch is built and uploaded.
+std::shared_ptr<Array> device_batch(const std::vector<std::shared_ptr<Array>>& arrs,
+                                    const std::vector<int64_t>& bshape, const std::vector<int64_t>& stride,
+                                    int64_t item, bool ragged, double pad_value, int dim, bool has_dim, int device) {
+  const auto type = arrs.front()->type();
+  const int64_t isz = itemsize(type), bytes = shape_size(bshape) * isz;
+  void* ptr = nullptr;
+  check(mxd_malloc_device(&ptr, std::max<int64_t>(bytes, 1), device));
+  std::shared_ptr<void> mem(ptr, [device](void* p) { (void)mxd_free_device(p, device); });
+  auto res = std::make_shared<Array>(type, bshape, mem, device);
+  bool fused = !has_dim && !ragged && arrs.front()->ndim() == 3;
+  for (const auto& a : arrs) fused = fused && a->pending() && a->shape(2) == bshape[3];
+  if (fused) {
+    std::vector<mxd_image> launch;
+    auto* base = static_cast<uint8_t*>(ptr);
+    for (size_t i = 0; i < arrs.size(); i++)
+      launch.push_back(plan_desc(*arrs[i]->plan(), base + (int64_t)i * item * isz, stride[0] * isz));
+    check(mxd_resize_crop_to_device(launch.data(), (int32_t)launch.size(), out_dtype(type), device));
+    return res;
+  }
+  auto host = batch_arrays(arrs, pad_value, dim, has_dim, -1);
+  check(mxd_memcpy_h2d(ptr, host->data(), bytes, device));
+  return res;
+}
+}  // namespace
+
 // array::batch (Array.cpp:465-541) + BatchShape::add (core/BatchShape.cpp:26-66).
 std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& arrs, double pad_value, int dim,
-                                    bool has_dim) {
+                                    bool has_dim, int device) {
   const auto type = arrs.front()->type();
+  for (const auto& a : arrs)
+    if (a->device() >= 0) throw std::runtime_error("Array: cannot batch device-resident arrays");
   const int nd = arrs.front()->ndim();
   if (has_dim) {
     if (dim < 0) dim += nd;
@@ -739,15 +775,16 @@ std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& a
     item = full_stride[dim];
   }
 
-  auto res = std::make_shared<Array>(type, bshape, alloc_bytes(shape_size(bshape) * itemsize(type)));
   bool ragged = false;
   for (const auto& a : arrs)
     for (int d = 0; d < nd; d++)
       if (a->shape()[d] != (has_dim ? bshape[d] : bshape[d + 1]) && !(has_dim && d == dim)) ragged = true;
+  const int64_t isz = itemsize(type);
+  if (device >= 0) return device_batch(arrs, bshape, stride, item, ragged, pad_value, dim, has_dim, device);
+  auto res = std::make_shared<Array>(type, bshape, alloc_bytes(shape_size(bshape) * isz));
   if (ragged) fill(*res, pad_value);
 
   auto* base = static_cast<uint8_t*>(res->data());
-  const int64_t isz = itemsize(type);
   std::vector<mxd_image> launch;
   int64_t off = 0;
   for (const auto& a : arrs) {
@@ -768,7 +805,7 @@ std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& a
 
 // core::merge_batch (core/Utils.cpp:209-252)
 Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<std::string, double>& pad,
-                   const std::unordered_map<std::string, int>& dims) {
+                   const std::unordered_map<std::string, int>& dims, const DeviceOut& dev) {
   std::vector<std::string> keys;
   std::vector<std::vector<std::shared_ptr<Array>>> values;
   for (const auto& s : samples) {
@@ -787,8 +824,17 @@ Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<
   for (size_t k = 0; k < keys.size(); k++) {
     auto p = pad.find(keys[k]);
     auto d = dims.find(keys[k]);
+    int device = -1;
+    if (dev.device >= 0) {
+      bool on = false;
+      if (dev.keys.empty())
+        for (const auto& a : values[k]) on = on || a->pending();
+      else
+        on = std::find(dev.keys.begin(), dev.keys.end(), keys[k]) != dev.keys.end();
+      device = on ? dev.device : -1;
+    }
     out[keys[k]] = batch_arrays(values[k], p == pad.end() ? 0.0 : p->second, d == dims.end() ? 0 : d->second,
-                                d != dims.end());
+                                d != dims.end(), device);
   }
   return out;
 }
@@ -871,8 +917,8 @@ Sample BufferTransform::get(int64_t idx) const {
 
 // buffer/Batch.cpp:10-25,52-68
 BufferBatch::BufferBatch(std::shared_ptr<Buffer> b, int64_t batch_size, std::unordered_map<std::string, double> pad,
-                         std::unordered_map<std::string, int> dims)
-    : b_(std::move(b)), bs_(batch_size), pad_(std::move(pad)), dims_(std::move(dims)) {
+                         std::unordered_map<std::string, int> dims, DeviceOut out)
+    : b_(std::move(b)), bs_(batch_size), pad_(std::move(pad)), dims_(std::move(dims)), out_(std::move(out)) {
   if (bs_ <= 0) throw std::runtime_error("Batch: batch size must be positive");
   size_ = (b_->size() + bs_ - 1) / bs_;
 }
@@ -882,7 +928,7 @@ Sample BufferBatch::get(int64_t idx) const {
   const int64_t n = std::min(bs_, b_->size() - idx * bs_);
   std::vector<Sample> samples(n);
   for (int64_t i = 0; i < n; i++) samples[i] = b_->get(idx * bs_ + i);
-  return merge_batch(samples, pad_, dims_);
+  return merge_batch(samples, pad_, dims_, out_);
 }
 
 // ------------------------------------------------------------------ streams
@@ -914,8 +960,8 @@ Sample StreamTransform::next() const {
 
 // stream/Batch.cpp:10-39
 StreamBatch::StreamBatch(std::shared_ptr<Stream> s, int64_t batch_size, std::unordered_map<std::string, double> pad,
-                         std::unordered_map<std::string, int> dims)
-    : s_(std::move(s)), bs_(batch_size), pad_(std::move(pad)), dims_(std::move(dims)) {
+                         std::unordered_map<std::string, int> dims, DeviceOut out)
+    : s_(std::move(s)), bs_(batch_size), pad_(std::move(pad)), dims_(std::move(dims)), out_(std::move(out)) {
   if (bs_ <= 0) throw std::runtime_error("Batch: batch size must be positive");
 }
 
@@ -926,7 +972,7 @@ Sample StreamBatch::next() const {
     if (s.empty()) break;
     samples.push_back(std::move(s));
   }
-  return samples.empty() ? Sample() : merge_batch(samples, pad_, dims_);
+  return samples.empty() ? Sample() : merge_batch(samples, pad_, dims_, out_);
 }
 
 // stream/Prefetch.cpp:9-66

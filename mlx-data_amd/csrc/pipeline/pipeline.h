@@ -63,6 +63,9 @@ class Array {
  public:
   Array(DType type, std::vector<int64_t> shape);                      // zero-initialised storage
   Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data);
+  // Device-resident storage (a batch made with batch(..., device=d)):
+  // data() is then a device pointer on `device`.
+  Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data, int device);
   explicit Array(std::shared_ptr<const ImagePlan> plan);              // lazy image
 
   DType type() const { return type_; }
@@ -75,12 +78,15 @@ class Array {
   void* data() const;
   const std::shared_ptr<const ImagePlan>& plan() const { return plan_; }
   bool pending() const;
+  // -1: host memory; else the HIP device holding data().
+  int device() const { return device_; }
 
  private:
   DType type_;
   std::vector<int64_t> shape_;
   mutable std::shared_ptr<void> data_;
   std::shared_ptr<const ImagePlan> plan_;
+  int device_ = -1;
   mutable std::mutex mu_;
 };
 
@@ -275,10 +281,20 @@ class LoadImage : public KeyTransformOp {
 // ---------------------------------------------------------------- batching
 // array::batch semantics (pad with pad_value to the max shape; optional
 // concatenation dim).  Pending image plans of one key become one fused launch.
+// device >= 0: the batch is made in that device's memory:
+// pending images are written there by the kernel (host sources staged, no
+// D2H); anything else is batched on the host and uploaded once.
 std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& arrs, double pad_value, int dim,
-                                    bool has_dim);
+                                    bool has_dim, int device = -1);
+
+// Where merge_batch puts each key: device < 0 everything on the host; else
+// the listed keys on `device`, or (empty list) every key with a pending image.
+struct DeviceOut {
+  int device = -1;
+  std::vector<std::string> keys;
+};
 Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<std::string, double>& pad,
-                   const std::unordered_map<std::string, int>& dims);
+                   const std::unordered_map<std::string, int>& dims, const DeviceOut& out = {});
 
 // ---------------------------------------------------------------- threads
 class ThreadPool {
@@ -339,7 +355,7 @@ class BufferTransform : public Buffer {
 class BufferBatch : public Buffer {
  public:
   BufferBatch(std::shared_ptr<Buffer> b, int64_t batch_size, std::unordered_map<std::string, double> pad,
-              std::unordered_map<std::string, int> dims);
+              std::unordered_map<std::string, int> dims, DeviceOut out = {});
   int64_t size() const override { return size_; }
   Sample get(int64_t idx) const override;
 
@@ -348,6 +364,7 @@ class BufferBatch : public Buffer {
   int64_t bs_, size_;
   std::unordered_map<std::string, double> pad_;
   std::unordered_map<std::string, int> dims_;
+  DeviceOut out_;
 };
 
 // ---------------------------------------------------------------- streams
@@ -384,7 +401,7 @@ class StreamTransform : public Stream {
 class StreamBatch : public Stream {
  public:
   StreamBatch(std::shared_ptr<Stream> s, int64_t batch_size, std::unordered_map<std::string, double> pad,
-              std::unordered_map<std::string, int> dims);
+              std::unordered_map<std::string, int> dims, DeviceOut out = {});
   Sample next() const override;
   void reset() override { s_->reset(); }
 
@@ -393,6 +410,7 @@ class StreamBatch : public Stream {
   int64_t bs_;
   std::unordered_map<std::string, double> pad_;
   std::unordered_map<std::string, int> dims_;
+  DeviceOut out_;
 };
 
 class Prefetch : public Stream {

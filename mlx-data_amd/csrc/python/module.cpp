@@ -76,8 +76,12 @@ std::shared_ptr<Array> from_bytes(const char* p, size_t n) {
   return a;
 }
 
+struct DeviceArray;
+std::shared_ptr<Array> device_array_of(py::handle obj);
+
 std::shared_ptr<Array> to_array(py::handle obj) {
   if (py::isinstance<py::array>(obj)) return from_numpy(obj.cast<py::array>());
+  if (auto d = device_array_of(obj)) return d;
   if (py::isinstance<py::bool_>(obj) || py::isinstance<py::int_>(obj)) return scalar_i64(obj.cast<int64_t>());
   if (py::isinstance<py::float_>(obj)) return scalar_f64(obj.cast<double>());
   if (py::isinstance<py::bytes>(obj)) {
@@ -115,6 +119,18 @@ std::shared_ptr<Array> to_array(py::handle obj) {
 }
 
 // ------------------------------------------------------------ Array -> numpy
+py::dtype np_dtype(DType t) {
+  switch (t) {
+    case DType::Int8: return py::dtype("b");
+    case DType::UInt8: return py::dtype("B");
+    case DType::Int32: return py::dtype("i4");
+    case DType::Int64: return py::dtype("i8");
+    case DType::Float: return py::dtype("f");
+    case DType::Double: return py::dtype("d");
+    default: throw std::runtime_error("internal error: unknown type");
+  }
+}
+
 py::array to_numpy(const std::shared_ptr<Array>& a) {
   void* data;
   {
@@ -122,16 +138,7 @@ py::array to_numpy(const std::shared_ptr<Array>& a) {
     py::gil_scoped_release nogil;
     data = a->data();
   }
-  py::dtype dt;
-  switch (a->type()) {
-    case DType::Int8: dt = py::dtype("b"); break;
-    case DType::UInt8: dt = py::dtype("B"); break;
-    case DType::Int32: dt = py::dtype("i4"); break;
-    case DType::Int64: dt = py::dtype("i8"); break;
-    case DType::Float: dt = py::dtype("f"); break;
-    case DType::Double: dt = py::dtype("d"); break;
-    default: throw std::runtime_error("internal error: unknown type");
-  }
+  py::dtype dt = np_dtype(a->type());
   auto* keep = new std::shared_ptr<Array>(a);
   py::capsule owner(keep, [](void* p) { delete static_cast<std::shared_ptr<Array>*>(p); });
   std::vector<int64_t> shape = a->shape(), strides(shape.size());
@@ -143,9 +150,94 @@ py::array to_numpy(const std::shared_ptr<Array>& a) {
   return py::array(dt, shape, strides, data, owner);
 }
 
+// ------------------------------------------------------------ device arrays
+// DLPack (v0.8 ABI, dlpack.h): a device batch is handed to consumers
+// (torch.from_dlpack, ...) without a copy.  Only the layout is restated here.
+struct DLDevice {
+  int32_t device_type;  // kDLROCM = 10
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code;  // kDLInt 0, kDLUInt 1, kDLFloat 2
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+
+DLDataType dl_dtype(DType t) {
+  switch (t) {
+    case DType::UInt8: return {1, 8, 1};
+    case DType::Int8: return {0, 8, 1};
+    case DType::Int32: return {0, 32, 1};
+    case DType::Int64: return {0, 64, 1};
+    case DType::Float: return {2, 32, 1};
+    case DType::Double: return {2, 64, 1};
+    default: throw std::runtime_error("internal error: unknown type");
+  }
+}
+
+// The Python face of a device-resident Array.
+struct DeviceArray {
+  std::shared_ptr<Array> a;
+};
+
+struct DLHolder {
+  std::shared_ptr<Array> a;
+  std::vector<int64_t> shape;
+  DLManagedTensor t{};
+};
+
+py::capsule to_dlpack(const std::shared_ptr<Array>& a) {
+  auto* h = new DLHolder{a, a->shape(), {}};
+  h->t.dl_tensor.data = a->data();
+  h->t.dl_tensor.device = {kDLROCM, a->device()};
+  h->t.dl_tensor.ndim = a->ndim();
+  h->t.dl_tensor.dtype = dl_dtype(a->type());
+  h->t.dl_tensor.shape = h->shape.data();
+  h->t.dl_tensor.strides = nullptr;  // compact row-major
+  h->t.manager_ctx = h;
+  h->t.deleter = [](DLManagedTensor* t) { delete static_cast<DLHolder*>(t->manager_ctx); };
+  // A capsule never consumed ("dltensor" still its name) frees the tensor.
+  return py::capsule(&h->t, "dltensor", [](PyObject* cap) {
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (t && t->deleter) t->deleter(t);
+    }
+  });
+}
+
+py::array device_to_numpy(const std::shared_ptr<Array>& a) {
+  py::array host = to_numpy(std::make_shared<Array>(a->type(), a->shape()));
+  {
+    py::gil_scoped_release nogil;
+    if (a->nbytes() > 0 && mxd_memcpy_d2h(host.mutable_data(), a->data(), (size_t)a->nbytes(), a->device()) != MXD_OK)
+      throw std::runtime_error(mxd_last_error());
+  }
+  return host;
+}
+
+py::object to_py(const std::shared_ptr<Array>& a) {
+  if (a->device() >= 0) return py::cast(DeviceArray{a});
+  return to_numpy(a);
+}
+
 py::dict to_dict(const Sample& s) {
   py::dict d;
-  for (const auto& kv : s) d[py::str(kv.first)] = to_numpy(kv.second);
+  for (const auto& kv : s) d[py::str(kv.first)] = to_py(kv.second);
   return d;
 }
 
@@ -177,7 +269,7 @@ void dataset_ops(py::class_<D, std::shared_ptr<D>>& cls, Wrap wrap) {
                key,
                [fn](const std::shared_ptr<Array>& x) {
                  py::gil_scoped_acquire gil;
-                 return to_array((*fn)(to_numpy(x)));
+                 return to_array((*fn)(to_py(x)));
                },
                output_key);
            return wrap(self, op);
@@ -253,10 +345,48 @@ void dataset_ops(py::class_<D, std::shared_ptr<D>>& cls, Wrap wrap) {
 using PadMap = std::unordered_map<std::string, double>;
 using DimMap = std::unordered_map<std::string, int>;
 
+std::shared_ptr<Array> device_array_of(py::handle obj) {
+  if (!py::isinstance<DeviceArray>(obj)) return nullptr;
+  return obj.cast<const DeviceArray&>().a;
+}
+
+// batch(..., device=None | int, device_keys=None | [str])
+DeviceOut device_out(const py::object& device, const py::object& keys) {
+  DeviceOut o;
+  if (!device.is_none()) {
+    o.device = device.cast<int>();
+    if (o.device < 0) throw std::invalid_argument("batch: device must be a device index >= 0");
+  }
+  if (!keys.is_none()) o.keys = keys.cast<std::vector<std::string>>();
+  if (!o.keys.empty() && o.device < 0) throw std::invalid_argument("batch: device_keys needs device");
+  return o;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_pipeline, m) {
   m.doc() = "mlx.data image-path operator surface over the gfx950 resize/crop kernels";
+
+  py::class_<DeviceArray>(m, "DeviceArray",
+                          "A batch tensor in device memory (batch(..., device=d)): DLPack producer "
+                          "(__dlpack__ / __dlpack_device__, kDLROCM), numpy() copies it to the host.")
+      .def_property_readonly("shape", [](const DeviceArray& d) { return py::tuple(py::cast(d.a->shape())); })
+      .def_property_readonly("dtype", [](const DeviceArray& d) { return np_dtype(d.a->type()); })
+      .def_property_readonly("device", [](const DeviceArray& d) { return d.a->device(); })
+      .def_property_readonly("data_ptr", [](const DeviceArray& d) { return reinterpret_cast<uintptr_t>(d.a->data()); })
+      .def_property_readonly("nbytes", [](const DeviceArray& d) { return d.a->nbytes(); })
+      .def("__dlpack__", [](const DeviceArray& d, py::kwargs) { return to_dlpack(d.a); })
+      .def("__dlpack_device__", [](const DeviceArray& d) { return py::make_tuple(kDLROCM, d.a->device()); })
+      .def("numpy", [](const DeviceArray& d) { return device_to_numpy(d.a); })
+      .def("__array__", [](const DeviceArray& d, py::args, py::kwargs) { return device_to_numpy(d.a); })
+      .def("__len__", [](const DeviceArray& d) { return d.a->ndim() ? d.a->shape(0) : 0; })
+      .def("__repr__", [](const DeviceArray& d) {
+        std::ostringstream o;
+        o << "DeviceArray(shape=(";
+        for (int i = 0; i < d.a->ndim(); i++) o << (i ? ", " : "") << d.a->shape(i);
+        o << (d.a->ndim() == 1 ? ",)" : ")") << ", device=" << d.a->device() << ")";
+        return o.str();
+      });
 
   py::class_<Buffer, std::shared_ptr<Buffer>> buffer(m, "Buffer");
   py::class_<Stream, std::shared_ptr<Stream>> stream(m, "Stream");
@@ -290,10 +420,13 @@ PYBIND11_MODULE(_pipeline, m) {
       })
       .def(
           "batch",
-          [](const std::shared_ptr<Buffer>& b, int64_t batch_size, PadMap pad, DimMap dim) -> std::shared_ptr<Buffer> {
-            return std::make_shared<BufferBatch>(b, batch_size, std::move(pad), std::move(dim));
+          [](const std::shared_ptr<Buffer>& b, int64_t batch_size, PadMap pad, DimMap dim, py::object device,
+             py::object device_keys) -> std::shared_ptr<Buffer> {
+            return std::make_shared<BufferBatch>(b, batch_size, std::move(pad), std::move(dim),
+                                                 device_out(device, device_keys));
           },
-          py::arg("batch_size"), py::arg("pad") = PadMap{}, py::arg("dim") = DimMap{})
+          py::arg("batch_size"), py::arg("pad") = PadMap{}, py::arg("dim") = DimMap{}, py::arg("device") = py::none(),
+          py::arg("device_keys") = py::none())
       .def(
           "ordered_prefetch",
           [](const std::shared_ptr<Buffer>& b, int prefetch_size, int num_threads) -> std::shared_ptr<Stream> {
@@ -318,10 +451,13 @@ PYBIND11_MODULE(_pipeline, m) {
            })
       .def(
           "batch",
-          [](const std::shared_ptr<Stream>& s, int64_t batch_size, PadMap pad, DimMap dim) -> std::shared_ptr<Stream> {
-            return std::make_shared<StreamBatch>(s, batch_size, std::move(pad), std::move(dim));
+          [](const std::shared_ptr<Stream>& s, int64_t batch_size, PadMap pad, DimMap dim, py::object device,
+             py::object device_keys) -> std::shared_ptr<Stream> {
+            return std::make_shared<StreamBatch>(s, batch_size, std::move(pad), std::move(dim),
+                                                 device_out(device, device_keys));
           },
-          py::arg("batch_size"), py::arg("pad") = PadMap{}, py::arg("dim") = DimMap{})
+          py::arg("batch_size"), py::arg("pad") = PadMap{}, py::arg("dim") = DimMap{}, py::arg("device") = py::none(),
+          py::arg("device_keys") = py::none())
       .def(
           "prefetch",
           [](const std::shared_ptr<Stream>& s, int prefetch_size, int num_threads) -> std::shared_ptr<Stream> {

@@ -25,7 +25,8 @@ EXPORTS = (
     "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
     "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
     "mxd_event_create", "mxd_event_destroy", "mxd_event_record", "mxd_event_synchronize", "mxd_event_elapsed_ms",
-    "mxd_resize_crop_host", "mxd_release_host_buffers",
+    "mxd_resize_crop_host", "mxd_resize_crop_to_device", "mxd_memcpy_h2d", "mxd_memcpy_d2h",
+    "mxd_release_host_buffers",
     "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
 )
@@ -173,6 +174,11 @@ def describe_plan(entry, out_dtype=MXD_U8, device=0):
 
 def resize_crop_host(images, n, out_dtype, device=0):
     check(lib().mxd_resize_crop_host(images, n, out_dtype, device))
+
+
+def resize_crop_to_device(images, n, out_dtype, device=0):
+    """Host sources, device destinations (mxd_resize_crop_to_device)."""
+    check(lib().mxd_resize_crop_to_device(images, n, out_dtype, device))
 
 
 def jpeg_info(data):

@@ -19,7 +19,10 @@ build's one addition to the surface) replaces the trailing
 ``key_transform(..., lambda x: x.astype("float32") / 255)``: the same launch
 then writes the float32 batch, bit-identical to that lambda.  With several
 devices (``set_devices``) one batch is split into contiguous slices, one per
-device.  Reading an unbatched image materialises it with its own launch.
+device.  ``batch(n, device=d)`` builds the image keys' batches in device
+memory instead (``DeviceArray``: DLPack producer, ``numpy()`` copies back);
+import torch before this package when torch consumes them, so both share one
+HIP runtime.  Reading an unbatched image materialises it with its own launch.
 There is no CPU resize: without a visible GPU the image ops raise.
 
 ``load_image`` decodes JPEG natively (``csrc/pipeline/jpeg.cpp``, the
@@ -33,9 +36,10 @@ import numpy as np
 
 from . import capi  # noqa: F401  (loads libmxd_amd.so before anything else binds a HIP runtime)
 from . import _pipeline  # noqa: F401
-from ._pipeline import Buffer, Stream, buffer_from_vector, devices, set_devices, set_image_decoder, set_state
+from ._pipeline import (Buffer, DeviceArray, Stream, buffer_from_vector, devices, set_devices, set_image_decoder,
+                        set_state)
 
-__all__ = ["Buffer", "Stream", "buffer_from_vector", "set_state", "set_devices", "devices"]
+__all__ = ["Buffer", "Stream", "DeviceArray", "buffer_from_vector", "set_state", "set_devices", "devices"]
 
 
 def _decode(path, data, from_memory, info):
