@@ -1,0 +1,152 @@
+"""End-to-end pipeline benchmark through the operator surface (SURVEY.md §8d
+C1 / C4; VERDICT r1 missing 6): JPEG files on disk -> load_image (native
+decoder) -> image_resize_smallest_side 256 -> image_center_crop 224 -> batch
+-> f32 / 255 -> prefetch(workers, workers), timed like the reference's
+harness (benchmarks/comparative/caltech101/mlx_data.py:23-72: whole-dataset
+iteration at 1, 8 and 16 workers), beside the reference-algorithm CPU
+restatement of the same chain on the same files and threads.
+
+Variants per worker count:
+  ref_form   the reference chain verbatim (batch, then
+             key_transform(lambda x: x.astype("float32") / 255))
+  fused      image_to_float before batch: the kernel writes the f32 batch
+  device     fused + batch(..., device=0): the batch stays in HBM (DLPack)
+  cpu        Pillow (libjpeg-turbo) decode -> oracle C stbir restatement ->
+             crop -> batch -> numpy /255 on a thread pool of the same size
+Datasets (synthetic stand-ins, seeded smooth noise, Pillow q=90 JPEGs):
+  c1  300x200 / 200x300 (Caltech-101-like), batch 32
+  c4  500x375 / 375x500 / 500x333 (ImageNet-like), batch 128
+Prints one JSON line per (dataset, variant, workers)."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "mlx-data_amd"), os.path.join(REPO, "oracle")]
+
+DATASETS = {
+    "c1": dict(sizes=[(300, 200), (300, 200), (200, 300)], batch=32),
+    "c4": dict(sizes=[(500, 375), (375, 500), (500, 333)], batch=128),
+}
+
+
+def smooth(rng, h, w):
+    gh, gw = h // 24 + 2, w // 24 + 2
+    grid = rng.integers(0, 256, (gh, gw, 3)).astype(np.float32)
+    yi = np.minimum(np.arange(h) * (gh - 1) // max(1, h - 1), gh - 2)
+    xi = np.minimum(np.arange(w) * (gw - 1) // max(1, w - 1), gw - 2)
+    f = grid[yi][:, xi] * 0.6 + grid[yi + 1][:, xi + 1] * 0.4 + rng.normal(0, 12, (h, w, 3))
+    return np.clip(f, 0, 255).astype(np.uint8)
+
+
+def make_files(root, name, n):
+    from PIL import Image
+
+    rng = np.random.default_rng({"c1": 11, "c4": 2}[name])
+    sizes = DATASETS[name]["sizes"]
+    files = []
+    for i in range(n):
+        w, h = sizes[int(rng.integers(0, len(sizes)))]
+        d = os.path.join(root, name, f"class{i % 16}")
+        os.makedirs(d, exist_ok=True)
+        p = os.path.join(d, f"img{i}.jpg")
+        Image.fromarray(smooth(rng, h, w)).save(p, quality=90)
+        files.append(p)
+    return files
+
+
+def run_surface(files, batch, workers, variant):
+    from mlx_data_amd import data as dx
+
+    samples = [dict(image=f.encode("ascii"), label=i) for i, f in enumerate(files)]
+    d = (dx.buffer_from_vector(samples).shuffle().to_stream().load_image("image")
+         .image_resize_smallest_side("image", 256).image_center_crop("image", 224, 224))
+    if variant == "ref_form":
+        d = d.batch(batch).key_transform("image", lambda x: x.astype("float32") / 255)
+    elif variant == "fused":
+        d = d.image_to_float("image").batch(batch)
+    else:
+        d = d.image_to_float("image").batch(batch, device=0)
+    d = d.prefetch(workers, workers)
+    n = 0
+    t0 = time.perf_counter()
+    for s in d:
+        n += len(s["label"])
+    return n, time.perf_counter() - t0
+
+
+def run_cpu(files, batch, workers):
+    """The reference's CPU path restated: libjpeg-turbo decode (Pillow), the
+    oracle's stbir restatement, crop, batch, /255 -- one batch per task."""
+    from PIL import Image
+    import oracle as O
+
+    lib = O.lib()
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    order = np.random.default_rng(0).permutation(len(files))
+    nb = (len(files) + batch - 1) // batch
+    nxt = [0]
+    lock = threading.Lock()
+
+    def one_batch(b):
+        idx = order[b * batch:(b + 1) * batch]
+        crops = np.empty((len(idx), 224, 224, 3), np.uint8)
+        for k, i in enumerate(idx):
+            img = np.ascontiguousarray(np.asarray(Image.open(files[i]).convert("RGB")))
+            h, w = img.shape[:2]
+            rc = lib.orc_resize_smallest_side_center_crop(img.ctypes.data_as(u8p), w, h, 3, 256, 224, 224,
+                                                          crops[k].ctypes.data_as(u8p))
+            assert rc == 0
+        return crops.astype("float32") / 255
+
+    def worker():
+        while True:
+            with lock:
+                b = nxt[0]
+                nxt[0] += 1
+            if b >= nb:
+                return
+            one_batch(b)
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=worker) for _ in range(workers)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return len(files), time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--datasets", default="c1,c4")
+    ap.add_argument("--images", type=int, default=2048)
+    ap.add_argument("--workers", default="1,8,16")
+    ap.add_argument("--variants", default="ref_form,fused,device,cpu")
+    ap.add_argument("--cpu-images", type=int, default=512, help="files the CPU restatement runs over")
+    args = ap.parse_args()
+    workers = [int(w) for w in args.workers.split(",")]
+    with tempfile.TemporaryDirectory() as root:
+        for name in args.datasets.split(","):
+            files = make_files(root, name, args.images)
+            B = DATASETS[name]["batch"]
+            for v in args.variants.split(","):
+                for w in workers:
+                    if v == "cpu":
+                        n, dt = run_cpu(files[:args.cpu_images], B, w)
+                    else:
+                        run_surface(files[:2 * B], B, w, v)  # warm-up: decoder, tables, pinned buffers
+                        n, dt = run_surface(files, B, w, v)
+                    print(json.dumps(dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
+                                          images_per_s=round(n / dt, 1), batch=B)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
