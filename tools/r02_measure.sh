@@ -20,7 +20,8 @@ run bench 400 python bench.py
 run bench_c3 300 python bench.py --workload c3 --steps 20 --warmup 3 --no-cpu
 run bench_c4 300 python bench.py --workload c4 --steps 50 --warmup 5 --no-cpu
 run bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu
-run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --no-cpu
+# the bench's own launches only (the e2e leg's chunked launches would mix into the average)
+run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --no-cpu --no-e2e
 cut -c1-220 gpurun_out/${TAG}_prof/run_kernel_stats.csv
 for w in c2 c3 c4 c5; do
   i=0
@@ -29,7 +30,8 @@ for w in c2 c3 c4 c5; do
     run ${w}pmc_p$i 120 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_${w}pmc_p$i -o run -- python3 bench.py --workload $w --steps 10 --warmup 2 --no-cpu --no-e2e --no-copy
   done
 done
+python3 tools/make_traffic.py $TAG r02/$TAG > /dev/null
 if [ "${2:-}" != "skip-pipeline" ]; then
-  run pipeline 900 python tools/bench_pipeline.py
+  run pipeline 900 python tools/bench_pipeline.py --images 4096 --cpu-images 2048
 fi
 exit 0
