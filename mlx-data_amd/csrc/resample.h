@@ -67,7 +67,16 @@ struct WaveCfg {
 // block (a multiple of S whose iterations are a multiple of the ring), words
 // per iteration entry (row + S weights).
 constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; }
-constexpr int scatter_ring_slots(int dmax) { return 12 % dmax == 0 ? 12 : (2 * dmax <= 12 ? 2 * dmax : dmax); }
+// Ring target: 6 (4 slots at DMAX 4) keeps the C2 kernel at 118 VGPRs, i.e.
+// 4 waves per SIMD; 12 (166 VGPRs, 3 waves) measured 3 % slower on C2 and
+// 1-2 % on C4/C5 (tools/ab.sh, profiles/r02/ring_ab.txt).  Tuning builds
+// override it with -DMXD_RING=<n> (kernel and host together).
+#ifndef MXD_RING
+#define MXD_RING 6
+#endif
+constexpr int scatter_ring_slots(int dmax) {
+  return MXD_RING % dmax == 0 ? MXD_RING : (2 * dmax <= MXD_RING ? 2 * dmax : dmax);
+}
 constexpr int scatter_block_groups(int s, int dmax) {
   return scatter_ring_slots(dmax) / scatter_gcd(scatter_ring_slots(dmax), s * dmax) * s;
 }
