@@ -18,6 +18,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -1000,6 +1001,31 @@ void free_slot_buffers(Slot& s) {
 
 constexpr int kCtxPerDevice = 4;
 
+// Host-side byte moves of the host path (footprint staging into pinned
+// memory, copy-out of results) are bound by one core's memory bandwidth;
+// they are split over helper threads, fewer when several host-path calls run
+// at once (prefetch workers already spread the work).
+std::atomic<int> g_host_calls{0};
+
+template <class F>
+void parallel_items(int32_t first, int32_t end, int64_t bytes, F&& f) {
+  const int32_t n = end - first;
+  const int hw = std::max(1u, std::thread::hardware_concurrency());
+  int t = std::min<int64_t>({8, hw / std::max(1, g_host_calls.load()), n, bytes >> 20});
+  if (t <= 1) {
+    for (int32_t i = first; i < end; i++) f(i);
+    return;
+  }
+  std::atomic<int32_t> next{first};
+  auto work = [&] {
+    for (int32_t i; (i = next.fetch_add(1)) < end;) f(i);
+  };
+  std::vector<std::thread> ts;
+  for (int k = 1; k < t; k++) ts.emplace_back(work);
+  work();
+  for (auto& th : ts) th.join();
+}
+
 class HostPool {
  public:
   HostCtx* acquire(int32_t device) {
@@ -1312,6 +1338,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (int rc = validate(images[i], i)) return rc;
   if (int rc = check_device(device)) return rc;
   DeviceGuard g(device);
+  g_host_calls.fetch_add(1);
+  struct CallCount {
+    ~CallCount() { g_host_calls.fetch_sub(1); }
+  } call_count;
   // Per image: the staged footprint (columns from x0, 16-byte aligned so both
   // kernel families read it as they would the whole image) and its offsets.
   struct Stage {
@@ -1360,7 +1390,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventSynchronize(sl.done));
     pending[k & 1] = -1;
     if (dst_device) return MXD_OK;  // the kernel wrote the destinations
-    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+    int64_t bytes = 0;
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) bytes += st[i].out_row * images[i].crop_h;
+    parallel_items(chunks[k].first, chunks[k].second, bytes, [&](int32_t i) {
       const mxd_image& im = images[i];
       uint8_t* d = static_cast<uint8_t*>(im.dst);
       const uint8_t* src = sl.pin_out + st[i].out_off;
@@ -1370,7 +1402,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         for (int32_t r = 0; r < im.crop_h; r++)
           std::memcpy(d + (size_t)r * im.dst_stride, src + (size_t)r * st[i].out_row, st[i].out_row);
       }
-    }
+    });
     return MXD_OK;
   };
   for (int k = 0; k < (int)chunks.size(); k++) {
@@ -1393,13 +1425,17 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const int32_t cn = chunks[k].second - chunks[k].first;
     std::vector<mxd_image> dev_imgs(images + chunks[k].first, images + chunks[k].second);
     std::vector<Stored> where(cn);
-    for (int32_t j = 0; j < cn; j++) {
-      const int32_t i = chunks[k].first + j;
+    parallel_items(chunks[k].first, chunks[k].second, in_bytes, [&](int32_t i) {
       const mxd_image& im = images[i];
       const Stage& s = st[i];
       uint8_t* stage = sl.pin_in + s.in_off;
       const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
       for (int32_t r = 0; r < s.rows; r++) std::memcpy(stage + r * s.pitch, from + (int64_t)r * im.src_stride, s.copy);
+    });
+    for (int32_t j = 0; j < cn; j++) {
+      const int32_t i = chunks[k].first + j;
+      const mxd_image& im = images[i];
+      const Stage& s = st[i];
       where[j] = Stored{sl.dev_in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
       dev_imgs[j].src = sl.dev_in + s.in_off;  // checked by validate() only; `where` says what is stored
       dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
