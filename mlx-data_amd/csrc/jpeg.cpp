@@ -61,12 +61,24 @@ std::string hex2(int v) {
 // ---------------------------------------------------------------- Huffman
 constexpr int kLook = 9;
 
+// AC fast path: for a kLook-bit lookahead whose code AND magnitude bits both
+// fit in it, the decoded coefficient, its zero run and the bits to consume
+// (stb_image's fast-AC idea).  run == kEob marks an end-of-block-class symbol
+// (size 0, run != 15); len == 0: take the general path.
+constexpr uint8_t kEob = 0xFF;
+struct FastAC {
+  int16_t val;
+  uint8_t run;
+  uint8_t len;
+};
+
 struct Huff {
   bool present = false;
   uint16_t look[1 << kLook];  // (length << 8) | symbol, 0 = longer code
   int32_t maxcode[18];
   int32_t valoffset[18];
   uint8_t vals[256];
+  FastAC fac[1 << kLook];
 };
 
 // jdhuff.c jpeg_make_d_derived_tbl
@@ -109,6 +121,19 @@ void build_huff(Huff& h, const uint8_t* bits /* [17], bits[0] unused */, const u
       for (int ctr = 1 << (kLook - l); ctr > 0; ctr--) h.look[lookbits + ctr - 1] = (uint16_t)((l << 8) | vals[p]);
     }
   std::memcpy(h.vals, vals, n);
+  for (int i = 0; i < (1 << kLook); i++) {
+    FastAC f{0, 0, 0};
+    if (const int e = h.look[i]) {
+      const int l = e >> 8, rs = e & 0xff, r = rs >> 4, sz = rs & 15;
+      if (sz == 0) {
+        f = FastAC{0, (uint8_t)(r == 15 ? 15 : kEob), (uint8_t)l};
+      } else if (l + sz <= kLook) {
+        const int v = (i >> (kLook - l - sz)) & ((1 << sz) - 1);
+        f = FastAC{(int16_t)(v < (1 << (sz - 1)) ? v + ((-1) << sz) + 1 : v), (uint8_t)r, (uint8_t)(l + sz)};
+      }
+    }
+    h.fac[i] = f;
+  }
   h.present = true;
 }
 
@@ -123,6 +148,20 @@ struct Bits {
   bool insufficient = false;
 
   void fill() {
+    // Fast path: the next 8 bytes hold no 0xFF (no stuffing, no marker).
+    if (cnt <= 56 && !at_marker && end - p >= 8) {
+      uint64_t w;
+      std::memcpy(&w, p, 8);
+      const uint64_t x = ~w;
+      if (((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) == 0) {
+        const int k = (64 - cnt) >> 3;
+        const uint64_t be = __builtin_bswap64(w);
+        buf |= (be >> (64 - 8 * k)) << (64 - cnt - 8 * k);
+        p += k;
+        cnt += 8 * k;
+        return;
+      }
+    }
     while (cnt <= 56) {
       if (at_marker || p >= end) return;
       const uint8_t b = *p;
@@ -367,26 +406,123 @@ void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) 
   }
 }
 
-// ---------------------------------------------------------------- colour
-struct ColorTables {
-  int cr_r[256], cb_b[256];
-  int32_t cr_g[256], cb_g[256];
-  ColorTables() {
-    constexpr int kScale = 16;
-    constexpr int32_t kHalf = (int32_t)1 << (kScale - 1);
-    auto fix = [](double x) { return (int32_t)(x * (1 << kScale) + 0.5); };
-    for (int i = 0; i < 256; i++) {
-      const int32_t x = i - 128;
-      cr_r[i] = (int)((fix(1.40200) * x + kHalf) >> kScale);
-      cb_b[i] = (int)((fix(1.77200) * x + kHalf) >> kScale);
-      cr_g[i] = -fix(0.71414) * x;
-      cb_g[i] = -fix(0.34414) * x + kHalf;
-    }
+// The same transform in 32-bit lanes, vectorised across the 8 columns (pass
+// 1) and, after a transpose, the 8 rows (pass 2).  Exact whenever no
+// intermediate leaves int32: the dequantised inputs and the pass-1 outputs
+// are checked below 2^14 in magnitude (every product then stays below 2^31),
+// otherwise the block goes to idct_islow.  The post-IDCT range table is
+// applied as its arithmetic equivalent: wrap to 10 bits, +128, clamp.
+template <int S>
+inline void idct_1d8(const int32_t* in, int32_t* out) {
+  // in[k * 8 + l], out[k * 8 + l]: lane l, coefficient / sample k
+  for (int l = 0; l < 8; l++) {
+    const int32_t z2a = in[16 + l], z3a = in[48 + l];
+    const int32_t z1a = (z2a + z3a) * FIX_0_541196100;
+    const int32_t t2 = z1a + z3a * -FIX_1_847759065;
+    const int32_t t3 = z1a + z2a * FIX_0_765366865;
+    const int32_t t0 = (in[l] + in[32 + l]) * (1 << kConstBits);
+    const int32_t t1 = (in[l] - in[32 + l]) * (1 << kConstBits);
+    const int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+    int32_t o0 = in[56 + l], o1 = in[40 + l], o2 = in[24 + l], o3 = in[8 + l];
+    int32_t z1 = o0 + o3, z2 = o1 + o2, z3 = o0 + o2, z4 = o1 + o3;
+    const int32_t z5 = (z3 + z4) * FIX_1_175875602;
+    o0 *= FIX_0_298631336;
+    o1 *= FIX_2_053119869;
+    o2 *= FIX_3_072711026;
+    o3 *= FIX_1_501321110;
+    z1 *= -FIX_0_899976223;
+    z2 *= -FIX_2_562915447;
+    z3 = z3 * -FIX_1_961570560 + z5;
+    z4 = z4 * -FIX_0_390180644 + z5;
+    o0 += z1 + z3;
+    o1 += z2 + z4;
+    o2 += z2 + z3;
+    o3 += z1 + z4;
+    constexpr int32_t r = 1 << (S - 1);
+    out[l] = (t10 + o3 + r) >> S;
+    out[56 + l] = (t10 - o3 + r) >> S;
+    out[8 + l] = (t11 + o2 + r) >> S;
+    out[48 + l] = (t11 - o2 + r) >> S;
+    out[16 + l] = (t12 + o1 + r) >> S;
+    out[40 + l] = (t12 - o1 + r) >> S;
+    out[24 + l] = (t13 + o0 + r) >> S;
+    out[32 + l] = (t13 - o0 + r) >> S;
   }
-};
-const ColorTables kColor;
+}
 
-inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+__attribute__((target_clones("avx2", "default"))) bool idct_islow32(const int16_t* in, const uint16_t* q,
+                                                                    uint8_t* out, int stride) {
+  int32_t d[64], ws[64], wt[64], o[64];
+  int32_t m = 0;
+  for (int i = 0; i < 64; i++) {
+    d[i] = (int32_t)in[i] * (int32_t)q[i];
+    m |= d[i] >= 0 ? d[i] : -d[i];
+  }
+  if (m >= (1 << 14)) return false;
+  idct_1d8<kConstBits - kPass1Bits>(d, ws);  // ws[k * 8 + c]: row k of column c
+  m = 0;
+  for (int i = 0; i < 64; i++) m |= ws[i] >= 0 ? ws[i] : -ws[i];
+  if (m >= (1 << 14)) return false;
+  for (int r = 0; r < 8; r++)
+    for (int c = 0; c < 8; c++) wt[c * 8 + r] = ws[r * 8 + c];
+  idct_1d8<kConstBits + kPass1Bits + 3>(wt, o);  // o[c * 8 + r]: column c of row r
+  for (int i = 0; i < 64; i++) {
+    const int32_t v = (((o[i] + 512) & 1023) - 512) + 128;
+    o[i] = v < 0 ? 0 : v > 255 ? 255 : v;
+  }
+  for (int r = 0; r < 8; r++)
+    for (int c = 0; c < 8; c++) out[(size_t)r * stride + c] = (uint8_t)o[c * 8 + r];
+  return true;
+}
+
+inline void idct_block(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) {
+  if (!idct_islow32(in, q, out, stride)) idct_islow(in, q, out, stride);
+}
+
+// ---------------------------------------------------------------- colour
+// jdsample.c h2v2_fancy_upsample for one output row from its two input rows
+// (in0 nearer): column sums first, then the 3:1 horizontal blend -- the same
+// integer formula, laid out without a loop-carried dependency.
+__attribute__((target_clones("avx2", "default"))) void h2v2_fancy_row(const uint8_t* in0, const uint8_t* in1,
+                                                                      int dw, uint8_t* t, int16_t* cs) {
+  for (int x = 0; x < dw; x++) cs[x] = (int16_t)(in0[x] * 3 + in1[x]);
+  t[0] = (uint8_t)((cs[0] * 4 + 8) >> 4);
+  t[1] = (uint8_t)((cs[0] * 3 + cs[1] + 7) >> 4);
+  for (int x = 1; x < dw - 1; x++) {
+    t[2 * x] = (uint8_t)((cs[x] * 3 + cs[x - 1] + 8) >> 4);
+    t[2 * x + 1] = (uint8_t)((cs[x] * 3 + cs[x + 1] + 7) >> 4);
+  }
+  t[2 * dw - 2] = (uint8_t)((cs[dw - 1] * 3 + cs[dw - 2] + 8) >> 4);
+  t[2 * dw - 1] = (uint8_t)((cs[dw - 1] * 4 + 7) >> 4);
+}
+
+// jdcolor.c ycc_rgb_convert for one row, in the integer arithmetic its tables
+// hold (FIX(x) = round(x * 2^16); Cr->R and Cb->B rounded by ONE_HALF, the G
+// term shifted after summing), so it vectorises; YCCK -> CMYK inverts.
+constexpr int32_t kFixCrR = 91881, kFixCbB = 116130, kFixCrG = 46802, kFixCbG = 22554, kHalf16 = 1 << 15;
+
+__attribute__((target_clones("avx2", "default"))) void ycc_rgb_row(const uint8_t* Y, const uint8_t* Cb,
+                                                                   const uint8_t* Cr, uint8_t* o, int W,
+                                                                   bool invert) {
+  for (int x = 0; x < W; x++) {
+    const int32_t y = Y[x], cb = Cb[x] - 128, cr = Cr[x] - 128;
+    int32_t r = y + ((kFixCrR * cr + kHalf16) >> 16);
+    int32_t g = y + ((-kFixCbG * cb + kHalf16 - kFixCrG * cr) >> 16);
+    int32_t b = y + ((kFixCbB * cb + kHalf16) >> 16);
+    r = r < 0 ? 0 : r > 255 ? 255 : r;
+    g = g < 0 ? 0 : g > 255 ? 255 : g;
+    b = b < 0 ? 0 : b > 255 ? 255 : b;
+    if (invert) {
+      r = 255 - r;
+      g = 255 - g;
+      b = 255 - b;
+    }
+    o[3 * x] = (uint8_t)r;
+    o[3 * x + 1] = (uint8_t)g;
+    o[3 * x + 2] = (uint8_t)b;
+  }
+}
+
 
 // ---------------------------------------------------------------- decoder
 struct Component {
@@ -630,6 +766,15 @@ struct Decoder {
           c.dc_pred = s;
           blk[0] = (int16_t)s;
           for (int k = 1; k < 64; k++) {
+            if (bits.cnt < 16) bits.fill();
+            const FastAC f = ha.fac[bits.peek(kLook)];
+            if (f.len) {
+              bits.consume(f.len);
+              if (f.run == kEob) break;
+              k += f.run;
+              blk[kNatural[k]] = f.val;
+              continue;
+            }
             int rs = bits.decode(ha);
             const int r = rs >> 4;
             s = rs & 15;
@@ -642,7 +787,7 @@ struct Decoder {
             }
           }
         }
-        idct_islow(blk, quant(c), c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
+        idct_block(blk, quant(c), c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
       });
       return;
     }
@@ -678,6 +823,14 @@ struct Decoder {
           return;
         }
         for (int k = ss; k <= se; k++) {
+          if (bits.cnt < 16) bits.fill();
+          const FastAC f = ha.fac[bits.peek(kLook)];
+          if (f.len && f.run != kEob) {
+            bits.consume(f.len);
+            k += f.run;
+            blk[kNatural[k]] = (int16_t)(f.val * (1 << al));
+            continue;
+          }
           const int rs = bits.decode(ha);
           int r = rs >> 4;
           const int s = rs & 15;
@@ -783,93 +936,64 @@ struct Decoder {
 
   int color_space() const;  // 0 grey, 1 YCbCr, 2 RGB, 3 CMYK, 4 YCCK
 
-  // Component c upsampled to full size, rows [0, height), cols [0, width).
-  void upsample(const Component& c, std::vector<uint8_t>& out) const {
-    const int W = width, H = height;
-    out.resize((size_t)W * H);
+  // Row y of component c upsampled to full width (jdsample.c), into o (>= width
+  // bytes; scratch >= 2 * dw + 2 bytes); returns the row (o, or the plane row
+  // itself when c is full size).
+  const uint8_t* upsample_row(const Component& c, int y, uint8_t* o, uint8_t* scratch) const {
+    const int W = width;
     const int stride = c.bw * 8;
     const uint8_t* pl = c.plane.data();
     const int hx = max_h / c.h, vx = max_v / c.v;
     const bool h2 = c.h * 2 == max_h, v2 = c.v * 2 == max_v;
-    auto row = [&](int y) { return pl + (size_t)std::min(std::max(y, 0), c.dh - 1) * stride; };
-    if (c.h == max_h && c.v == max_v) {
-      for (int y = 0; y < H; y++) std::memcpy(out.data() + (size_t)y * W, pl + (size_t)y * stride, W);
-      return;
-    }
-    std::vector<uint8_t> tmp(2 * (size_t)c.dw + 2);
+    auto row = [&](int yy) { return pl + (size_t)std::min(std::max(yy, 0), c.dh - 1) * stride; };
+    if (c.h == max_h && c.v == max_v) return pl + (size_t)y * stride;
     if (h2 && c.v == max_v) {
-      // jdsample.c h2v1_fancy_upsample (or h2v1_upsample when dw <= 2)
-      for (int y = 0; y < H; y++) {
-        const uint8_t* in = pl + (size_t)y * stride;
-        uint8_t* o = tmp.data();
-        if (c.dw > 2) {
-          int v = in[0];
-          o[0] = (uint8_t)v;
-          o[1] = (uint8_t)((v * 3 + in[1] + 2) >> 2);
-          for (int x = 1; x < c.dw - 1; x++) {
-            v = in[x] * 3;
-            o[2 * x] = (uint8_t)((v + in[x - 1] + 1) >> 2);
-            o[2 * x + 1] = (uint8_t)((v + in[x + 1] + 2) >> 2);
-          }
-          v = in[c.dw - 1];
-          o[2 * c.dw - 2] = (uint8_t)((v * 3 + in[c.dw - 2] + 1) >> 2);
-          o[2 * c.dw - 1] = (uint8_t)v;
-        } else {
-          for (int x = 0; x < c.dw; x++) o[2 * x] = o[2 * x + 1] = in[x];
+      // h2v1_fancy_upsample (or h2v1_upsample when dw <= 2)
+      const uint8_t* in = pl + (size_t)y * stride;
+      uint8_t* t = scratch;
+      if (c.dw > 2) {
+        int v = in[0];
+        t[0] = (uint8_t)v;
+        t[1] = (uint8_t)((v * 3 + in[1] + 2) >> 2);
+        for (int x = 1; x < c.dw - 1; x++) {
+          v = in[x] * 3;
+          t[2 * x] = (uint8_t)((v + in[x - 1] + 1) >> 2);
+          t[2 * x + 1] = (uint8_t)((v + in[x + 1] + 2) >> 2);
         }
-        std::memcpy(out.data() + (size_t)y * W, o, W);
+        v = in[c.dw - 1];
+        t[2 * c.dw - 2] = (uint8_t)((v * 3 + in[c.dw - 2] + 1) >> 2);
+        t[2 * c.dw - 1] = (uint8_t)v;
+      } else {
+        for (int x = 0; x < c.dw; x++) t[2 * x] = t[2 * x + 1] = in[x];
       }
-      return;
+      return t;
     }
     if (c.h == max_h && v2) {
-      // jdsample.c h1v2_fancy_upsample
-      for (int y = 0; y < H; y++) {
-        const int iy = y >> 1;
-        const bool below = y & 1;
-        const uint8_t* in0 = row(iy);
-        const uint8_t* in1 = row(below ? iy + 1 : iy - 1);
-        const int bias = below ? 2 : 1;
-        uint8_t* o = out.data() + (size_t)y * W;
-        for (int x = 0; x < W; x++) o[x] = (uint8_t)((in0[x] * 3 + in1[x] + bias) >> 2);
-      }
-      return;
+      // h1v2_fancy_upsample
+      const int iy = y >> 1;
+      const bool below = y & 1;
+      const uint8_t* in0 = row(iy);
+      const uint8_t* in1 = row(below ? iy + 1 : iy - 1);
+      const int bias = below ? 2 : 1;
+      for (int x = 0; x < W; x++) o[x] = (uint8_t)((in0[x] * 3 + in1[x] + bias) >> 2);
+      return o;
     }
     if (h2 && v2 && c.dw > 2) {
-      // jdsample.c h2v2_fancy_upsample
-      for (int y = 0; y < H; y++) {
-        const int iy = y >> 1;
-        const bool below = y & 1;
-        const uint8_t* in0 = row(iy);
-        const uint8_t* in1 = row(below ? iy + 1 : iy - 1);
-        uint8_t* o = tmp.data();
-        int thiscol = in0[0] * 3 + in1[0];
-        int nextcol = in0[1] * 3 + in1[1];
-        o[0] = (uint8_t)((thiscol * 4 + 8) >> 4);
-        o[1] = (uint8_t)((thiscol * 3 + nextcol + 7) >> 4);
-        int lastcol = thiscol;
-        thiscol = nextcol;
-        for (int x = 1; x < c.dw - 1; x++) {
-          nextcol = in0[x + 1] * 3 + in1[x + 1];
-          o[2 * x] = (uint8_t)((thiscol * 3 + lastcol + 8) >> 4);
-          o[2 * x + 1] = (uint8_t)((thiscol * 3 + nextcol + 7) >> 4);
-          lastcol = thiscol;
-          thiscol = nextcol;
-        }
-        o[2 * c.dw - 2] = (uint8_t)((thiscol * 3 + lastcol + 8) >> 4);
-        o[2 * c.dw - 1] = (uint8_t)((thiscol * 4 + 7) >> 4);
-        std::memcpy(out.data() + (size_t)y * W, o, W);
-      }
-      return;
+      // h2v2_fancy_upsample
+      const int iy = y >> 1;
+      const bool below = y & 1;
+      const uint8_t* in0 = row(iy);
+      const uint8_t* in1 = row(below ? iy + 1 : iy - 1);
+      h2v2_fancy_row(in0, in1, c.dw, scratch, reinterpret_cast<int16_t*>(scratch + 2 * c.dw + 2));
+      return scratch;
     }
     if (max_h % c.h != 0 || max_v % c.v != 0) fail("Fractional sampling not implemented yet");
     // int_upsample / h2v1_upsample / h2v2_upsample: replication.  Source rows
     // come from the padded plane (not clamped), like the row groups libjpeg
     // replicates.
-    for (int y = 0; y < H; y++) {
-      const uint8_t* in = pl + (size_t)(y / vx) * stride;
-      uint8_t* o = out.data() + (size_t)y * W;
-      for (int x = 0; x < W; x++) o[x] = in[x / hx];
-    }
+    const uint8_t* in = pl + (size_t)(y / vx) * stride;
+    for (int x = 0; x < W; x++) o[x] = in[x / hx];
+    return o;
   }
 
   void output(uint8_t* dst, int64_t dst_stride) {
@@ -879,7 +1003,7 @@ struct Decoder {
         const uint16_t* q = quant(c);
         for (int by = 0; by < c.bh; by++)
           for (int bx = 0; bx < c.bw; bx++)
-            idct_islow(c.coef.data() + ((size_t)by * c.bw + bx) * 64, q,
+            idct_block(c.coef.data() + ((size_t)by * c.bw + bx) * 64, q,
                        c.plane.data() + (size_t)by * 8 * c.bw * 8 + (size_t)bx * 8, c.bw * 8);
       }
     const int cs = color_space();
@@ -893,38 +1017,29 @@ struct Decoder {
       }
       return;
     }
-    std::vector<uint8_t> up[4];
     const int nuse = ncomp == 4 && cs == 3 ? 3 : ncomp;  // CMYK: K is dropped by the caller
-    for (int i = 0; i < nuse; i++) upsample(comp[i], up[i]);
+    // per component: an output row, and scratch = 2 dw + 2 upsampled bytes +
+    // dw int16 column sums (dw <= W)
+    const size_t rb = ((size_t)W + 63) & ~(size_t)63, sb = ((size_t)4 * W + 64) & ~(size_t)63;
+    std::vector<uint8_t> buf(3 * (rb + sb) + 64);
+    uint8_t* base = reinterpret_cast<uint8_t*>(((uintptr_t)buf.data() + 63) & ~(uintptr_t)63);
+    uint8_t* rowbuf[3];
+    uint8_t* scratch[3];
+    for (int i = 0; i < 3; i++) {
+      rowbuf[i] = base + (size_t)i * (rb + sb);
+      scratch[i] = rowbuf[i] + rb;
+    }
     for (int y = 0; y < H; y++) {
-      const uint8_t* a = up[0].data() + (size_t)y * W;
-      const uint8_t* b = up[1].data() + (size_t)y * W;
-      const uint8_t* c = up[2].data() + (size_t)y * W;
+      const uint8_t* r3[3];
+      for (int i = 0; i < 3 && i < nuse; i++) r3[i] = upsample_row(comp[i], y, rowbuf[i], scratch[i]);
       uint8_t* o = dst + (size_t)y * dst_stride;
-      if (cs == 1 || cs == 4) {
-        // ycc_rgb_convert; YCCK -> CMYK inverts the converted RGB
+      if (cs == 1 || cs == 4) ycc_rgb_row(r3[0], r3[1], r3[2], o, W, cs == 4);
+      else
         for (int x = 0; x < W; x++) {
-          const int Y = a[x], cb = b[x], cr = c[x];
-          const int r = Y + kColor.cr_r[cr];
-          const int g = Y + (int)((kColor.cb_g[cb] + kColor.cr_g[cr]) >> 16);
-          const int bl = Y + kColor.cb_b[cb];
-          if (cs == 1) {
-            o[3 * x] = clamp255(r);
-            o[3 * x + 1] = clamp255(g);
-            o[3 * x + 2] = clamp255(bl);
-          } else {
-            o[3 * x] = clamp255(255 - r);
-            o[3 * x + 1] = clamp255(255 - g);
-            o[3 * x + 2] = clamp255(255 - bl);
-          }
+          o[3 * x] = r3[0][x];
+          o[3 * x + 1] = r3[1][x];
+          o[3 * x + 2] = r3[2][x];
         }
-      } else {
-        for (int x = 0; x < W; x++) {
-          o[3 * x] = a[x];
-          o[3 * x + 1] = b[x];
-          o[3 * x + 2] = c[x];
-        }
-      }
     }
   }
 };
