@@ -400,6 +400,22 @@ def main():
     # barrier and host syncs between them add no device work).
     kernel_ms = e0.elapsed_ms(e1) / args.steps
 
+    # The same launches with descriptor caching off: every batch uploads its
+    # descriptor array (what a batch of fresh pointers costs); reported, not
+    # the headline.
+    fresh_ms = None
+    if args.steps > 0:
+        prev = capi.set_kernel_policy(args.policy | capi.MXD_POLICY_NO_DESC_CACHE)
+        k = max(10, args.steps // 2)
+        stream.synchronize()
+        e0.record(stream)
+        for i in range(k):
+            step(i)
+        e1.record(stream)
+        stream.synchronize()
+        fresh_ms = e0.elapsed_ms(e1) / k
+        capi.set_kernel_policy(prev)
+
     alg_bytes = sum(footprint_bytes(capi, sw, sh, C, *g[:6]) for (sw, sh), g in zip(sizes, geoms)) + sum(out_bytes)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     copy_gbs = capi.copy_bandwidth(1 << 30, dev, 20) if not args.no_copy else None
@@ -407,6 +423,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.workload),
                 "alg_bytes_per_launch": int(alg_bytes), "alg_bytes_per_image": round(alg_bytes / B, 1),
                 "kernel_ms_per_launch": round(kernel_ms, 5),
+                "ms_per_launch_fresh_descriptors": round(fresh_ms, 5) if fresh_ms else None,
                 "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
                 "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None}
 

@@ -118,8 +118,17 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
  * MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
  * of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
  * general workgroup-tile kernel; MXD_POLICY_NARROW: wave kernels keep the
- * narrow per-lane window (no wide RGB strips).  Returns the previous policy. */
-enum mxd_policy { MXD_POLICY_AUTO = 0, MXD_POLICY_NO_SCATTER = 1, MXD_POLICY_NO_WAVE = 2, MXD_POLICY_NARROW = 4 };
+ * narrow per-lane window (no wide RGB strips); MXD_POLICY_NO_DESC_CACHE:
+ * every batch uploads its descriptor array even when a cached slot holds the
+ * same bytes (measures the per-batch upload of fresh descriptors).  Returns
+ * the previous policy. */
+enum mxd_policy {
+  MXD_POLICY_AUTO = 0,
+  MXD_POLICY_NO_SCATTER = 1,
+  MXD_POLICY_NO_WAVE = 2,
+  MXD_POLICY_NARROW = 4,
+  MXD_POLICY_NO_DESC_CACHE = 8
+};
 int mxd_set_kernel_policy(int32_t policy);
 
 /* The kernel mxd_resize_crop_batch would run for one image on `device`

@@ -142,6 +142,10 @@ TableCache& host_tables() {
 // ---------------------------------------------------------------------------
 // Per-(device, stream) descriptor workspace: pinned staging + device copy of
 // the ImgDev array.  Re-uploads are skipped when the batch is unchanged.
+// Kernel policy (mxd_set_kernel_policy): a process-wide tuning / test switch
+// between kernels that compute identical results.
+std::atomic<int32_t> g_policy{0};
+
 struct Workspace {
   std::mutex mu;
   // Descriptor slots: each launch reads its descriptors from one slot's
@@ -155,8 +159,10 @@ struct Workspace {
     ImgDev* dev = nullptr;
     size_t cap = 0, count = 0;
     hipEvent_t copied = nullptr, used = nullptr;
+    uint64_t last_use = 0;
   } slot[kSlots];
   int cur = -1;
+  uint64_t clock = 0;
   hipStream_t copy = nullptr;
   // Fork/join helpers: the launches of a mixed batch (one per kernel shape)
   // run concurrently on these streams, so one launch's tail overlaps the
@@ -229,15 +235,28 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t n = descs.size();
   const size_t bytes = sizeof(ImgDev) * n;
-  if (ws->cur >= 0) {
-    Workspace::Slot& c = ws->slot[ws->cur];
-    if (c.count == n && std::memcmp(c.host, descs.data(), bytes) == 0) {  // same batch again
-      *dev_out = c.dev;
-      return MXD_OK;
+  // A batch whose descriptors a slot already holds (a loop over fixed device
+  // buffers) launches from that slot's device copy: no upload, no
+  // cross-stream wait once the copy has landed.  Slots are immutable while
+  // cached, so concurrent readers are safe.
+  if (!(g_policy.load() & MXD_POLICY_NO_DESC_CACHE))
+    for (int k = 0; k < Workspace::kSlots; k++) {
+      Workspace::Slot& c = ws->slot[k];
+      if (c.count == n && c.host && std::memcmp(c.host, descs.data(), bytes) == 0) {
+        ws->cur = k;
+        c.last_use = ++ws->clock;
+        if (hipEventQuery(c.copied) != hipSuccess) MXD_HIP(hipStreamWaitEvent(s, c.copied, 0));
+        *dev_out = c.dev;
+        return MXD_OK;
+      }
     }
-  }
   if (!ws->copy) MXD_HIP(hipStreamCreateWithFlags(&ws->copy, hipStreamNonBlocking));
-  ws->cur = (ws->cur + 1) % Workspace::kSlots;
+  // the least recently used slot takes the new batch
+  int victim = 0;
+  for (int k = 1; k < Workspace::kSlots; k++)
+    if (ws->slot[k].last_use < ws->slot[victim].last_use) victim = k;
+  ws->cur = victim;
+  ws->slot[victim].last_use = ++ws->clock;
   Workspace::Slot& c = ws->slot[ws->cur];
   if (!c.copied) {
     MXD_HIP(hipEventCreateWithFlags(&c.copied, hipEventDisableTiming));
@@ -281,9 +300,6 @@ struct ImgPlan {
   int32_t pp = 0;  // source pixels per lane
 };
 
-// Kernel policy (mxd_set_kernel_policy): a process-wide tuning / test switch
-// between kernels that compute identical results.
-std::atomic<int32_t> g_policy{0};
 
 // Shape of the scatter schedule for crop rows [off, off+len) of a vertical
 // table, valid for bands starting at any row: dmax = most source rows that are

@@ -38,6 +38,7 @@ MXD_POLICY_AUTO = 0
 MXD_POLICY_NO_SCATTER = 1
 MXD_POLICY_NO_WAVE = 2
 MXD_POLICY_NARROW = 4
+MXD_POLICY_NO_DESC_CACHE = 8
 
 
 class MxdImage(ctypes.Structure):

@@ -23,6 +23,8 @@ run bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu
 # the bench's own launches only (the e2e leg's chunked launches would mix into the average)
 run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --no-cpu --no-e2e
 cut -c1-220 gpurun_out/${TAG}_prof/run_kernel_stats.csv
+run prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c4 -o run -- python3 bench.py --workload c4 --no-cpu --no-e2e
+cut -c1-220 gpurun_out/${TAG}_prof_c4/run_kernel_stats.csv
 for w in c2 c3 c4 c5; do
   i=0
   for grp in FETCH_SIZE WRITE_SIZE "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU"; do
