@@ -12,7 +12,8 @@ Variants per worker count:
   fused      image_to_float before batch: the kernel writes the f32 batch
   device     fused + batch(..., device=0): the batch stays in HBM (DLPack)
   cpu        Pillow (libjpeg-turbo) decode -> oracle C stbir restatement ->
-             crop -> batch -> numpy /255 on a thread pool of the same size
+             crop per batch on a pool of that many worker processes, numpy
+             /255 of each batch in the consumer
 Datasets (synthetic stand-ins, seeded smooth noise, Pillow q=90 JPEGs):
   c1  300x200 / 200x300 (Caltech-101-like), batch 32
   c4  500x375 / 375x500 / 500x333 (ImageNet-like), batch 128
@@ -20,10 +21,10 @@ Prints one JSON line per (dataset, variant, workers)."""
 import argparse
 import ctypes
 import json
+import multiprocessing
 import os
 import sys
 import tempfile
-import threading
 import time
 
 import numpy as np
@@ -82,46 +83,44 @@ def run_surface(files, batch, workers, variant):
     return n, time.perf_counter() - t0
 
 
-def run_cpu(files, batch, workers):
-    """The reference's CPU path restated: libjpeg-turbo decode (Pillow), the
-    oracle's stbir restatement, crop, batch, /255 -- one batch per task."""
+def _cpu_batch(args):
+    """One batch of the reference chain on the CPU (a worker process):
+    libjpeg-turbo decode (Pillow), the oracle's stbir restatement + crop."""
+    files, = args
     from PIL import Image
     import oracle as O
 
     lib = O.lib()
     u8p = ctypes.POINTER(ctypes.c_uint8)
+    crops = np.empty((len(files), 224, 224, 3), np.uint8)
+    for k, f in enumerate(files):
+        img = np.ascontiguousarray(np.asarray(Image.open(f).convert("RGB")))
+        h, w = img.shape[:2]
+        rc = lib.orc_resize_smallest_side_center_crop(img.ctypes.data_as(u8p), w, h, 3, 256, 224, 224,
+                                                      crops[k].ctypes.data_as(u8p))
+        assert rc == 0
+    return crops
+
+
+def run_cpu(files, batch, workers):
+    """The reference's CPU path restated on `workers` processes (the reference
+    runs it on a C++ thread pool; processes keep Python's GIL out of the
+    measurement): decode + resize + crop per batch in a worker, the batch's
+    astype(float32) / 255 in the consumer like the reference's key_transform."""
+    from concurrent.futures import ProcessPoolExecutor
+
     order = np.random.default_rng(0).permutation(len(files))
-    nb = (len(files) + batch - 1) // batch
-    nxt = [0]
-    lock = threading.Lock()
-
-    def one_batch(b):
-        idx = order[b * batch:(b + 1) * batch]
-        crops = np.empty((len(idx), 224, 224, 3), np.uint8)
-        for k, i in enumerate(idx):
-            img = np.ascontiguousarray(np.asarray(Image.open(files[i]).convert("RGB")))
-            h, w = img.shape[:2]
-            rc = lib.orc_resize_smallest_side_center_crop(img.ctypes.data_as(u8p), w, h, 3, 256, 224, 224,
-                                                          crops[k].ctypes.data_as(u8p))
-            assert rc == 0
-        return crops.astype("float32") / 255
-
-    def worker():
-        while True:
-            with lock:
-                b = nxt[0]
-                nxt[0] += 1
-            if b >= nb:
-                return
-            one_batch(b)
-
-    t0 = time.perf_counter()
-    ts = [threading.Thread(target=worker) for _ in range(workers)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    return len(files), time.perf_counter() - t0
+    chunks = [[files[i] for i in order[b:b + batch]] for b in range(0, len(files), batch)]
+    # fork: main() runs every CPU leg before this process touches the GPU
+    with ProcessPoolExecutor(max_workers=workers, mp_context=multiprocessing.get_context("fork")) as ex:
+        list(ex.map(_cpu_batch, [(c[:2],) for c in chunks[:workers]]))  # warm the workers
+        t0 = time.perf_counter()
+        n = 0
+        for crops in ex.map(_cpu_batch, [(c,) for c in chunks]):
+            x = crops.astype("float32") / 255
+            n += len(x)
+        dt = time.perf_counter() - t0
+    return n, dt
 
 
 def main():
@@ -133,17 +132,20 @@ def main():
     ap.add_argument("--cpu-images", type=int, default=512, help="files the CPU restatement runs over")
     args = ap.parse_args()
     workers = [int(w) for w in args.workers.split(",")]
+    variants = args.variants.split(",")
+    # CPU legs first: their worker processes fork before any GPU call here
+    order = [v for v in variants if v == "cpu"] + [v for v in variants if v != "cpu"]
     with tempfile.TemporaryDirectory() as root:
-        for name in args.datasets.split(","):
-            files = make_files(root, name, args.images)
-            B = DATASETS[name]["batch"]
-            for v in args.variants.split(","):
+        files = {name: make_files(root, name, args.images) for name in args.datasets.split(",")}
+        for v in order:
+            for name, fl in files.items():
+                B = DATASETS[name]["batch"]
                 for w in workers:
                     if v == "cpu":
-                        n, dt = run_cpu(files[:args.cpu_images], B, w)
+                        n, dt = run_cpu(fl[:args.cpu_images], B, w)
                     else:
-                        run_surface(files[:2 * B], B, w, v)  # warm-up: decoder, tables, pinned buffers
-                        n, dt = run_surface(files, B, w, v)
+                        run_surface(fl[:2 * B], B, w, v)  # warm-up: decoder, tables, pinned buffers
+                        n, dt = run_surface(fl, B, w, v)
                     print(json.dumps(dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
                                           images_per_s=round(n / dt, 1), batch=B)), flush=True)
 
