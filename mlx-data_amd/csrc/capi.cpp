@@ -149,10 +149,11 @@ std::atomic<int32_t> g_policy{0};
 struct Workspace {
   std::mutex mu;
   // Descriptor slots: each launch reads its descriptors from one slot's
-  // device copy; a new batch takes the next slot, whose host staging is
-  // refilled once the launch that last used it has finished.  The upload runs
-  // on a copy stream while the previous launch computes, and the launch waits
-  // for it, so consecutive batches never serialize behind an H2D copy.
+  // device copy.  A batch whose descriptors a slot holds reuses it; a new one
+  // takes the least recently used slot once the launches that read it are
+  // done, and uploads on a copy stream while the previous launch computes.
+  // Launches wait for their slot's upload, so consecutive batches never
+  // serialize behind an H2D copy.
   static constexpr int kSlots = 4;
   struct Slot {
     ImgDev* host = nullptr;  // pinned
@@ -160,6 +161,7 @@ struct Workspace {
     size_t cap = 0, count = 0;
     hipEvent_t copied = nullptr, used = nullptr;
     uint64_t last_use = 0;
+    bool unrecorded_hits = false;  // launched from since `used` was last recorded
   } slot[kSlots];
   int cur = -1;
   uint64_t clock = 0;
@@ -228,7 +230,8 @@ int validate(const mxd_image& im, int32_t i) {
 // Uploads descs to the stream's workspace (skipped when unchanged) and returns
 // the device copy.
 int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream, ImgDev** dev_out,
-                 std::unique_lock<std::mutex>* hold, Workspace** ws_out = nullptr) {
+                 std::unique_lock<std::mutex>* hold, Workspace** ws_out = nullptr, bool* hit = nullptr) {
+  if (hit) *hit = false;
   Workspace* ws = workspaces().get(device, stream);
   if (ws_out) *ws_out = ws;
   *hold = std::unique_lock<std::mutex>(ws->mu);
@@ -246,7 +249,11 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
         ws->cur = k;
         c.last_use = ++ws->clock;
         if (hipEventQuery(c.copied) != hipSuccess) MXD_HIP(hipStreamWaitEvent(s, c.copied, 0));
+        // No per-launch event (it costs ~2.5 us between kernels): the slot's
+        // readers are fenced when it is next overwritten (below).
+        c.unrecorded_hits = true;
         *dev_out = c.dev;
+        if (hit) *hit = true;
         return MXD_OK;
       }
     }
@@ -262,7 +269,17 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
     MXD_HIP(hipEventCreateWithFlags(&c.copied, hipEventDisableTiming));
     MXD_HIP(hipEventCreateWithFlags(&c.used, hipEventDisableTiming));
   } else {
-    MXD_HIP(hipEventSynchronize(c.used));  // the launch that last read this slot is done
+    // Launched from by cache hits since `used` was recorded: fence them now
+    // (after every launch enqueued so far).  Only a working-set change evicts
+    // such a slot; a stream of fresh batches never has hits.
+    if (c.unrecorded_hits) {
+      MXD_HIP(hipEventRecord(c.used, s));
+      c.unrecorded_hits = false;
+    }
+    // Host-side wait: the launches that read this slot are done.  (Ordering
+    // the upload after them on the GPU instead, with a wait of the copy
+    // stream on the compute stream, measured ms-long stalls.)
+    MXD_HIP(hipEventSynchronize(c.used));
   }
   if (n > c.cap) {
     if (c.dev) MXD_HIP(hipFree(c.dev));
@@ -798,7 +815,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   ImgDev* dev = nullptr;
   std::unique_lock<std::mutex> hold;
   Workspace* ws = nullptr;
-  if (int rc = upload_descs(descs, device, stream, &dev, &hold, &ws)) return rc;
+  bool hit = false;
+  if (int rc = upload_descs(descs, device, stream, &dev, &hold, &ws, &hit)) return rc;
   // Several launches: fork them over the caller's stream and the workspace's
   // helper streams (largest first), join back before return, so one launch's
   // tail overlaps the next.
@@ -840,7 +858,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
     MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
   }
-  return release_descs(ws, stream);
+  return hit ? MXD_OK : release_descs(ws, stream);
 }
 
 // ---------------------------------------------------------------------------

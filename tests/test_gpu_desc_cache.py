@@ -1,0 +1,59 @@
+"""GPU: the descriptor-slot cache of mxd_resize_crop_batch (capi.cpp
+upload_descs).  Seven distinct batches (more than the four slots) launched
+back to back on one stream in an order that mixes cache hits, evictions of
+slots that were only ever hit, and fresh uploads, with no host sync in
+between; every batch writes its own output buffers, and each batch's images
+are crops of different windows, so a launch that read another batch's (or a
+half-overwritten) descriptor array would leave wrong bytes behind."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as O
+from gpu_util import synth
+from mlx_data_amd import capi
+
+pytestmark = pytest.mark.gpu
+
+
+def test_slot_reuse_under_back_to_back_launches():
+    imgs = [synth(300 + 20 * i, 400 + 30 * i, 3, 50 + i) for i in range(4)]
+    pitch = [(im.shape[1] * 3 + 15) // 16 * 16 for im in imgs]
+    src = [capi.DeviceBuffer(p * im.shape[0], 0) for p, im in zip(pitch, imgs)]
+    for b, p, im in zip(src, pitch, imgs):
+        host = np.zeros((im.shape[0], p), np.uint8)
+        host[:, :im.shape[1] * 3] = im.reshape(im.shape[0], -1)
+        b.upload(host)
+    batches = []  # (descriptor array, n, [(dst buffer, expected)])
+    for k in range(7):
+        entries, outs = [], []
+        for i, im in enumerate(imgs):
+            h, w = im.shape[:2]
+            rw, rh = O.smallest_side_dims(w, h, 96 + 8 * k)
+            cw, ch = 48, 40
+            cx, cy = (rw - cw) * (k + 1) // 8, (rh - ch) * (7 - k) // 8
+            flip = (k + i) % 2
+            d = capi.DeviceBuffer(cw * ch * 3, 0)
+            d.memset(0)
+            want = O.crop(O.resize(im, rw, rh), cx, cy, cw, ch)
+            outs.append((d, O.hflip(want) if flip else want))
+            entries.append(dict(src=src[i].ptr, src_stride=pitch[i], src_w=w, src_h=h, channels=3, resize_w=rw,
+                                resize_h=rh, crop_x=cx, crop_y=cy, crop_w=cw, crop_h=ch, flip=flip, dst=d.ptr,
+                                dst_stride=cw * 3))
+        arr, n = capi.make_images(entries)
+        batches.append((arr, n, outs))
+    capi.check(capi.lib().mxd_stream_synchronize(ctypes.c_void_p(None)))  # the memsets above
+    stream = capi.Stream(0)
+    order = [0, 1, 0, 2, 3, 0, 4, 1, 5, 6, 0, 5, 6, 2, 3, 4, 0, 1, 6] * 3
+    for k in order:
+        arr, n, _ = batches[k]
+        capi.resize_crop_batch(arr, n, capi.MXD_U8, 0, stream.handle)
+    stream.synchronize()
+    for arr, n, outs in batches:
+        for d, want in outs:
+            got = d.download(want.shape, np.uint8)
+            assert np.abs(got.astype(int) - want.astype(int)).max() <= 1
+            d.free()
+    for b in src:
+        b.free()
