@@ -259,7 +259,23 @@ def timed_steps(ranks, step, sync, steps):
     return ranks.max(t1 - t0), t1 - t0
 
 
-def bench_line(workload, world, batch, steps, warmup, wall, roofline, cpu, e2e):
+def manifest(capi, dev):
+    """Run manifest: device, ROCm, host cores, decoder."""
+    m = {"host_cores": host_cores(), "jpeg": "native (libjpeg-turbo ISLOW semantics, mxd_jpeg_decode)"}
+    try:
+        name, arch, cus = capi.device_properties(dev)
+        m.update(gpu=name, arch=arch, compute_units=cus)
+    except Exception:  # noqa: BLE001  (a manifest never fails the bench)
+        pass
+    try:
+        with open("/opt/rocm/.info/version") as f:
+            m["rocm"] = f.read().strip()
+    except OSError:
+        pass
+    return m
+
+
+def bench_line(workload, world, batch, steps, warmup, wall, roofline, cpu, e2e, man=None):
     w = WORKLOADS[workload]
     return {
         "metric": METRIC,
@@ -279,6 +295,7 @@ def bench_line(workload, world, batch, steps, warmup, wall, roofline, cpu, e2e):
         "roofline": roofline,
         "cpu_baseline": cpu,
         "e2e": e2e,
+        "manifest": man,
     }
 
 
@@ -440,7 +457,7 @@ def main():
         dst.free()
     if ranks.rank == 0:
         print(json.dumps(bench_line(args.workload, ranks.world, B, args.steps, args.warmup, wall, roofline, cpu,
-                                    e2e)), flush=True)
+                                    e2e, manifest(capi, dev))), flush=True)
     ranks.close()
 
 

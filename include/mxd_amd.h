@@ -88,6 +88,10 @@ typedef struct mxd_image {
 int mxd_abi_version(void);
 const char* mxd_last_error(void);
 int mxd_device_count(int* count);
+/* Run manifest (SURVEY.md §5 metrics): marketing name, gcnArchName and
+ * compute-unit count of `device`; strings are NUL-terminated, truncated to
+ * their buffer. */
+int mxd_device_properties(int32_t device, char* name, size_t name_len, char* arch, size_t arch_len, int32_t* cus);
 
 /* ---- reference geometry (host only, no device needed) ------------------ */
 

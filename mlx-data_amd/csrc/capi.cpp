@@ -1141,6 +1141,21 @@ int mxd_abi_version(void) { return MXD_ABI_VERSION; }
 const char* mxd_last_error(void) { return g_error.c_str(); }
 
 
+int mxd_device_properties(int32_t device, char* name, size_t name_len, char* arch, size_t arch_len, int32_t* cus) {
+  if (int rc = check_device(device)) return rc;
+  hipDeviceProp_t p{};
+  MXD_HIP(hipGetDeviceProperties(&p, device));
+  auto put = [](char* dst, size_t n, const char* src) {
+    if (!dst || n == 0) return;
+    std::strncpy(dst, src, n - 1);
+    dst[n - 1] = 0;
+  };
+  put(name, name_len, p.name);
+  put(arch, arch_len, p.gcnArchName);
+  if (cus) *cus = p.multiProcessorCount;
+  return MXD_OK;
+}
+
 int mxd_device_count(int* count) {
   if (!count) return fail(MXD_ERR_INVALID, "mxd: null count");
   MXD_HIP(hipGetDeviceCount(count));

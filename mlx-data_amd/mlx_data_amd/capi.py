@@ -18,7 +18,7 @@ MXD_F32_DIV255 = 1
 
 # Every symbol include/mxd_amd.h declares.
 EXPORTS = (
-    "mxd_abi_version", "mxd_last_error", "mxd_device_count",
+    "mxd_abi_version", "mxd_last_error", "mxd_device_count", "mxd_device_properties",
     "mxd_resize_smallest_side_dims", "mxd_center_crop_origin", "mxd_axis_taps",
     "mxd_resize_crop_batch", "mxd_set_kernel_policy", "mxd_describe_plan", "mxd_copy_bandwidth",
     "mxd_set_device", "mxd_malloc_device", "mxd_free_device", "mxd_malloc_pinned", "mxd_free_pinned",
@@ -108,6 +108,13 @@ def check(rc):
     if rc != MXD_OK:
         raise MxdError(rc, lib().mxd_last_error().decode())
     return rc
+
+
+def device_properties(device=0):
+    """(name, gcnArchName, compute units) of a device."""
+    name, arch, cus = ctypes.create_string_buffer(256), ctypes.create_string_buffer(64), ctypes.c_int32()
+    check(lib().mxd_device_properties(device, name, ctypes.c_size_t(256), arch, ctypes.c_size_t(64), ctypes.byref(cus)))
+    return name.value.decode(), arch.value.decode(), cus.value
 
 
 def resize_smallest_side_dims(w, h, size):

@@ -284,3 +284,32 @@ def test_random_area_crop_errors():
     for (a, r, n), msg in cases:
         with pytest.raises(RuntimeError, match=msg):
             b.image_random_area_crop("image", a, r, num_trial=n)
+
+
+def test_worker_errors_reach_the_consumer():
+    """SURVEY.md §5 failure handling: an exception raised inside a prefetch
+    worker (stream/Prefetch.cpp:48 future::get) surfaces at the consumer's
+    next(), with its message; ordered_prefetch likewise; the pipeline can be
+    dropped afterwards without hanging (Prefetch::~Prefetch drains)."""
+    def boom(x):
+        if int(x[0]) == 5:
+            raise ValueError("bad sample 5")
+        return x
+
+    samples = [dict(i=np.array([k], np.int64)) for k in range(12)]
+    s = dx.buffer_from_vector(samples).to_stream().key_transform("i", boom).prefetch(4, 4)
+    with pytest.raises(ValueError, match="bad sample 5"):
+        for _ in s:
+            pass
+    del s
+    o = dx.buffer_from_vector(samples).key_transform("i", boom).ordered_prefetch(3, 3)
+    seen = []
+    with pytest.raises(ValueError, match="bad sample 5"):
+        for x in o:
+            seen.append(int(x["i"][0]))
+    assert seen == [0, 1, 2, 3, 4]
+    del o
+    # a missing file through load_image: the reference's message, via a worker
+    m = dx.buffer_from_vector([dict(f=b"/nonexistent/x.jpg")]).to_stream().load_image("f").prefetch(2, 2)
+    with pytest.raises(RuntimeError, match="could not load"):
+        next(iter(m))
