@@ -1378,6 +1378,17 @@ namespace {
 // The host path: host sources (footprints staged through pinned memory),
 // results to host (dst_device false: D2H + copy-out) or straight into device
 // destinations (dst_device true).
+// Page-locked host memory of this HIP runtime (hipHostMalloc'd or
+// registered): the DMA engines can read / write it in place.
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not an error here
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
@@ -1396,6 +1407,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   struct Stage {
     int32_t x0, y0, rows;
     int64_t pitch, copy, in_off, out_off, out_row;
+    bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
   };
   std::vector<Stage> st(n);
   for (int32_t i = 0; i < n; i++) {
@@ -1415,6 +1427,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     s.copy = std::min<int64_t>((int64_t)(im.src_w - s.x0) * c, want);
     s.pitch = (want + 15) & ~(int64_t)15;
     s.out_row = (int64_t)im.crop_w * c * elem;
+    s.src_pinned = host_pinned(im.src);
+    s.dst_pinned = !dst_device && host_pinned(im.dst);
+    if (!dst_device && im.dst_stride < s.out_row)
+      return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
   }
   // Chunks of about kChunk staged bytes (at least one image each).
   constexpr int64_t kChunk = 24 << 20;
@@ -1442,6 +1458,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     int64_t bytes = 0;
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++) bytes += st[i].out_row * images[i].crop_h;
     parallel_items(chunks[k].first, chunks[k].second, bytes, [&](int32_t i) {
+      if (st[i].dst_pinned) return;  // DMA'd straight into place
       const mxd_image& im = images[i];
       uint8_t* d = static_cast<uint8_t*>(im.dst);
       const uint8_t* src = sl.pin_out + st[i].out_off;
@@ -1458,13 +1475,26 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     Slot& sl = ctx.slot[k & 1];
     if (pending[k & 1] >= 0)
       if (int rc = copy_out(pending[k & 1])) return rc;
+    // Staged images first (one H2D / D2H each way covers them), directly
+    // DMA'd ones after them.
     int64_t in_bytes = 0, out_bytes = 0;
-    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
-      st[i].in_off = in_bytes;
-      in_bytes += (st[i].pitch * st[i].rows + 255) & ~(int64_t)255;
-      st[i].out_off = out_bytes;
-      out_bytes += (st[i].out_row * images[i].crop_h + 255) & ~(int64_t)255;
-    }
+    for (int pass = 0; pass < 2; pass++)
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+        if (st[i].src_pinned == (pass == 1)) {
+          st[i].in_off = in_bytes;
+          in_bytes += (st[i].pitch * st[i].rows + 255) & ~(int64_t)255;
+        }
+    int64_t in_staged = 0, out_staged = 0;
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+      if (!st[i].src_pinned) in_staged = std::max(in_staged, st[i].in_off + st[i].pitch * st[i].rows);
+    for (int pass = 0; pass < 2; pass++)
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+        if (st[i].dst_pinned == (pass == 1)) {
+          st[i].out_off = out_bytes;
+          out_bytes += (st[i].out_row * images[i].crop_h + 255) & ~(int64_t)255;
+        }
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+      if (!st[i].dst_pinned) out_staged = std::max(out_staged, st[i].out_off + st[i].out_row * images[i].crop_h);
     if (int rc = grow_pinned(&sl.pin_in, &sl.pin_in_cap, in_bytes)) return rc;
     if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, in_bytes)) return rc;
     if (!dst_device) {
@@ -1474,9 +1504,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const int32_t cn = chunks[k].second - chunks[k].first;
     std::vector<mxd_image> dev_imgs(images + chunks[k].first, images + chunks[k].second);
     std::vector<Stored> where(cn);
-    parallel_items(chunks[k].first, chunks[k].second, in_bytes, [&](int32_t i) {
+    parallel_items(chunks[k].first, chunks[k].second, in_staged, [&](int32_t i) {
       const mxd_image& im = images[i];
       const Stage& s = st[i];
+      if (s.src_pinned) return;
       uint8_t* stage = sl.pin_in + s.in_off;
       const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
       for (int32_t r = 0; r < s.rows; r++) std::memcpy(stage + r * s.pitch, from + (int64_t)r * im.src_stride, s.copy);
@@ -1493,9 +1524,26 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         dev_imgs[j].dst_stride = s.out_row;
       }
     }
-    MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_bytes, hipMemcpyHostToDevice, sl.stream));
+    if (in_staged > 0) MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+      const Stage& s = st[i];
+      if (!s.src_pinned) continue;
+      const mxd_image& im = images[i];
+      const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
+      MXD_HIP(hipMemcpy2DAsync(sl.dev_in + s.in_off, s.pitch, from, im.src_stride, s.copy, s.rows,
+                               hipMemcpyHostToDevice, sl.stream));
+    }
     if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
-    if (!dst_device) MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_bytes, hipMemcpyDeviceToHost, sl.stream));
+    if (!dst_device) {
+      if (out_staged > 0)
+        MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_staged, hipMemcpyDeviceToHost, sl.stream));
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+        const Stage& s = st[i];
+        if (!s.dst_pinned) continue;
+        MXD_HIP(hipMemcpy2DAsync(images[i].dst, images[i].dst_stride, sl.dev_out + s.out_off, s.out_row, s.out_row,
+                                 images[i].crop_h, hipMemcpyDeviceToHost, sl.stream));
+      }
+    }
     MXD_HIP(hipEventRecord(sl.done, sl.stream));
     pending[k & 1] = k;
     // results of the previous chunk, while this one runs

@@ -1,0 +1,77 @@
+"""GPU: the host path (mxd_resize_crop_host) with page-locked memory.  Sources
+and destinations that are page-locked are DMA'd in place (2-D copies of the
+footprint rows / output rows) instead of being staged; a batch may mix both
+kinds.  Results must equal the all-pageable call byte for byte."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from gpu_util import synth
+from mlx_data_amd import capi
+
+pytestmark = pytest.mark.gpu
+
+
+class Pinned:
+    def __init__(self, nbytes):
+        self.p = ctypes.c_void_p()
+        capi.check(capi.lib().mxd_malloc_pinned(ctypes.byref(self.p), ctypes.c_size_t(nbytes)))
+        self.a = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.p.value))
+
+    def free(self):
+        capi.check(capi.lib().mxd_free_pinned(self.p))
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_pinned_and_pageable_mix(f32):
+    elem = 4 if f32 else 1
+    imgs = [synth(960, 1280, 3, 1), synth(375, 500, 3, 2), synth(200, 300, 3, 3), synth(333, 500, 3, 4),
+            synth(61, 47, 3, 5)]
+    geoms = []
+    for im in imgs:
+        h, w = im.shape[:2]
+        rw, rh = capi.resize_smallest_side_dims(w, h, 64)
+        cw, ch = min(rw, 56), min(rh, 56)
+        geoms.append((rw, rh, (rw - cw) // 2, (rh - ch) // 2, cw, ch, 0))
+    pins = []
+
+    def run(pin_src, pin_dst):
+        entries, outs = [], []
+        for k, (im, g) in enumerate(zip(imgs, geoms)):
+            h, w, c = im.shape
+            pitch = w * c + (7 if k % 2 else 0)  # odd pitches too
+            if pin_src[k]:
+                ps = Pinned(pitch * h)
+                pins.append(ps)
+                src = ps.a.reshape(h, pitch)
+                src_ptr = ps.p.value
+            else:
+                src = np.zeros((h, pitch), np.uint8)
+                src_ptr = src.ctypes.data
+            src[:, :w * c] = im.reshape(h, -1)
+            row = g[4] * c * elem + (16 if k == 2 else 0)
+            if pin_dst[k]:
+                pd = Pinned(row * g[5])
+                pins.append(pd)
+                dst, dst_ptr = pd.a.reshape(g[5], row), pd.p.value
+            else:
+                dst = np.zeros((g[5], row), np.uint8)
+                dst_ptr = dst.ctypes.data
+            outs.append((dst, src))
+            entries.append(dict(src=src_ptr, src_stride=pitch, src_w=w, src_h=h, channels=c, resize_w=g[0],
+                                resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6],
+                                dst=dst_ptr, dst_stride=row))
+        arr, n = capi.make_images(entries)
+        capi.resize_crop_host(arr, n, capi.MXD_F32_DIV255 if f32 else capi.MXD_U8, 0)
+        return [d[:, :g[4] * im.shape[2] * elem].copy() for (d, _), g, im in zip(outs, geoms, imgs)]
+
+    try:
+        want = run([0] * 5, [0] * 5)
+        for ps, pd in [([1] * 5, [1] * 5), ([1, 0, 1, 0, 1], [0, 1, 1, 0, 0]), ([0] * 5, [1] * 5)]:
+            got = run(ps, pd)
+            for a, b in zip(got, want):
+                assert np.array_equal(a, b)
+    finally:
+        for p in pins:
+            p.free()
