@@ -5,6 +5,7 @@
 // per-stream descriptor workspace, and the launch.  No exceptions cross the
 // ABI: every entry point returns a status and leaves a thread-local message.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <numeric>
@@ -1044,7 +1045,12 @@ std::atomic<int> g_host_calls{0};
 template <class F>
 void parallel_items(int32_t first, int32_t end, int64_t bytes, F&& f) {
   const int32_t n = end - first;
-  const int hw = std::max(1u, std::thread::hardware_concurrency());
+  static const int hw = [] {  // the cores this process may run on (a container's share, not the machine)
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) return std::max(1, CPU_COUNT(&set));
+    return std::max(1, (int)std::thread::hardware_concurrency());
+  }();
   int t = std::min<int64_t>({8, hw / std::max(1, g_host_calls.load()), n, bytes >> 20});
   if (t <= 1) {
     for (int32_t i = first; i < end; i++) f(i);

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <numeric>
 #include <stdexcept>
 
@@ -47,6 +48,65 @@ std::shared_ptr<void> alloc_bytes(int64_t n) {
   void* p = nullptr;
   if (posix_memalign(&p, 64, std::max<int64_t>(n, 1)) != 0) throw std::bad_alloc();
   return std::shared_ptr<void>(p, std::free);
+}
+
+// Image batch tensors (tens of MB each) come from a pool of page-locked
+// blocks: the host path DMAs results straight into them (no staging copy-out)
+// and a recycled block costs no page faults, where a fresh allocation of that
+// size is first-touched page by page.  Blocks are recycled by size (the batch
+// shape of a pipeline repeats); at most kMaxCached bytes wait unused.  Without
+// a device (CPU-only runs) the pool turns itself off.
+class BatchPool {
+ public:
+  std::shared_ptr<void> get(int64_t n) {
+    const size_t cap = ((size_t)n + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+    void* p = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (off_) return nullptr;
+      auto it = free_.find(cap);
+      if (it != free_.end() && !it->second.empty()) {
+        p = it->second.back();
+        it->second.pop_back();
+        cached_ -= cap;
+      }
+    }
+    if (!p && mxd_malloc_pinned(&p, cap) != MXD_OK) {
+      std::lock_guard<std::mutex> lk(mu_);
+      off_ = true;
+      return nullptr;
+    }
+    return std::shared_ptr<void>(p, [this, cap](void* q) { put(q, cap); });
+  }
+
+ private:
+  static constexpr size_t kMaxCached = (size_t)2 << 30;
+  void put(void* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (cached_ + cap <= kMaxCached) {
+        free_[cap].push_back(p);
+        cached_ += cap;
+        return;
+      }
+    }
+    (void)mxd_free_pinned(p);
+  }
+  std::mutex mu_;
+  std::map<size_t, std::vector<void*>> free_;
+  size_t cached_ = 0;
+  bool off_ = false;
+};
+
+BatchPool& batch_pool() {
+  static BatchPool* p = new BatchPool();  // never destroyed: outlives every Array
+  return *p;
+}
+
+std::shared_ptr<void> alloc_batch_bytes(int64_t n) {
+  if (n >= (4 << 20) && !devices().empty())
+    if (auto p = batch_pool().get(n)) return p;
+  return alloc_bytes(n);
 }
 
 void check(int rc) {
@@ -781,7 +841,10 @@ std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& a
       if (a->shape()[d] != (has_dim ? bshape[d] : bshape[d + 1]) && !(has_dim && d == dim)) ragged = true;
   const int64_t isz = itemsize(type);
   if (device >= 0) return device_batch(arrs, bshape, stride, item, ragged, pad_value, dim, has_dim, device);
-  auto res = std::make_shared<Array>(type, bshape, alloc_bytes(shape_size(bshape) * isz));
+  bool images = false;
+  for (const auto& a : arrs) images = images || a->pending();
+  const int64_t total = shape_size(bshape) * isz;
+  auto res = std::make_shared<Array>(type, bshape, images ? alloc_batch_bytes(total) : alloc_bytes(total));
   if (ragged) fill(*res, pad_value);
 
   auto* base = static_cast<uint8_t*>(res->data());

@@ -251,8 +251,27 @@ Sample to_sample(py::handle obj) {
 // A Python callable that may be destroyed from a worker thread.
 std::shared_ptr<py::function> hold(py::function f) {
   return std::shared_ptr<py::function>(new py::function(std::move(f)), [](py::function* p) {
+    if (_Py_IsFinalizing()) return;  // the interpreter is going: taking the GIL would block forever
     py::gil_scoped_acquire gil;
     delete p;
+  });
+}
+
+// A prefetching stream or buffer whose last Python reference goes away joins
+// its worker threads, and those may be waiting for the GIL (a Python
+// key_transform, the image decoder): destroy it with the GIL released.  At
+// interpreter exit the workers can no longer take the GIL at all, so the
+// object is left to the process teardown.
+template <class T>
+std::shared_ptr<T> nogil_owned(T* obj) {
+  return std::shared_ptr<T>(obj, [](T* o) {
+    if (_Py_IsFinalizing()) return;
+    if (PyGILState_Check()) {
+      py::gil_scoped_release nogil;
+      delete o;
+    } else {
+      delete o;
+    }
   });
 }
 
@@ -430,7 +449,7 @@ PYBIND11_MODULE(_pipeline, m) {
       .def(
           "ordered_prefetch",
           [](const std::shared_ptr<Buffer>& b, int prefetch_size, int num_threads) -> std::shared_ptr<Stream> {
-            return std::make_shared<OrderedPrefetch>(b, prefetch_size, num_threads);
+            return nogil_owned<Stream>(new OrderedPrefetch(b, prefetch_size, num_threads));
           },
           py::arg("prefetch_size"), py::arg("num_threads"));
 
@@ -461,7 +480,7 @@ PYBIND11_MODULE(_pipeline, m) {
       .def(
           "prefetch",
           [](const std::shared_ptr<Stream>& s, int prefetch_size, int num_threads) -> std::shared_ptr<Stream> {
-            return std::make_shared<Prefetch>(s, prefetch_size, num_threads);
+            return nogil_owned<Stream>(new Prefetch(s, prefetch_size, num_threads));
           },
           py::arg("prefetch_size"), py::arg("num_threads"));
 

@@ -313,3 +313,32 @@ def test_worker_errors_reach_the_consumer():
     m = dx.buffer_from_vector([dict(f=b"/nonexistent/x.jpg")]).to_stream().load_image("f").prefetch(2, 2)
     with pytest.raises(RuntimeError, match="could not load"):
         next(iter(m))
+
+
+def test_dropping_a_busy_prefetch_does_not_deadlock():
+    """Prefetch::~Prefetch joins its workers (stream/Prefetch.cpp:21-27); when
+    they run a Python key_transform they need the GIL, so the last reference
+    must be dropped with the GIL released (module.cpp nogil_owned)."""
+    import gc
+    import threading
+    import time
+
+    def slow(x):
+        time.sleep(0.01)
+        return x
+
+    samples = [dict(i=np.array([k], np.int64)) for k in range(64)]
+    s = dx.buffer_from_vector(samples).to_stream().key_transform("i", slow).prefetch(8, 4)
+    assert int(next(iter(s))["i"][0]) == 0  # workers now busy in `slow`
+    done = threading.Event()
+
+    def drop():
+        nonlocal s
+        del s
+        gc.collect()
+        done.set()
+
+    t = threading.Thread(target=drop)
+    t.start()
+    t.join(timeout=20)
+    assert done.is_set()

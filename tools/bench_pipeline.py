@@ -144,7 +144,9 @@ def main():
                     if v == "cpu":
                         n, dt = run_cpu(fl[:args.cpu_images], B, w)
                     else:
-                        run_surface(fl[:2 * B], B, w, v)  # warm-up: decoder, tables, pinned buffers
+                        # warm-up with every worker busy twice over: tap tables, host-path
+                        # contexts and the recycled batch buffers reach their steady state
+                        run_surface(fl[:min(len(fl), 2 * B * w)], B, w, v)
                         n, dt = run_surface(fl, B, w, v)
                     print(json.dumps(dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
                                           images_per_s=round(n / dt, 1), batch=B)), flush=True)
