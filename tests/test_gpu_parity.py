@@ -151,3 +151,51 @@ def test_full_size_c2_batch_properties():
         assert np.array_equal(f.view(np.uint32), LUT[a].view(np.uint32))
     for i in (0, 77, 255):
         check(u8[i], oracle_out(imgs[i], geoms[i]))
+
+
+def test_full_size_c3_mixed_batch_properties():
+    """BASELINE config 3 at full size: 512 images of six resolutions (480p-4K,
+    seed 1 like bench.py) -> 256 -> center 224 u8 in one call: one launch per
+    kernel shape.  Checks: determinism, per-size constant images exact, and
+    one image of every size against the oracle."""
+    sizes = [(640, 480), (1280, 720), (1280, 960), (1920, 1080), (2560, 1440), (3840, 2160)]
+    pick = np.random.default_rng(1).integers(0, len(sizes), 512)
+    base = {s: synth(s[1], s[0], 3, 10 + k) for k, s in enumerate(sizes)}
+    imgs = [base[sizes[k]] for k in pick]
+    # every 16th image is a constant frame of its size
+    for j in range(0, 512, 16):
+        w, h = sizes[pick[j]]
+        imgs[j] = np.full((h, w, 3), 37 + j % 200, np.uint8)
+    geoms = [center_geom(im) for im in imgs]
+    a = run_device(imgs, geoms)
+    b = run_device(imgs, geoms)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    for j in range(0, 512, 16):
+        assert (a[j] == imgs[j][0, 0, 0]).all()
+    done = set()
+    for j, k in enumerate(pick):
+        if k not in done and j % 16:
+            check(a[j], oracle_out(imgs[j], geoms[j]))
+            done.add(k)
+    assert len(done) == len(sizes)
+
+
+def test_full_size_c5_random_crop_flip_batch():
+    """BASELINE config 5 at full size: 128 x 3840x2160 -> 512 -> random 448 +
+    mirror (the bench's draws), u8, one launch; every 32nd frame against the
+    oracle, all frames deterministic."""
+    rng = np.random.default_rng(3)
+    frame = synth(2160, 3840, 3, 5)
+    imgs = [frame] * 128
+    rw, rh = O.smallest_side_dims(3840, 2160, 512)
+    geoms = [(rw, rh, int(rng.integers(0, rw - 448 + 1)), int(rng.integers(0, rh - 448 + 1)), 448, 448,
+              int(rng.random() <= 0.5)) for _ in range(128)]
+    a = run_device(imgs, geoms)
+    b = run_device(imgs, geoms)
+    full = O.resize(frame, rw, rh)
+    for j, (x, y, g) in enumerate(zip(a, b, geoms)):
+        assert np.array_equal(x, y)
+        if j % 32 == 0:
+            want = full[g[3]:g[3] + 448, g[2]:g[2] + 448]
+            check(x, want[:, ::-1] if g[6] else want)
