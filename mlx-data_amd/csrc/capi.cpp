@@ -1497,7 +1497,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
         if (st[i].dst_pinned == (pass == 1)) {
           st[i].out_off = out_bytes;
-          out_bytes += (st[i].out_row * images[i].crop_h + 255) & ~(int64_t)255;
+          // page-locked destinations back to back (one copy per contiguous run)
+          const int64_t b = st[i].out_row * images[i].crop_h;
+          out_bytes += pass == 1 && (st[i].out_row & 3) == 0 ? b : (b + 255) & ~(int64_t)255;
         }
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
       if (!st[i].dst_pinned) out_staged = std::max(out_staged, st[i].out_off + st[i].out_row * images[i].crop_h);
@@ -1543,11 +1545,32 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (!dst_device) {
       if (out_staged > 0)
         MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_staged, hipMemcpyDeviceToHost, sl.stream));
-      for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+      // Page-locked destinations: straight from the device.  Images packed
+      // back to back both here and in the destination (a batch tensor) go as
+      // one copy; strided ones as 2-D copies.
+      for (int32_t i = chunks[k].first; i < chunks[k].second;) {
         const Stage& s = st[i];
-        if (!s.dst_pinned) continue;
-        MXD_HIP(hipMemcpy2DAsync(images[i].dst, images[i].dst_stride, sl.dev_out + s.out_off, s.out_row, s.out_row,
-                                 images[i].crop_h, hipMemcpyDeviceToHost, sl.stream));
+        if (!s.dst_pinned) {
+          i++;
+          continue;
+        }
+        const int64_t bytes_i = s.out_row * images[i].crop_h;
+        if (images[i].dst_stride != s.out_row) {
+          MXD_HIP(hipMemcpy2DAsync(images[i].dst, images[i].dst_stride, sl.dev_out + s.out_off, s.out_row, s.out_row,
+                                   images[i].crop_h, hipMemcpyDeviceToHost, sl.stream));
+          i++;
+          continue;
+        }
+        int32_t j = i + 1;
+        int64_t run = bytes_i;
+        while (j < chunks[k].second && st[j].dst_pinned && images[j].dst_stride == st[j].out_row &&
+               static_cast<uint8_t*>(images[j].dst) == static_cast<uint8_t*>(images[i].dst) + run &&
+               st[j].out_off == s.out_off + run) {
+          run += st[j].out_row * images[j].crop_h;
+          j++;
+        }
+        MXD_HIP(hipMemcpyAsync(images[i].dst, sl.dev_out + s.out_off, run, hipMemcpyDeviceToHost, sl.stream));
+        i = j;
       }
     }
     MXD_HIP(hipEventRecord(sl.done, sl.stream));

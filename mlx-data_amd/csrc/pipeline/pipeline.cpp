@@ -81,16 +81,29 @@ class BatchPool {
 
  private:
   static constexpr size_t kMaxCached = (size_t)2 << 30;
+  // Returns a block; over the cap, blocks of OTHER sizes are freed first (a
+  // pipeline whose batch shape changed keeps its new shape's blocks).
   void put(void* p, size_t cap) {
+    std::vector<void*> drop;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (cached_ + cap <= kMaxCached) {
-        free_[cap].push_back(p);
-        cached_ += cap;
-        return;
+      free_[cap].push_back(p);
+      cached_ += cap;
+      for (auto it = free_.begin(); cached_ > kMaxCached && it != free_.end(); ++it) {
+        if (it->first == cap) continue;
+        while (cached_ > kMaxCached && !it->second.empty()) {
+          drop.push_back(it->second.back());
+          it->second.pop_back();
+          cached_ -= it->first;
+        }
+      }
+      if (cached_ > kMaxCached) {
+        drop.push_back(free_[cap].back());
+        free_[cap].pop_back();
+        cached_ -= cap;
       }
     }
-    (void)mxd_free_pinned(p);
+    for (void* q : drop) (void)mxd_free_pinned(q);
   }
   std::mutex mu_;
   std::map<size_t, std::vector<void*>> free_;
