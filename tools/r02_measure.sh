@@ -33,6 +33,8 @@ for w in c2 c3 c4 c5; do
   done
 done
 python3 tools/make_traffic.py $TAG r02/$TAG > /dev/null
+# N>1 rehearsal on this one GPU: two ranks through torch.distributed.run, both on device 0
+run dist2 240 env MXD_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu
 if [ "${2:-}" != "skip-pipeline" ]; then
   run pipeline 900 python tools/bench_pipeline.py --images 4096 --cpu-images 2048
 fi
