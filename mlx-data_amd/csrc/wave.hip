@@ -54,7 +54,11 @@
 namespace mxd {
 namespace {
 
-constexpr int kWaves = 4;
+// Waves per workgroup (tuning builds: -DMXD_WAVES=<1|2|4|8>).
+#ifndef MXD_WAVES
+#define MXD_WAVES 4
+#endif
+constexpr int kWaves = MXD_WAVES;
 constexpr int kLanes = 64;
 
 // Timing-only ablations, compiled in only when the library is built with

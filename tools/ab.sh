@@ -11,7 +11,7 @@ restore() { cp gpurun_out/.product.so mlx-data_amd/libmxd_amd.so; }
 for pass in 1 2; do
   for w in $WLS; do
     for v in $VARS; do
-      if [ $v = 0 ]; then restore; else cp tools/abl/libmxd_amd_$v.so mlx-data_amd/libmxd_amd.so; fi
+      if [ $v = 0 ]; then restore; else cp ${ABL_DIR:-tools/abl}/libmxd_amd_$v.so mlx-data_amd/libmxd_amd.so || exit 1; fi
       timeout -k 10 120 python bench.py --workload $w --no-cpu --no-e2e --no-copy ${BENCH_ARGS:-} > gpurun_out/${TAG}_${w}_${v}_$pass.log 2>&1 || { restore; exit 1; }
       echo "$pass $w $v $(grep -o '"kernel_ms_per_launch": [0-9.]*' gpurun_out/${TAG}_${w}_${v}_$pass.log)"
     done

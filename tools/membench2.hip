@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void c2_kmix(const uint8_t* __restrict__ base,
       if constexpr (LB == 12) ring[d] = __builtin_amdgcn_raw_buffer_load_b96(r, voff, min(row + d + DEPTH, r1 - 1) * kStride, 0);
       else ring[d] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, min(row + d + DEPTH, r1 - 1) * kStride, 0);
       const int want = (int)((row + d - r0) / 3.768f) + oy0;
-      if (write && want > oy && oy < oy1) {
+      if (write == 1 && want > oy && oy < oy1) {
         char* orow = o + (size_t)oy * kOutRow;
         for (int b = lane; b * SB < ob; b += 64) {
           if constexpr (SB == 12) *reinterpret_cast<f32x3*>(orow + 12 * b) = f32x3{acc[0], acc[1], acc[2]};
@@ -203,6 +203,16 @@ __global__ __launch_bounds__(256) void c2_kmix(const uint8_t* __restrict__ base,
       }
     }
   }
+  // write == 2: the band's stores deferred until all its reads are done (a
+  // single-round launch then reads chip-wide first and writes after)
+  if (write == 2)
+    for (oy = oy0; oy < oy1; oy++) {
+      char* orow = o + (size_t)oy * kOutRow;
+      for (int b = lane; b * SB < ob; b += 64) {
+        if constexpr (SB == 12) *reinterpret_cast<f32x3*>(orow + 12 * b) = f32x3{acc[0], acc[1], acc[2]};
+        else *reinterpret_cast<f4*>(orow + 16 * b) = f4{acc[0], acc[1], acc[2], acc[3]};
+      }
+    }
   if (acc[0] == -1.0f) out[lane] = acc[1];
 }
 
@@ -391,7 +401,9 @@ int main(int argc, char** argv) {
       {"4x8 bands", 12, 12, 8, 4, 768, 633, 672, 4},
       {"4x2 bands", 12, 12, 2, 4, 768, 633, 672, 4},
     };
+    const bool defer_only = argv[1][1] == 'd';
     for (int k : {1, 4, 8, 16}) {
+      if (defer_only) break;
       for (int nb : {4, 8}) {
         snprintf(name, sizeof name, "wg burst K=%d nb=%d (4 strips, full-row writes)", k, nb);
         auto go = [&] {
@@ -407,7 +419,8 @@ int main(int argc, char** argv) {
     }
     for (const V& v : vs) {
       if (v.wb > 1024) continue;
-      for (int write : {0, 1}) {
+      for (int write : {0, 1, 2}) {
+        if (defer_only && write == 0) continue;
         const int units = kImgs * v.nb * v.ns;
         snprintf(name, sizeof name, "%s w=%d", v.n, write);
         auto go = [&] {
@@ -418,7 +431,7 @@ int main(int argc, char** argv) {
           else if (v.lb == 12 && v.sb == 16) c2_kmix<12, 16, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
           else c2_kmix<16, 16, 8><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, v.wb, v.step, v.ob, v.halo, write);
         };
-        timeit(name, rd + write * wr, go);
+        timeit(name, rd + (write ? wr : 0), go);
       }
     }
     return 0;
