@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MXD_ABI_VERSION 2
+#define MXD_ABI_VERSION 3
 
 enum mxd_status {
   MXD_OK = 0,
@@ -215,6 +215,54 @@ int mxd_jpeg_info(const uint8_t* data, size_t size, int32_t* width, int32_t* hei
  * or unsupported data. */
 int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, int32_t width,
                     int32_t height);
+
+/* ---- split JPEG decode with the device-side finish (SURVEY.md §8f f1,
+ * "later a device-side decode") ---------------------------------------------
+ *
+ * The same decode in two halves: mxd_jpeg_coefs_decode runs the host part
+ * (markers + Huffman entropy decode, every error mxd_jpeg_decode reports)
+ * and keeps the quantised DCT coefficients; dequantisation + ISLOW IDCT,
+ * chroma upsampling and colour conversion run later -- on the host
+ * (mxd_jpeg_coefs_finish) or on the GPU inside mxd_jpeg_resize_crop_host /
+ * _to_device, which decode, resize, crop and mirror a whole batch in one call
+ * (what load_image -> image_resize_smallest_side -> image_center_crop ->
+ * batch do per sample: ImageJPEG.cpp:99-146 + the resize/crop rows above).
+ * Every route gives the bytes mxd_jpeg_decode (then mxd_resize_crop_*) gives. */
+typedef struct mxd_jpeg_coefs mxd_jpeg_coefs;
+
+/* Entropy-decodes `data` (which may be freed afterwards) into *out; release
+ * with mxd_jpeg_coefs_free.  MXD_ERR_INVALID with libjpeg's message. */
+int mxd_jpeg_coefs_decode(const uint8_t* data, size_t size, mxd_jpeg_coefs** out);
+int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs);
+
+/* Image size; *device_ok = 1 when the GPU can finish it (grey, YCbCr or RGB;
+ * CMYK / YCCK finish on the host only). */
+int mxd_jpeg_coefs_info(const mxd_jpeg_coefs* coefs, int32_t* width, int32_t* height, int32_t* device_ok);
+
+/* Host finish: height rows of width*3 bytes at dst_stride (thread-safe; the
+ * handle stays valid). */
+int mxd_jpeg_coefs_finish(const mxd_jpeg_coefs* coefs, uint8_t* dst, int64_t dst_stride);
+
+/* One image of a decode + resize + crop batch: the window (win_x, win_y,
+ * win_w, win_h) of the decoded image is the source of an mxd_image with
+ * channels 3 (the whole image: 0, 0, width, height); the rest as mxd_image. */
+typedef struct mxd_jpeg_image {
+  const mxd_jpeg_coefs* coefs;
+  int32_t win_x, win_y, win_w, win_h;
+  int32_t resize_w, resize_h;
+  int32_t crop_x, crop_y, crop_w, crop_h;
+  int32_t flip;
+  int32_t reserved;
+  void* dst;
+  int64_t dst_stride;
+} mxd_jpeg_image;
+
+/* Host destinations (like mxd_resize_crop_host): coefficients staged through
+ * pinned memory, IDCT + colour + resample kernels on `device`, results back. */
+int mxd_jpeg_resize_crop_host(const mxd_jpeg_image* images, int32_t n, int32_t out_dtype, int32_t device);
+
+/* Device destinations on `device` (like mxd_resize_crop_to_device). */
+int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int32_t out_dtype, int32_t device);
 
 /* ---- pixel maps: rotate / affine and channel reduction --
  *

@@ -25,6 +25,7 @@
 
 #include "mxd_amd.h"
 #include "jpeg.h"
+#include "jpegdev.h"
 #include "pixmap.h"
 #include "resample.h"
 #include "taps.h"
@@ -997,6 +998,8 @@ struct Slot {
   size_t dev_in_cap = 0;
   uint8_t* dev_out = nullptr;
   size_t dev_out_cap = 0;
+  uint8_t* dev_mid = nullptr;  // JPEG chunks: IDCT samples + decoded RGB images
+  size_t dev_mid_cap = 0;
 };
 
 struct HostCtx {
@@ -1030,8 +1033,9 @@ void free_slot_buffers(Slot& s) {
   if (s.pin_out) (void)hipHostFree(s.pin_out);
   if (s.dev_in) (void)hipFree(s.dev_in);
   if (s.dev_out) (void)hipFree(s.dev_out);
-  s.pin_in = s.pin_out = s.dev_in = s.dev_out = nullptr;
-  s.pin_in_cap = s.pin_out_cap = s.dev_in_cap = s.dev_out_cap = 0;
+  if (s.dev_mid) (void)hipFree(s.dev_mid);
+  s.pin_in = s.pin_out = s.dev_in = s.dev_out = s.dev_mid = nullptr;
+  s.pin_in_cap = s.pin_out_cap = s.dev_in_cap = s.dev_out_cap = s.dev_mid_cap = 0;
 }
 
 constexpr int kCtxPerDevice = 4;
@@ -1353,7 +1357,8 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop) {
 }
 
 namespace {
-int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device);
+int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device,
+              const mxd_jpeg_image* jpeg = nullptr);
 }  // namespace
 
 int mxd_resize_crop_host(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device) {
@@ -1395,7 +1400,85 @@ bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device) {
+// Chunk tables of a JPEG chunk (device-side finish, jpegdev.h): where the
+// coefficients, descriptors and quantisation tables sit in the staged input,
+// and the decoded images in the slot's dev_mid buffer.
+struct JpegChunk {
+  std::vector<mxd::JpegPlaneDev> planes;
+  std::vector<mxd::JpegImgDev> imgs;
+  std::vector<uint16_t> qtabs;
+  int64_t planes_off = 0, imgs_off = 0, q_off = 0, end = 0;  // in the staged input
+  int64_t samples = 0, rgb_off = 0, mid_bytes = 0;             // in dev_mid
+  int64_t nblocks = 0, max_quad_rows = 0;
+};
+
+const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
+
+int64_t rgb_pitch(int32_t w) { return (((int64_t)w * 3 + 63) & ~(int64_t)63) + 64; }
+
+// Lays out the chunk [first, end) of a JPEG batch whose coefficients are staged
+// at in_off[i]; the tables follow at `tables_at`.
+void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const std::vector<int64_t>& in_off,
+                int64_t tables_at, JpegChunk* out) {
+  JpegChunk& c = *out;
+  c = JpegChunk();
+  auto up = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
+  for (int32_t i = first; i < end; i++) {
+    const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
+    mxd::JpegImgDev m{};
+    m.ncomp = info.ncomp == 1 ? 1 : 3;
+    m.rgb = info.color_space == 2 ? 1 : 0;
+    m.width = info.width;
+    m.height = info.height;
+    m.pitch = (int32_t)rgb_pitch(info.width);
+    m.quads = (info.width + 3) / 4;
+    for (int k = 0; k < m.ncomp; k++) {
+      const mxd::jpeg::CoefPlane& cp = info.comp[k];
+      mxd::JpegPlaneDev p{};
+      p.coef = (in_off[i] + cp.off * 2) / 2;
+      p.out = c.samples;
+      p.first_block = c.nblocks;
+      p.bw = cp.bw;
+      p.bh = cp.bh;
+      p.qtab = (int32_t)c.qtabs.size();
+      p.coded = cp.coded ? 1 : 0;
+      c.qtabs.insert(c.qtabs.end(), cp.q, cp.q + 64);
+      c.planes.push_back(p);
+      m.plane[k] = c.samples;
+      m.stride[k] = cp.bw * 8;
+      m.dw[k] = cp.dw;
+      m.dh[k] = cp.dh;
+      m.hx[k] = info.max_h / cp.h;
+      m.vx[k] = info.max_v / cp.v;
+      // jpeg.cpp upsample_row's choice
+      const bool h2 = cp.h * 2 == info.max_h, v2 = cp.v * 2 == info.max_v;
+      const bool hf = cp.h == info.max_h, vf = cp.v == info.max_v;
+      m.mode[k] = hf && vf                ? mxd::kUpFull
+                  : h2 && vf              ? (cp.dw > 2 ? mxd::kUpH2V1 : mxd::kUpRep)
+                  : hf && v2              ? mxd::kUpH1V2
+                  : h2 && v2 && cp.dw > 2 ? mxd::kUpH2V2
+                                          : mxd::kUpRep;
+      c.samples += up((int64_t)cp.bw * 8 * cp.bh * 8, 256);
+      c.nblocks += (int64_t)cp.bw * cp.bh;
+    }
+    m.out = c.mid_bytes;  // relative to rgb_off, fixed below
+    c.mid_bytes += up((int64_t)m.pitch * m.height, 256);
+    c.max_quad_rows = std::max<int64_t>(c.max_quad_rows, (int64_t)m.height * m.quads);
+    c.imgs.push_back(m);
+  }
+  c.rgb_off = c.samples;
+  c.mid_bytes += c.samples;
+  c.planes_off = up(tables_at, 256);
+  c.imgs_off = up(c.planes_off + (int64_t)(c.planes.size() * sizeof(mxd::JpegPlaneDev)), 256);
+  c.q_off = up(c.imgs_off + (int64_t)(c.imgs.size() * sizeof(mxd::JpegImgDev)), 256);
+  c.end = c.q_off + (int64_t)(c.qtabs.size() * sizeof(uint16_t));
+}
+
+// jpeg != nullptr: images[i] is jpeg[i] as an mxd_image (3 channels, the
+// window as the source); its "source" is the image's coefficients, staged
+// whole, and the chunk's kernels first decode them into dev_mid.
+int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device,
+              const mxd_jpeg_image* jpeg) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
   if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
   if (n == 0) return MXD_OK;
@@ -1413,11 +1496,26 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   struct Stage {
     int32_t x0, y0, rows;
     int64_t pitch, copy, in_off, out_off, out_row;
+    int64_t in_size;              // staged bytes (footprint rows, or a JPEG's coefficients)
     bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
   };
   std::vector<Stage> st(n);
   for (int32_t i = 0; i < n; i++) {
     const mxd_image& im = images[i];
+    if (jpeg) {
+      Stage& s = st[i];
+      const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jpeg[i].coefs));
+      s.x0 = s.y0 = 0;
+      s.rows = im.src_h;
+      s.pitch = s.copy = 0;
+      s.in_size = info.coef_count * 2;
+      s.out_row = (int64_t)im.crop_w * im.channels * elem;
+      s.src_pinned = false;
+      s.dst_pinned = !dst_device && host_pinned(im.dst);
+      if (!dst_device && im.dst_stride < s.out_row)
+        return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+      continue;
+    }
     const DevTable *xt = nullptr, *yt = nullptr;
     if (int rc = tables().get(device, im.src_w, im.resize_w, &xt)) return rc;
     if (int rc = tables().get(device, im.src_h, im.resize_h, &yt)) return rc;
@@ -1432,6 +1530,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const int64_t want = (int64_t)(xh + 1 - s.x0) * c + 32;  // + the kernels' read-ahead inside a row
     s.copy = std::min<int64_t>((int64_t)(im.src_w - s.x0) * c, want);
     s.pitch = (want + 15) & ~(int64_t)15;
+    s.in_size = s.pitch * s.rows;
     s.out_row = (int64_t)im.crop_w * c * elem;
     s.src_pinned = host_pinned(im.src);
     s.dst_pinned = !dst_device && host_pinned(im.dst);
@@ -1444,8 +1543,8 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   for (int32_t i = 0; i < n;) {
     int32_t j = i;
     int64_t bytes = 0;
-    while (j < n && (j == i || bytes + st[j].pitch * st[j].rows <= kChunk)) {
-      bytes += st[j].pitch * st[j].rows;
+    while (j < n && (j == i || bytes + st[j].in_size <= kChunk)) {
+      bytes += st[j].in_size;
       j++;
     }
     chunks.push_back({i, j});
@@ -1488,11 +1587,19 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
         if (st[i].src_pinned == (pass == 1)) {
           st[i].in_off = in_bytes;
-          in_bytes += (st[i].pitch * st[i].rows + 255) & ~(int64_t)255;
+          in_bytes += (st[i].in_size + 255) & ~(int64_t)255;
         }
     int64_t in_staged = 0, out_staged = 0;
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
-      if (!st[i].src_pinned) in_staged = std::max(in_staged, st[i].in_off + st[i].pitch * st[i].rows);
+      if (!st[i].src_pinned) in_staged = std::max(in_staged, st[i].in_off + st[i].in_size);
+    JpegChunk jc;
+    if (jpeg) {
+      std::vector<int64_t> off(n, 0);
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++) off[i] = st[i].in_off;
+      jpeg_chunk(jpeg, chunks[k].first, chunks[k].second, off, in_bytes, &jc);
+      in_bytes = in_staged = jc.end;  // coefficients, then the chunk's tables, in one copy
+      if (int rc = grow_device(&sl.dev_mid, &sl.dev_mid_cap, jc.mid_bytes)) return rc;
+    }
     for (int pass = 0; pass < 2; pass++)
       for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
         if (st[i].dst_pinned == (pass == 1)) {
@@ -1515,15 +1622,37 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     parallel_items(chunks[k].first, chunks[k].second, in_staged, [&](int32_t i) {
       const mxd_image& im = images[i];
       const Stage& s = st[i];
+      if (jpeg) {
+        std::memcpy(sl.pin_in + s.in_off, mxd::jpeg::coef_info(coefs_of(jpeg[i].coefs)).coef, s.in_size);
+        return;
+      }
       if (s.src_pinned) return;
       uint8_t* stage = sl.pin_in + s.in_off;
       const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
       for (int32_t r = 0; r < s.rows; r++) std::memcpy(stage + r * s.pitch, from + (int64_t)r * im.src_stride, s.copy);
     });
+    if (jpeg) {
+      std::memcpy(sl.pin_in + jc.planes_off, jc.planes.data(), jc.planes.size() * sizeof(mxd::JpegPlaneDev));
+      for (auto& m : jc.imgs) m.out += jc.rgb_off;
+      std::memcpy(sl.pin_in + jc.imgs_off, jc.imgs.data(), jc.imgs.size() * sizeof(mxd::JpegImgDev));
+      std::memcpy(sl.pin_in + jc.q_off, jc.qtabs.data(), jc.qtabs.size() * sizeof(uint16_t));
+    }
     for (int32_t j = 0; j < cn; j++) {
       const int32_t i = chunks[k].first + j;
       const mxd_image& im = images[i];
       const Stage& s = st[i];
+      if (jpeg) {
+        const mxd::JpegImgDev& m = jc.imgs[j];
+        const uint8_t* win = sl.dev_mid + m.out + (int64_t)jpeg[i].win_y * m.pitch + (int64_t)jpeg[i].win_x * 3;
+        where[j] = Stored{win, m.pitch, 0, 0, im.src_h};
+        dev_imgs[j].src = win;
+        dev_imgs[j].src_stride = m.pitch;
+        if (!dst_device) {
+          dev_imgs[j].dst = sl.dev_out + s.out_off;
+          dev_imgs[j].dst_stride = s.out_row;
+        }
+        continue;
+      }
       where[j] = Stored{sl.dev_in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
       dev_imgs[j].src = sl.dev_in + s.in_off;  // checked by validate() only; `where` says what is stored
       dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
@@ -1533,6 +1662,15 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       }
     }
     if (in_staged > 0) MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
+    if (jpeg) {
+      mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
+                            reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
+                            reinterpret_cast<const mxd::JpegPlaneDev*>(sl.dev_in + jc.planes_off),
+                            (int32_t)jc.planes.size(), jc.nblocks, sl.dev_mid, sl.stream);
+      mxd::launch_jpeg_color(sl.dev_mid, reinterpret_cast<const mxd::JpegImgDev*>(sl.dev_in + jc.imgs_off), cn,
+                             jc.max_quad_rows, sl.dev_mid, sl.stream);
+      MXD_HIP(hipGetLastError());
+    }
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
       const Stage& s = st[i];
       if (!s.src_pinned) continue;
@@ -1586,6 +1724,82 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   return MXD_OK;
 }
 }  // namespace
+
+namespace {
+int jpeg_path(const mxd_jpeg_image* jimg, int32_t n, int32_t out_dtype, int32_t device, bool dst_device) {
+  if (n < 0 || (n > 0 && !jimg)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  std::vector<mxd_image> imgs(n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_jpeg_image& j = jimg[i];
+    const std::string at = " (image " + std::to_string(i) + ")";
+    if (!j.coefs) return fail(MXD_ERR_INVALID, "mxd: null coefs" + at);
+    const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(j.coefs));
+    if (!info.device_ok)
+      return fail(MXD_ERR_UNSUPPORTED, "mxd: CMYK / YCCK JPEGs finish on the host (mxd_jpeg_coefs_finish)" + at);
+    if (j.win_w <= 0 || j.win_h <= 0)
+      return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
+    if (j.win_x < 0 || j.win_y < 0 || (int64_t)j.win_x + j.win_w > info.width ||
+        (int64_t)j.win_y + j.win_h > info.height)
+      return fail(MXD_ERR_INVALID, "mxd: source window outside the image" + at);
+    mxd_image& m = imgs[i];
+    m.src = reinterpret_cast<const uint8_t*>(j.coefs);  // validated, never read: host_path decodes the coefficients
+    m.src_stride = (int64_t)j.win_w * 3;
+    m.src_w = j.win_w;
+    m.src_h = j.win_h;
+    m.channels = 3;
+    m.resize_w = j.resize_w;
+    m.resize_h = j.resize_h;
+    m.crop_x = j.crop_x;
+    m.crop_y = j.crop_y;
+    m.crop_w = j.crop_w;
+    m.crop_h = j.crop_h;
+    m.flip = j.flip;
+    m.dst = j.dst;
+    m.dst_stride = j.dst_stride;
+  }
+  return host_path(imgs.data(), n, out_dtype, device, dst_device, jimg);
+}
+}  // namespace
+
+int mxd_jpeg_coefs_decode(const uint8_t* data, size_t size, mxd_jpeg_coefs** out) {
+  if (!data || !out) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  std::string err;
+  mxd::jpeg::Coefs* c = mxd::jpeg::decode_coefs(data, size, &err);
+  if (!c) return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
+  *out = reinterpret_cast<mxd_jpeg_coefs*>(c);
+  return MXD_OK;
+}
+
+int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs) {
+  mxd::jpeg::free_coefs(reinterpret_cast<mxd::jpeg::Coefs*>(coefs));
+  return MXD_OK;
+}
+
+int mxd_jpeg_coefs_info(const mxd_jpeg_coefs* coefs, int32_t* width, int32_t* height, int32_t* device_ok) {
+  if (!coefs || !width || !height || !device_ok) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(coefs));
+  *width = info.width;
+  *height = info.height;
+  *device_ok = info.device_ok ? 1 : 0;
+  return MXD_OK;
+}
+
+int mxd_jpeg_coefs_finish(const mxd_jpeg_coefs* coefs, uint8_t* dst, int64_t dst_stride) {
+  if (!coefs || !dst) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(coefs));
+  if (dst_stride < (int64_t)info.width * 3) return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than a row");
+  std::string err;
+  if (!mxd::jpeg::finish(coefs_of(coefs), dst, dst_stride, &err)) return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
+  return MXD_OK;
+}
+
+int mxd_jpeg_resize_crop_host(const mxd_jpeg_image* images, int32_t n, int32_t out_dtype, int32_t device) {
+  return jpeg_path(images, n, out_dtype, device, false);
+}
+
+int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int32_t out_dtype, int32_t device) {
+  return jpeg_path(images, n, out_dtype, device, true);
+}
 
 int mxd_release_host_buffers(void) {
   host_pool().trim();

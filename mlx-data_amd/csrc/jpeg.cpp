@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -531,10 +532,11 @@ struct Component {
   int dw = 0, dh = 0;          // downsampled width / height (samples)
   int bw = 0, bh = 0;          // blocks per row / column in the MCU-padded grid
   int wib = 0, hib = 0;        // width / height in blocks of the component proper
-  std::vector<int16_t> coef;   // bw*bh blocks of 64 (progressive / deferred IDCT)
-  std::vector<uint8_t> plane;  // bw*8 x bh*8 samples
+  int64_t off = 0;             // first coefficient in Decoder::coefbuf (progressive / deferred IDCT)
+  std::vector<uint8_t> plane;  // bw*8 x bh*8 samples (sequential, IDCT at once)
   int dc_pred = 0;
-  int coef_bits_known = 0;     // progressive: set when any DC scan seen
+  bool coded = false;          // a scan carried it (sequential: else its samples stay 0)
+  uint16_t q[64];              // quantisation table latched for it
 };
 
 struct Decoder {
@@ -553,6 +555,14 @@ struct Decoder {
   Component comp[4];
   bool frame = false, any_scan = false;
   int eobrun = 0;
+  // defer: keep the coefficients of sequential scans too (decode_coefs) and
+  // run no IDCT while parsing.
+  bool defer = false;
+  std::vector<int16_t> coefbuf;  // every component's bw*bh blocks of 64, natural order
+
+  int16_t* cblk(const Component& c, int bx, int by) {
+    return coefbuf.data() + c.off + ((int64_t)by * c.bw + bx) * 64;
+  }
 
   Decoder(const uint8_t* d, size_t n) : data(d), size(n) {}
 
@@ -636,6 +646,7 @@ struct Decoder {
     }
     mcux = (width + 8 * max_h - 1) / (8 * max_h);
     mcuy = (height + 8 * max_v - 1) / (8 * max_v);
+    int64_t total = 0;
     for (int i = 0; i < ncomp; i++) {
       Component& c = comp[i];
       c.dw = (int)(((int64_t)width * c.h + max_h - 1) / max_h);
@@ -644,9 +655,11 @@ struct Decoder {
       c.hib = (c.dh + 7) / 8;
       c.bw = mcux * c.h;
       c.bh = mcuy * c.v;
-      c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
-      if (progressive) c.coef.assign((size_t)c.bw * c.bh * 64, 0);
+      c.off = total;
+      total += (int64_t)c.bw * c.bh * 64;
+      if (!progressive && !defer) c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
     }
+    if (progressive || defer) coefbuf.assign((size_t)total, 0);
     frame = true;
   }
 
@@ -752,11 +765,13 @@ struct Decoder {
     if (!progressive) {
       for (int i = 0; i < ns; i++) {
         if (!dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present) fail("Huffman table was not defined");
-        quant(*sc[i]);
+        std::memcpy(sc[i]->q, quant(*sc[i]), sizeof sc[i]->q);  // latched at the scan
+        sc[i]->coded = true;
       }
-      int16_t blk[64];
+      int16_t local[64];
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
-        std::memset(blk, 0, sizeof blk);
+        int16_t* blk = defer ? cblk(c, bx, by) : local;
+        std::memset(blk, 0, 64 * sizeof(int16_t));
         if (!skip) {
           const Huff& hd = dc[c.dc_tbl];
           const Huff& ha = ac[c.ac_tbl];
@@ -787,7 +802,7 @@ struct Decoder {
             }
           }
         }
-        idct_block(blk, quant(c), c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
+        if (!defer) idct_block(blk, c.q, c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
       });
       return;
     }
@@ -797,7 +812,7 @@ struct Decoder {
         for (int i = 0; i < ns; i++)
           if (!dc[sc[i]->dc_tbl].present) fail("Huffman table was not defined");
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
-        int16_t* blk = c.coef.data() + ((size_t)by * c.bw + bx) * 64;
+        int16_t* blk = cblk(c, bx, by);
         if (ah == 0) {
           if (skip) return;
           int s = bits.decode(dc[c.dc_tbl]);
@@ -817,7 +832,7 @@ struct Decoder {
     if (ah == 0) {
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
         if (skip) return;
-        int16_t* blk = c.coef.data() + ((size_t)by * c.bw + bx) * 64;
+        int16_t* blk = cblk(c, bx, by);
         if (eobrun > 0) {
           eobrun--;
           return;
@@ -852,7 +867,7 @@ struct Decoder {
     const int p1 = 1 << al, m1 = -1 * (1 << al);
     for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
       if (skip) return;
-      int16_t* blk = c.coef.data() + ((size_t)by * c.bw + bx) * 64;
+      int16_t* blk = cblk(c, bx, by);
       int k = ss;
       if (eobrun == 0) {
         for (; k <= se; k++) {
@@ -939,10 +954,9 @@ struct Decoder {
   // Row y of component c upsampled to full width (jdsample.c), into o (>= width
   // bytes; scratch >= 2 * dw + 2 bytes); returns the row (o, or the plane row
   // itself when c is full size).
-  const uint8_t* upsample_row(const Component& c, int y, uint8_t* o, uint8_t* scratch) const {
+  const uint8_t* upsample_row(const Component& c, const uint8_t* pl, int y, uint8_t* o, uint8_t* scratch) const {
     const int W = width;
     const int stride = c.bw * 8;
-    const uint8_t* pl = c.plane.data();
     const int hx = max_h / c.h, vx = max_v / c.v;
     const bool h2 = c.h * 2 == max_h, v2 = c.v * 2 == max_v;
     auto row = [&](int yy) { return pl + (size_t)std::min(std::max(yy, 0), c.dh - 1) * stride; };
@@ -996,22 +1010,44 @@ struct Decoder {
     return o;
   }
 
-  void output(uint8_t* dst, int64_t dst_stride) {
-    if (progressive)
-      for (int i = 0; i < ncomp; i++) {
-        Component& c = comp[i];
-        const uint16_t* q = quant(c);
-        for (int by = 0; by < c.bh; by++)
-          for (int bx = 0; bx < c.bw; bx++)
-            idct_block(c.coef.data() + ((size_t)by * c.bw + bx) * 64, q,
-                       c.plane.data() + (size_t)by * 8 * c.bw * 8 + (size_t)bx * 8, c.bw * 8);
-      }
+  // After parse(): a progressive image latches every component's table now
+  // (they may change between scans); sequential scans latched theirs.
+  void finalize() {
+    if (!progressive) return;
+    for (int i = 0; i < ncomp; i++) {
+      std::memcpy(comp[i].q, quant(comp[i]), sizeof comp[i].q);
+      comp[i].coded = true;
+    }
+  }
+
+  // Components output() reads: grey -> 1; CMYK -> 3 (K is dropped).
+  int used_components() const { return ncomp == 1 ? 1 : ncomp == 4 && color_space() == 3 ? 3 : ncomp; }
+
+  // Samples of component i: the plane decoded in place (sequential), else the
+  // IDCT of its coefficients into `store` (zeros for a component no scan
+  // carried, as the in-place planes keep).
+  const uint8_t* samples(int i, std::vector<uint8_t>& store) const {
+    const Component& c = comp[i];
+    if (!progressive && !defer) return c.plane.data();
+    store.assign((size_t)c.bw * 8 * c.bh * 8, 0);
+    if (c.coded)
+      for (int by = 0; by < c.bh; by++)
+        for (int bx = 0; bx < c.bw; bx++)
+          idct_block(coefbuf.data() + c.off + ((int64_t)by * c.bw + bx) * 64, c.q,
+                     store.data() + (size_t)by * 8 * c.bw * 8 + (size_t)bx * 8, c.bw * 8);
+    return store.data();
+  }
+
+  void output(uint8_t* dst, int64_t dst_stride) const {
+    std::vector<uint8_t> store[4];
+    const uint8_t* pl[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int i = 0; i < used_components(); i++) pl[i] = samples(i, store[i]);
     const int cs = color_space();
     const int W = width, H = height;
     if (ncomp == 1) {
       const Component& c = comp[0];
       for (int y = 0; y < H; y++) {
-        const uint8_t* in = c.plane.data() + (size_t)y * c.bw * 8;
+        const uint8_t* in = pl[0] + (size_t)y * c.bw * 8;
         uint8_t* o = dst + (size_t)y * dst_stride;
         for (int x = 0; x < W; x++) o[3 * x] = o[3 * x + 1] = o[3 * x + 2] = in[x];
       }
@@ -1031,7 +1067,7 @@ struct Decoder {
     }
     for (int y = 0; y < H; y++) {
       const uint8_t* r3[3];
-      for (int i = 0; i < 3 && i < nuse; i++) r3[i] = upsample_row(comp[i], y, rowbuf[i], scratch[i]);
+      for (int i = 0; i < 3 && i < nuse; i++) r3[i] = upsample_row(comp[i], pl[i], y, rowbuf[i], scratch[i]);
       uint8_t* o = dst + (size_t)y * dst_stride;
       if (cs == 1 || cs == 4) ycc_rgb_row(r3[0], r3[1], r3[2], o, W, cs == 4);
       else
@@ -1062,6 +1098,81 @@ int Decoder::color_space() const {
 }
 
 }  // namespace
+
+struct Coefs {
+  Decoder d;
+  Coefs(const uint8_t* data, size_t size) : d(data, size) {}
+};
+
+Coefs* decode_coefs(const uint8_t* data, size_t size, std::string* err) {
+  try {
+    auto c = std::make_unique<Coefs>(data, size);
+    Decoder& d = c->d;
+    d.defer = true;
+    d.parse();
+    if (!d.frame) fail("Invalid JPEG file structure: missing SOF marker");
+    if (d.ncomp == 2 || d.color_space() < 0) fail("unhandled format");
+    d.finalize();
+    // output()'s one failure, checked here so it comes from the decode call
+    // (upsampling reaches it exactly for non-integral factors)
+    if (d.ncomp > 1)
+      for (int i = 0; i < d.used_components(); i++)
+        if (d.max_h % d.comp[i].h != 0 || d.max_v % d.comp[i].v != 0) fail("Fractional sampling not implemented yet");
+    d.data = nullptr;
+    d.size = 0;
+    return c.release();
+  } catch (const Error& e) {
+    if (err) *err = e.msg;
+    return nullptr;
+  } catch (const std::bad_alloc&) {
+    if (err) *err = "Insufficient memory";
+    return nullptr;
+  }
+}
+
+void free_coefs(Coefs* c) { delete c; }
+
+CoefInfo coef_info(const Coefs* c) {
+  const Decoder& d = c->d;
+  CoefInfo r{};
+  r.width = d.width;
+  r.height = d.height;
+  r.ncomp = d.ncomp;
+  r.used = d.used_components();
+  r.color_space = d.color_space();
+  r.max_h = d.max_h;
+  r.max_v = d.max_v;
+  r.coef = d.coefbuf.data();
+  r.coef_count = (int64_t)d.coefbuf.size();
+  for (int i = 0; i < d.ncomp; i++) {
+    const Component& k = d.comp[i];
+    CoefPlane& p = r.comp[i];
+    p.h = k.h;
+    p.v = k.v;
+    p.dw = k.dw;
+    p.dh = k.dh;
+    p.bw = k.bw;
+    p.bh = k.bh;
+    p.coded = k.coded;
+    p.off = k.off;
+    p.q = k.q;
+  }
+  r.device_ok = d.ncomp == 1 || (d.ncomp == 3 && (r.color_space == 1 || r.color_space == 2));
+  return r;
+}
+
+bool finish(const Coefs* c, uint8_t* dst, int64_t dst_stride, std::string* err) {
+  try {
+    c->d.output(dst, dst_stride);
+    return true;
+  } catch (const Error& e) {
+    if (err) *err = e.msg;
+    return false;
+  } catch (const std::bad_alloc&) {
+    if (err) *err = "Insufficient memory";
+    return false;
+  }
+}
 
 bool is_jpeg(const uint8_t* data, size_t size) {
   return size >= 3 && data[0] == 0xFF && data[1] == 0xD8 && data[2] == 0xFF;
@@ -1102,6 +1213,7 @@ bool decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, 
     if (!d.frame) fail("Invalid JPEG file structure: missing SOF marker");
     if (d.width != width || d.height != height) fail("mxd: output buffer does not match the image size");
     if (d.ncomp == 2 || d.color_space() < 0) fail("unhandled format");
+    d.finalize();
     d.output(dst, dst_stride);
     return true;
   } catch (const Error& e) {

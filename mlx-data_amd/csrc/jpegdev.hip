@@ -1,0 +1,221 @@
+// jpegdev.hip -- device-side finish of a split JPEG decode (see jpegdev.h).
+//
+// jpeg_idct: one thread per 8x8 block: dequantise, jidctint.c ISLOW (13-bit
+//   constants, PASS1_BITS 2, 64-bit intermediates like libjpeg-turbo's JLONG;
+//   its all-zero-AC shortcuts are exact, so the plain transform gives the same
+//   bytes), the post-IDCT range limit as arithmetic (wrap to 10 bits, +128,
+//   clamp), eight 8-byte row stores into the component's sample plane.
+// jpeg_color: one thread per four horizontal output pixels of one image:
+//   each component's sample by jdsample.c's rule for its sampling factors
+//   (fancy triangle upsampling h2v1 / h1v2 / h2v2 with jpeg.cpp's edge cases,
+//   replication otherwise), jdcolor.c's 16-bit fixed-point YCbCr -> RGB (or
+//   RGB / grey as is), one 12-byte store.
+// Both are bound by nothing that matters next to the host's entropy decode
+// (a few GB/s of coefficients at most); they are written for exactness and
+// plain coalesced access, not tuned.
+#include "jpegdev.h"
+
+namespace mxd {
+namespace {
+
+using i64 = long long;
+
+constexpr int kConstBits = 13;
+constexpr int kPass1Bits = 2;
+constexpr i64 F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633, F1501 = 12299,
+              F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
+
+__device__ __forceinline__ i64 descale(i64 x, int n) { return (x + ((i64)1 << (n - 1))) >> n; }
+
+__device__ __forceinline__ uint32_t range_limit(i64 x) {
+  const int v = (int)((x + 512) & 1023) - 512 + 128;
+  return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+}
+
+// One 1-D pass over 8 values (even part from 0/2/4/6, odd part from 1/3/5/7),
+// jidctint.c's arithmetic; outputs in natural order before descaling.
+__device__ __forceinline__ void idct8(i64 d0, i64 d1, i64 d2, i64 d3, i64 d4, i64 d5, i64 d6, i64 d7, i64* o) {
+  const i64 z1e = (d2 + d6) * F0541;
+  const i64 t2 = z1e + d6 * -F1847;
+  const i64 t3 = z1e + d2 * F0765;
+  const i64 t0 = (d0 + d4) * (1 << kConstBits);
+  const i64 t1 = (d0 - d4) * (1 << kConstBits);
+  const i64 t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+  i64 a0 = d7, a1 = d5, a2 = d3, a3 = d1;
+  i64 z1 = a0 + a3, z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
+  const i64 z5 = (z3 + z4) * F1175;
+  a0 *= F0298;
+  a1 *= F2053;
+  a2 *= F3072;
+  a3 *= F1501;
+  z1 *= -F0899;
+  z2 *= -F2562;
+  z3 = z3 * -F1961 + z5;
+  z4 = z4 * -F0390 + z5;
+  a0 += z1 + z3;
+  a1 += z2 + z4;
+  a2 += z2 + z3;
+  a3 += z1 + z4;
+  o[0] = t10 + a3;
+  o[7] = t10 - a3;
+  o[1] = t11 + a2;
+  o[6] = t11 - a2;
+  o[2] = t12 + a1;
+  o[5] = t12 - a1;
+  o[3] = t13 + a0;
+  o[4] = t13 - a0;
+}
+
+__global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coef, const uint16_t* __restrict__ qt,
+                                                 const JpegPlaneDev* __restrict__ planes, int nplanes, i64 nblocks,
+                                                 uint8_t* __restrict__ samples) {
+  const i64 g = (i64)blockIdx.x * 256 + threadIdx.x;
+  if (g >= nblocks) return;
+  int lo = 0, hi = nplanes - 1;  // the last plane whose first block is <= g
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (planes[mid].first_block <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  const JpegPlaneDev p = planes[lo];
+  const i64 b = g - p.first_block;
+  const int by = (int)(b / p.bw), bx = (int)(b - (i64)by * p.bw);
+  const int stride = p.bw * 8;
+  uint8_t* out = samples + p.out + (i64)by * 8 * stride + bx * 8;
+  if (!p.coded) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) *reinterpret_cast<uint2*>(out + (i64)r * stride) = make_uint2(0, 0);
+    return;
+  }
+  int32_t d[64];
+  {
+    const int4* cp = reinterpret_cast<const int4*>(coef + p.coef + b * 64);
+    const uint4* qp = reinterpret_cast<const uint4*>(qt + p.qtab);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int4 c = cp[k];
+      const uint4 q = qp[k];
+      const int32_t cw[4] = {c.x, c.y, c.z, c.w};
+      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        d[8 * k + 2 * j] = (int32_t)(int16_t)(cw[j] & 0xffff) * (int32_t)(qw[j] & 0xffff);
+        d[8 * k + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)cw[j] >> 16) * (int32_t)(qw[j] >> 16);
+      }
+    }
+  }
+  // pass 1: columns -> int workspace (descaled by CONST_BITS - PASS1_BITS)
+  int32_t ws[64];
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    i64 o[8];
+    idct8(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c], o);
+#pragma unroll
+    for (int r = 0; r < 8; r++) ws[8 * r + c] = (int32_t)descale(o[r], kConstBits - kPass1Bits);
+  }
+  // pass 2: rows -> samples
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int32_t* w = ws + 8 * r;
+    i64 o[8];
+    idct8(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    uint32_t lo4 = 0, hi4 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      lo4 |= range_limit(descale(o[c], kConstBits + kPass1Bits + 3)) << (8 * c);
+      hi4 |= range_limit(descale(o[c + 4], kConstBits + kPass1Bits + 3)) << (8 * c);
+    }
+    *reinterpret_cast<uint2*>(out + (i64)r * stride) = make_uint2(lo4, hi4);
+  }
+}
+
+// Component k's sample at output (x, y) (jpeg.cpp upsample_row).
+__device__ __forceinline__ int sample_at(const uint8_t* __restrict__ pl, const JpegImgDev& m, int k, int x, int y) {
+  const int stride = m.stride[k];
+  switch (m.mode[k]) {
+    case kUpFull:
+      return pl[(i64)y * stride + x];
+    case kUpH2V1: {
+      const uint8_t* in = pl + (i64)y * stride;
+      const int i = x >> 1, dw = m.dw[k];
+      const int v = in[i] * 3;
+      if (x & 1) return i == dw - 1 ? in[i] : (v + in[i + 1] + 2) >> 2;
+      return i == 0 ? in[0] : (v + in[i - 1] + 1) >> 2;
+    }
+    case kUpH1V2:
+    case kUpH2V2: {
+      const int iy = y >> 1, below = y & 1, dh = m.dh[k];
+      const int ny = min(max(below ? iy + 1 : iy - 1, 0), dh - 1);
+      const uint8_t* in0 = pl + (i64)min(iy, dh - 1) * stride;
+      const uint8_t* in1 = pl + (i64)ny * stride;
+      if (m.mode[k] == kUpH1V2) return (in0[x] * 3 + in1[x] + (below ? 2 : 1)) >> 2;
+      const int i = x >> 1, dw = m.dw[k];
+      const int cs = in0[i] * 3 + in1[i];
+      if (x & 1) return i == dw - 1 ? (cs * 4 + 7) >> 4 : (cs * 3 + in0[i + 1] * 3 + in1[i + 1] + 7) >> 4;
+      return i == 0 ? (cs * 4 + 8) >> 4 : (cs * 3 + in0[i - 1] * 3 + in1[i - 1] + 8) >> 4;
+    }
+    default:
+      return pl[(i64)(y / m.vx[k]) * stride + x / m.hx[k]];
+  }
+}
+
+constexpr int kFixCrR = 91881, kFixCbB = 116130, kFixCrG = 46802, kFixCbG = 22554, kHalf16 = 1 << 15;
+
+__device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+__global__ __launch_bounds__(256) void jpeg_color(const uint8_t* __restrict__ samples,
+                                                  const JpegImgDev* __restrict__ imgs, uint8_t* __restrict__ rgb) {
+  const JpegImgDev& m = imgs[blockIdx.y];
+  const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (i64)m.height * m.quads) return;
+  const int y = (int)(t / m.quads);
+  const int x0 = (int)(t - (i64)y * m.quads) * 4;
+  uint32_t px[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int x = min(x0 + j, m.width - 1);  // pixels past the row end: a copy of the last (padding bytes)
+    if (m.ncomp == 1) {
+      const uint32_t v = samples[m.plane[0] + (i64)y * m.stride[0] + x];
+      px[j][0] = px[j][1] = px[j][2] = v;
+      continue;
+    }
+    const int c0 = sample_at(samples + m.plane[0], m, 0, x, y);
+    const int c1 = sample_at(samples + m.plane[1], m, 1, x, y);
+    const int c2 = sample_at(samples + m.plane[2], m, 2, x, y);
+    if (m.rgb) {
+      px[j][0] = (uint32_t)c0;
+      px[j][1] = (uint32_t)c1;
+      px[j][2] = (uint32_t)c2;
+    } else {
+      const int cb = c1 - 128, cr = c2 - 128;
+      px[j][0] = clamp255(c0 + ((kFixCrR * cr + kHalf16) >> 16));
+      px[j][1] = clamp255(c0 + ((-kFixCbG * cb + kHalf16 - kFixCrG * cr) >> 16));
+      px[j][2] = clamp255(c0 + ((kFixCbB * cb + kHalf16) >> 16));
+    }
+  }
+  const uint32_t w0 = px[0][0] | px[0][1] << 8 | px[0][2] << 16 | px[1][0] << 24;
+  const uint32_t w1 = px[1][1] | px[1][2] << 8 | px[2][0] << 16 | px[2][1] << 24;
+  const uint32_t w2 = px[2][2] | px[3][0] << 8 | px[3][1] << 16 | px[3][2] << 24;
+  uint32_t* o = reinterpret_cast<uint32_t*>(rgb + m.out + (i64)y * m.pitch + (i64)x0 * 3);
+  o[0] = w0;
+  o[1] = w1;
+  o[2] = w2;
+}
+
+}  // namespace
+
+void launch_jpeg_idct(const int16_t* coef, const uint16_t* qtabs, const JpegPlaneDev* planes, int32_t nplanes,
+                      int64_t nblocks, uint8_t* samples, hipStream_t stream) {
+  if (nblocks <= 0 || nplanes <= 0) return;
+  hipLaunchKernelGGL(jpeg_idct, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, stream, coef, qtabs, planes,
+                     nplanes, (i64)nblocks, samples);
+}
+
+void launch_jpeg_color(const uint8_t* samples, const JpegImgDev* imgs, int32_t n, int64_t max_quad_rows, uint8_t* rgb,
+                       hipStream_t stream) {
+  if (n <= 0 || max_quad_rows <= 0) return;
+  hipLaunchKernelGGL(jpeg_color, dim3((unsigned)((max_quad_rows + 255) / 256), (unsigned)n), dim3(256), 0, stream,
+                     samples, imgs, rgb);
+}
+
+}  // namespace mxd

@@ -19,6 +19,14 @@
 namespace mxd {
 namespace pipe {
 
+struct JpegSource {
+  mxd_jpeg_coefs* coefs;
+  explicit JpegSource(mxd_jpeg_coefs* c) : coefs(c) {}
+  ~JpegSource() { (void)mxd_jpeg_coefs_free(coefs); }
+  JpegSource(const JpegSource&) = delete;
+  JpegSource& operator=(const JpegSource&) = delete;
+};
+
 int64_t itemsize(DType t) {
   switch (t) {
     case DType::UInt8:
@@ -161,24 +169,77 @@ mxd_image plan_desc(const ImagePlan& p, void* dst, int64_t dst_stride) {
   return d;
 }
 
-// Runs the descriptors (one fused launch per device).  Several devices:
-// contiguous slices [k n / D, (k + 1) n / D), slice 0 on the calling thread,
-// the others on their own threads; the first failing slice's message wins.
-void run_host(const std::vector<mxd_image>& descs, int32_t dtype) {
-  if (descs.empty()) return;
+// An image plan and where its result goes.
+struct Job {
+  ImagePlan plan;
+  void* dst;
+  int64_t stride;
+};
+
+mxd_jpeg_image jpeg_desc(const ImagePlan& p, const JpegSource& j, void* dst, int64_t dst_stride) {
+  mxd_jpeg_image d{};
+  d.coefs = j.coefs;
+  d.win_x = (int32_t)p.sx;
+  d.win_y = (int32_t)p.sy;
+  d.win_w = (int32_t)p.sw;
+  d.win_h = (int32_t)p.sh;
+  d.resize_w = (int32_t)p.resize_w;
+  d.resize_h = (int32_t)p.resize_h;
+  d.crop_x = (int32_t)p.crop_x;
+  d.crop_y = (int32_t)p.crop_y;
+  d.crop_w = (int32_t)p.crop_w;
+  d.crop_h = (int32_t)p.crop_h;
+  d.flip = p.flip ? 1 : 0;
+  d.dst = dst;
+  d.dst_stride = dst_stride;
+  return d;
+}
+
+// One device's share of the jobs: plans over entropy-decoded JPEGs in one
+// decode + resize call (the GPU finishes the decode), the rest in one resize
+// call.  Returns the C ABI status (message in mxd_last_error()).
+int run_on(const Job* jobs, size_t n, int32_t dtype, int device, bool dst_device) {
+  std::vector<mxd_image> plain;
+  std::vector<mxd_jpeg_image> jp;
+  std::vector<std::shared_ptr<const JpegSource>> keep;  // alive for the call
+  for (size_t i = 0; i < n; i++) {
+    const Job& j = jobs[i];
+    if (auto src = j.plan.src->jpeg()) {
+      jp.push_back(jpeg_desc(j.plan, *src, j.dst, j.stride));
+      keep.push_back(std::move(src));
+    } else {
+      plain.push_back(plan_desc(j.plan, j.dst, j.stride));
+    }
+  }
+  if (!jp.empty()) {
+    const int rc = dst_device ? mxd_jpeg_resize_crop_to_device(jp.data(), (int32_t)jp.size(), dtype, device)
+                              : mxd_jpeg_resize_crop_host(jp.data(), (int32_t)jp.size(), dtype, device);
+    if (rc != MXD_OK) return rc;
+  }
+  if (plain.empty()) return MXD_OK;
+  return dst_device ? mxd_resize_crop_to_device(plain.data(), (int32_t)plain.size(), dtype, device)
+                    : mxd_resize_crop_host(plain.data(), (int32_t)plain.size(), dtype, device);
+}
+
+// Runs the jobs into host destinations (one fused launch per device and
+// source kind).  Several devices: contiguous slices [k n / D, (k + 1) n / D),
+// slice 0 on the calling thread, the others on their own threads; the first
+// failing slice's message wins.
+void run_host(const std::vector<Job>& jobs, int32_t dtype) {
+  if (jobs.empty()) return;
   const std::vector<int> devs = devices();
   if (devs.empty()) throw std::runtime_error("mxd: no HIP device visible (the image path runs only on the GPU)");
-  const size_t n = descs.size();
+  const size_t n = jobs.size();
   const size_t k = std::min(devs.size(), n);
   const uint64_t first = g_rr.fetch_add(k);
   if (k == 1) {
-    check(mxd_resize_crop_host(descs.data(), (int32_t)n, dtype, devs[first % devs.size()]));
+    check(run_on(jobs.data(), n, dtype, devs[first % devs.size()], false));
     return;
   }
   std::vector<std::string> err(k);
   auto slice = [&](size_t s) {
     const size_t b = s * n / k, e = (s + 1) * n / k;
-    if (mxd_resize_crop_host(descs.data() + b, (int32_t)(e - b), dtype, devs[(first + s) % devs.size()]) != MXD_OK)
+    if (run_on(jobs.data() + b, e - b, dtype, devs[(first + s) % devs.size()], false) != MXD_OK)
       err[s] = mxd_last_error();  // thread-local: read on the failing thread
   };
   std::vector<std::thread> workers;
@@ -191,7 +252,16 @@ void run_host(const std::vector<mxd_image>& descs, int32_t dtype) {
 
 int32_t out_dtype(DType t) { return t == DType::Float ? MXD_F32_DIV255 : MXD_U8; }
 
+std::atomic<int> g_device_decode{-1};  // -1: not set (on when a device is visible)
+
 }  // namespace
+
+void set_device_decode(bool on) { g_device_decode.store(on ? 1 : 0); }
+
+bool device_decode() {
+  const int v = g_device_decode.load();
+  return v < 0 ? !devices().empty() : v == 1;
+}
 
 int64_t ImagePlan::channels() const { return src->shape(2); }
 
@@ -215,6 +285,14 @@ Array::Array(std::shared_ptr<const ImagePlan> plan)
       shape_({plan->crop_h, plan->crop_w, plan->channels()}),
       plan_(std::move(plan)) {}
 
+Array::Array(std::shared_ptr<const JpegSource> jpeg, int64_t height, int64_t width)
+    : type_(DType::UInt8), shape_({height, width, 3}), jpeg_(std::move(jpeg)) {}
+
+std::shared_ptr<const JpegSource> Array::jpeg() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return data_ ? nullptr : jpeg_;
+}
+
 int64_t Array::shape(int d) const {
   if (d < 0) d += ndim();
   if (d < 0 || d >= ndim()) throw std::runtime_error("Array: out of bound dimension");
@@ -233,8 +311,15 @@ void* Array::data() const {
   if (!data_ && plan_) {
     auto buf = alloc_bytes(nbytes());
     const int64_t row = shape_[1] * shape_[2] * itemsize(type_);
-    run_host({plan_desc(*plan_, buf.get(), row)}, out_dtype(type_));
+    run_host({Job{*plan_, buf.get(), row}}, out_dtype(type_));
     data_ = buf;
+  }
+  if (!data_ && jpeg_) {
+    // host finish of a lazy decode read directly
+    auto buf = alloc_bytes(nbytes());
+    check(mxd_jpeg_coefs_finish(jpeg_->coefs, static_cast<uint8_t*>(buf.get()), shape_[1] * 3));
+    data_ = buf;
+    jpeg_.reset();
   }
   return data_.get();
 }
@@ -398,16 +483,16 @@ std::shared_ptr<Array> stack_frames(const std::vector<std::shared_ptr<Array>>& f
   auto out = std::make_shared<Array>(f0->type(), std::vector<int64_t>{(int64_t)frames.size(), h, w, c});
   const int64_t isz = itemsize(f0->type()), bytes = h * w * c * isz;
   auto* dst = static_cast<uint8_t*>(out->data());
-  std::vector<mxd_image> descs;
+  std::vector<Job> jobs;
   for (size_t i = 0; i < frames.size(); i++) {
     const auto& f = frames[i];
     if (f->type() != f0->type()) throw std::runtime_error("applyVideo: frame type inconsistent during transform");
     if (f->plan() && f->pending())
-      descs.push_back(plan_desc(*f->plan(), dst + i * bytes, w * c * isz));
+      jobs.push_back(Job{*f->plan(), dst + i * bytes, w * c * isz});
     else
       std::memcpy(dst + i * bytes, f->data(), bytes);
   }
-  run_host(descs, out_dtype(f0->type()));  // every pending frame in one launch
+  run_host(jobs, out_dtype(f0->type()));  // every pending frame in one launch
   return out;
 }
 
@@ -697,6 +782,18 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
       return out;
     }
     if (!ok) throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
+    if (device_decode()) {
+      // entropy decode only; the GPU finishes it in the batch launch
+      mxd_jpeg_coefs* c = nullptr;
+      if (mxd_jpeg_coefs_decode(bytes, nbytes, &c) != MXD_OK)
+        throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
+      auto src = std::make_shared<const JpegSource>(c);
+      int32_t cw = 0, ch = 0, dev_ok = 0;
+      check(mxd_jpeg_coefs_info(c, &cw, &ch, &dev_ok));
+      auto out = std::make_shared<Array>(src, ch, cw);
+      if (!dev_ok) out->data();  // CMYK / YCCK: the host finishes it now
+      return out;
+    }
     auto out = std::make_shared<Array>(DType::UInt8, std::vector<int64_t>{h, w, 3}, alloc_bytes((int64_t)h * w * 3));
     if (mxd_jpeg_decode(bytes, nbytes, static_cast<uint8_t*>(out->data()), (int64_t)w * 3, w, h) != MXD_OK) {
       const std::string e = jpeg_error();
@@ -765,6 +862,19 @@ void fill(Array& a, double v) {
 }  // namespace
 
 namespace {
+// An array whose pixels a batch launch produces: a pending plan, or a lazy
+// JPEG decode (as the identity plan over it).
+bool deferred(const Array& a) { return a.pending() || (a.type() == DType::UInt8 && a.jpeg()); }
+
+ImagePlan deferred_plan(const std::shared_ptr<Array>& a) {
+  if (a->plan() && a->pending()) return *a->plan();
+  ImagePlan p;
+  p.src = a;
+  p.sw = p.resize_w = p.crop_w = a->shape(1);
+  p.sh = p.resize_h = p.crop_h = a->shape(0);
+  return p;
+}
+
 // batch_arrays into device memory.  The fused case -- every array a pending
 // image filling the batch's pixel slots, nothing to pad -- has the kernel
 // write the batch in place; otherwise the host batch is built and uploaded.
@@ -778,13 +888,13 @@ std::shared_ptr<Array> device_batch(const std::vector<std::shared_ptr<Array>>& a
   std::shared_ptr<void> mem(ptr, [device](void* p) { (void)mxd_free_device(p, device); });
   auto res = std::make_shared<Array>(type, bshape, mem, device);
   bool fused = !has_dim && !ragged && arrs.front()->ndim() == 3;
-  for (const auto& a : arrs) fused = fused && a->pending() && a->shape(2) == bshape[3];
+  for (const auto& a : arrs) fused = fused && deferred(*a) && a->shape(2) == bshape[3];
   if (fused) {
-    std::vector<mxd_image> launch;
+    std::vector<Job> jobs;
     auto* base = static_cast<uint8_t*>(ptr);
     for (size_t i = 0; i < arrs.size(); i++)
-      launch.push_back(plan_desc(*arrs[i]->plan(), base + (int64_t)i * item * isz, stride[0] * isz));
-    check(mxd_resize_crop_to_device(launch.data(), (int32_t)launch.size(), out_dtype(type), device));
+      jobs.push_back(Job{deferred_plan(arrs[i]), base + (int64_t)i * item * isz, stride[0] * isz});
+    check(run_on(jobs.data(), jobs.size(), out_dtype(type), device, true));
     return res;
   }
   auto host = batch_arrays(arrs, pad_value, dim, has_dim, -1);
@@ -855,21 +965,21 @@ std::shared_ptr<Array> batch_arrays(const std::vector<std::shared_ptr<Array>>& a
   const int64_t isz = itemsize(type);
   if (device >= 0) return device_batch(arrs, bshape, stride, item, ragged, pad_value, dim, has_dim, device);
   bool images = false;
-  for (const auto& a : arrs) images = images || a->pending();
+  for (const auto& a : arrs) images = images || deferred(*a);
   const int64_t total = shape_size(bshape) * isz;
   auto res = std::make_shared<Array>(type, bshape, images ? alloc_batch_bytes(total) : alloc_bytes(total));
   if (ragged) fill(*res, pad_value);
 
   auto* base = static_cast<uint8_t*>(res->data());
-  std::vector<mxd_image> launch;
+  std::vector<Job> launch;
   int64_t off = 0;
   for (const auto& a : arrs) {
-    // Pending HWC images in the default stacking layout whose pixels fill
-    // the batch's pixel slots (same channel count) go to the fused kernel,
-    // which writes rows straight into the batch; the rest (and a channel
-    // count the batch pads) are materialised and copied.
-    if (!has_dim && a->pending() && nd == 3 && a->shape(2) == bshape[3]) {
-      launch.push_back(plan_desc(*a->plan(), base + off * isz, stride[0] * isz));
+    // Pending HWC images (and lazy JPEG decodes) in the default stacking
+    // layout whose pixels fill the batch's pixel slots (same channel count)
+    // go to the fused kernels, which write rows straight into the batch; the
+    // rest (and a channel count the batch pads) are materialised and copied.
+    if (!has_dim && deferred(*a) && nd == 3 && a->shape(2) == bshape[3]) {
+      launch.push_back(Job{deferred_plan(a), base + off * isz, stride[0] * isz});
     } else {
       copy_to_strided(base, off, static_cast<const uint8_t*>(a->data()), a->shape(), stride, isz);
     }
@@ -904,7 +1014,7 @@ Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<
     if (dev.device >= 0) {
       bool on = false;
       if (dev.keys.empty())
-        for (const auto& a : values[k]) on = on || a->pending();
+        for (const auto& a : values[k]) on = on || deferred(*a);
       else
         on = std::find(dev.keys.begin(), dev.keys.end(), keys[k]) != dev.keys.end();
       device = on ? dev.device : -1;

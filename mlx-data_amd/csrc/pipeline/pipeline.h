@@ -39,6 +39,13 @@ int64_t itemsize(DType t);
 
 class Array;
 
+// An entropy-decoded JPEG (mxd_jpeg_coefs_decode): load_image's output when
+// the device finish is on (set_device_decode).  Its pixels come from the host
+// finish on first direct access, or from the GPU finish inside the batch
+// launch that resizes / crops it (mxd_jpeg_resize_crop_*); the bytes are the
+// same either way.
+struct JpegSource;
+
 // Pixel work that has not run yet: take the window (sx, sy, sw, sh) of `src`,
 // resize it to resize_w x resize_h (identity when equal), keep the crop window
 // of that, mirror it if `flip`.  The output is `crop_h x crop_w x C` uint8.
@@ -67,6 +74,7 @@ class Array {
   // data() is then a device pointer on `device`.
   Array(DType type, std::vector<int64_t> shape, std::shared_ptr<void> data, int device);
   explicit Array(std::shared_ptr<const ImagePlan> plan);              // lazy image
+  Array(std::shared_ptr<const JpegSource> jpeg, int64_t height, int64_t width);  // lazy decode, (H, W, 3)
 
   DType type() const { return type_; }
   const std::vector<int64_t>& shape() const { return shape_; }
@@ -78,6 +86,8 @@ class Array {
   void* data() const;
   const std::shared_ptr<const ImagePlan>& plan() const { return plan_; }
   bool pending() const;
+  // The entropy-decoded JPEG of a lazy decode not materialised yet, else null.
+  std::shared_ptr<const JpegSource> jpeg() const;
   // -1: host memory; else the HIP device holding data().
   int device() const { return device_; }
 
@@ -86,6 +96,7 @@ class Array {
   std::vector<int64_t> shape_;
   mutable std::shared_ptr<void> data_;
   std::shared_ptr<const ImagePlan> plan_;
+  mutable std::shared_ptr<const JpegSource> jpeg_;
   int device_ = -1;
   mutable std::mutex mu_;
 };
@@ -101,6 +112,13 @@ std::shared_ptr<Array> check_key(const Sample& s, const std::string& key);
 // offsets, so the batch is identical to a single-device one.
 void set_devices(const std::vector<int>& devices);
 std::vector<int> devices();
+
+// load_image's JPEG route: on (the default when a device is visible), only
+// the entropy decode runs in load_image and the GPU finishes the decode inside
+// the batch launch; off, load_image decodes whole on the
+// host.  Identical bytes either way.
+void set_device_decode(bool on);
+bool device_decode();
 
 // ---------------------------------------------------------------- state
 struct State {

@@ -497,6 +497,8 @@ PYBIND11_MODULE(_pipeline, m) {
   m.def("set_state", &set_state, py::arg("seed") = 1234);
   m.def("set_devices", &set_devices, py::arg("devices"));
   m.def("devices", &devices);
+  m.def("set_device_decode", &set_device_decode, py::arg("on"));
+  m.def("device_decode", &device_decode);
 
   // The decoder holds a Python callable: drop it before the interpreter goes.
   py::module_::import("atexit").attr("register")(py::cpp_function([] { set_image_decoder(nullptr); }));

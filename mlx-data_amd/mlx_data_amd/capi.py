@@ -29,6 +29,8 @@ EXPORTS = (
     "mxd_release_host_buffers",
     "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
+    "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_free", "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
+    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device",
 )
 
 MXD_AFFINE = 0
@@ -78,6 +80,28 @@ class MxdPixmap(ctypes.Structure):
         ("dst", ctypes.c_void_p),
         ("dst_stride", ctypes.c_int64),
         ("params", ctypes.c_float * 6),
+    ]
+
+
+class MxdJpegImage(ctypes.Structure):
+    """struct mxd_jpeg_image (include/mxd_amd.h): decode + resize + crop."""
+
+    _fields_ = [
+        ("coefs", ctypes.c_void_p),
+        ("win_x", ctypes.c_int32),
+        ("win_y", ctypes.c_int32),
+        ("win_w", ctypes.c_int32),
+        ("win_h", ctypes.c_int32),
+        ("resize_w", ctypes.c_int32),
+        ("resize_h", ctypes.c_int32),
+        ("crop_x", ctypes.c_int32),
+        ("crop_y", ctypes.c_int32),
+        ("crop_w", ctypes.c_int32),
+        ("crop_h", ctypes.c_int32),
+        ("flip", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("dst", ctypes.c_void_p),
+        ("dst_stride", ctypes.c_int64),
     ]
 
 
@@ -206,6 +230,62 @@ def jpeg_decode(data):
     check(lib().mxd_jpeg_decode(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes),
                                 out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(w * 3), w, h))
     return out
+
+
+class JpegCoefs:
+    """An entropy-decoded JPEG (mxd_jpeg_coefs_decode): the host half of the
+    split decode; finish() runs the rest on the host, make_jpeg_images() hands
+    it to the GPU finish."""
+
+    def __init__(self, data):
+        buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
+        h = ctypes.c_void_p()
+        check(lib().mxd_jpeg_coefs_decode(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes),
+                                          ctypes.byref(h)))
+        self.handle = h.value
+        w, hh, ok = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib().mxd_jpeg_coefs_info(ctypes.c_void_p(self.handle), ctypes.byref(w), ctypes.byref(hh),
+                                        ctypes.byref(ok)))
+        self.width, self.height, self.device_ok = w.value, hh.value, bool(ok.value)
+
+    def finish(self):
+        """Host finish: (H, W, 3) uint8, the bytes jpeg_decode gives."""
+        out = np.empty((self.height, self.width, 3), np.uint8)
+        check(lib().mxd_jpeg_coefs_finish(ctypes.c_void_p(self.handle), out.ctypes.data_as(ctypes.c_void_p),
+                                          ctypes.c_int64(self.width * 3)))
+        return out
+
+    def close(self):
+        if self.handle:
+            lib().mxd_jpeg_coefs_free(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_jpeg_images(entries):
+    """entries: dicts with the mxd_jpeg_image fields (coefs: a JpegCoefs; the
+    window defaults to the whole image) -> ctypes array."""
+    entries = list(entries)
+    arr = (MxdJpegImage * max(1, len(entries)))()
+    for i, e in enumerate(entries):
+        c = e["coefs"]
+        e = dict(dict(win_x=0, win_y=0, win_w=c.width, win_h=c.height), **e)
+        for k, v in e.items():
+            setattr(arr[i], k, c.handle if k == "coefs" else v)
+    return arr, len(entries)
+
+
+def jpeg_resize_crop_host(images, n, out_dtype, device=0):
+    check(lib().mxd_jpeg_resize_crop_host(images, n, out_dtype, device))
+
+
+def jpeg_resize_crop_to_device(images, n, out_dtype, device=0):
+    check(lib().mxd_jpeg_resize_crop_to_device(images, n, out_dtype, device))
 
 
 def rotate_geometry(w, h, angle, crop=False):

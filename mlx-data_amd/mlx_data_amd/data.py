@@ -25,10 +25,13 @@ import torch before this package when torch consumes them, so both share one
 HIP runtime.  Reading an unbatched image materialises it with its own launch.
 There is no CPU resize: without a visible GPU the image ops raise.
 
-``load_image`` decodes JPEG natively (``csrc/pipeline/jpeg.cpp``, the
-reference's libjpeg path, ``core/image/ImageJPEG.cpp``); other formats go to a
-Pillow hook that follows the reference's stb_image rules
-(``core/image/ImageSTBI.cpp``: 1/2/3 channels kept, 4 -> 3, 16-bit >> 8).
+``load_image`` decodes JPEG natively (``csrc/jpeg.cpp``, the reference's
+libjpeg path, ``core/image/ImageJPEG.cpp``).  With a device visible it runs
+only the entropy decode and the batch launch finishes the decode on the GPU
+(IDCT, upsampling, colour; ``csrc/jpegdev.hip``) before resizing, with the
+same bytes; ``set_device_decode(False)`` decodes whole on the host instead.
+Other formats go to a Pillow hook that follows the reference's stb_image
+rules (``core/image/ImageSTBI.cpp``: 1/2/3 channels kept, 4 -> 3, 16-bit >> 8).
 """
 import io
 
@@ -36,10 +39,11 @@ import numpy as np
 
 from . import capi  # noqa: F401  (loads libmxd_amd.so before anything else binds a HIP runtime)
 from . import _pipeline  # noqa: F401
-from ._pipeline import (Buffer, DeviceArray, Stream, buffer_from_vector, devices, set_devices, set_image_decoder,
-                        set_state)
+from ._pipeline import (Buffer, DeviceArray, Stream, buffer_from_vector, device_decode, devices, set_device_decode,
+                        set_devices, set_image_decoder, set_state)
 
-__all__ = ["Buffer", "Stream", "DeviceArray", "buffer_from_vector", "set_state", "set_devices", "devices"]
+__all__ = ["Buffer", "Stream", "DeviceArray", "buffer_from_vector", "set_state", "set_devices", "devices",
+           "set_device_decode", "device_decode"]
 
 
 def _decode(path, data, from_memory, info):

@@ -1,0 +1,198 @@
+"""GPU: the device-side finish of the split JPEG decode (csrc/jpegdev.hip,
+mxd_jpeg_resize_crop_host / _to_device).
+
+* identity geometry: the GPU-decoded image equals the host decode byte for
+  byte (and so Pillow's libjpeg-turbo: tests/test_jpeg.py pins the host
+  decoder) -- committed fixtures and Pillow-encoded images of every sampling
+  layout, progressive, restart intervals, odd sizes;
+* resize + crop + mirror, u8 and f32, windows (random_area_crop): equal to
+  mxd_resize_crop_host on the host-decoded pixels (same kernels, same bytes);
+* batches spanning several staging chunks, device destinations;
+* the operator surface: load_image -> resize -> crop -> batch gives the same
+  batches with the device finish on and off."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from mlx_data_amd import capi
+
+pytestmark = pytest.mark.gpu
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "jpeg.npz"))
+CASES = sorted(k[:-4] for k in GOLD.files if k.endswith("_jpg") and not k.startswith("cmyk"))
+
+
+def _encode(a, **kw):
+    from PIL import Image
+
+    b = io.BytesIO()
+    Image.fromarray(a if a.shape[2] == 3 else a[:, :, 0]).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _smooth(rng, h, w, c=3):
+    gh, gw = h // 16 + 2, w // 16 + 2
+    grid = rng.integers(0, 256, (gh, gw, c)).astype(np.float32)
+    yi = np.minimum(np.arange(h) * (gh - 1) // max(1, h - 1), gh - 2)
+    xi = np.minimum(np.arange(w) * (gw - 1) // max(1, w - 1), gw - 2)
+    f = grid[yi][:, xi] * 0.6 + grid[yi + 1][:, xi + 1] * 0.4 + rng.normal(0, 14, (h, w, c))
+    return np.clip(f, 0, 255).astype(np.uint8)
+
+
+def _host_ref(pixels, geoms, f32):
+    """mxd_resize_crop_host on host-decoded pixels: the expected bytes."""
+    elem = 4 if f32 else 1
+    outs, entries = [], []
+    for im, (wx, wy, ww, wh, rw, rh, cx, cy, cw, ch, flip) in zip(pixels, geoms):
+        win = np.ascontiguousarray(im[wy:wy + wh, wx:wx + ww])
+        o = np.zeros((ch, cw * 3 * elem), np.uint8)
+        outs.append((o, win))
+        entries.append(dict(src=win.ctypes.data, src_stride=ww * 3, src_w=ww, src_h=wh, channels=3, resize_w=rw,
+                            resize_h=rh, crop_x=cx, crop_y=cy, crop_w=cw, crop_h=ch, flip=flip, dst=o.ctypes.data,
+                            dst_stride=cw * 3 * elem))
+    arr, n = capi.make_images(entries)
+    capi.resize_crop_host(arr, n, capi.MXD_F32_DIV255 if f32 else capi.MXD_U8, 0)
+    return [o for o, _ in outs]
+
+
+def _gpu(coefs, geoms, f32, device_dst=False):
+    elem = 4 if f32 else 1
+    outs, entries, bufs = [], [], []
+    for c, (wx, wy, ww, wh, rw, rh, cx, cy, cw, ch, flip) in zip(coefs, geoms):
+        row = cw * 3 * elem
+        if device_dst:
+            d = capi.DeviceBuffer(row * ch, 0)
+            d.memset(0)
+            bufs.append((d, row, ch))
+            ptr = d.ptr
+        else:
+            o = np.zeros((ch, row), np.uint8)
+            outs.append(o)
+            ptr = o.ctypes.data
+        entries.append(dict(coefs=c, win_x=wx, win_y=wy, win_w=ww, win_h=wh, resize_w=rw, resize_h=rh, crop_x=cx,
+                            crop_y=cy, crop_w=cw, crop_h=ch, flip=flip, dst=ptr, dst_stride=row))
+    arr, n = capi.make_jpeg_images(entries)
+    dt = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
+    if device_dst:
+        capi.jpeg_resize_crop_to_device(arr, n, dt, 0)
+        for d, row, ch in bufs:
+            outs.append(d.download((ch, row), np.uint8))
+            d.free()
+    else:
+        capi.jpeg_resize_crop_host(arr, n, dt, 0)
+    return outs
+
+
+def _identity(c):
+    return (0, 0, c.width, c.height, c.width, c.height, 0, 0, c.width, c.height, 0)
+
+
+def test_fixtures_identity_decode():
+    coefs = [capi.JpegCoefs(GOLD[f"{k}_jpg"]) for k in CASES]
+    got = _gpu(coefs, [_identity(c) for c in coefs], False)
+    for k, g, c in zip(CASES, got, coefs):
+        assert np.array_equal(g.reshape(c.height, c.width, 3), GOLD[f"{k}_rgb"]), k
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_encoded_layouts_identity_decode(seed):
+    rng = np.random.default_rng(seed)
+    datas = []
+    for i in range(12):
+        h, w = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        grey = i % 6 == 5
+        kw = dict(quality=int(rng.integers(10, 101)), progressive=bool(rng.random() < 0.4))
+        if not grey:
+            kw["subsampling"] = i % 3
+        if rng.random() < 0.3:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 5))
+        datas.append(_encode(_smooth(rng, h, w, 1 if grey else 3), **kw))
+    coefs = [capi.JpegCoefs(d) for d in datas]
+    got = _gpu(coefs, [_identity(c) for c in coefs], False)
+    for d, g, c in zip(datas, got, coefs):
+        assert np.array_equal(g.reshape(c.height, c.width, 3), capi.jpeg_decode(d))
+
+
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("device_dst", [False, True])
+def test_resize_crop_windows_equal_host_pixels(f32, device_dst):
+    rng = np.random.default_rng(7)
+    datas, geoms = [], []
+    for i in range(24):
+        h, w = int(rng.integers(40, 700)), int(rng.integers(40, 700))
+        datas.append(_encode(_smooth(rng, h, w), quality=90, subsampling=i % 3, progressive=i % 5 == 0))
+        ww, wh = int(rng.integers(8, w + 1)), int(rng.integers(8, h + 1))
+        wx, wy = int(rng.integers(0, w - ww + 1)), int(rng.integers(0, h - wh + 1))
+        rw, rh = int(rng.integers(16, 400)), int(rng.integers(16, 400))
+        cw, ch = int(rng.integers(1, rw + 1)), int(rng.integers(1, rh + 1))
+        cx, cy = int(rng.integers(0, rw - cw + 1)), int(rng.integers(0, rh - ch + 1))
+        geoms.append((wx, wy, ww, wh, rw, rh, cx, cy, cw, ch, i % 2))
+    coefs = [capi.JpegCoefs(d) for d in datas]
+    want = _host_ref([capi.jpeg_decode(d) for d in datas], geoms, f32)
+    got = _gpu(coefs, geoms, f32, device_dst)
+    for g, w_ in zip(got, want):
+        assert np.array_equal(g, w_)
+
+
+def test_chunked_batch_of_large_images():
+    """~150 MB of coefficients: several staging chunks over both slots."""
+    rng = np.random.default_rng(3)
+    base = [_encode(_smooth(rng, 960, 1280), quality=85, subsampling=s) for s in (0, 2)]
+    datas = [base[i % 2] for i in range(40)]
+    coefs = [capi.JpegCoefs(d) for d in datas]
+    geoms = []
+    for i, c in enumerate(coefs):
+        rw, rh = capi.resize_smallest_side_dims(c.width, c.height, 256)
+        cx, cy = capi.center_crop_origin(rw, rh, 224, 224)
+        geoms.append((0, 0, c.width, c.height, rw, rh, cx, cy, 224, 224, i % 3 == 0))
+    want = _host_ref([capi.jpeg_decode(d) for d in datas], geoms, True)
+    got = _gpu(coefs, geoms, True)
+    for g, w_ in zip(got, want):
+        assert np.array_equal(g, w_)
+
+
+def test_host_only_colour_spaces_are_refused():
+    c = capi.JpegCoefs(GOLD["cmyk_jpg"])
+    assert not c.device_ok
+    with pytest.raises(capi.MxdError, match="host"):
+        _gpu([c], [_identity(c)], False)
+
+
+@pytest.mark.parametrize("variant", ["u8", "f32", "device"])
+def test_pipeline_device_decode_on_off(variant, tmp_path):
+    from mlx_data_amd import data as dx
+
+    rng = np.random.default_rng(11)
+    samples = []
+    for i in range(37):
+        h, w = int(rng.integers(120, 520)), int(rng.integers(120, 520))
+        p = tmp_path / f"{i}.jpg"
+        if i % 9 == 4:  # grey
+            p.write_bytes(_encode(_smooth(rng, h, w, 1), quality=88))
+        else:
+            p.write_bytes(_encode(_smooth(rng, h, w), quality=88, subsampling=i % 3, progressive=i % 4 == 1))
+        samples.append(dict(image=str(p).encode(), label=i))
+    samples.append(dict(image=os.path.join(str(tmp_path), "cmyk.jpg").encode(), label=99))
+    (tmp_path / "cmyk.jpg").write_bytes(GOLD["cmyk_jpg"].tobytes())
+
+    def run(on):
+        before = dx.device_decode()
+        dx.set_device_decode(on)
+        try:
+            dx.set_state(5)
+            d = (dx.buffer_from_vector(samples).load_image("image").image_random_area_crop("image", (0.3, 1.0),
+                                                                                         (0.75, 1.33))
+                 .image_resize("image", 96, 80).image_random_h_flip("image", 0.5))
+            d = d.image_to_float("image") if variant != "u8" else d
+            d = d.batch(8, device=0) if variant == "device" else d.batch(8)
+            batches = [d[i] for i in range(len(d))]
+            return [np.asarray(b["image"].numpy() if variant == "device" else b["image"]) for b in batches]
+        finally:
+            dx.set_device_decode(before)
+
+    on, off = run(True), run(False)
+    assert len(on) == len(off) == 5
+    for a, b in zip(on, off):
+        assert a.dtype == b.dtype and np.array_equal(a, b)
