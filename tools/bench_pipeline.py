@@ -11,6 +11,9 @@ Variants per worker count:
              key_transform(lambda x: x.astype("float32") / 255))
   fused      image_to_float before batch: the kernel writes the f32 batch
   device     fused + batch(..., device=0): the batch stays in HBM (DLPack)
+  *_hostdec  the same with set_device_decode(False): the whole JPEG decode on
+             the host (default with a device: entropy decode on the host,
+             IDCT / upsampling / colour in the batch launch)
   cpu        Pillow (libjpeg-turbo) decode -> oracle C stbir restatement ->
              crop per batch on a pool of that many worker processes, numpy
              /255 of each batch in the consumer
@@ -66,6 +69,17 @@ def make_files(root, name, n):
 def run_surface(files, batch, workers, variant):
     from mlx_data_amd import data as dx
 
+    hostdec = variant.endswith("_hostdec")
+    variant = variant[:-len("_hostdec")] if hostdec else variant
+    prev = dx.device_decode()
+    dx.set_device_decode(not hostdec)
+    try:
+        return _run_surface(dx, files, batch, workers, variant)
+    finally:
+        dx.set_device_decode(prev)
+
+
+def _run_surface(dx, files, batch, workers, variant):
     samples = [dict(image=f.encode("ascii"), label=i) for i, f in enumerate(files)]
     d = (dx.buffer_from_vector(samples).shuffle().to_stream().load_image("image")
          .image_resize_smallest_side("image", 256).image_center_crop("image", 224, 224))

@@ -216,6 +216,72 @@ __global__ __launch_bounds__(256) void c2_kmix(const uint8_t* __restrict__ base,
   if (acc[0] == -1.0f) out[lane] = acc[1];
 }
 
+// Lane-ownership probe (mode 'l'): unit = (image, band, strip) as in the wave
+// kernel.  MODE 0: lane l owns 24 B at 24 l of a window starting 12-B aligned
+// (the P = 8 RGB layout: one b128 + one b64 per lane and row, each instruction
+// touching every line of the window).  MODE 1: lane l owns the 16 B at 16 l of
+// a window aligned down to 16 B (one b128 per lane and row: 1 KiB contiguous
+// per instruction).  Lanes past the strip's bytes issue no request.  Output
+// strip rows of `ob` bytes, 12 B per lane, every 3.768 source rows.
+template <int MODE, int DEPTH>
+__global__ __launch_bounds__(256) void c2_lanes(const uint8_t* __restrict__ base, float* __restrict__ out, int nbands,
+                                                int strips, int write) {
+  constexpr int LB = MODE == 0 ? 24 : 16;
+  const int lane = threadIdx.x & 63;
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int per_img = nbands * strips;
+  if (unit >= kImgs * per_img) return;
+  const int img = unit / per_img;
+  const int rest = unit - img * per_img;
+  const int band = rest / strips, strip = rest - band * strips;
+  const uint8_t* p = base + (size_t)img * kRows * kStride;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, kRows * kStride, 0x00020000);
+  // strip window: output columns [224 s / strips, 224 (s+1) / strips) need
+  // source pixels ~[x0 * 3.768 - 4, x1 * 3.768 + 4) of the footprint
+  const int ox0 = 224 * strip / strips, ox1 = 224 * (strip + 1) / strips;
+  const int px0 = max(0, (int)(ox0 * 3.768f) - 4), px1 = min(844, (int)(ox1 * 3.768f) + 4);
+  int b0 = kFb0 + 3 * px0;
+  b0 = MODE == 0 ? b0 - (b0 % 12) : b0 & ~15;
+  const int wbytes = kFb0 + 3 * px1 - b0;
+  const int voff = LB * lane < wbytes ? b0 + LB * lane : kNoLoad;
+  const int oy0 = band * kOutRows / nbands, oy1 = (band + 1) * kOutRows / nbands;
+  const int r0 = kFy0 + max(0, (int)(oy0 * 3.768f) - 4), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
+  const int ob = (ox1 - ox0) * 12;
+  char* o = reinterpret_cast<char*>(out) + (size_t)img * kOutRows * kOutRow + ox0 * 12;
+  u32x4 ra[DEPTH];
+  unsigned rb[DEPTH][2];
+  auto load = [&](int d, int row) {
+    ra[d] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, row * kStride, 0);
+    if constexpr (MODE == 0) {
+      typedef unsigned u2 __attribute__((ext_vector_type(2)));
+      const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff + 16, row * kStride, 0);
+      rb[d][0] = v.x, rb[d][1] = v.y;
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) load(d, min(r0 + d, r1 - 1));
+  float acc[4] = {0, 0, 0, 0};
+  int oy = oy0;
+  for (int row = r0; row < r1; row += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      acc[0] += (float)(ra[d].x & 255);
+      acc[1] += (float)(ra[d].y >> 24);
+      acc[2] += (float)(ra[d].z & 255) + (float)(ra[d].w >> 24);
+      if constexpr (MODE == 0) acc[3] += (float)(rb[d][0] & 255) + (float)(rb[d][1] >> 24);
+      load(d, min(row + d + DEPTH, r1 - 1));
+      const int want = (int)((row + d - r0) / 3.768f) + oy0;
+      if (write && want > oy && oy < oy1) {
+        char* orow = o + (size_t)oy * kOutRow;
+        for (int b = lane; b * 12 < ob; b += 64)
+          *reinterpret_cast<f32x3*>(orow + 12 * b) = f32x3{acc[0], acc[1], acc[2] + acc[3]};
+        oy++;
+      }
+    }
+  }
+  if (acc[0] == -1.0f) out[lane] = acc[1];
+}
+
 int g_iter = 0;  // launches alternate source / output buffers on g_iter's parity
 
 
@@ -375,6 +441,35 @@ int main(int argc, char** argv) {
                                                           3.768f, rpb, write);
           });
         }
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'l') {
+    uint8_t* src2;
+    float* out2;
+    CHECK(hipMalloc(&src2, bytes));
+    CHECK(hipMalloc(&out2, bytes));
+    CHECK(hipMemset(src2, 3, bytes));
+    const uint8_t* srcs[2] = {reinterpret_cast<const uint8_t*>(a), src2};
+    float* outs[2] = {reinterpret_cast<float*>(b), out2};
+    const double rd = (double)kImgs * (kFy1 - kFy0) * kNeed, wr = (double)kImgs * kOutRows * kOutRow;
+    struct V { const char* n; int mode, ns, nb; };
+    const V vs[] = {{"24B lanes (P=8 now) 2 strips x 8 bands", 0, 2, 8},
+                    {"16B lanes aligned 3 strips x 5 bands", 1, 3, 5},
+                    {"16B lanes aligned 3 strips x 6 bands", 1, 3, 6},
+                    {"16B lanes aligned 3 strips x 10 bands", 1, 3, 10},
+                    {"16B lanes aligned 4 strips x 4 bands", 1, 4, 4},
+                    {"24B lanes (P=8 now) 2 strips x 8 bands (again)", 0, 2, 8}};
+    for (const V& v : vs)
+      for (int write : {0, 1}) {
+        const int units = kImgs * v.nb * v.ns;
+        snprintf(name, sizeof name, "%s w=%d", v.n, write);
+        timeit(name, rd + (write ? wr : 0), [&] {
+          const uint8_t* src = srcs[g_iter & 1];
+          float* out = outs[g_iter & 1];
+          if (v.mode == 0) c2_lanes<0, 6><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, write);
+          else c2_lanes<1, 6><<<(units + 3) / 4, 256>>>(src, out, v.nb, v.ns, write);
+        });
+      }
     return 0;
   }
   if (argc > 1 && argv[1][0] == 'k') {
