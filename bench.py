@@ -6,7 +6,12 @@ image_resize_smallest_side(256) -> image_center_crop(224, 224) -> float32 / 255,
 one fused kernel launch per step over the whole batch (one "step" = one pass
 of the hot path over one batch).  Two source sets and two output batches
 alternate step by step (different HBM addresses), so no step re-reads bytes
-the previous one left in the 256 MiB Infinity Cache.
+the previous one left in the 256 MiB Infinity Cache.  Consecutive steps are
+independent batches and alternate over two HIP streams (`--streams`, each
+stream with its own sets), the way the pipeline's prefetch workers each launch
+on their own stream: one batch's drain overlaps the next one's start.  `value`
+is images / wall time of the K steps; the roofline's per-launch kernel time is
+measured separately, the same launches back to back on ONE stream.
 
 Multi-GPU: one process per GPU.  `--gpus N` without a launcher spawns N rank
 processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
@@ -25,7 +30,9 @@ Extra fields:
   roofline      HBM roofline of the fused kernel: algorithmic bytes per launch
                 (source footprint the kept window depends on + output bytes, per
                 image, summed over the batch) / average launch time from HIP
-                events recorded on the kernel's own stream; `traffic` = HBM bytes
+                events recorded on the kernel's own stream (launches back to
+                back on one stream); `sustained_gbs` = the same bytes per step
+                / the timed wall per step (streams overlapped); `traffic` = HBM bytes
                 per launch from the PMC summary recorded for this workload in
                 profiles/traffic.json; `copy_ceiling_gbs` = the measured
                 streaming-copy rate of this box.
@@ -339,6 +346,8 @@ def main():
     ap.add_argument("--policy", type=int, default=0, help=argparse.SUPPRESS)
     # input/output sets that alternate step by step (1 = every step re-reads the same batch)
     ap.add_argument("--sets", type=int, default=2, help=argparse.SUPPRESS)
+    # streams the timed steps alternate over (independent batches, like prefetch workers)
+    ap.add_argument("--streams", type=int, default=2)
     # timing plumbing without a GPU (tests/test_bench_dist.py): each step sleeps
     ap.add_argument("--simulate", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -386,11 +395,16 @@ def main():
         for (sw, sh), o, pt in zip(sizes, offs, pitches):
             host[o:o + pt * sh] = base[:pt * sh]
     stream = capi.Stream(dev)
+    streams = [stream] + [capi.Stream(dev) for _ in range(max(1, args.streams) - 1)]
     mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
     L = capi.lib()
     hs = ctypes.c_void_p(stream.handle)
     sets = []
-    for _ in range(max(1, args.sets)):
+    # a stream never shares its input/output set with another stream
+    nsets = max(1, args.sets)
+    if args.streams > 1:
+        nsets = (nsets + args.streams - 1) // args.streams * args.streams
+    for _ in range(nsets):
         src = capi.DeviceBuffer(total, dev)
         dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
         src.upload(host, stream=stream)
@@ -401,20 +415,28 @@ def main():
         imgs, n = capi.make_images(entries)
         sets.append((src, dst, imgs, n))
 
-    def step(i):
-        _, _, imgs, n = sets[i % len(sets)]
-        capi.check(L.mxd_resize_crop_batch(imgs, n, mode, dev, hs))
+    shs = [ctypes.c_void_p(s.handle) for s in streams]
 
-    for i in range(args.warmup):
+    def step(i, ns=len(streams)):
+        _, _, imgs, n = sets[i % len(sets)]
+        capi.check(L.mxd_resize_crop_batch(imgs, n, mode, dev, shs[i % ns]))
+
+    def sync_all():
+        for s in streams:
+            s.synchronize()
+
+    for i in range(args.warmup + len(streams)):
         step(i)
+    wall, _ = timed_steps(ranks, step, sync_all, args.steps)
+    # Per-launch kernel time for the roofline: the same launches back to back
+    # on ONE stream, bracketed by HIP events on that stream (the kernel's own).
     e0, e1 = capi.Event(), capi.Event()
-    stream.synchronize()
+    sync_all()
     e0.record(stream)
-    wall, _ = timed_steps(ranks, step, stream.synchronize, args.steps)
+    for i in range(args.steps):
+        step(i, 1)
     e1.record(stream)
     stream.synchronize()
-    # The events bracket exactly the timed launches on the kernel's stream (the
-    # barrier and host syncs between them add no device work).
     kernel_ms = e0.elapsed_ms(e1) / args.steps
 
     # The same launches with descriptor caching off: every batch uploads its
@@ -427,7 +449,7 @@ def main():
         stream.synchronize()
         e0.record(stream)
         for i in range(k):
-            step(i)
+            step(i, 1)
         e1.record(stream)
         stream.synchronize()
         fresh_ms = e0.elapsed_ms(e1) / k
@@ -440,6 +462,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.workload),
                 "alg_bytes_per_launch": int(alg_bytes), "alg_bytes_per_image": round(alg_bytes / B, 1),
                 "kernel_ms_per_launch": round(kernel_ms, 5),
+                "sustained_gbs": round(alg_bytes / (wall / max(1, args.steps)) / 1e9, 1) if args.steps else None,
                 "ms_per_launch_fresh_descriptors": round(fresh_ms, 5) if fresh_ms else None,
                 "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
                 "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None}
@@ -456,8 +479,10 @@ def main():
         src.free()
         dst.free()
     if ranks.rank == 0:
-        print(json.dumps(bench_line(args.workload, ranks.world, B, args.steps, args.warmup, wall, roofline, cpu,
-                                    e2e, manifest(capi, dev))), flush=True)
+        line = bench_line(args.workload, ranks.world, B, args.steps, args.warmup, wall, roofline, cpu, e2e,
+                          manifest(capi, dev))
+        line["config"]["streams"] = len(streams)
+        print(json.dumps(line), flush=True)
     ranks.close()
 
 
