@@ -39,7 +39,8 @@ Extra fields:
   cpu_baseline  the oracle's C restatement of the reference CPU path
                 (stbir-semantics resize -> crop -> batch -> numpy /255) on a
                 bounded sample at 1, 8 and all of this rank's cores (rank 0,
-                N = 1, c2 only), with Pillow BILINEAR as an independent CPU point.
+                N = 1, c2 only), with Pillow BILINEAR and torch-CPU bilinear
+                antialias on all cores as independent CPU points.
   e2e           the product's host-resident path (mxd_resize_crop_host: host
                 images in, host batch out, pinned staging of each image's
                 source footprint, H2D / kernel / D2H overlapped in chunks):
@@ -208,12 +209,32 @@ def cpu_baseline(sample_per_thread=24):
         pil = round(nb * per_batch / dt, 2)
     except ImportError:
         pass
+    tch = None
+    try:
+        # torch CPU: uint8 NCHW (channels-last) bilinear with antialias (the
+        # tent filter stbir uses when downsampling), intra-op threads = cores
+        import torch
+        import torch.nn.functional as F
+
+        prev = torch.get_num_threads()
+        torch.set_num_threads(cores)
+        tsrc = torch.from_numpy(np.stack(srcs)).permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+        nb = max(1, cores * sample_per_thread // per_batch)
+        t0 = time.perf_counter()
+        for b in range(nb):
+            r = F.interpolate(tsrc, size=(256, 341), mode="bilinear", antialias=True, align_corners=False)
+            _ = r[:, :, 16:240, 58:282].permute(0, 2, 3, 1).float() / 255
+        tch = round(nb * per_batch / (time.perf_counter() - t0), 2)
+        torch.set_num_threads(prev)
+    except Exception:  # noqa: BLE001  (an extra CPU point never fails the bench)
+        pass
     return {"value": points[str(cores)], "unit": "images/s", "cores": cores, "kind": "port",
-            "points": points, "pillow_bilinear": pil,
+            "points": points, "pillow_bilinear": pil, "torch_cpu_antialias": tch,
             "sample": f"C2 shapes (1280x960 -> resize 256 -> crop 224 -> batch {per_batch} -> f32/255), "
                       f"{sample_per_thread} images per thread per point; oracle C restatement of stbir + numpy "
                       f"normalize, threads = cores; pillow_bilinear = Pillow resize(BILINEAR) + crop + /255 "
-                      f"on all cores (independent CPU point)"}
+                      f"on all cores, torch_cpu_antialias = torch interpolate(bilinear, antialias) on uint8 + crop + /255 "
+                      f"with cores intra-op threads (independent CPU points)"}
 
 
 class Ranks:
