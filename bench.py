@@ -93,13 +93,14 @@ def footprint_bytes(capi, src_w, src_h, c, rw, rh, cx, cy, cw, ch):
     return rows * cols * c
 
 
-def make_workload(capi, name, batch, rank):
+def make_workload(capi, name, batch, rank, c3_sizes=None):
     """(sizes [(w, h)], geoms [(rw, rh, cx, cy, cw, ch, flip)], f32) for one rank."""
     if name == "c2":
         sizes = [(1280, 960)] * batch
     elif name == "c3":
         rng = np.random.default_rng(1)
-        sizes = [C3_SIZES[i] for i in rng.integers(0, len(C3_SIZES), batch)]
+        pool = c3_sizes or C3_SIZES
+        sizes = [pool[i] for i in rng.integers(0, len(pool), batch)]
     elif name == "c4":
         rng = np.random.default_rng(2)
         sizes = [C4_SIZES[i] for i in rng.integers(0, len(C4_SIZES), batch)]
@@ -365,6 +366,8 @@ def main():
     ap.add_argument("--no-copy", action="store_true")
     # kernel policy (include/mxd_amd.h mxd_policy; tuning measurements only)
     ap.add_argument("--policy", type=int, default=0, help=argparse.SUPPRESS)
+    # tuning: C3 drawn from these sizes only ("WxH,WxH")
+    ap.add_argument("--c3-sizes", default="", help=argparse.SUPPRESS)
     # input/output sets that alternate step by step (1 = every step re-reads the same batch)
     ap.add_argument("--sets", type=int, default=2, help=argparse.SUPPRESS)
     # streams the timed steps alternate over (independent batches, like prefetch workers)
@@ -395,7 +398,8 @@ def main():
     capi.check(capi.lib().mxd_set_device(dev))
     if args.policy:
         capi.set_kernel_policy(args.policy)
-    sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank)
+    c3_sizes = [tuple(int(v) for v in t.split("x")) for t in args.c3_sizes.split(",") if t]
+    sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank, c3_sizes)
     elem = 4 if f32 else 1
 
     # Sources packed in one device buffer per set (256-B aligned slots, rows

@@ -122,23 +122,29 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
  * MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
  * of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
  * general workgroup-tile kernel; MXD_POLICY_NARROW: wave kernels keep the
- * narrow per-lane window (no wide RGB strips); MXD_POLICY_NO_DESC_CACHE:
- * every batch uploads its descriptor array even when a cached slot holds the
- * same bytes (measures the per-batch upload of fresh descriptors).  Returns
- * the previous policy. */
+ * narrow per-lane window (no wide RGB strips, no byte lanes);
+ * MXD_POLICY_NO_DESC_CACHE: every batch uploads its descriptor array even
+ * when a cached slot holds the same bytes (measures the per-batch upload of
+ * fresh descriptors); MXD_POLICY_NO_BYTES: RGB scatter kernels keep whole
+ * pixels per lane instead of 16 contiguous bytes per lane (by default byte
+ * lanes run where they need no more strips); MXD_POLICY_BYTES: byte lanes
+ * wherever a kernel exists.  Returns the previous policy. */
 enum mxd_policy {
   MXD_POLICY_AUTO = 0,
   MXD_POLICY_NO_SCATTER = 1,
   MXD_POLICY_NO_WAVE = 2,
   MXD_POLICY_NARROW = 4,
-  MXD_POLICY_NO_DESC_CACHE = 8
+  MXD_POLICY_NO_DESC_CACHE = 8,
+  MXD_POLICY_NO_BYTES = 16,
+  MXD_POLICY_BYTES = 32
 };
 int mxd_set_kernel_policy(int32_t policy);
 
 /* The kernel mxd_resize_crop_batch would run for one image on `device`
  * (diagnostics, tests): info[0] = 1 wave kernel / 0 general kernel, then kind
  * (0 gather, 2 scatter), tap bucket, scatter S, scatter DMAX, output pixels
- * per lane, strips, source pixels per lane.  Host only: needs no device. */
+ * per lane, strips, source pixels per lane (RGB 16: byte lanes, 16 bytes per
+ * lane).  Host only: needs no device. */
 int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device, int32_t* info8);
 
 /* Measured device-memory ceiling: a 16-byte-per-lane streaming copy of `bytes`

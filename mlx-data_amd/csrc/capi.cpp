@@ -559,6 +559,44 @@ bool wave_layout_ok(const mxd_image& im, const Stored& st, int32_t out_dtype) {
          st.stride * (int64_t)st.rows < ((int64_t)1 << 31);
 }
 
+// Byte-lane strips (RGB, wave_byte_lanes): every strip's source span, from
+// the 16-byte boundary at or below its first byte (relative to the 4-byte
+// aligned stored base), fits the byte window, and its 16-byte chunks rounded
+// up stay inside the row stride (so the last stored row never reads past the
+// buffer's records).  Fewest strips first, then the smallest q.
+bool wave_strips_bytes(const DevTable& xt, const mxd_image& im, const Stored& st, int32_t* nstrips, int32_t* tx,
+                       int32_t* q) {
+  const int32_t c = im.channels, win = mxd::wave_byte_window();
+  const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(st.base) & 3);
+  int32_t best = 0;
+  for (int32_t qq : {1, 2, 4}) {
+    const int32_t max_tx = mxd::wave_lanes() * qq;
+    for (int32_t ns = (im.crop_w + max_tx - 1) / max_tx; ns <= im.crop_w && (best == 0 || ns < best); ns++) {
+      const int32_t t = (im.crop_w + ns - 1) / ns;
+      if ((im.crop_w + t - 1) / t != ns) continue;
+      bool ok = true;
+      for (int32_t ox0 = 0; ox0 < im.crop_w && ok; ox0 += t) {
+        const int32_t ox1 = std::min(ox0 + t, im.crop_w);
+        const int32_t xa = im.flip ? im.crop_w - ox1 : ox0;
+        const int32_t xb = im.flip ? im.crop_w - 1 - ox0 : ox1 - 1;
+        const int32_t lo = xt.first[im.crop_x + xa];
+        const int32_t hi = xt.first[im.crop_x + xb] + xt.count[im.crop_x + xb] - 1;
+        const int64_t b0 = ((int64_t)(lo - st.x0) * c + shift) & ~(int64_t)15;
+        const int64_t nb = (int64_t)(hi + 1 - st.x0) * c + shift - b0;
+        ok = nb <= win && b0 + (nb + 15) / 16 * 16 <= st.stride;
+      }
+      if (ok) {
+        best = ns;
+        *nstrips = ns;
+        *tx = t;
+        *q = qq;
+        break;
+      }
+    }
+  }
+  return best > 0;
+}
+
 // Chooses the wave kernel of one image (p.wave = false: the general kernel):
 // over the lane widths available for its channel count, the one that cuts
 // the crop into the fewest strips (narrow strips read more halo and more,
@@ -575,7 +613,8 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
   const int32_t xb = mxd::wave_taps_bucket(p.xt->width);
   const int32_t gb = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
   const int32_t dp = mxd::wave_default_p(c);
-  const int32_t widths[2] = {dp, c == 3 && !(g_policy.load() & MXD_POLICY_NARROW) ? 8 : dp};
+  const int32_t policy = g_policy.load();
+  const int32_t widths[2] = {dp, c == 3 && !(policy & MXD_POLICY_NARROW) ? 8 : dp};
   for (int32_t pp : widths) {
     if (p.wave && pp == p.pp) continue;
     int32_t ns = 0, tx = 0, q = 0;
@@ -602,6 +641,29 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
     }
     cand.wave = true;
     p = cand;
+  }
+  // RGB scatter: byte lanes (one 1-KiB contiguous load per wave and row)
+  // when they cut the crop into no more strips than pixel lanes do, at <= 2
+  // output pixels per lane (measured: 720p -> 224 with two strips 4 % faster;
+  // with more strips -- their narrower 341-pixel window -- or a single 224-column
+  // strip (C4) pixel lanes were 2-10 % faster; profiles/r02/bytes_ab.txt).
+  if (c == 3 && sh.s > 0 && xb > 0 && !(policy & (MXD_POLICY_NO_BYTES | MXD_POLICY_NARROW))) {
+    int32_t ns = 0, tx = 0, q = 0;
+    if (wave_strips_bytes(*p.xt, im, st, &ns, &tx, &q) &&
+        ((policy & MXD_POLICY_BYTES) || !p.wave || p.kind != 2 || (ns <= p.nstrips && q <= 2)) &&
+        mxd::wave_has_kernel(mxd::WaveCfg{c, f32, xb, 0, 0, 2, sh.s, sh.dmax, q, 0, 16})) {
+      p.wave = true;
+      p.nstrips = ns;
+      p.tx = tx;
+      p.q = q;
+      p.pp = 16;
+      p.shift = 0;
+      p.kind = 2;
+      p.bucket = xb;
+      p.s = sh.s;
+      p.dmax = sh.dmax;
+      p.p = sh.p;
+    }
   }
 }
 
@@ -741,7 +803,9 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       d.tile_begin = g.units;
       d.nstrips = p.nstrips;
       d.tx = p.tx;
-      g.units += d.nstrips * ((im.crop_h + d.ty - 1) / d.ty);
+      const int32_t u = d.nstrips * ((im.crop_h + d.ty - 1) / d.ty);
+      g.cfg.per_img = k == g.first ? u : (g.cfg.per_img == u ? u : 0);
+      g.units += u;
     }
     g.cfg.nunits = g.units;
   }

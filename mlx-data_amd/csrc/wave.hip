@@ -101,17 +101,28 @@ using Rsrc = __amdgpu_buffer_rsrc_t;
 
 enum Kind { kGather = 0, kScatter = 2 };
 
-// Per-channel-count layout: P source pixels (P*C bytes) per lane; the
-// default P fills 16 bytes (12 for RGB), P = 8 widens an RGB window to 512
-// pixels (fewer, wider strips per row).
+// Lane layouts.  Pixel lanes (planar): P source pixels (P*C bytes) per lane;
+// the default P fills 16 bytes (12 for RGB), P = 8 widens an RGB window to
+// 512 pixels (fewer, wider strips per row); the V pass keeps C channel planes.
+// Byte lanes (RGB with P = 16, `B`): lane l owns the 16 bytes at 16 l of a
+// 1-KiB window, so every row load is one b128 per lane and 1 KiB contiguous
+// per wave-instruction; the V pass runs on bytes in memory order (it is
+// per-byte anyway) and the LDS row keeps that order, so the H pass reads
+// channel c of pixel x at float C x + c.
 template <int C_, int P_ = (C_ == 1 ? 16 : C_ == 2 ? 8 : 4)>
 struct Lay {
   static constexpr int C = C_;
   static constexpr int P = P_;
-  static constexpr int LB = P * C;      // bytes per lane
-  static constexpr int ND = LB / 4;     // dwords per lane
-  static constexpr int WPX = kLanes * P;  // window pixels
-  static constexpr int PL = WPX + kPad;   // floats per plane
+  static constexpr bool B = C == 3 && P == 16;  // byte lanes
+  static constexpr int VC = B ? 1 : C;          // V-pass planes
+  static constexpr int LB = B ? 16 : P * C;     // bytes per lane
+  static constexpr int ND = LB / 4;             // dwords per lane
+  static constexpr int VP = LB / VC;            // V-pass values per lane and plane
+  static constexpr int WPX = kLanes * VP;       // window pixels (byte lanes: bytes)
+  static constexpr int PAD = B ? 64 : kPad;     // zeroed floats past each plane (padded taps)
+  static constexpr int PL = WPX + PAD;          // floats per plane
+  static constexpr int HS = B ? C : 1;          // floats between adjacent pixels of a plane
+  static constexpr int CS = B ? 1 : PL;         // floats between the channels of a pixel
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int n) {
@@ -240,8 +251,8 @@ __device__ __forceinline__ void zero_planes(float (&acc)[C][P]) {
 
 // V sums -> the wave's LDS planes (lane l: pixels P l .. P l + P - 1).
 template <class L>
-__device__ __forceinline__ void write_planes(float* planes, const float (&acc)[L::C][L::P], int lane) {
-  constexpr int C = L::C, P = L::P;
+__device__ __forceinline__ void write_planes(float* planes, const float (&acc)[L::VC][L::VP], int lane) {
+  constexpr int C = L::VC, P = L::VP;
 #pragma unroll
   for (int c = 0; c < C; c++)
 #pragma unroll
@@ -266,18 +277,14 @@ __device__ __forceinline__ const ImgDev& find_image(const ImgDev* imgs, int nimg
   return imgs[lo];
 }
 
-// Window of output columns [ox0, ox1): first source pixel wp0 (aligned so that
-// wp0 * C is a multiple of 4) and pixel count (<= WPX, checked on the host).
-template <int C>
-__device__ __forceinline__ void strip_window(cgfloat* xtab, int xs, int crop_w, int flip, int ox0, int ox1, int* wp0,
-                                             int* npx) {
-  constexpr int A = C == 2 ? 2 : C == 4 ? 1 : 4;
+// Window of output columns [ox0, ox1): first and last source pixel their taps
+// read.
+__device__ __forceinline__ void strip_span(cgfloat* xtab, int xs, int crop_w, int flip, int ox0, int ox1, int* lo,
+                                           int* hi) {
   const int xa = flip ? crop_w - ox1 : ox0;
   const int xb = flip ? crop_w - 1 - ox0 : ox1 - 1;
-  const int lo = __float_as_int(xtab[xa * xs]);
-  const int hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
-  *wp0 = lo & ~(A - 1);
-  *npx = hi + 1 - *wp0;
+  *lo = __float_as_int(xtab[xa * xs]);
+  *hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
 }
 
 // Horizontal pass of one strip: lane l owns output pixels l + 64 q (q < Q).
@@ -288,7 +295,8 @@ struct HStrip {
   int pos[Q];  // first tap, in pixels from the window start
   int npx;     // output pixels of the strip
 
-  __device__ __forceinline__ void init(cgfloat* xtab, int xs, int crop_w, int flip, int ox0, int ox1, int wp0,
+  // base: pos = first tap * HS - base is the first tap's float in a plane
+  __device__ __forceinline__ void init(cgfloat* xtab, int xs, int crop_w, int flip, int ox0, int ox1, int base,
                                        int lane) {
     npx = ox1 - ox0;
 #pragma unroll
@@ -297,7 +305,7 @@ struct HStrip {
       const int ox = ox0 + px;
       const int xc = flip ? crop_w - 1 - ox : ox;
       cgfloat* xe = xtab + xc * xs;
-      pos[q] = __float_as_int(xe[0]) - wp0;
+      pos[q] = __float_as_int(xe[0]) * L::HS - base;
 #pragma unroll
       for (int k = 0; k < T; k++) wx[q][k] = xe[kTapHeader + k];  // zero padded past the tap count
     }
@@ -312,10 +320,10 @@ struct HStrip {
       float s[C];
 #pragma unroll
       for (int c = 0; c < C; c++) {
-        const float* pl = planes + c * L::PL + pos[q];
+        const float* pl = planes + c * L::CS + pos[q];
         float a = 0.0f;
 #pragma unroll
-        for (int k = 0; k < T; k++) a = __builtin_fmaf(wx[q][k], pl[k], a);
+        for (int k = 0; k < T; k++) a = __builtin_fmaf(wx[q][k], pl[k * L::HS], a);
         s[c] = encode(a);
       }
       if (q > 0 && kLanes * q >= npx) break;  // uniform: no lane has pixels left
@@ -349,15 +357,15 @@ struct HStrip {
 
 // Runs a band's scatter schedule (see the top of the file); on_row(acc, y) is
 // called with the V sums of every completed output row y.
-template <class L, int S, int DMAX, bool SHIFT, class OnRow>
+template <class L, int S, int DMAX, bool SHIFT, class OnRow, class Start>
 __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const Src<L, SHIFT>& src, OnRow&& on_row,
-                                             bool sync = false) {
-  constexpr int C = L::C;
+                                             Start&& start, bool sync = false) {
+  constexpr int C = L::VC;
   constexpr int R = scatter_ring_slots(DMAX);
   constexpr int LA = R - 1;  // iterations loaded ahead
   constexpr int BG = scatter_block_groups(S, DMAX);
   constexpr int E = scatter_entry_words(S);
-  constexpr int P = L::P;
+  constexpr int P = L::VP;
   const int ngroups = sched[0];
   kint* gout = sched + 1;
   kint* itab = sched + entry_off;
@@ -369,6 +377,8 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
     __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's counted waits assume it
     ring[decltype(ic)::value] = src.load(itab[decltype(ic)::value * E + 1]);
   });
+  __builtin_amdgcn_sched_barrier(0);
+  start();  // after the prologue loads (see resample_wave)
   __builtin_amdgcn_sched_barrier(0);
   for (int gb = 0; gb < ngroups; gb += BG) {
     kint* blk = itab + gb * DMAX * E;
@@ -407,21 +417,30 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
   }
 }
 
+// bytes per lane of Lay<c, p> (a plain function: template arguments do not
+// parse inside __launch_bounds__)
+constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; }
+
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
-__global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES) void resample_wave(const ImgDev* __restrict__ imgs, int nimgs,
-                                                                    int nunits) {
+__global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES) void resample_wave(
+    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = Lay<C, P>;
   constexpr int PL = L::PL;
+  constexpr int VC = L::VC, VP = L::VP;
   const int lane = threadIdx.x & (kLanes - 1);
   const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
-  float* __restrict__ planes = smem + (threadIdx.x >> 6) * (C * PL);
+  float* __restrict__ planes = smem + (threadIdx.x >> 6) * (VC * PL);
 #pragma unroll
-  for (int c = 0; c < C; c++)
-    if (lane < kPad) planes[c * PL + L::WPX + lane] = 0.0f;  // padded taps read zeros
+  for (int c = 0; c < VC; c++)
+#pragma unroll
+    for (int i = 0; i < L::PAD; i += kLanes)
+      if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
   if (unit >= nunits) return;
 
-  const ImgDev& im = find_image(imgs, nimgs, unit);
+  // per_img > 0: every image has per_img units (no search: the wave issues
+  // its first row loads one dependent descriptor load after it starts)
+  const ImgDev& im = per_img > 0 ? imgs[unit / per_img] : find_image(imgs, nimgs, unit);
   const int nstrips = __builtin_amdgcn_readfirstlane(im.nstrips);
   const int crop_w = __builtin_amdgcn_readfirstlane(im.crop_w);
   const int crop_h = __builtin_amdgcn_readfirstlane(im.crop_h);
@@ -445,9 +464,11 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
   const int ox0 = strip * strip_cols;
   const int ox1 = min(ox0 + strip_cols, crop_w);
 
-  int wp0, npx;
-  strip_window<C>(xtab, xs, crop_w, flip, ox0, ox1, &wp0, &npx);
+  int lo, hi;
+  strip_span(xtab, xs, crop_w, flip, ox0, ox1, &lo, &hi);
+  const int sx0 = __builtin_amdgcn_readfirstlane(im.src_x0);
   Src<L, SHIFT> src;
+  int hbase;  // HStrip base (see HStrip::init)
   {
     void* base = uniform_ptr<void*>(im.src);
     const int stride = __builtin_amdgcn_readfirstlane((int)im.src_stride);
@@ -456,26 +477,44 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
     src.dead = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0, 0x00020000);
     src.stride = stride;
     src.y0 = __builtin_amdgcn_readfirstlane(im.src_y0);
-    // window start, bytes past the 4-byte aligned base of the stored region
-    const int fbyte = (wp0 - __builtin_amdgcn_readfirstlane(im.src_x0)) * C + shift;
-    src.sh = fbyte & 3;
-    src.voff = P * lane < npx ? (fbyte & ~3) + L::LB * lane : kNoLoad;
+    if constexpr (L::B) {
+      // byte lanes: window = the span's bytes from a 16-byte boundary past the
+      // 4-byte aligned base (the host checked it fits 1 KiB and, 16-byte chunks
+      // rounded up, stays inside the row's stride)
+      const int b0 = ((lo - sx0) * C + shift) & ~15;
+      const int nb = (hi + 1 - sx0) * C + shift - b0;
+      src.sh = 0;
+      src.voff = L::LB * lane < nb ? b0 + L::LB * lane : kNoLoad;
+      hbase = sx0 * C - shift + b0;
+    } else {
+      constexpr int A = C == 2 ? 2 : C == 4 ? 1 : 4;  // wp0 * C a multiple of 4
+      const int wp0 = lo & ~(A - 1);
+      const int npx = hi + 1 - wp0;
+      // window start, bytes past the 4-byte aligned base of the stored region
+      const int fbyte = (wp0 - sx0) * C + shift;
+      src.sh = fbyte & 3;
+      src.voff = P * lane < npx ? (fbyte & ~3) + L::LB * lane : kNoLoad;
+      hbase = wp0;
+    }
   }
   HStrip<L, F32, T, Q> hs;
-  hs.init(xtab, xs, crop_w, flip, ox0, ox1, wp0, lane);
-  // The horizontal weights are loaded once; retire them here so the waits the
-  // compiler places in the row loop only ever cover the row loads.
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  // The horizontal weights are loaded once, right after the band's first row
+  // loads (their latencies overlap), and retired together with those rows, so
+  // the waits the compiler places in the row loop only ever cover row loads.
+  auto start = [&] {
+    hs.init(xtab, xs, crop_w, flip, ox0, ox1, hbase, lane);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  };
 
   char* dcol = dst + (int64_t)ox0 * C * (F32 ? 4 : 1);
   // V row of output row y done: planes to LDS, H pass and store.
-  auto finish_row = [&](const float (&acc)[C][P], int y) {
+  auto finish_row = [&](const float (&acc)[VC][VP], int y) {
     if constexpr ((MXD_ABLATE & 4) != 0) {
       float t = 0.0f;
 #pragma unroll
-      for (int c = 0; c < C; c++)
+      for (int c = 0; c < VC; c++)
 #pragma unroll
-        for (int p = 0; p < P; p++) t += acc[c][p];
+        for (int p = 0; p < VP; p++) t += acc[c][p];
       if (t == -1.0f) planes[lane] = t;
       GLOBAL_PTR(float, dcol + (int64_t)y * dstride)[lane] = 0.0f;
       return;
@@ -495,13 +534,13 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
     };
     auto step = [&](const Raw<L::ND>* R, int y) {
       kfloat* ye = ytab + y * ys;
-      float acc[C][P];
-      zero_planes<C, P>(acc);
+      float acc[VC][VP];
+      zero_planes<VC, VP>(acc);
 #pragma unroll
       for (int k = 0; k < T; k++) {  // zero padded past the tap count
-        float x[C][P];
-        to_planes<C, P>(R[k], x);
-        fma_planes<C, P>(acc, ye[kTapHeader + k], x);
+        float x[VC][VP];
+        to_planes<VC, VP>(R[k], x);
+        fma_planes<VC, VP>(acc, ye[kTapHeader + k], x);
       }
       finish_row(acc, y);
     };
@@ -512,6 +551,7 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
     // stay partial.
     Raw<L::ND> RA[T], RB[T];
     load_rows(RA, oy0, true);
+    start();
     for (int y = oy0;; y += 2) {
       load_rows(RB, min(y + 1, crop_h - 1), y + 1 < oy1);
       step(RA, y);
@@ -523,12 +563,12 @@ __global__ __launch_bounds__(kWaves* kLanes, P * C > 16 ? MXD_MIN_WAVES_WIDE : M
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row,
+    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start,
                                     nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0);
   }
 }
 
-using WaveKernel = void (*)(const ImgDev*, int, int);
+using WaveKernel = void (*)(const ImgDev*, int, int, int);
 
 constexpr int default_p(int c) { return c == 1 ? 16 : c == 2 ? 8 : 4; }
 
@@ -576,6 +616,10 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == P_)              \
     return cfg.shift ? resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, true>                  \
                      : resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, false>;
+  // byte lanes (P = 16): any base alignment, no realignment variant
+#define MXD_SCATTER_B(S_, D_, T_, Q_)                                                             \
+  if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == 16)              \
+    return resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false>;
   MXD_SCATTER(2, 4, 8, 2, 8)    // 960 -> 256 (C2)
   MXD_SCATTER(2, 4, 8, 1, 4)
   MXD_SCATTER(2, 5, 10, 2, 8)   // 1080 -> 256, 2160 -> 512 (C5)
@@ -591,6 +635,21 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   MXD_SCATTER(2, 2, 3, 2, 4)    // 375 / 333 -> 256 (C4)
   MXD_SCATTER(2, 2, 3, 4, 8)
   MXD_SCATTER(3, 1, 2, 4, 4)    // upsampling (200 -> 256)
+  // byte lanes: 1 KiB windows (341 RGB pixels) per strip row
+  MXD_SCATTER_B(2, 4, 8, 2)     // 960 -> 256 (C2: 3 strips of 75)
+  MXD_SCATTER_B(2, 4, 8, 1)
+  MXD_SCATTER_B(2, 5, 10, 2)    // 1080 -> 256, 2160 -> 512 (C5: 6 strips of 75)
+  MXD_SCATTER_B(2, 5, 10, 1)
+  MXD_SCATTER_B(2, 6, 12, 1)    // 1440 -> 256 (4 strips of 56)
+  MXD_SCATTER_B(2, 6, 12, 2)
+  MXD_SCATTER_B(2, 9, 17, 1)    // 2160 -> 256 (6 strips of 38)
+  MXD_SCATTER_B(2, 3, 6, 2)     // 720 -> 256 (2 strips of 112)
+  MXD_SCATTER_B(2, 2, 4, 2)     // 480 -> 256
+  MXD_SCATTER_B(2, 2, 4, 4)
+  MXD_SCATTER_B(2, 2, 3, 4)     // 375 / 333 -> 256 (C4: one strip)
+  MXD_SCATTER_B(2, 2, 3, 2)
+  MXD_SCATTER_B(3, 1, 2, 4)     // upsampling (200 -> 256)
+#undef MXD_SCATTER_B
 #undef MXD_SCATTER
   return nullptr;
 }
@@ -610,6 +669,11 @@ WaveKernel select_kernel(const WaveCfg& cfg) {
 
 int lds_bytes(const WaveCfg& cfg) { return kWaves * wave_plane_floats(cfg.channels, cfg.p) * (int)sizeof(float); }
 
+template <int C, int P>
+constexpr int plane_floats() {
+  return Lay<C, P>::VC * Lay<C, P>::PL;
+}
+
 }  // namespace
 
 int wave_taps_bucket(int taps) {
@@ -625,7 +689,14 @@ int wave_window_px(int channels, int p) { return kLanes * p; }
 
 int wave_window_align(int channels) { return channels == 2 ? 2 : channels == 4 ? 1 : 4; }
 
-int wave_plane_floats(int channels, int p) { return channels * (kLanes * p + kPad); }
+bool wave_byte_lanes(int channels, int p) { return channels == 3 && p == 16; }
+
+int wave_byte_window() { return kLanes * 16; }
+
+int wave_plane_floats(int channels, int p) {
+  if (wave_byte_lanes(channels, p)) return plane_floats<3, 16>();
+  return channels * (kLanes * p + kPad);
+}
 
 int wave_lanes() { return kLanes; }
 
@@ -652,7 +723,7 @@ int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
   if (!k) return -2;
   const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
-                     imgs, cfg.nimgs, cfg.nunits);
+                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

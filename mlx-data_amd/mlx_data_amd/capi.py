@@ -41,6 +41,8 @@ MXD_POLICY_NO_SCATTER = 1
 MXD_POLICY_NO_WAVE = 2
 MXD_POLICY_NARROW = 4
 MXD_POLICY_NO_DESC_CACHE = 8
+MXD_POLICY_NO_BYTES = 16
+MXD_POLICY_BYTES = 32
 
 
 class MxdImage(ctypes.Structure):

@@ -96,3 +96,52 @@ def test_channel_count_checked_like_verify_image():
     with pytest.raises(capi.MxdError, match="channels must be 0 <= c <= 4") as e:
         capi.resize_crop_batch(arr, n, capi.MXD_U8)
     assert e.value.code == 1
+
+
+def _entry(w=1280, h=960, stride=None, rw=341, rh=256, cx=58, cy=16, **kw):
+    e = dict(src_w=w, src_h=h, src_stride=stride or w * 3, channels=3, resize_w=rw, resize_h=rh, crop_x=cx,
+             crop_y=cy, crop_w=224, crop_h=224, flip=0, dst_stride=224 * 3 * 4)
+    e.update(kw)
+    return e
+
+
+def _plan(entry, policy=0):
+    prev = capi.set_kernel_policy(policy)
+    try:
+        return capi.describe_plan(entry, capi.MXD_F32_DIV255)
+    finally:
+        capi.set_kernel_policy(prev)
+
+
+def test_rgb_scatter_lane_layouts():
+    """RGB scatter plans (host only): byte lanes (p = 16: 16 contiguous bytes
+    per lane, 1-KiB windows) when they need no more strips than pixel lanes at
+    <= 2 output pixels per lane -- 720p -> 224, two strips -- and pixel lanes
+    otherwise: C2's 960 -> 256 takes two 512-pixel strips with pixel lanes,
+    three with byte lanes; ImageNet shapes (C4) one strip either way, q = 4
+    (profiles/r02/bytes_ab.txt).  MXD_POLICY_NO_BYTES keeps pixel lanes,
+    MXD_POLICY_BYTES takes byte lanes wherever a kernel exists."""
+    p = _plan(_entry())
+    assert (p["wave"], p["kind"], p["taps"], p["s"], p["dmax"]) == (1, 2, 8, 2, 4)
+    assert (p["p"], p["nstrips"], p["q"]) == (8, 2, 2)
+    b = _plan(_entry(), capi.MXD_POLICY_BYTES)
+    assert (b["p"], b["nstrips"], b["q"]) == (16, 3, 2)
+    hd = _entry(1280, 720, 3840, 455, 256, cx=(455 - 224) // 2)
+    assert (_plan(hd)["p"], _plan(hd)["nstrips"]) == (16, 2)
+    assert _plan(hd, capi.MXD_POLICY_NO_BYTES)["p"] == 8
+    c4 = _entry(500, 375, 1500, 341, 256)
+    assert (_plan(c4)["p"], _plan(c4)["nstrips"], _plan(c4)["q"]) == (8, 1, 4)
+    assert (_plan(c4, capi.MXD_POLICY_BYTES)["p"], _plan(c4, capi.MXD_POLICY_BYTES)["q"]) == (16, 4)
+
+
+def test_byte_lanes_stay_inside_the_row():
+    """A window reaching the last pixel of a tightly packed row would read its
+    last 16-byte chunk past the row (and past the buffer on the last row):
+    such crops keep pixel lanes, even when byte lanes are forced."""
+    forced = capi.MXD_POLICY_BYTES
+    assert _plan(_entry(500, 375, 1500, 341, 256), forced)["p"] == 16
+    right = _entry(500, 375, 1500, 341, 256, cx=341 - 224)
+    p = _plan(right, forced)
+    assert p["wave"] == 1 and p["p"] != 16
+    # the same crop with 16-byte padded rows fits
+    assert _plan(dict(right, src_stride=1504), forced)["p"] == 16

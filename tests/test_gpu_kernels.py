@@ -1,5 +1,6 @@
 """GPU: the kernels of the fused stage -- the wave kernels of
-mlx-data_amd/csrc/wave.hip (scatter schedule, gather) and the general tile
+mlx-data_amd/csrc/wave.hip (scatter schedule with byte lanes or pixel lanes,
+gather) and the general tile
 kernel of resample.hip -- give bit-identical outputs on the same inputs (each
 sums an output row's taps in the same order from 0), and the default choice
 matches the oracle (+-1 per channel, < 0.2 % of channels differing).  The
@@ -16,6 +17,8 @@ from mlx_data_amd import capi
 
 KINDS = [
     ("default", capi.MXD_POLICY_AUTO),
+    ("pixel_lanes", capi.MXD_POLICY_NO_BYTES),
+    ("byte_lanes", capi.MXD_POLICY_BYTES),
     ("gather", capi.MXD_POLICY_NO_SCATTER),
     ("general", capi.MXD_POLICY_NO_WAVE),
 ]
