@@ -6,22 +6,25 @@ import oracle as O
 from mlx_data_amd import capi
 
 
-def run_device(images, geoms, f32=False, src_align=16, dst_pad=0, device=0, rgba_weighted=0):
+def run_device(images, geoms, f32=False, src_align=16, dst_pad=0, device=0, rgba_weighted=0, base_shift=0,
+               src_pad=0):
     """images: list of (H, W, C) uint8; geoms: (rw, rh, cx, cy, cw, ch, flip).
 
     Sources are packed into one device buffer with row pitch rounded up to
-    ``src_align`` bytes (1 = tightly packed, exercising the unaligned path).
+    ``src_align`` bytes (1 = tightly packed, exercising the unaligned path),
+    each image starting ``base_shift`` bytes past a 256-byte boundary, rows
+    ``src_pad`` bytes longer than the pixels before rounding.
     Returns the list of outputs (uint8, or float32 when f32)."""
     elem = 4 if f32 else 1
     pitches, offs, total = [], [], 0
     for img in images:
         h, w, c = img.shape
-        p = (w * c + src_align - 1) // src_align * src_align
+        p = (w * c + src_pad + src_align - 1) // src_align * src_align
         pitches.append(p)
-        offs.append(total)
+        offs.append(total + base_shift)
         total += (p * h + 255) // 256 * 256
     src = capi.DeviceBuffer(total + 256, device)
-    host = np.zeros(total, np.uint8)
+    host = np.zeros(total + 256, np.uint8)
     for img, p, o in zip(images, pitches, offs):
         h, w, c = img.shape
         host[o : o + p * h].reshape(h, p)[:, : w * c] = img.reshape(h, w * c)
