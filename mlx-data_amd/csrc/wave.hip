@@ -86,6 +86,40 @@ constexpr int kLanes = 64;
 #endif
 constexpr int kPad = 32;  // floats after each plane: padded taps read zeros there
 
+// Progress-based wave priority (tuning builds: -DMXD_PRIO=0 turns it off).
+// All units of a launch do about the same work and start together, but the
+// SIMD arbiter issues oldest-first, so without it a CU's first workgroup
+// finishes its band in ~95 us and its last in ~141 us (C2, tools/stamps.sh):
+// the launch then drains for ~60 us with ever fewer waves feeding HBM.  Each
+// wave lowers its s_setprio level as it completes quarters of its band, so
+// waves that are behind win the arbiter and the band ends line up.
+#ifndef MXD_PRIO
+#define MXD_PRIO 1
+#endif
+
+__device__ __forceinline__ void progress_prio(int done, int total) {
+  if constexpr (MXD_PRIO != 0) {
+    const int level = 3 - (4 * done) / (total + 1);  // 3 at the start .. 0 in the last quarter
+    switch (level) {
+      case 3: __builtin_amdgcn_s_setprio(3); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(0); break;
+    }
+  }
+}
+
+// Diagnostic builds only (-DMXD_STAMPS=1, tools/stamps.sh; never in the
+// product library): every unit's start and end time (s_memrealtime, 100 MHz)
+// from its wave's lane 0, read back with mxd_debug_stamps.
+#ifndef MXD_STAMPS
+#define MXD_STAMPS 0
+#endif
+#if MXD_STAMPS
+constexpr int kMaxStamped = 32768;
+__device__ unsigned long long g_stamps[2 * kMaxStamped];
+#endif
+
 #define GLOBAL_PTR(T, p) ((__attribute__((address_space(1))) T*)(p))
 using cgfloat = const __attribute__((address_space(1))) float;
 // Constant address space: uniform loads through it are scalar (s_load).
@@ -414,6 +448,7 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
       if constexpr (MXD_SYNC_STRIPS != 0)
         if (sync) __builtin_amdgcn_s_barrier();
     });
+    progress_prio(gb + BG, ngroups);
   }
 }
 
@@ -421,22 +456,16 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
 // parse inside __launch_bounds__)
 constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; }
 
+// One unit (image, band, strip) by the calling wave; planes = its LDS rows.
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
-__global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES) void resample_wave(
-    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int nimgs, int per_img, int unit,
+                                         float* __restrict__ planes, int lane) {
   using L = Lay<C, P>;
-  constexpr int PL = L::PL;
   constexpr int VC = L::VC, VP = L::VP;
-  const int lane = threadIdx.x & (kLanes - 1);
-  const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
-  float* __restrict__ planes = smem + (threadIdx.x >> 6) * (VC * PL);
-#pragma unroll
-  for (int c = 0; c < VC; c++)
-#pragma unroll
-    for (int i = 0; i < L::PAD; i += kLanes)
-      if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
-  if (unit >= nunits) return;
+  progress_prio(0, 1);
+#if MXD_STAMPS
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // per_img > 0: every image has per_img units (no search: the wave issues
   // its first row loads one dependent descriptor load after it starts)
@@ -553,6 +582,7 @@ __global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAV
     load_rows(RA, oy0, true);
     start();
     for (int y = oy0;; y += 2) {
+      progress_prio(y - oy0, oy1 - oy0);
       load_rows(RB, min(y + 1, crop_h - 1), y + 1 < oy1);
       step(RA, y);
       if (y + 1 >= oy1) break;
@@ -566,6 +596,29 @@ __global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAV
     scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start,
                                     nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0);
   }
+#if MXD_STAMPS
+  if (lane == 0 && unit < kMaxStamped) {
+    g_stamps[2 * unit] = t_start;
+    g_stamps[2 * unit + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+}
+
+template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
+__global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES) void resample_wave(
+    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  using L = Lay<C, P>;
+  constexpr int PL = L::PL;
+  const int lane = threadIdx.x & (kLanes - 1);
+  const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
+  float* __restrict__ planes = smem + (threadIdx.x >> 6) * (L::VC * PL);
+#pragma unroll
+  for (int c = 0; c < L::VC; c++)
+#pragma unroll
+    for (int i = 0; i < L::PAD; i += kLanes)
+      if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
+  if (unit < nunits) run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT>(imgs, nimgs, per_img, unit, planes, lane);
 }
 
 using WaveKernel = void (*)(const ImgDev*, int, int, int);
@@ -739,3 +792,12 @@ int wave_capacity(const WaveCfg& cfg, int device) {
 }
 
 }  // namespace mxd
+
+#if MXD_STAMPS
+// Copies the first n units' (start, end) stamps of the last stamped launches.
+extern "C" int mxd_debug_stamps(unsigned long long* host, int n) {
+  if (n > mxd::kMaxStamped) n = mxd::kMaxStamped;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mxd::g_stamps), sizeof(unsigned long long) * 2 * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -329,7 +329,9 @@ def test_dropping_a_busy_prefetch_does_not_deadlock():
 
     samples = [dict(i=np.array([k], np.int64)) for k in range(64)]
     s = dx.buffer_from_vector(samples).to_stream().key_transform("i", slow).prefetch(8, 4)
-    assert int(next(iter(s))["i"][0]) == 0  # workers now busy in `slow`
+    # workers now busy in `slow` (which sample a future gets is up to the
+    # threads: each calls the upstream next(), stream/Prefetch.cpp:38-49)
+    assert 0 <= int(next(iter(s))["i"][0]) < 64
     done = threading.Event()
 
     def drop():
