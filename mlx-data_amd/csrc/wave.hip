@@ -160,6 +160,9 @@ struct Lay {
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int n) {
+#ifdef MXD_NO_XCD_REMAP  // diagnostic builds: consecutive blocks on consecutive XCDs
+  return b;
+#endif
   const int q = n >> 3, r = n & 7;
   const int xcd = b & 7, idx = b >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;

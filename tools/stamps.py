@@ -69,7 +69,10 @@ res = {
 nb = (len(a) + 3) // 4
 q = (nb + 7) // 8
 ids = np.nonzero(np.frombuffer(buf, np.uint64).reshape(N, 2)[:, 0] > 0)[0]
-xcd = np.minimum((ids // 4) // q, 7)
+xcd = np.minimum((ids // 4) // q, 7) if os.environ.get("NO_XCD_REMAP") is None else (ids // 4) % 8
+img = ids // max(1, len(a) // bench.WORKLOADS[w]["batch"])
+res["image_octile_unit_us_median"] = [round(float(np.median(dur[(img * 8 // bench.WORKLOADS[w]["batch"]) == k])), 1)
+                                      for k in range(8)]
 res["xcd_unit_us_median"] = [round(float(np.median(dur[xcd == x])), 1) for x in range(8)]
 res["xcd_end_us_max"] = [round(float(en[xcd == x].max()), 1) for x in range(8)]
 res["wave_in_block_median"] = [round(float(np.median(dur[ids % 4 == k])), 1) for k in range(4)]

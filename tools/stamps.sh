@@ -1,6 +1,6 @@
 #!/bin/bash
 # Unit start/end stamps of the wave kernel (diagnostic build, -DMXD_STAMPS=1).
-#   tools/stamps.sh build        (here: tools/libmxd_amd_stamps.so)
+#   tools/stamps.sh build        (here: tools/libmxd_amd_stamps.so; extra flags in STAMP_FLAGS)
 #   tools/stamps.sh run [w ...]  (GPU box: swaps the build in, tools/stamps.py per workload, restores)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -8,7 +8,7 @@ if [ "$1" = build ]; then
   mkdir -p tools/abl
   cd mlx-data_amd
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
-    -DMXD_STAMPS=1 -c csrc/wave.hip -o build/wave_stamps.o || exit 1
+    -DMXD_STAMPS=1 ${STAMP_FLAGS:-} -c csrc/wave.hip -o build/wave_stamps.o || exit 1
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave_stamps.o build/pixmap.o \
     build/capi.o build/taps.o build/jpeg.o build/jpegdev.o -o ../tools/libmxd_amd_stamps.so || exit 1
   exit 0
