@@ -128,7 +128,9 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
  * fresh descriptors); MXD_POLICY_NO_BYTES: RGB scatter kernels keep whole
  * pixels per lane instead of 16 contiguous bytes per lane (by default byte
  * lanes run where they need no more strips); MXD_POLICY_BYTES: byte lanes
- * wherever a kernel exists.  Returns the previous policy. */
+ * wherever a kernel exists; MXD_POLICY_NO_ZERO_COPY: the host path DMAs
+ * page-locked sources' footprint rows to the device (2-D copies) instead of
+ * letting the kernel read them in place.  Returns the previous policy. */
 enum mxd_policy {
   MXD_POLICY_AUTO = 0,
   MXD_POLICY_NO_SCATTER = 1,
@@ -136,7 +138,8 @@ enum mxd_policy {
   MXD_POLICY_NARROW = 4,
   MXD_POLICY_NO_DESC_CACHE = 8,
   MXD_POLICY_NO_BYTES = 16,
-  MXD_POLICY_BYTES = 32
+  MXD_POLICY_BYTES = 32,
+  MXD_POLICY_NO_ZERO_COPY = 64
 };
 int mxd_set_kernel_policy(int32_t policy);
 

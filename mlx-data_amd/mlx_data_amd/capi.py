@@ -43,6 +43,7 @@ MXD_POLICY_NARROW = 4
 MXD_POLICY_NO_DESC_CACHE = 8
 MXD_POLICY_NO_BYTES = 16
 MXD_POLICY_BYTES = 32
+MXD_POLICY_NO_ZERO_COPY = 64
 
 
 class MxdImage(ctypes.Structure):
