@@ -129,8 +129,9 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
  * pixels per lane instead of 16 contiguous bytes per lane (by default byte
  * lanes run where they need no more strips); MXD_POLICY_BYTES: byte lanes
  * wherever a kernel exists; MXD_POLICY_NO_ZERO_COPY: the host path DMAs
- * page-locked sources' footprint rows to the device (2-D copies) instead of
- * letting the kernel read them in place.  Returns the previous policy. */
+ * page-locked sources' footprint rows to the device (2-D copies) and results
+ * back to page-locked destinations instead of letting the kernel read and
+ * write them in place over PCIe.  Returns the previous policy. */
 enum mxd_policy {
   MXD_POLICY_AUTO = 0,
   MXD_POLICY_NO_SCATTER = 1,

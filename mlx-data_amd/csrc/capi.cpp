@@ -1574,6 +1574,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     int64_t in_size;              // staged bytes (footprint rows, or a JPEG's coefficients)
     bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
     const uint8_t* src_dev;       // zero copy: the kernel reads the page-locked source in place
+    uint8_t* dst_dev;             // zero copy: the kernel writes the page-locked destination in place
   };
   std::vector<Stage> st(n);
   for (int32_t i = 0; i < n; i++) {
@@ -1589,6 +1590,8 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       s.src_pinned = false;
       s.src_dev = nullptr;
       s.dst_pinned = !dst_device && host_pinned(im.dst);
+      s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
+                      ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
       if (!dst_device && im.dst_stride < s.out_row)
         return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
       continue;
@@ -1615,6 +1618,8 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     // copy of the same bytes (tools/pcie_probe.py).
     s.src_dev = s.src_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY) ? host_device_ptr(im.src) : nullptr;
     s.dst_pinned = !dst_device && host_pinned(im.dst);
+    s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
+                    ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
     if (!dst_device && im.dst_stride < s.out_row)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
   }
@@ -1683,7 +1688,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     }
     for (int pass = 0; pass < 2; pass++)
       for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
-        if (st[i].dst_pinned == (pass == 1)) {
+        if (st[i].dst_pinned == (pass == 1) && !st[i].dst_dev) {
           st[i].out_off = out_bytes;
           // page-locked destinations back to back (one copy per contiguous run)
           const int64_t b = st[i].out_row * images[i].crop_h;
@@ -1728,9 +1733,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         where[j] = Stored{win, m.pitch, 0, 0, im.src_h};
         dev_imgs[j].src = win;
         dev_imgs[j].src_stride = m.pitch;
-        if (!dst_device) {
+        if (!dst_device && !s.dst_dev) {
           dev_imgs[j].dst = sl.dev_out + s.out_off;
           dev_imgs[j].dst_stride = s.out_row;
+        } else if (s.dst_dev) {
+          dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
         }
         continue;
       }
@@ -1744,9 +1751,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         dev_imgs[j].src = sl.dev_in + s.in_off;  // checked by validate() only; `where` says what is stored
       }
       dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
-      if (!dst_device) {
+      if (!dst_device && !s.dst_dev) {
         dev_imgs[j].dst = sl.dev_out + s.out_off;
         dev_imgs[j].dst_stride = s.out_row;
+      } else if (s.dst_dev) {
+        dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
       }
     }
     if (in_staged > 0) MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
@@ -1776,7 +1785,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       // one copy; strided ones as 2-D copies.
       for (int32_t i = chunks[k].first; i < chunks[k].second;) {
         const Stage& s = st[i];
-        if (!s.dst_pinned) {
+        if (!s.dst_pinned || s.dst_dev) {
           i++;
           continue;
         }
