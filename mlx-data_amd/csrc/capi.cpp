@@ -1702,6 +1702,12 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       if (int rc = grow_pinned(&sl.pin_out, &sl.pin_out_cap, out_bytes)) return rc;
       if (int rc = grow_device(&sl.dev_out, &sl.dev_out_cap, out_bytes)) return rc;
     }
+    // Zero copy through the staging buffers too: the kernel reads staged
+    // footprints from the page-locked slot buffer and writes results into its
+    // page-locked output buffer (no H2D / D2H DMA step in between).
+    const bool zc = !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY) && !jpeg;
+    const uint8_t* pin_in_dev = zc ? host_device_ptr(sl.pin_in) : nullptr;
+    uint8_t* pin_out_dev = zc && !dst_device && sl.pin_out ? const_cast<uint8_t*>(host_device_ptr(sl.pin_out)) : nullptr;
     const int32_t cn = chunks[k].second - chunks[k].first;
     std::vector<mxd_image> dev_imgs(images + chunks[k].first, images + chunks[k].second);
     std::vector<Stored> where(cn);
@@ -1747,18 +1753,20 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         where[j] = Stored{base, im.src_stride, s.x0, s.y0, s.rows};
         dev_imgs[j].src = base;
       } else {
-        where[j] = Stored{sl.dev_in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
-        dev_imgs[j].src = sl.dev_in + s.in_off;  // checked by validate() only; `where` says what is stored
+        const uint8_t* in = pin_in_dev ? pin_in_dev : sl.dev_in;
+        where[j] = Stored{in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
+        dev_imgs[j].src = in + s.in_off;  // checked by validate() only; `where` says what is stored
       }
       dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
       if (!dst_device && !s.dst_dev) {
-        dev_imgs[j].dst = sl.dev_out + s.out_off;
+        dev_imgs[j].dst = (pin_out_dev ? pin_out_dev : sl.dev_out) + s.out_off;
         dev_imgs[j].dst_stride = s.out_row;
       } else if (s.dst_dev) {
         dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
       }
     }
-    if (in_staged > 0) MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
+    if (in_staged > 0 && !pin_in_dev)
+      MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
     if (jpeg) {
       mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
@@ -1778,7 +1786,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     }
     if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
     if (!dst_device) {
-      if (out_staged > 0)
+      if (out_staged > 0 && !pin_out_dev)
         MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_staged, hipMemcpyDeviceToHost, sl.stream));
       // Page-locked destinations: straight from the device.  Images packed
       // back to back both here and in the destination (a batch tensor) go as
