@@ -42,8 +42,9 @@ Extra fields:
                 N = 1, c2 only), with Pillow BILINEAR and torch-CPU bilinear
                 antialias on all cores as independent CPU points.
   e2e           the product's host-resident path (mxd_resize_crop_host: host
-                images in, host batch out, pinned staging of each image's
-                source footprint, H2D / kernel / D2H overlapped in chunks):
+                images in, host batch out; the kernel reads each image's
+                source footprint and writes results over PCIe, from / to
+                page-locked memory -- in place when the caller's buffers are):
                 the PCIe-inclusive rate, never `value`.
 """
 import argparse
@@ -557,9 +558,11 @@ def e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev):
         capi.check(L.mxd_free_pinned(pin_out))
     return {"value": round(B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
             "pinned_value": round(B * k / (td - tc), 1), "pinned_matches_pageable": same,
-            "note": "mxd_resize_crop_host: pinned staging of each image's source footprint, H2D / fused kernel / "
-                    "D2H overlapped over chunks of the batch, host batch out; synchronous per call. pinned_value: "
-                    "host images and batch in page-locked memory, DMA'd in place"}
+            "note": "mxd_resize_crop_host: each image's source footprint staged into page-locked memory by "
+                    "helper threads and read by the fused kernel over PCIe, results written over PCIe into "
+                    "page-locked staging and copied out; chunks overlapped over two slots; synchronous per call. "
+                    "pinned_value: host images and batch in page-locked memory, read and written in place by the "
+                    "kernel (zero copy)"}
 
 
 if __name__ == "__main__":

@@ -67,10 +67,15 @@ constexpr int kLanes = 64;
 #ifndef MXD_ABLATE
 #define MXD_ABLATE 0
 #endif
-// Tuning builds (-DMXD_NT_STORE=1, -DMXD_MIN_WAVES=<n>): nontemporal output
-// stores; minimum waves per SIMD the register allocation must allow.
+// f32 output stores are nontemporal (MXD_NT_STORE, default 1; tuning builds
+// -DMXD_NT_STORE=0): results are written once and never read back here, and
+// with plain stores the dirty lines they leave in each XCD's L2 are written
+// back at the kernel's end -- C4 (77 MB of f32 per launch) measured 0.0325 ->
+// 0.0263 ms per launch, C2 0.1536 -> 0.1505 (profiles/r02/nt_store_ab.txt).
+// Tuning builds (-DMXD_MIN_WAVES=<n>): minimum waves per SIMD the register
+// allocation must allow.
 #ifndef MXD_NT_STORE
-#define MXD_NT_STORE 0
+#define MXD_NT_STORE 1
 #endif
 #ifndef MXD_MIN_WAVES
 #define MXD_MIN_WAVES 3
@@ -166,6 +171,15 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
   const int q = n >> 3, r = n & 7;
   const int xcd = b & 7, idx = b >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// One f32 output store (vector memory; nontemporal unless MXD_NT_STORE == 0).
+template <class V, class T>
+__device__ __forceinline__ void store_out(V* p, T v) {
+  if constexpr (MXD_NT_STORE != 0)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
 }
 
 // Exact f32 q/255.0f for q in 0..255 (checked for all 256 values).
@@ -369,23 +383,20 @@ struct HStrip {
         if constexpr (F32) {
           auto* d = GLOBAL_PTR(float, drow) + px * C;
           if constexpr (C == 1) {
-            d[0] = div255(s[0]);
+            store_out(d, div255(s[0]));
           } else if constexpr (C == 2) {
-            *reinterpret_cast<__attribute__((address_space(1))) f32x2*>(d) = f32x2{div255(s[0]), div255(s[1])};
+            store_out(reinterpret_cast<__attribute__((address_space(1))) f32x2*>(d), f32x2{div255(s[0]), div255(s[1])});
           } else if constexpr (C == 3) {
-            const f32x3 v = {div255(s[0]), div255(s[1]), div255(s[2])};
-            if constexpr (MXD_NT_STORE != 0)
-              __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) f32x3*>(d));
-            else
-              *reinterpret_cast<__attribute__((address_space(1))) f32x3*>(d) = v;
+            store_out(reinterpret_cast<__attribute__((address_space(1))) f32x3*>(d),
+                      f32x3{div255(s[0]), div255(s[1]), div255(s[2])});
           } else {
-            *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(d) =
-                f32x4{div255(s[0]), div255(s[1]), div255(s[2]), div255(s[3])};
+            store_out(reinterpret_cast<__attribute__((address_space(1))) f32x4*>(d),
+                      f32x4{div255(s[0]), div255(s[1]), div255(s[2]), div255(s[3])});
           }
         } else {
           auto* d = GLOBAL_PTR(uint8_t, drow) + px * C;
 #pragma unroll
-          for (int c = 0; c < C; c++) d[c] = (uint8_t)s[c];
+          for (int c = 0; c < C; c++) d[c] = (uint8_t)s[c];  // byte stores: nontemporal measured no better
         }
       }
     }
