@@ -75,3 +75,55 @@ def test_pinned_and_pageable_mix(f32):
     finally:
         for p in pins:
             p.free()
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_zero_copy_equals_dma(f32):
+    """Zero copy (the kernel reads footprints and writes results over PCIe,
+    in place in page-locked buffers or from / to the host path's page-locked
+    staging) gives the bytes of the DMA form (MXD_POLICY_NO_ZERO_COPY)."""
+    elem = 4 if f32 else 1
+    imgs = [synth(960, 1280, 3, 11), synth(375, 500, 3, 12), synth(500, 333, 3, 13), synth(720, 1280, 3, 14)]
+    geoms = []
+    for k, im in enumerate(imgs):
+        h, w = im.shape[:2]
+        rw, rh = capi.resize_smallest_side_dims(w, h, 256)
+        cx = 0 if k == 1 else rw - 224 if k == 2 else (rw - 224) // 2
+        geoms.append((rw, rh, cx, (rh - 224) // 2, 224, 224, k % 2))
+    pins = []
+
+    def run(policy, pinned):
+        prev = capi.set_kernel_policy(policy)
+        try:
+            entries, outs = [], []
+            for im, g in zip(imgs, geoms):
+                h, w, c = im.shape
+                row = g[4] * c * elem
+                if pinned:
+                    ps, pd = Pinned(h * w * c), Pinned(row * g[5])
+                    pins.extend([ps, pd])
+                    src, sp = ps.a.reshape(h, w * c), ps.p.value
+                    dst, dp = pd.a.reshape(g[5], row), pd.p.value
+                else:
+                    src = np.zeros((h, w * c), np.uint8)
+                    dst = np.zeros((g[5], row), np.uint8)
+                    sp, dp = src.ctypes.data, dst.ctypes.data
+                src[:] = im.reshape(h, -1)
+                outs.append((dst, src))
+                entries.append(dict(src=sp, src_stride=w * c, src_w=w, src_h=h, channels=c, resize_w=g[0],
+                                    resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6],
+                                    dst=dp, dst_stride=row))
+            arr, n = capi.make_images(entries)
+            capi.resize_crop_host(arr, n, capi.MXD_F32_DIV255 if f32 else capi.MXD_U8, 0)
+            return [d.copy() for d, _ in outs]
+        finally:
+            capi.set_kernel_policy(prev)
+
+    try:
+        want = run(capi.MXD_POLICY_NO_ZERO_COPY, False)
+        for policy, pinned in [(0, False), (0, True), (capi.MXD_POLICY_NO_ZERO_COPY, True)]:
+            for a, b in zip(run(policy, pinned), want):
+                assert np.array_equal(a, b), (policy, pinned)
+    finally:
+        for p in pins:
+            p.free()
