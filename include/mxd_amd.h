@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MXD_ABI_VERSION 3
+#define MXD_ABI_VERSION 4
 
 enum mxd_status {
   MXD_OK = 0,
@@ -118,8 +118,11 @@ int mxd_axis_taps(int32_t in_size, int32_t out_size, int32_t crop_off, int32_t c
 int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream);
 
 /* Kernel policy: a process-wide switch between kernels that compute
- * bit-identical results (for tests and tuning; default 0 = automatic choice).
- * MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
+ * bit-identical results (for tests and tuning; default 0 = automatic choice:
+ * the band kernel -- one workgroup streams an image band's source rows into
+ * LDS by LDS-DMA -- wherever its classes fit, else a wave kernel, else the
+ * general kernel).  MXD_POLICY_NO_BAND: never the band kernel (any of the
+ * wave-kernel bits below implies it).  MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
  * of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
  * general workgroup-tile kernel; MXD_POLICY_NARROW: wave kernels keep the
  * narrow per-lane window (no wide RGB strips, no byte lanes);
@@ -140,16 +143,32 @@ enum mxd_policy {
   MXD_POLICY_NO_DESC_CACHE = 8,
   MXD_POLICY_NO_BYTES = 16,
   MXD_POLICY_BYTES = 32,
-  MXD_POLICY_NO_ZERO_COPY = 64
+  MXD_POLICY_NO_ZERO_COPY = 64,
+  MXD_POLICY_NO_BAND = 128
 };
 int mxd_set_kernel_policy(int32_t policy);
 
-/* The kernel mxd_resize_crop_batch would run for one image on `device`
- * (diagnostics, tests): info[0] = 1 wave kernel / 0 general kernel, then kind
+/* Tuning knobs (process-wide, for measurements; 0 = automatic).  Returns the
+ * previous value, or -1 for an unknown knob.
+ * MXD_TUNE_BAND_ROWS: output rows per band-kernel unit;
+ * MXD_TUNE_BAND_LA: row groups the band kernel keeps in flight per unit. */
+enum mxd_tune { MXD_TUNE_BAND_ROWS = 0, MXD_TUNE_BAND_LA = 1, MXD_TUNE_COUNT = 2 };
+int mxd_set_tuning(int32_t knob, int32_t value);
+
+/* The wave-kernel plan of one image on `device`, i.e. what runs when the
+ * band kernel declines it or is off (diagnostics, tests): info[0] = 1 wave
+ * kernel / 0 general kernel, then kind
  * (0 gather, 2 scatter), tap bucket, scatter S, scatter DMAX, output pixels
  * per lane, strips, source pixels per lane (RGB 16: byte lanes, 16 bytes per
  * lane).  Host only: needs no device. */
 int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device, int32_t* info8);
+
+/* The band-kernel plan of one image (host only): info[0] = 1 when the band
+ * kernel takes it (under the current policy), then horizontal tap class, row
+ * slots per group (DB), accumulator slots, source window KiB per strip row,
+ * strips, strip columns, prologue groups, most new source rows per output
+ * row, groups in flight, LDS bytes per workgroup, 0. */
+int mxd_describe_band_plan(const mxd_image* image, int32_t out_dtype, int32_t* info12);
 
 /* Measured device-memory ceiling: a 16-byte-per-lane streaming copy of `bytes`
  * (read + write counted), averaged over `iters` launches, in GB/s. */

@@ -1,0 +1,403 @@
+// band.hip -- the row-stream kernel of the fused resize + crop (+ hflip) (+ /255)
+// stage; structure and LDS layout in band.h.
+//
+// Reference arithmetic replaced: core::image::resize -> stbir_resize_uint8_linear
+// (mlx/data/core/image/ImageTransform.cpp:41-62, triangle filter :7-9), then
+// core::image::crop / hflip (:64-73, :123-140) and the benchmark's
+// astype(float32) / 255 (benchmarks/comparative/caltech101/mlx_data.py:46).
+//
+// Why this shape (measured on the wave kernel): ~4,000 waves
+// each streaming its own band of 1.5-KiB row pieces sat at the probe floor of
+// that access pattern (~0.15 ms for C2).  Here one workgroup streams whole
+// contiguous footprint rows (1 KiB per LDS-DMA instruction) of one band, the
+// loads need no VGPRs, and every output row leaves as one contiguous run of
+// 12-byte (f32 RGB) stores.
+#include <hip/hip_runtime.h>
+
+#include "band.h"
+#include "devutil.h"
+
+namespace mxd {
+namespace {
+
+using namespace dev;
+
+constexpr int kThreads = kBandThreads;
+constexpr int kLanes = 64;
+constexpr int kWaves = kThreads / kLanes;
+constexpr int kChunk = kBandChunk;
+constexpr int E = kBandEntryWords;
+// A voffset past any buffer: the range check drops the access (loads: no
+// request, zeros; stores: nothing written).
+constexpr int kNoLoad = 0x7ffffff0;
+using lds_u8 = __attribute__((address_space(3))) uint8_t;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// f32 results are stored nontemporally (written once, never read here; the
+// wave kernel measured 0.0325 -> 0.0263 ms on C4 from it).  Tuning builds:
+// -DMXD_BAND_NT=0.
+#ifndef MXD_BAND_NT
+#define MXD_BAND_NT 1
+#endif
+constexpr int kStoreAux = MXD_BAND_NT ? 2 : 0;  // gfx950 cache-policy bits: 2 = nt
+
+#define RFL(x) __builtin_amdgcn_readfirstlane(x)
+
+// s_waitcnt vmcnt(n) for a run-time, wave-uniform n (the count is an
+// immediate); n > 63 waits for 63 (more than asked: always safe).
+__device__ __forceinline__ void wait_vmcnt(int n) {
+#define MXD_VMC(k) \
+  case k:          \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
+    break;
+#define MXD_VMC8(b) MXD_VMC(b) MXD_VMC(b + 1) MXD_VMC(b + 2) MXD_VMC(b + 3) MXD_VMC(b + 4) MXD_VMC(b + 5) \
+    MXD_VMC(b + 6) MXD_VMC(b + 7)
+  switch (n < 63 ? n : 63) {
+    MXD_VMC8(0) MXD_VMC8(8) MXD_VMC8(16) MXD_VMC8(24) MXD_VMC8(32) MXD_VMC8(40) MXD_VMC8(48) MXD_VMC8(56)
+    default:
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#undef MXD_VMC8
+#undef MXD_VMC
+}
+
+// Workgroup barrier for LDS hand-offs: this wave's LDS writes done, then
+// s_barrier.  LDS-DMA data is covered by each wave's own wait_vmcnt before it
+// (a __syncthreads() would also wait vmcnt(0) and drain the ring).
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One output pixel's C encoded channels to the buffer (vector stores; SW of
+// them per wave and output row, the same in every wave: inactive lanes carry
+// an out-of-range offset).
+template <int C, bool F32>
+constexpr int store_instrs() {
+  return (!F32 && C == 3) ? 3 : 1;
+}
+
+template <int C, bool F32>
+__device__ __forceinline__ void store_pixel(__amdgpu_buffer_rsrc_t rs, int voff, const float (&q)[C]) {
+  if constexpr (F32) {
+    if constexpr (C == 1) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(div255(q[0])), rs, voff, 0, kStoreAux);
+    } else if constexpr (C == 2) {
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(div255(q[0])), __float_as_uint(div255(q[1]))}, rs,
+                                            voff, 0, kStoreAux);
+    } else if constexpr (C == 3) {
+      __builtin_amdgcn_raw_buffer_store_b96(
+          u32x3{__float_as_uint(div255(q[0])), __float_as_uint(div255(q[1])), __float_as_uint(div255(q[2]))}, rs,
+          voff, 0, kStoreAux);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(div255(q[0])), __float_as_uint(div255(q[1])),
+                                                   __float_as_uint(div255(q[2])), __float_as_uint(div255(q[3]))},
+                                             rs, voff, 0, kStoreAux);
+    }
+  } else {
+    const uint32_t b0 = (uint32_t)q[0];
+    if constexpr (C == 1) {
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b0, rs, voff, 0, 0);
+    } else if constexpr (C == 2) {
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(b0 | ((uint32_t)q[1] << 8)), rs, voff, 0, 0);
+    } else if constexpr (C == 3) {
+      // byte stores (a pixel's 3 bytes are not 2-byte aligned every other
+      // pixel); an out-of-range voffset stays out of range 1 or 2 bytes on
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b0, rs, voff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(uint32_t)q[1], rs, voff + 1, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(uint32_t)q[2], rs, voff + 2, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(b0 | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24),
+                                            rs, voff, 0, 0);
+    }
+  }
+}
+
+template <int C, bool F32, int NQ, int T, int S, int DB>
+__global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __restrict__ imgs, int nimgs, int nunits,
+                                                             int per_img, int la) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int DS = DB > 4 ? DB : 4;     // row slots per area (>= 4: NQ KiB of floats fit)
+  constexpr int AREA = DS * NQ * kChunk;  // bytes per ring area
+  constexpr int KW = (DB * NQ + kWaves - 1) / kWaves;  // LDS-DMA instructions per wave and group
+  constexpr int SW = store_instrs<C, F32>();
+  constexpr int ELEM = F32 ? 4 : 1;
+  constexpr int NX = 4 * NQ;  // source bytes per thread and row
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kLanes - 1);
+  const int wave = RFL(tid >> 6);
+  const int unit = RFL(xcd_remap(blockIdx.x, gridDim.x));
+  if (unit >= nunits) return;  // the whole workgroup
+
+  const ImgDev& im = per_img > 0 ? imgs[unit / per_img] : find_image(imgs, nimgs, unit);
+  const int nstrips = RFL(im.nstrips);
+  const int crop_w = RFL(im.crop_w);
+  const int crop_h = RFL(im.crop_h);
+  const int fl = RFL(im.flip);
+  const int flip = fl & 1, shift = fl >> 8;  // see ImgDev::flip
+  const int band_rows = RFL(im.ty);
+  const int strip_cols = RFL(im.tx);
+  const int xs = kTapHeader + RFL(im.xwidth);
+  cgfloat* xtab = MXD_GLOBAL_PTR(const float, im.xtab);
+  const int local = unit - RFL(im.tile_begin);
+  const int band = local / nstrips;
+  const int strip = local - band * nstrips;
+  const int oy0 = band * band_rows;
+  const int nrows = min(band_rows, crop_h - oy0);
+  const int ox0 = strip * strip_cols;
+  const int npx = min(strip_cols, crop_w - ox0);
+
+  // Source: one descriptor over the stored region, rows addressed through the
+  // range-checked voffset (rows and columns outside it read zeros).
+  int lo, hi;
+  strip_span(xtab, xs, crop_w, flip, ox0, ox0 + npx, &lo, &hi);
+  lo = RFL(lo);
+  hi = RFL(hi);
+  const int sx0 = RFL(im.src_x0), y0 = RFL(im.src_y0);
+  const int stride = RFL((int)im.src_stride), rows = RFL(im.src_h), srcw = RFL(im.src_w);
+  const __amdgpu_buffer_rsrc_t src =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.src), (short)0,
+                                        src_records(shift, rows, stride, (srcw - sx0) * C), 0x00020000);
+  const int b0 = ((lo - sx0) * C + shift) & ~15;  // window start: 16-byte boundary past the aligned base
+  const int bend = (hi + 1 - sx0) * C + shift;    // one past the strip's last source byte
+
+  // Destination: the image's output rows.
+  const int dstride = RFL((int)im.dst_stride);
+  const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr<void*>(im.dst), (short)0, (crop_h - 1) * dstride + crop_w * C * ELEM, 0x00020000);
+
+  // Schedule of this band: [P, -, -, -] then entries [group][DB][E] =
+  // source row (-1: none), S weights (slot s = output row g - P + s).
+  kint* sched = uniform_ptr<kint*>(im.ytab) + band * RFL(im.ywidth);
+  const int P = sched[0];
+  const int ngroups = P + nrows;
+  kint* ent = sched + E;
+
+  // Horizontal pass: thread = one output pixel of the strip row (pixels in
+  // contiguous runs per wave, so each wave's stores are one contiguous run).
+  const int ppw = (npx + kWaves - 1) / kWaves;
+  const int px = wave * ppw + lane;
+  const bool hact = lane < ppw && px < npx;
+  float wx[T];
+  int vb;  // float index (in the vertical row) of tap 0, channel 0
+  {
+    const int ox = ox0 + min(px, npx - 1);
+    const int xc = flip ? crop_w - 1 - ox : ox;
+    cgfloat* xe = xtab + xc * xs;
+    vb = (__float_as_int(xe[0]) - sx0) * C + shift - b0;
+#pragma unroll
+    for (int k = 0; k < T; k++) wx[k] = xe[kTapHeader + k];  // zero padded past the tap count
+  }
+  const int scol = (ox0 + px) * C * ELEM;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): table loads done before the ring starts counting
+
+  const int rg = la + 1;
+  const uint32_t sink = (uint32_t)(rg * AREA);  // 1 KiB for loads of absent rows
+
+  // LDS-DMA of a group's rows into area a: item i = wave + 4 m is row slot
+  // i / NQ, 1-KiB piece i % NQ; lane = 16 bytes of the piece.  dma_rows reads
+  // this wave's source rows of group g (the schedule holds one all-absent
+  // group after the last, so the loads need no guard).
+  auto dma_rows = [&](int g, int (&dr)[KW]) {
+    const int gl = min(g, ngroups);
+    static_for<KW>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      const int j = (wave + kWaves * m) / NQ;
+      dr[m] = j < DB ? ent[(gl * DB + j) * E] : -1;
+    });
+  };
+  auto issue = [&](const int (&dr)[KW], int a) {
+    static_for<KW>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      const int i = wave + kWaves * m;
+      const int j = i / NQ, k = i - (i / NQ) * NQ;
+      const int row = dr[m];
+      const int c = b0 + kChunk * k + 16 * lane;
+      const int voff = (row >= 0 && c < bend) ? (row - y0) * stride + c : kNoLoad;
+      const uint32_t to = row >= 0 ? (uint32_t)(a * AREA + (j * NQ + k) * kChunk) : sink;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_u8*)(smem + to), 16, voff, 0, 0, 0);
+    });
+  };
+
+  float acc[S][NX];
+#pragma unroll
+  for (int s = 0; s < S; s++)
+#pragma unroll
+    for (int i = 0; i < NX; i++) acc[s][i] = 0.0f;
+
+  // Vertical pass of group g (accumulator slot SL = g mod S) from area a:
+  // thread t converts dwords t, t + 256, ... of each row slot.  Row slots
+  // and their schedule entries are read in batches of up to 4 before any use
+  // (absent rows read stale bytes that are never used), so the latencies
+  // overlap.
+  auto vpass = [&](auto slc, int g, int a) {
+    constexpr int SL = decltype(slc)::value;
+    constexpr int JB = DB < 4 ? DB : 4;
+    const uint32_t* rb = reinterpret_cast<const uint32_t*>(smem + a * AREA);
+    kint* eg = ent + g * DB * E;
+    static_for<(DB + JB - 1) / JB>([&](auto bc) {
+      constexpr int j0 = decltype(bc)::value * JB;
+      constexpr int JN = DB - j0 < JB ? DB - j0 : JB;
+      int ev[JN * E];
+#pragma unroll
+      for (int q = 0; q < JN * E; q++) ev[q] = eg[j0 * E + q];
+      uint32_t d[JN][NQ];
+#pragma unroll
+      for (int j = 0; j < JN; j++)
+#pragma unroll
+        for (int k = 0; k < NQ; k++) d[j][k] = rb[((j0 + j) * NQ + k) * (kChunk / 4) + tid];
+      static_for<JN>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int* e = ev + j * E;
+        if (e[0] >= 0) {
+          float x[NX];
+#pragma unroll
+          for (int i = 0; i < NX; i++) x[i] = (float)((d[j][i >> 2] >> (8 * (i & 3))) & 0xffu);
+          static_for<S>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const float w = __int_as_float(e[1 + s]);
+            if (s == 0 || w != 0.0f) {
+#pragma unroll
+              for (int i = 0; i < NX; i++) acc[(SL + s) % S][i] = __builtin_fmaf(w, x[i], acc[(SL + s) % S][i]);
+            }
+          });
+        }
+      });
+    });
+  };
+
+  // Finished vertical row (slot SL) -> area a as f32 in byte order.  The
+  // stores are inline asm: hipcc would otherwise wait vmcnt(0) before them
+  // (an LDS store after in-flight LDS-DMA it cannot prove disjoint), which
+  // drains the ring; the areas in flight are never this one (band.h).
+  auto vwrite = [&](auto slc, int a) {
+    constexpr int SL = decltype(slc)::value;
+    const uint32_t addr = (uint32_t)(uintptr_t)(smem + a * AREA) + 16u * tid;
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+      const f32x4 v = {acc[SL][4 * k], acc[SL][4 * k + 1], acc[SL][4 * k + 2], acc[SL][4 * k + 3]};
+      asm volatile("ds_write_b128 %0, %1" ::"v"(addr + (uint32_t)(k * kChunk * 4)), "v"(v) : "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < NX; i++) acc[SL][i] = 0.0f;
+  };
+
+  // Horizontal pass of output row y from the vertical row in area a.
+  auto hpass = [&](int a, int y) {
+    const float* vf = reinterpret_cast<const float*>(smem + a * AREA) + vb;
+    float q[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      float h = 0.0f;
+#pragma unroll
+      for (int k = 0; k < T; k++) h = __builtin_fmaf(wx[k], vf[k * C + c], h);
+      q[c] = encode(h);
+    }
+    store_pixel<C, F32>(dst, hact ? y * dstride + scol : kNoLoad, q);
+  };
+
+  for (int g = 0; g < la; g++) {
+    int dr[KW];
+    dma_rows(g, dr);
+    issue(dr, g);
+  }
+  int acur = 0, aprev = rg - 1;  // areas of groups g and g - 1
+  bool done = false;
+  for (int g0 = 0;; g0 += S) {
+    static_for<S>([&](auto sc) {
+      const int g = g0 + decltype(sc)::value;
+      if (done || g > ngroups) {
+        done = true;
+        return;
+      }
+      int dr[KW];
+      dma_rows(g + la, dr);
+      // Vector-memory ops this wave issued after group g's LDS-DMA: the DMA
+      // of the la - 1 groups after it, and the stores of the steps since.
+      const int first_st = max(g - la + 1, P + 1);
+      wait_vmcnt((la - 1) * KW + SW * max(0, g - first_st));
+      barrier_lds();  // group g's rows and output row g - 1 - P's vertical row visible
+      if (g > P) hpass(aprev, oy0 + g - 1 - P);
+      if (g < ngroups) vpass(sc, g, acur);
+      barrier_lds();  // area acur's rows and area aprev's vertical row consumed
+      if (g < ngroups && g >= P) vwrite(sc, acur);
+      issue(dr, aprev);  // group g + la: (g + la) mod (la + 1) == (g - 1) mod (la + 1)
+      aprev = acur;
+      acur = acur + 1 == rg ? 0 : acur + 1;
+    });
+    if (done) break;
+  }
+  // no LDS-DMA may land after the workgroup's LDS is reassigned
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+using BandKernel = void (*)(const ImgDev*, int, int, int, int);
+
+constexpr int kNumClasses = sizeof(kBandClasses) / sizeof(kBandClasses[0]);
+
+int class_index(const BandCfg& cfg) {
+  for (int i = 0; i < kNumClasses; i++)
+    if (kBandClasses[i].taps == cfg.taps && kBandClasses[i].db == cfg.db && kBandClasses[i].s == cfg.s) return i;
+  return -1;
+}
+
+template <int C, bool F32, int NQ, int... CI>
+BandKernel pick_class(int ci, std::integer_sequence<int, CI...>) {
+  BandKernel k = nullptr;
+  ((ci == CI ? (k = resample_band<C, F32, NQ, kBandClasses[CI].taps, kBandClasses[CI].s, kBandClasses[CI].db>,
+                0)
+             : 0),
+   ...);
+  return k;
+}
+
+template <int C, bool F32>
+BandKernel pick_nq(int nq, int ci) {
+  const auto seq = std::make_integer_sequence<int, kNumClasses>{};
+  switch (nq) {
+    case 1: return pick_class<C, F32, 1>(ci, seq);
+    case 2: return pick_class<C, F32, 2>(ci, seq);
+    case 3: return pick_class<C, F32, 3>(ci, seq);
+    case 4: return pick_class<C, F32, 4>(ci, seq);
+    default: return nullptr;
+  }
+}
+
+// Kernels are built for RGB (what load_image produces for JPEG and the
+// configurations measure); other channel counts take wave.hip / resample.hip.
+BandKernel select_kernel(const BandCfg& cfg) {
+  const int ci = class_index(cfg);
+  if (ci < 0 || cfg.channels != 3 || cfg.la < 1) return nullptr;
+  return cfg.f32 ? pick_nq<3, true>(cfg.nq, ci) : pick_nq<3, false>(cfg.nq, ci);
+}
+
+}  // namespace
+
+int band_lds_bytes(const BandCfg& cfg) {
+  const int ds = cfg.db > 4 ? cfg.db : 4;
+  return (cfg.la + 1) * ds * cfg.nq * kChunk + kChunk;
+}
+
+bool band_has_kernel(const BandCfg& cfg) { return select_kernel(cfg) != nullptr; }
+
+int band_capacity(const BandCfg& cfg, int device) {
+  const BandKernel k = select_kernel(cfg);
+  if (!k) return 0;
+  int blocks = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(k), kThreads,
+                                                   band_lds_bytes(cfg)) != hipSuccess)
+    return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return blocks * cus;
+}
+
+int launch_band(const BandCfg& cfg, const ImgDev* imgs, void* stream) {
+  const BandKernel k = select_kernel(cfg);
+  if (!k) return -2;
+  hipLaunchKernelGGL(k, dim3(cfg.nunits), dim3(kThreads), band_lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
+                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.la);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace mxd

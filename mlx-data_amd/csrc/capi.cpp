@@ -24,6 +24,8 @@
 #include <vector>
 
 #include "mxd_amd.h"
+#include "band.h"
+#include "band_plan.h"
 #include "jpeg.h"
 #include "jpegdev.h"
 #include "pixmap.h"
@@ -147,6 +149,8 @@ TableCache& host_tables() {
 // Kernel policy (mxd_set_kernel_policy): a process-wide tuning / test switch
 // between kernels that compute identical results.
 std::atomic<int32_t> g_policy{0};
+// Tuning knobs (mxd_set_tuning): 0 = automatic.
+std::atomic<int32_t> g_tune[MXD_TUNE_COUNT] = {};
 
 struct Workspace {
   std::mutex mu;
@@ -200,6 +204,7 @@ WorkspacePool& workspaces() {
 constexpr int32_t kTileRows = 32;          // output rows per tile
 constexpr int32_t kStripBytes = 1536;      // target source-footprint bytes per strip row
 constexpr int32_t kLdsBudget = 40 * 1024;  // bytes of LDS for the f32 row group
+constexpr int32_t kBandMaxRows = 128;      // band kernel: most output rows per unit
 
 int32_t strip_chunks(const DevTable& xt, int32_t crop_x, int32_t crop_w, int32_t ox0, int32_t ox1, bool flip,
                      int32_t c, int32_t vec) {
@@ -311,6 +316,8 @@ int release_descs(Workspace* ws, void* stream) {
 struct ImgPlan {
   const DevTable* xt = nullptr;
   const DevTable* yt = nullptr;
+  bool band = false;     // runs on the band kernel (band.hip)
+  mxd::BandPlan bp;      // its plan
   bool wave = false;     // runs on a wave kernel (wave.hip), else the general tile kernel
   int32_t bucket = -1;   // wave kernel tap bucket
   int32_t kind = 0;      // wave kernel: 0 gather, 2 scatter
@@ -458,6 +465,47 @@ SchedCache& schedules() {
   return *c;
 }
 
+mxd::AxisView axis_view(const DevTable& t) {
+  return mxd::AxisView{t.first.data(), t.count.data(), t.w.data(), t.width, t.padded};
+}
+
+// Band-kernel schedules (layout: band_plan.h) in device memory, one per
+// (device, vertical geometry, crop rows, band height, class, prologue).
+class BandSchedCache {
+ public:
+  int get(int32_t device, const DevTable& yt, int32_t src_h, int32_t resize_h, int32_t crop_y, int32_t crop_h,
+          int32_t ty, int32_t db, int32_t s, int32_t prologue, const DevSched** out) {
+    std::lock_guard<std::mutex> lock(mu_);
+    const auto key = std::make_tuple(device, src_h, resize_h, crop_y, crop_h, ty, db, s, prologue);
+    auto it = map_.find(key);
+    if (it != map_.end()) {
+      *out = it->second.get();
+      return MXD_OK;
+    }
+    auto sched = std::make_unique<DevSched>();
+    std::vector<int32_t> words;
+    if (!mxd::band_schedule(axis_view(yt), crop_y, crop_h, ty, db, s, prologue, &words, &sched->band_words))
+      return fail(MXD_ERR_INVALID, "mxd: band schedule does not fit its class");
+    DeviceGuard g(device);
+    MXD_HIP(hipMalloc(reinterpret_cast<void**>(&sched->ptr), words.size() * sizeof(int32_t)));
+    MXD_HIP(hipMemcpy(sched->ptr, words.data(), words.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    *out = sched.get();
+    map_[key] = std::move(sched);
+    return MXD_OK;
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<std::tuple<int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t>,
+           std::unique_ptr<DevSched>>
+      map_;
+};
+
+BandSchedCache& band_schedules() {
+  static BandSchedCache* c = new BandSchedCache();
+  return *c;
+}
+
 // Wave path strips: q output pixels per lane (strip_cols <= 64 q) and every
 // strip's source window (start aligned down to wave_window_align()) within
 // wave_window_px() pixels.  Fewest strips first (least halo re-reading and
@@ -496,8 +544,8 @@ bool wave_strips(const DevTable& xt, const mxd_image& im, int32_t pp, int32_t* n
 // wave slots: a last round that is only partly filled leaves the HBM queue
 // short of loads while it drains.  Pick the fewest rounds whose band height
 // stays <= kMaxBand, then the smallest band height whose unit count fits them.
-int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_t capacity) {
-  constexpr int32_t kMinBand = 8, kMaxBand = 64;
+int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_t capacity, int32_t kMaxBand = 64) {
+  constexpr int32_t kMinBand = 8;
 #ifdef MXD_TUNING_ENV  // tuning builds only (tools/ablate8.sh): never read by the product library
   if (const char* e = std::getenv("MXD_BAND_ROWS")) return std::max(1, std::atoi(e));
 #endif
@@ -520,6 +568,19 @@ int32_t band_rows(const std::vector<std::pair<int32_t, int32_t>>& strips, int32_
     while (ty < max_h && units(ty) > slots) ty++;
     if (units(ty) <= slots || ty >= max_h) return std::min(ty, max_h);
   }
+}
+
+int32_t band_capacity_cached(const mxd::BandCfg& cfg, int32_t device) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int, int, int, int, int>, int32_t> cache;
+  const auto key = std::make_tuple(device, cfg.channels, cfg.f32, cfg.nq, cfg.taps, cfg.s, cfg.db, cfg.la);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  DeviceGuard g(device);
+  const int32_t c = mxd::band_capacity(cfg, device);
+  cache[key] = c;
+  return c;
 }
 
 int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device) {
@@ -595,6 +656,40 @@ bool wave_strips_bytes(const DevTable& xt, const mxd_image& im, const Stored& st
     }
   }
   return best > 0;
+}
+
+// The band kernel (band.hip) for one image when its class, strips and
+// layout fit (p.band = false: wave or general kernel).  Any wave-kernel
+// policy bit turns it off, so those policies keep selecting what they name.
+constexpr int32_t kWavePolicies = MXD_POLICY_NO_SCATTER | MXD_POLICY_NO_WAVE | MXD_POLICY_NARROW |
+                                  MXD_POLICY_NO_BYTES | MXD_POLICY_BYTES;
+void plan_band(const mxd_image& im, const Stored& st, int32_t f32, ImgPlan& p) {
+  p.band = false;
+  if (g_policy.load() & (MXD_POLICY_NO_BAND | kWavePolicies)) return;
+  const int64_t c = im.channels, elem = f32 ? 4 : 1;
+  const int64_t shift = (int64_t)(reinterpret_cast<uintptr_t>(st.base) & 3);
+  const int64_t row = (int64_t)(im.src_w - st.x0) * c;
+  const int64_t src_records = shift + (int64_t)(st.rows - 1) * st.stride + std::min(row, st.stride);
+  const int64_t dst_records = (int64_t)(im.crop_h - 1) * im.dst_stride + (int64_t)im.crop_w * c * elem;
+  if (st.stride <= 0 || src_records >= ((int64_t)1 << 31) || im.dst_stride < 0 ||
+      dst_records >= ((int64_t)1 << 31))
+    return;
+  mxd::BandImage bi{};
+  bi.channels = im.channels;
+  bi.f32 = f32;
+  bi.crop_x = im.crop_x;
+  bi.crop_y = im.crop_y;
+  bi.crop_w = im.crop_w;
+  bi.crop_h = im.crop_h;
+  bi.flip = im.flip ? 1 : 0;
+  bi.src_w = im.src_w;
+  bi.x0 = st.x0;
+  bi.shift = (int32_t)shift;
+  bi.stride = st.stride;
+  bi.dst_stride = im.dst_stride;
+  bi.dst = reinterpret_cast<uintptr_t>(im.dst);
+  p.bp = mxd::band_plan_image(axis_view(*p.xt), axis_view(*p.yt), bi, g_tune[MXD_TUNE_BAND_LA].load());
+  p.band = p.bp.ok;
 }
 
 // Chooses the wave kernel of one image (p.wave = false: the general kernel):
@@ -723,8 +818,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     ImgPlan& p = plans[i];
     if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
     if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
-    if (!no_wave) plan_wave(im, stored ? stored[i] : whole(im), f32, out_dtype, p);
-    if (!p.wave) slow.push_back(i);
+    if (!no_wave) {
+      plan_band(im, stored ? stored[i] : whole(im), f32, p);
+      if (!p.band) plan_wave(im, stored ? stored[i] : whole(im), f32, out_dtype, p);
+    }
+    if (!p.band && !p.wave) slow.push_back(i);
   }
   DeviceGuard guard(device);
   auto fill = [&](ImgDev& d, int32_t i, const ImgPlan& p) {
@@ -748,9 +846,67 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     d.flip = im.flip ? 1 : 0;
   };
 
+  // Descriptors of one upload: band-kernel images first, then wave-kernel
+  // images, then the general kernel's.
+  std::vector<ImgDev> descs(n);
+
+  // Band launches: one per (class, window KiB, lookahead).
+  auto bkey = [&](int32_t i) {
+    const mxd::BandPlan& b = plans[i].bp;
+    return std::make_tuple(b.cls, b.nq, b.la);
+  };
+  std::vector<int32_t> border;
+  for (int32_t i = 0; i < n; i++)
+    if (plans[i].band) border.push_back(i);
+  std::stable_sort(border.begin(), border.end(), [&](int32_t a, int32_t b) { return bkey(a) < bkey(b); });
+  const int32_t nbd = (int32_t)border.size();
+  struct BandGroup {
+    int32_t first, count, units;
+    mxd::BandCfg cfg;
+  };
+  std::vector<BandGroup> bgroups;
+  for (int32_t k = 0; k < nbd; k++) {
+    const mxd::BandPlan& b = plans[border[k]].bp;
+    if (bgroups.empty() || bkey(border[bgroups.back().first]) != bkey(border[k]))
+      bgroups.push_back({k, 0, 0, mxd::BandCfg{channels, f32, b.nq, b.taps, b.s, b.db, b.la, 0, 0, 0}});
+    bgroups.back().count++;
+  }
+  for (BandGroup& g : bgroups) {
+    g.cfg.nimgs = g.count;
+    std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
+    for (int32_t k = g.first; k < g.first + g.count; k++)
+      strips.push_back({plans[border[k]].bp.nstrips, images[border[k]].crop_h});
+    const int32_t forced = g_tune[MXD_TUNE_BAND_ROWS].load();
+    const int32_t ty = forced > 0 ? forced : band_rows(strips, band_capacity_cached(g.cfg, device), kBandMaxRows);
+    for (int32_t k = g.first; k < g.first + g.count; k++) {
+      const int32_t i = border[k];
+      const mxd_image& im = images[i];
+      const ImgPlan& p = plans[i];
+      ImgDev& d = descs[k];
+      fill(d, i, p);
+      const uintptr_t a = reinterpret_cast<uintptr_t>(d.src);
+      d.src = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
+      d.flip |= (int32_t)(a & 3) << 8;
+      d.ty = std::min(ty, im.crop_h);
+      const DevSched* sc = nullptr;
+      if (int rc = band_schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty, p.bp.db,
+                                        p.bp.s, p.bp.prologue, &sc))
+        return rc;
+      d.ytab = reinterpret_cast<const float*>(sc->ptr);
+      d.ywidth = sc->band_words;
+      d.group = 0;
+      d.tile_begin = g.units;
+      d.nstrips = p.bp.nstrips;
+      d.tx = p.bp.tx;
+      const int32_t u = d.nstrips * ((im.crop_h + d.ty - 1) / d.ty);
+      g.cfg.per_img = k == g.first ? u : (g.cfg.per_img == u ? u : 0);
+      g.units += u;
+    }
+    g.cfg.nunits = g.units;
+  }
+
   // Wave launches: one per kernel (kind, tap bucket, scatter shape, q,
-  // shift); their descriptors come first in the one upload, the general
-  // kernel's after them.
+  // shift).
   auto key = [&](int32_t i) {
     const ImgPlan& p = plans[i];
     return std::make_tuple(p.kind, p.bucket, p.s, p.dmax, p.q, p.shift, p.pp);
@@ -760,7 +916,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (plans[i].wave) order.push_back(i);
   std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
   const int32_t nw = (int32_t)order.size();
-  std::vector<ImgDev> descs(n);
+  const int32_t wbase = nbd;  // first wave descriptor
   struct Group {
     int32_t first, count, units, ty;
     mxd::WaveCfg cfg;
@@ -782,7 +938,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const int32_t i = order[k];
       const mxd_image& im = images[i];
       const ImgPlan& p = plans[i];
-      ImgDev& d = descs[k];
+      ImgDev& d = descs[wbase + k];
       fill(d, i, p);
       // aligned base + byte shift (ImgDev::flip bits 8..)
       const uintptr_t a = reinterpret_cast<uintptr_t>(d.src);
@@ -856,7 +1012,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       group = std::max<int32_t>(1, std::min<int32_t>(group, kLdsBudget / (vw * 4)));
       group = std::min(group, ty);
       const int32_t nbands = (im.crop_h + ty - 1) / ty;
-      ImgDev& d = descs[nw + k];
+      ImgDev& d = descs[wbase + nw + k];
       fill(d, i, plans[i]);
       d.src = base0(i);
       d.src_h = im.src_h;
@@ -888,11 +1044,14 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   // tail overlaps the next.
   struct Launch {
     int64_t units;
-    int32_t group;  // -1: the general kernel
+    int32_t kind;   // 0 band, 1 wave, 2 general
+    int32_t group;
   };
   std::vector<Launch> launches;
-  for (size_t g = 0; g < groups.size(); g++) launches.push_back({groups[g].units, (int32_t)g});
-  if (!slow.empty()) launches.push_back({tiles, -1});
+  // (a band unit is a workgroup, ~4 wave units)
+  for (size_t g = 0; g < bgroups.size(); g++) launches.push_back({4 * (int64_t)bgroups[g].units, 0, (int32_t)g});
+  for (size_t g = 0; g < groups.size(); g++) launches.push_back({groups[g].units, 1, (int32_t)g});
+  if (!slow.empty()) launches.push_back({tiles, 2, -1});
   std::stable_sort(launches.begin(), launches.end(), [](const Launch& a, const Launch& b) { return a.units > b.units; });
   const int nfork = std::min<int>((int)launches.size() - 1, Workspace::kHelpers);
   if (nfork > 0) {
@@ -910,11 +1069,14 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const int lane = nfork > 0 ? (int)(k % (size_t)(nfork + 1)) : 0;
     void* s = lane == 0 ? stream : reinterpret_cast<void*>(ws->helper[lane - 1]);
     int rc = 0;
-    if (launches[k].group >= 0) {
+    if (launches[k].kind == 0) {
+      const BandGroup& g = bgroups[launches[k].group];
+      rc = mxd::launch_band(g.cfg, dev + g.first, s);
+    } else if (launches[k].kind == 1) {
       const Group& g = groups[launches[k].group];
-      rc = mxd::launch_wave(g.cfg, dev + g.first, s);
+      rc = mxd::launch_wave(g.cfg, dev + wbase + g.first, s);
     } else {
-      rc = mxd::launch_resample(cfg, dev + nw, s);
+      rc = mxd::launch_resample(cfg, dev + wbase + nw, s);
     }
     if (rc)
       return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
@@ -1275,6 +1437,30 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
 }
 
 int mxd_set_kernel_policy(int32_t policy) { return g_policy.exchange(policy); }
+
+int mxd_set_tuning(int32_t knob, int32_t value) {
+  if (knob < 0 || knob >= MXD_TUNE_COUNT) return -1;
+  return g_tune[knob].exchange(value);
+}
+
+int mxd_describe_band_plan(const mxd_image* image, int32_t out_dtype, int32_t* info12) {
+  if (!image || !info12) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  if (int rc = validate(*image, 0)) return rc;
+  ImgPlan p;
+  if (int rc = host_tables().get(0, image->src_w, image->resize_w, &p.xt)) return rc;
+  if (int rc = host_tables().get(0, image->src_h, image->resize_h, &p.yt)) return rc;
+  const int32_t f32 = out_dtype == MXD_F32_DIV255 ? 1 : 0;
+  plan_band(*image, whole(*image), f32, p);
+  const mxd::BandPlan& b = p.bp;
+  mxd::BandCfg cfg{};
+  cfg.nq = b.nq;
+  cfg.db = b.db;
+  cfg.la = b.la;
+  const int32_t v[12] = {p.band ? 1 : 0, b.taps, b.db, b.s, b.nq, b.nstrips, b.tx, b.prologue, b.dmax, b.la,
+                         b.ok ? mxd::band_lds_bytes(cfg) : 0, 0};
+  std::memcpy(info12, v, sizeof v);
+  return MXD_OK;
+}
 
 int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device, int32_t* info8) {
   if (!image || !info8) return fail(MXD_ERR_INVALID, "mxd: null argument");

@@ -9,9 +9,10 @@ namespace mxd {
 // One entry of a per-axis tap table in device memory: the first input index
 // and tap count stored as int bits, then `width` f32 weights, zero padded to
 // at least kMinTabWidth so the wave kernel can read T <= kMinTabWidth
-// weights of any entry unconditionally.
+// weights of any entry unconditionally (wave.hip reads up to 17, band.hip
+// up to its largest class, 25).
 constexpr int kTapHeader = 2;
-constexpr int kMinTabWidth = 24;
+constexpr int kMinTabWidth = 26;
 
 // Per-image parameters, resolved by the host (geometry already validated).
 // Each image is cut into nbands x nstrips tiles of ty output rows x tx output

@@ -49,10 +49,13 @@
 #include <type_traits>
 #include <utility>
 
+#include "devutil.h"
 #include "resample.h"
 
 namespace mxd {
 namespace {
+
+using namespace dev;
 
 // Waves per workgroup (tuning builds: -DMXD_WAVES=<1|2|4|8>).
 #ifndef MXD_WAVES
@@ -125,11 +128,7 @@ constexpr int kMaxStamped = 32768;
 __device__ unsigned long long g_stamps[2 * kMaxStamped];
 #endif
 
-#define GLOBAL_PTR(T, p) ((__attribute__((address_space(1))) T*)(p))
-using cgfloat = const __attribute__((address_space(1))) float;
-// Constant address space: uniform loads through it are scalar (s_load).
-using kfloat = const __attribute__((address_space(4))) float;
-using kint = const __attribute__((address_space(4))) int;
+#define GLOBAL_PTR(T, p) MXD_GLOBAL_PTR(T, p)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x3 __attribute__((ext_vector_type(3)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -164,15 +163,6 @@ struct Lay {
   static constexpr int CS = B ? 1 : PL;         // floats between the channels of a pixel
 };
 
-__device__ __forceinline__ int xcd_remap(int b, int n) {
-#ifdef MXD_NO_XCD_REMAP  // diagnostic builds: consecutive blocks on consecutive XCDs
-  return b;
-#endif
-  const int q = n >> 3, r = n & 7;
-  const int xcd = b & 7, idx = b >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
-
 // One f32 output store (vector memory; nontemporal unless MXD_NT_STORE == 0).
 template <class V, class T>
 __device__ __forceinline__ void store_out(V* p, T v) {
@@ -180,36 +170,6 @@ __device__ __forceinline__ void store_out(V* p, T v) {
     __builtin_nontemporal_store(v, p);
   else
     *p = v;
-}
-
-// Exact f32 q/255.0f for q in 0..255 (checked for all 256 values).
-__device__ __forceinline__ float div255(float q) {
-  const float inv = 1.0f / 255.0f;
-  const float r = q * inv;
-  const float e = __builtin_fmaf(-r, 255.0f, q);
-  return __builtin_fmaf(e, inv, r);
-}
-
-// stbir encode: (uint8)trunc(clamp(v*255 + 0.5, 0, 255)), v in byte units here.
-__device__ __forceinline__ float encode(float v) { return truncf(fminf(fmaxf(v + 0.5f, 0.0f), 255.0f)); }
-
-// A uniform pointer held in scalar registers.
-template <class P>
-__device__ __forceinline__ P uniform_ptr(const void* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  return (P)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
-}
-
-// Calls f(std::integral_constant<int, I>) for I = 0..N-1 (guaranteed unrolled,
-// so register-array indices derived from I are static).
-template <class F, int... Is>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // A voffset past any image (images are < 2^31 bytes): the buffer range check
@@ -316,26 +276,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// The image a unit belongs to (units are numbered through ImgDev::tile_begin).
-__device__ __forceinline__ const ImgDev& find_image(const ImgDev* imgs, int nimgs, int unit) {
-  int lo = 0, hi = nimgs - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (imgs[mid].tile_begin <= unit) lo = mid; else hi = mid - 1;
-  }
-  return imgs[lo];
-}
-
-// Window of output columns [ox0, ox1): first and last source pixel their taps
-// read.
-__device__ __forceinline__ void strip_span(cgfloat* xtab, int xs, int crop_w, int flip, int ox0, int ox1, int* lo,
-                                           int* hi) {
-  const int xa = flip ? crop_w - ox1 : ox0;
-  const int xb = flip ? crop_w - 1 - ox0 : ox1 - 1;
-  *lo = __float_as_int(xtab[xa * xs]);
-  *hi = __float_as_int(xtab[xb * xs]) + __float_as_int(xtab[xb * xs + 1]) - 1;
 }
 
 // Horizontal pass of one strip: lane l owns output pixels l + 64 q (q < Q).
@@ -516,7 +456,11 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
     void* base = uniform_ptr<void*>(im.src);
     const int stride = __builtin_amdgcn_readfirstlane((int)im.src_stride);
     const int rows = __builtin_amdgcn_readfirstlane(im.src_h);
-    src.live = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, stride * rows, 0x00020000);
+    // records end at the last stored row's last pixel (a page-locked source
+    // read in place must not be read past its image)
+    src.live = __builtin_amdgcn_make_buffer_rsrc(
+        base, (short)0, src_records(shift, rows, stride, (__builtin_amdgcn_readfirstlane(im.src_w) - sx0) * C),
+        0x00020000);
     src.dead = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0, 0x00020000);
     src.stride = stride;
     src.y0 = __builtin_amdgcn_readfirstlane(im.src_y0);

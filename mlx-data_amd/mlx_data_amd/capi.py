@@ -20,7 +20,8 @@ MXD_F32_DIV255 = 1
 EXPORTS = (
     "mxd_abi_version", "mxd_last_error", "mxd_device_count", "mxd_device_properties",
     "mxd_resize_smallest_side_dims", "mxd_center_crop_origin", "mxd_axis_taps",
-    "mxd_resize_crop_batch", "mxd_set_kernel_policy", "mxd_describe_plan", "mxd_copy_bandwidth",
+    "mxd_resize_crop_batch", "mxd_set_kernel_policy", "mxd_set_tuning", "mxd_describe_plan",
+    "mxd_describe_band_plan", "mxd_copy_bandwidth",
     "mxd_set_device", "mxd_malloc_device", "mxd_free_device", "mxd_malloc_pinned", "mxd_free_pinned",
     "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
     "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
@@ -44,6 +45,10 @@ MXD_POLICY_NO_DESC_CACHE = 8
 MXD_POLICY_NO_BYTES = 16
 MXD_POLICY_BYTES = 32
 MXD_POLICY_NO_ZERO_COPY = 64
+MXD_POLICY_NO_BAND = 128
+
+MXD_TUNE_BAND_ROWS = 0
+MXD_TUNE_BAND_LA = 1
 
 
 class MxdImage(ctypes.Structure):
@@ -196,15 +201,31 @@ def set_kernel_policy(policy):
     return lib().mxd_set_kernel_policy(int(policy))
 
 
+def set_tuning(knob, value):
+    """Process-wide tuning knob (MXD_TUNE_*; 0 = automatic); returns the previous value."""
+    return lib().mxd_set_tuning(int(knob), int(value))
+
+
 PLAN_FIELDS = ("wave", "kind", "taps", "s", "dmax", "q", "nstrips", "p")
 
 
 def describe_plan(entry, out_dtype=MXD_U8, device=0):
-    """The kernel mxd_resize_crop_batch picks for one image (host only)."""
+    """The wave-kernel plan of one image (what runs when the band kernel declines it; host only)."""
     arr, _ = make_images([dict(entry, src=entry.get("src", 256), dst=entry.get("dst", 256))])
     info = (ctypes.c_int32 * 8)()
     check(lib().mxd_describe_plan(arr, out_dtype, device, info))
     return dict(zip(PLAN_FIELDS, list(info)))
+
+
+BAND_FIELDS = ("band", "taps", "db", "s", "nq", "nstrips", "tx", "prologue", "dmax", "la", "lds_bytes")
+
+
+def describe_band_plan(entry, out_dtype=MXD_U8):
+    """The band-kernel plan of one image under the current policy (host only)."""
+    arr, _ = make_images([dict(entry, src=entry.get("src", 256), dst=entry.get("dst", 256))])
+    info = (ctypes.c_int32 * 12)()
+    check(lib().mxd_describe_band_plan(arr, out_dtype, info))
+    return dict(zip(BAND_FIELDS, list(info)))
 
 
 def resize_crop_host(images, n, out_dtype, device=0):

@@ -77,6 +77,21 @@ def resize(img, dw, dh, rgba_weighted=None):
     return out
 
 
+def resize_crop_vfirst(img, g):
+    """Kernel-order restatement (orc_resize_crop_vfirst): the geometry tuple
+    g = (rw, rh, cx, cy, cw, ch, flip) of a (H, W, C <= 3) uint8 image, summed
+    vertical-first in byte units with fmaf chains in tap order -- what the HIP
+    kernels must reproduce bit for bit."""
+    rw, rh, cx, cy, cw, ch, flip = g
+    img = np.ascontiguousarray(img)
+    h, w, c = img.shape
+    out = np.empty((ch, cw, c), np.uint8)
+    if lib().orc_resize_crop_vfirst(_ptr(img), w, h, c, ctypes.c_int64(w * c), _ptr(out), rw, rh, cx, cy, cw, ch,
+                                    int(bool(flip))):
+        raise ValueError("orc_resize_crop_vfirst failed")
+    return out
+
+
 def smallest_side_dims(w, h, size):
     tw, th = ctypes.c_int64(), ctypes.c_int64()
     if lib().orc_resize_smallest_side_dims(

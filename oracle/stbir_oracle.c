@@ -336,6 +336,73 @@ int orc_resize_u8(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw,
   return orc_resize_u8_layout(src, w, h, c, dst, dw, dh, c == 4);
 }
 
+/*
+ * Kernel-order restatement of resize -> crop -> hflip (SURVEY.md §8(c)2's
+ * "bit-exact when coefficient tables are shared" gate): the SAME tap tables as
+ * orc_resize_u8 (orc_axis_coeffs), but vertical pass first, in byte units
+ * (no decode to [0,1]), each sum an fmaf chain in tap order starting from 0,
+ * then the horizontal pass the same way, then stbir's encode
+ * (uint8)trunc(clamp(v + 0.5, 0, 255)).  This is the order the HIP kernels
+ * sum in (mlx-data_amd/csrc/band.hip, wave.hip), so they must match it bit for
+ * bit; it differs from the stbir-order restatement above only by f32
+ * rounding (+-1).  channels 1..3 (no alpha weighting).  Writes the crop
+ * window (cx, cy, cw, ch) of the (dw x dh) resize of the (w x h, row stride
+ * `stride` bytes) source, mirrored when flip, as ch x cw x c bytes.
+ */
+int orc_resize_crop_vfirst(const uint8_t* src, int w, int h, int c, int64_t stride, uint8_t* dst, int dw, int dh,
+                           int cx, int cy, int cw, int ch, int flip) {
+  if (w <= 0 || h <= 0 || dw <= 0 || dh <= 0 || c < 1 || c > 3) return -1;
+  if (cx < 0 || cy < 0 || cw <= 0 || ch <= 0 || cx + cw > dw || cy + ch > dh) return -1;
+  const int cwx = orc_axis_width(w, dw), cwy = orc_axis_width(h, dh);
+  int* x0 = (int*)malloc(sizeof(int) * (size_t)dw * 2);
+  int* y0 = (int*)malloc(sizeof(int) * (size_t)dh * 2);
+  float* wx = (float*)malloc(sizeof(float) * (size_t)dw * cwx);
+  float* wy = (float*)malloc(sizeof(float) * (size_t)dh * cwy);
+  float* vrow = (float*)malloc(sizeof(float) * (size_t)w * c);
+  int rc = -1;
+  if (!x0 || !y0 || !wx || !wy || !vrow) goto out;
+  if (orc_axis_coeffs(w, dw, cwx, x0, x0 + dw, wx)) goto out;
+  if (orc_axis_coeffs(h, dh, cwy, y0, y0 + dh, wy)) goto out;
+  /* only the source columns the window's horizontal taps read */
+  int xlo = x0[cx], xhi = x0[dw + cx];
+  for (int ox = cx; ox < cx + cw; ox++) {
+    if (x0[ox] < xlo) xlo = x0[ox];
+    if (x0[dw + ox] > xhi) xhi = x0[dw + ox];
+  }
+  for (int r = 0; r < ch; r++) {
+    const int oy = cy + r;
+    const int a = y0[oy], b = y0[dh + oy];
+    const float* cf = wy + (size_t)oy * cwy;
+    for (int i = xlo * c; i < (xhi + 1) * c; i++) {
+      float v = 0.0f;
+      for (int k = 0; k <= b - a; k++) v = fmaf(cf[k], (float)src[(size_t)(a + k) * stride + i], v);
+      vrow[i] = v;
+    }
+    uint8_t* d = dst + (size_t)r * cw * c;
+    for (int x = 0; x < cw; x++) {
+      const int ox = cx + (flip ? cw - 1 - x : x);
+      const int xa = x0[ox], xb = x0[dw + ox];
+      const float* cfx = wx + (size_t)ox * cwx;
+      for (int k2 = 0; k2 < c; k2++) {
+        float hsum = 0.0f;
+        for (int k = 0; k <= xb - xa; k++) hsum = fmaf(cfx[k], vrow[(xa + k) * c + k2], hsum);
+        float f = hsum + 0.5f;
+        if (f < 0.0f) f = 0.0f;
+        if (f > 255.0f) f = 255.0f;
+        d[x * c + k2] = (uint8_t)f;
+      }
+    }
+  }
+  rc = 0;
+out:
+  free(x0);
+  free(y0);
+  free(wx);
+  free(wy);
+  free(vrow);
+  return rc;
+}
+
 /* ImageCenterCrop::apply_image offsets (integer floor). */
 int orc_center_crop_origin(int64_t w, int64_t h, int64_t cw, int64_t ch, int64_t* x, int64_t* y) {
   if (ch > h || cw > w) return -1;

@@ -129,3 +129,18 @@ def test_resize_vs_pillow_bilinear(h, w):
     pil = np.asarray(Image.fromarray(img).resize((tw, th), Image.BILINEAR)).astype(np.int32)
     x, y = O.center_crop_origin(tw, th, 224, 224)
     assert np.abs(ours - pil)[y : y + 224, x : x + 224].max() <= 1
+
+
+def test_vfirst_restatement_within_one_of_stbir_order():
+    """The kernel-order restatement (vertical first, byte units, fmaf chains)
+    differs from the stbir-order one only by f32 rounding: +-1, rarely."""
+    rng = np.random.default_rng(4)
+    for (h, w, rw, rh, cx, cy, cw, ch) in [(96, 128, 43, 32, 5, 3, 30, 28), (50, 75, 96, 64, 10, 4, 56, 56),
+                                          (210, 380, 45, 25, 0, 0, 45, 25)]:
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        a = O.resize_crop_vfirst(img, (rw, rh, cx, cy, cw, ch, 0))
+        b = O.crop(O.resize(img, rw, rh), cx, cy, cw, ch)
+        d = np.abs(a.astype(int) - b.astype(int))
+        assert d.max() <= 1 and (d > 0).mean() < 0.01
+        m = O.resize_crop_vfirst(img, (rw, rh, cx, cy, cw, ch, 1))
+        assert np.array_equal(m, a[:, ::-1])
