@@ -1811,11 +1811,13 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   }
   // Chunks of about kChunk staged bytes (at least one image each).
   constexpr int64_t kChunk = 24 << 20;
+  // (and at most 65535 images: the JPEG colour kernel puts one image per grid row)
+  constexpr int32_t kChunkImages = 65535;
   std::vector<std::pair<int32_t, int32_t>> chunks;  // [first, end)
   for (int32_t i = 0; i < n;) {
     int32_t j = i;
     int64_t bytes = 0;
-    while (j < n && (j == i || bytes + st[j].in_size <= kChunk)) {
+    while (j < n && j - i < kChunkImages && (j == i || bytes + st[j].in_size <= kChunk)) {
       bytes += st[j].in_size;
       j++;
     }
@@ -1824,6 +1826,16 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   }
   CtxLease lease(device);
   HostCtx& ctx = *lease.ctx;
+  // On every exit (an error return included) the context goes back to the
+  // pool idle: no kernel of this call may still read its slot buffers or
+  // write the caller's destinations once the call has returned.
+  struct Drain {
+    HostCtx& c;
+    ~Drain() {
+      for (Slot& sl : c.slot)
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+    }
+  } drain{ctx};
   for (Slot& sl : ctx.slot)
     if (int rc = init_slot(sl)) return rc;
   int pending[2] = {-1, -1};  // chunk in flight on each slot

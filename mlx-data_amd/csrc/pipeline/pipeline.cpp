@@ -737,6 +737,16 @@ std::vector<uint8_t> read_file(const std::string& path) {
   return data;
 }
 
+// Up to `n` leading bytes of a file; false when it cannot be opened.
+bool read_prefix(const std::string& path, size_t n, std::vector<uint8_t>* out) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  out->resize(n);
+  out->resize(std::fread(out->data(), 1, n, f));
+  std::fclose(f);
+  return true;
+}
+
 // libjpeg's message without the C ABI's "load_jpeg: " prefix.
 std::string jpeg_error() {
   std::string m = mxd_last_error();
@@ -765,13 +775,35 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
   if (from_memory_) {
     bytes = static_cast<const uint8_t*>(x->data());
     nbytes = (size_t)x->nbytes();
-  } else {
-    file = read_file(path);
+  } else if (info_) {
+    // core::image::info -> stbi_info (ImageIO.cpp:26-32): the header only;
+    // (0, 0) when the file cannot be opened or parsed.  A JPEG's frame header
+    // follows its APP segments, so a short prefix is read first.
+    constexpr size_t kHead = 1 << 18;
+    if (!read_prefix(path, kHead, &file)) {
+      auto out = std::make_shared<Array>(DType::Int64, std::vector<int64_t>{2});
+      static_cast<int64_t*>(out->data())[0] = static_cast<int64_t*>(out->data())[1] = 0;
+      return out;
+    }
+    int32_t w = 0, h = 0, c = 0;
+    if (mxd_is_jpeg(file.data(), file.size()) && file.size() == kHead &&
+        mxd_jpeg_info(file.data(), file.size(), &w, &h, &c) != MXD_OK)
+      file = read_file(path);  // frame header past the prefix
     bytes = file.data();
     nbytes = file.size();
+  } else {
+    // load_jpeg's signature check (ImageJPEG.cpp:74-86) first: only JPEGs are
+    // read here, anything else goes to the stb_image hook by path.
+    std::vector<uint8_t> sig;
+    if (!read_prefix(path, 3, &sig)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+    if (mxd_is_jpeg(sig.data(), sig.size())) {
+      file = read_file(path);
+      bytes = file.data();
+      nbytes = file.size();
+    }
   }
   const std::string where = from_memory_ ? std::string("from memory") : "<" + path + ">";
-  if (mxd_is_jpeg(bytes, nbytes)) {
+  if (bytes && mxd_is_jpeg(bytes, nbytes)) {
     int32_t w = 0, h = 0, c = 0;
     const bool ok = mxd_jpeg_info(bytes, nbytes, &w, &h, &c) == MXD_OK;
     if (info_) {

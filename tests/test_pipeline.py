@@ -233,6 +233,28 @@ def test_load_image(tmp_path):
         dx.buffer_from_vector([dict(f=np.zeros(3, np.uint8))]).load_image("f")[0]
 
 
+def test_load_image_info_reads_headers_only(tmp_path):
+    """info=True is core::image::info -> stbi_info (core/image/ImageIO.cpp:26-32):
+    (0, 0) for a file that cannot be opened (no exception), the frame size of a
+    JPEG whose APP segments push its frame header far into the file, and the
+    non-JPEG formats through the stb_image hook."""
+    from PIL import Image
+
+    rng = np.random.default_rng(4)
+    arr = rng.integers(0, 256, (30, 50, 3), dtype=np.uint8)
+    Image.fromarray(arr).save(tmp_path / "a.jpg", quality=90)
+    Image.fromarray(arr).save(tmp_path / "c.png")
+    raw = (tmp_path / "a.jpg").read_bytes()
+    # five 60 KB APP15 segments (~300 KB) between SOI and the frame header
+    app = b"".join(b"\xff\xef" + (60002).to_bytes(2, "big") + bytes(60000) for _ in range(5))
+    (tmp_path / "big.jpg").write_bytes(raw[:2] + app + raw[2:])
+    b = dx.buffer_from_vector([dict(f=b"missing.jpg"), dict(f=b"a.jpg"), dict(f=b"big.jpg"), dict(f=b"c.png")])
+    info = b.load_image("f", prefix=str(tmp_path), info=True)
+    assert [info[i]["f"].tolist() for i in range(4)] == [[0, 0], [50, 30], [50, 30], [50, 30]]
+    big = dx.buffer_from_vector([dict(f=b"big.jpg")]).load_image("f", prefix=str(tmp_path))[0]["f"]
+    assert np.array_equal(big, np.asarray(Image.open(tmp_path / "a.jpg").convert("RGB")))
+
+
 AREA = np.load(os.path.join(os.path.dirname(__file__), "golden", "rng_area.npz"))
 AREA_CASES = sorted({int(k.split("_")[1]) for k in AREA.files})
 
