@@ -121,6 +121,23 @@ def make_workload(capi, name, batch, rank, c3_sizes=None):
     return sizes, geoms, WORKLOADS[name]["f32"]
 
 
+def kernel_name(capi, size, g, f32, policy):
+    """Which kernel family runs the workload's first image under `policy`."""
+    sw, sh = size
+    e = dict(src_w=sw, src_h=sh, src_stride=(sw * C + 15) // 16 * 16, channels=C, resize_w=g[0], resize_h=g[1],
+             crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6], dst_stride=g[4] * C * (4 if f32 else 1))
+    dt = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
+    prev = capi.set_kernel_policy(policy)
+    try:
+        b = capi.describe_band_plan(e, dt)
+        if b["band"]:
+            return "resample_band (taps {taps}, rows/group {db}, window {nq} KiB, strips {nstrips}, ahead {la})".format(**b)
+        w = capi.describe_plan(e, dt)
+        return "resample_wave" if w["wave"] else "resample_tiles"
+    finally:
+        capi.set_kernel_policy(prev)
+
+
 def load_traffic(workload):
     """HBM bytes per launch measured for this workload's kernel: the record
     profiles/traffic.json names for it (file, tag and corrected bytes)."""
@@ -373,6 +390,9 @@ def main():
     ap.add_argument("--sets", type=int, default=2, help=argparse.SUPPRESS)
     # streams the timed steps alternate over (independent batches, like prefetch workers)
     ap.add_argument("--streams", type=int, default=2)
+    # tuning knobs (include/mxd_amd.h mxd_tune; measurements only): band rows, groups ahead
+    ap.add_argument("--tune-rows", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--tune-la", type=int, default=0, help=argparse.SUPPRESS)
     # timing plumbing without a GPU (tests/test_bench_dist.py): each step sleeps
     ap.add_argument("--simulate", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -399,6 +419,10 @@ def main():
     capi.check(capi.lib().mxd_set_device(dev))
     if args.policy:
         capi.set_kernel_policy(args.policy)
+    if args.tune_rows:
+        capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, args.tune_rows)
+    if args.tune_la:
+        capi.set_tuning(capi.MXD_TUNE_BAND_LA, args.tune_la)
     c3_sizes = [tuple(int(v) for v in t.split("x")) for t in args.c3_sizes.split(",") if t]
     sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank, c3_sizes)
     elem = 4 if f32 else 1
@@ -490,6 +514,7 @@ def main():
                 "kernel_ms_per_launch": round(kernel_ms, 5),
                 "sustained_gbs": round(alg_bytes / (wall / max(1, args.steps)) / 1e9, 1) if args.steps else None,
                 "ms_per_launch_fresh_descriptors": round(fresh_ms, 5) if fresh_ms else None,
+                "kernel": kernel_name(capi, sizes[0], geoms[0], f32, args.policy),
                 "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
                 "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None}
 

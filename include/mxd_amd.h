@@ -122,8 +122,8 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
  * the band kernel -- one workgroup streams an image band's source rows into
  * LDS by LDS-DMA -- wherever its classes fit, else a wave kernel, else the
  * general kernel).  MXD_POLICY_NO_BAND: never the band kernel (any of the
- * wave-kernel bits below implies it).  MXD_POLICY_NO_SCATTER: wave kernels gather every output row's taps instead
- * of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
+ * wave-kernel bits below implies it).  MXD_POLICY_NO_SCATTER: wave kernels gather every
+ * output row's taps instead of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
  * general workgroup-tile kernel; MXD_POLICY_NARROW: wave kernels keep the
  * narrow per-lane window (no wide RGB strips, no byte lanes);
  * MXD_POLICY_NO_DESC_CACHE: every batch uploads its descriptor array even

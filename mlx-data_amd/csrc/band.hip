@@ -43,8 +43,55 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define MXD_BAND_NT 1
 #endif
 constexpr int kStoreAux = MXD_BAND_NT ? 2 : 0;  // gfx950 cache-policy bits: 2 = nt
+// Progress-based priority (as wave.hip's progress_prio; tuning builds
+// -DMXD_BAND_PRIO=0): the SIMD arbiter issues oldest-first, so the workgroups
+// sharing a CU would otherwise finish in age order (C2 stamps: units of one
+// launch ending between 120 and 161 us); each unit lowers its s_setprio level
+// as it completes quarters of its band, so units behind win the arbiter.
+#ifndef MXD_BAND_PRIO
+#define MXD_BAND_PRIO 1
+#endif
+__device__ __forceinline__ void band_prio(int done, int total) {
+  if constexpr (MXD_BAND_PRIO != 0) {
+    switch (3 - (4 * done) / (total + 1)) {
+      case 3: __builtin_amdgcn_s_setprio(3); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(0); break;
+    }
+  }
+}
+
+// Timing-only ablations (tools/band_variants.sh builds, never the product
+// library): 1 = no source loads, 2 = no output stores, 4 = no horizontal
+// arithmetic, 8 = no vertical arithmetic.
+#ifndef MXD_BAND_ABLATE
+#define MXD_BAND_ABLATE 0
+#endif
+
+// Branch-free vertical pass (see vpass); tuning builds: -DMXD_BAND_BRANCHLESS=0.
+#ifndef MXD_BAND_BRANCHLESS
+#define MXD_BAND_BRANCHLESS 1
+#endif
 
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
+
+// Diagnostic builds only (-DMXD_BAND_STAMPS=1, tools/band_stamps.sh; never
+// the product library): wave 0 of every unit sums the shader-clock cycles of
+// each segment of its steps, read back with mxd_debug_band_stamps.
+#ifndef MXD_BAND_STAMPS
+#define MXD_BAND_STAMPS 0
+#endif
+[[maybe_unused]] constexpr int kStampSegs = 10;  // setup, wait, barrier 1, H, V, barrier 2, write+issue, steps, start, end
+#if MXD_BAND_STAMPS
+constexpr int kMaxStamped = 8192;
+__device__ unsigned long long g_band_stamps[kStampSegs * kMaxStamped];
+#define MXD_STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define MXD_SEG(k, a, b) seg[k] += (b) - (a)
+#else
+#define MXD_STAMP(var)
+#define MXD_SEG(k, a, b)
+#endif
 
 // s_waitcnt vmcnt(n) for a run-time, wave-uniform n (the count is an
 // immediate); n > 63 waits for 63 (more than asked: always safe).
@@ -129,6 +176,11 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
   const int wave = RFL(tid >> 6);
   const int unit = RFL(xcd_remap(blockIdx.x, gridDim.x));
   if (unit >= nunits) return;  // the whole workgroup
+#if MXD_BAND_STAMPS
+  unsigned long long seg[kStampSegs] = {};
+  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
+  MXD_STAMP(t_setup0);
+#endif
 
   const ImgDev& im = per_img > 0 ? imgs[unit / per_img] : find_image(imgs, nimgs, unit);
   const int nstrips = RFL(im.nstrips);
@@ -214,7 +266,7 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
       const int j = i / NQ, k = i - (i / NQ) * NQ;
       const int row = dr[m];
       const int c = b0 + kChunk * k + 16 * lane;
-      const int voff = (row >= 0 && c < bend) ? (row - y0) * stride + c : kNoLoad;
+      const int voff = (row >= 0 && c < bend && !(MXD_BAND_ABLATE & 1)) ? (row - y0) * stride + c : kNoLoad;
       const uint32_t to = row >= 0 ? (uint32_t)(a * AREA + (j * NQ + k) * kChunk) : sink;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_u8*)(smem + to), 16, voff, 0, 0, 0);
     });
@@ -228,9 +280,12 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
 
   // Vertical pass of group g (accumulator slot SL = g mod S) from area a:
   // thread t converts dwords t, t + 256, ... of each row slot.  Row slots
-  // and their schedule entries are read in batches of up to 4 before any use
-  // (absent rows read stale bytes that are never used), so the latencies
-  // overlap.
+  // and their schedule entries are read in batches of up to 4 before any use,
+  // and (MXD_BAND_BRANCHLESS) every slot is converted and FMA'd into every
+  // accumulator unconditionally: absent rows and unused slots carry weight 0,
+  // and fma(0, x, acc) == acc for the finite x a byte converts to (a zero may
+  // change sign, which the encode cannot see), so the batch is one branch-free
+  // block the compiler can schedule.
   auto vpass = [&](auto slc, int g, int a) {
     constexpr int SL = decltype(slc)::value;
     constexpr int JB = DB < 4 ? DB : 4;
@@ -250,14 +305,18 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
       static_for<JN>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const int* e = ev + j * E;
-        if (e[0] >= 0) {
+        if (MXD_BAND_BRANCHLESS || e[0] >= 0) {
+          if constexpr ((MXD_BAND_ABLATE & 8) != 0) {
+            acc[SL][0] += __uint_as_float(d[j][0] & 0x3fffffffu);
+            return;
+          }
           float x[NX];
 #pragma unroll
           for (int i = 0; i < NX; i++) x[i] = (float)((d[j][i >> 2] >> (8 * (i & 3))) & 0xffu);
           static_for<S>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
             const float w = __int_as_float(e[1 + s]);
-            if (s == 0 || w != 0.0f) {
+            if (MXD_BAND_BRANCHLESS || s == 0 || w != 0.0f) {
 #pragma unroll
               for (int i = 0; i < NX; i++) acc[(SL + s) % S][i] = __builtin_fmaf(w, x[i], acc[(SL + s) % S][i]);
             }
@@ -283,18 +342,25 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
     for (int i = 0; i < NX; i++) acc[SL][i] = 0.0f;
   };
 
-  // Horizontal pass of output row y from the vertical row in area a.
-  auto hpass = [&](int a, int y) {
+  // Horizontal pass of output row y from the vertical row in area a; run
+  // every step (out = false: a prologue or first step, whose area holds no
+  // vertical row -- the result goes nowhere), so it shares a block with the
+  // vertical pass and every wave issues the same stores each step.
+  auto hpass = [&](int a, int y, bool out) {
     const float* vf = reinterpret_cast<const float*>(smem + a * AREA) + vb;
     float q[C];
 #pragma unroll
     for (int c = 0; c < C; c++) {
       float h = 0.0f;
+      if constexpr ((MXD_BAND_ABLATE & 4) != 0) {
+        h = vf[c];
+      } else {
 #pragma unroll
-      for (int k = 0; k < T; k++) h = __builtin_fmaf(wx[k], vf[k * C + c], h);
+        for (int k = 0; k < T; k++) h = __builtin_fmaf(wx[k], vf[k * C + c], h);
+      }
       q[c] = encode(h);
     }
-    store_pixel<C, F32>(dst, hact ? y * dstride + scol : kNoLoad, q);
+    store_pixel<C, F32>(dst, hact && out && !(MXD_BAND_ABLATE & 2) ? y * dstride + scol : kNoLoad, q);
   };
 
   for (int g = 0; g < la; g++) {
@@ -304,6 +370,10 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
   }
   int acur = 0, aprev = rg - 1;  // areas of groups g and g - 1
   bool done = false;
+#if MXD_BAND_STAMPS
+  MXD_STAMP(t_loop0);
+  MXD_SEG(0, t_setup0, t_loop0);
+#endif
   for (int g0 = 0;; g0 += S) {
     static_for<S>([&](auto sc) {
       const int g = g0 + decltype(sc)::value;
@@ -311,18 +381,34 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
         done = true;
         return;
       }
+      if ((g & 7) == 0) band_prio(g, ngroups);
       int dr[KW];
       dma_rows(g + la, dr);
       // Vector-memory ops this wave issued after group g's LDS-DMA: the DMA
       // of the la - 1 groups after it, and the stores of the steps since.
-      const int first_st = max(g - la + 1, P + 1);
-      wait_vmcnt((la - 1) * KW + SW * max(0, g - first_st));
+      MXD_STAMP(ta);
+      wait_vmcnt((la - 1) * KW + SW * min(g, la - 1));
+      MXD_STAMP(tb);
       barrier_lds();  // group g's rows and output row g - 1 - P's vertical row visible
-      if (g > P) hpass(aprev, oy0 + g - 1 - P);
-      if (g < ngroups) vpass(sc, g, acur);
+      MXD_STAMP(tc);
+      hpass(aprev, oy0 + g - 1 - P, g > P);
+      MXD_STAMP(td);
+      vpass(sc, g, acur);  // g == ngroups: the all-absent group, weights 0
+      MXD_STAMP(te);
       barrier_lds();  // area acur's rows and area aprev's vertical row consumed
+      MXD_STAMP(tf);
       if (g < ngroups && g >= P) vwrite(sc, acur);
       issue(dr, aprev);  // group g + la: (g + la) mod (la + 1) == (g - 1) mod (la + 1)
+#if MXD_BAND_STAMPS
+      MXD_STAMP(tg);
+      MXD_SEG(1, ta, tb);
+      MXD_SEG(2, tb, tc);
+      MXD_SEG(3, tc, td);
+      MXD_SEG(4, td, te);
+      MXD_SEG(5, te, tf);
+      MXD_SEG(6, tf, tg);
+      seg[7] += 1;
+#endif
       aprev = acur;
       acur = acur + 1 == rg ? 0 : acur + 1;
     });
@@ -330,6 +416,12 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
   }
   // no LDS-DMA may land after the workgroup's LDS is reassigned
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if MXD_BAND_STAMPS
+  seg[8] = t_real0;
+  seg[9] = __builtin_amdgcn_s_memrealtime();
+  if (wave == 0 && lane == 0 && unit < kMaxStamped)
+    for (int k = 0; k < kStampSegs; k++) g_band_stamps[kStampSegs * unit + k] = seg[k];
+#endif
 }
 
 using BandKernel = void (*)(const ImgDev*, int, int, int, int);
@@ -342,13 +434,29 @@ int class_index(const BandCfg& cfg) {
   return -1;
 }
 
+// Variant / diagnostic builds may instantiate one class and window only
+// (-DMXD_BAND_ONLY_CLASS=<index> -DMXD_BAND_ONLY_NQ=<KiB>, for fast A/B builds).
+template <int CI, int NQ>
+constexpr bool built() {
+#if defined(MXD_BAND_ONLY_CLASS) && defined(MXD_BAND_ONLY_NQ)
+  return CI == MXD_BAND_ONLY_CLASS && NQ == MXD_BAND_ONLY_NQ;
+#else
+  return true;
+#endif
+}
+
+template <int C, bool F32, int NQ, int CI>
+BandKernel class_kernel() {
+  if constexpr (built<CI, NQ>())
+    return resample_band<C, F32, NQ, kBandClasses[CI].taps, kBandClasses[CI].s, kBandClasses[CI].db>;
+  else
+    return nullptr;
+}
+
 template <int C, bool F32, int NQ, int... CI>
 BandKernel pick_class(int ci, std::integer_sequence<int, CI...>) {
   BandKernel k = nullptr;
-  ((ci == CI ? (k = resample_band<C, F32, NQ, kBandClasses[CI].taps, kBandClasses[CI].s, kBandClasses[CI].db>,
-                0)
-             : 0),
-   ...);
+  ((ci == CI ? (k = class_kernel<C, F32, NQ, CI>(), 0) : 0), ...);
   return k;
 }
 
@@ -401,3 +509,14 @@ int launch_band(const BandCfg& cfg, const ImgDev* imgs, void* stream) {
 }
 
 }  // namespace mxd
+
+#if MXD_BAND_STAMPS
+// Copies the first n units' segment sums of the last stamped launch.
+extern "C" int mxd_debug_band_stamps(unsigned long long* host, int n) {
+  if (n > mxd::kMaxStamped) n = mxd::kMaxStamped;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mxd::g_band_stamps),
+                             sizeof(unsigned long long) * mxd::kStampSegs * n, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif

@@ -21,6 +21,7 @@
 #include <string>
 #include <thread>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "mxd_amd.h"
@@ -762,6 +763,27 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
   }
 }
 
+// What a plan depends on: geometry, the stored region's layout and the
+// alignments of source and destination.
+struct PlanKey {
+  int32_t v[20];
+  bool operator==(const PlanKey& o) const { return std::memcmp(v, o.v, sizeof v) == 0; }
+};
+struct PlanKeyHash {
+  size_t operator()(const PlanKey& k) const {
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the words
+    for (int32_t x : k.v) h = (h ^ (uint32_t)x) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+PlanKey plan_key(const mxd_image& im, const Stored& st) {
+  const uint64_t ss = (uint64_t)st.stride, ds = (uint64_t)im.dst_stride;
+  return PlanKey{{im.src_w, im.src_h, im.channels, im.resize_w, im.resize_h, im.crop_x, im.crop_y, im.crop_w,
+                  im.crop_h, im.flip ? 1 : 0, im.rgba_weighted, st.x0, st.rows, (int32_t)ss, (int32_t)(ss >> 32),
+                  (int32_t)ds, (int32_t)(ds >> 32), (int32_t)(reinterpret_cast<uintptr_t>(st.base) & 15),
+                  (int32_t)(reinterpret_cast<uintptr_t>(im.dst) & 15), 0}};
+}
+
 int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, void* stream,
               const Stored* stored = nullptr) {
   if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
@@ -813,16 +835,31 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   const bool no_wave = (g_policy.load() & MXD_POLICY_NO_WAVE) != 0;
   std::vector<ImgPlan> plans(n);
   std::vector<int32_t> slow;  // images for the general kernel
-  for (int32_t i = 0; i < n; i++) {
-    const mxd_image& im = images[i];
-    ImgPlan& p = plans[i];
-    if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
-    if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
-    if (!no_wave) {
-      plan_band(im, stored ? stored[i] : whole(im), f32, p);
-      if (!p.band) plan_wave(im, stored ? stored[i] : whole(im), f32, out_dtype, p);
+  // Images of one geometry, layout and alignment share a plan (and later a
+  // schedule): planning walks tap tables, and a batch rarely holds more than
+  // a few shapes.  rep[i] = the first image with image i's key.
+  std::vector<int32_t> rep(n);
+  {
+    std::unordered_map<PlanKey, int32_t, PlanKeyHash> first_of;
+    first_of.reserve(16);
+    for (int32_t i = 0; i < n; i++) {
+      const mxd_image& im = images[i];
+      const Stored st = stored ? stored[i] : whole(im);
+      const auto ins = first_of.emplace(plan_key(im, st), i);
+      rep[i] = ins.first->second;
+      ImgPlan& p = plans[i];
+      if (!ins.second) {
+        p = plans[rep[i]];
+      } else {
+        if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
+        if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
+        if (!no_wave) {
+          plan_band(im, st, f32, p);
+          if (!p.band) plan_wave(im, st, f32, out_dtype, p);
+        }
+      }
+      if (!p.band && !p.wave) slow.push_back(i);
     }
-    if (!p.band && !p.wave) slow.push_back(i);
   }
   DeviceGuard guard(device);
   auto fill = [&](ImgDev& d, int32_t i, const ImgPlan& p) {
@@ -878,6 +915,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       strips.push_back({plans[border[k]].bp.nstrips, images[border[k]].crop_h});
     const int32_t forced = g_tune[MXD_TUNE_BAND_ROWS].load();
     const int32_t ty = forced > 0 ? forced : band_rows(strips, band_capacity_cached(g.cfg, device), kBandMaxRows);
+    std::unordered_map<int32_t, const DevSched*> sched_of;  // by rep[] (one geometry, one band height)
     for (int32_t k = g.first; k < g.first + g.count; k++) {
       const int32_t i = border[k];
       const mxd_image& im = images[i];
@@ -888,10 +926,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       d.src = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
       d.flip |= (int32_t)(a & 3) << 8;
       d.ty = std::min(ty, im.crop_h);
-      const DevSched* sc = nullptr;
-      if (int rc = band_schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty, p.bp.db,
-                                        p.bp.s, p.bp.prologue, &sc))
-        return rc;
+      const DevSched*& sc = sched_of[rep[i]];
+      if (!sc)
+        if (int rc = band_schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty, p.bp.db,
+                                          p.bp.s, p.bp.prologue, &sc))
+          return rc;
       d.ytab = reinterpret_cast<const float*>(sc->ptr);
       d.ywidth = sc->band_words;
       d.group = 0;
@@ -934,6 +973,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
     for (int32_t k = g.first; k < g.first + g.count; k++) strips.push_back({plans[order[k]].nstrips, images[order[k]].crop_h});
     g.ty = band_rows(strips, wave_capacity_cached(g.cfg, device));
+    std::unordered_map<int32_t, const DevSched*> sched_of;  // by rep[]
     for (int32_t k = g.first; k < g.first + g.count; k++) {
       const int32_t i = order[k];
       const mxd_image& im = images[i];
@@ -946,10 +986,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       d.flip |= (int32_t)(a & 3) << 8;
       d.ty = std::min(g.ty, im.crop_h);
       if (p.kind == 2) {
-        const DevSched* sc = nullptr;
-        if (int rc = schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
-                                     ScatterShape{p.s, p.dmax, p.p}, &sc))
-          return rc;
+        const DevSched*& sc = sched_of[rep[i]];
+        if (!sc)
+          if (int rc = schedules().get(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
+                                       ScatterShape{p.s, p.dmax, p.p}, &sc))
+            return rc;
         d.ytab = reinterpret_cast<const float*>(sc->ptr);
         d.ywidth = sc->band_words;
         d.group = sc->entry_off;

@@ -1,0 +1,105 @@
+"""Per-launch time of the fused stage over a grid of tuning settings, in one
+process on one box (A/B without box-to-box spread).
+
+  python tools/band_sweep.py [--workload c2] [--launches 20] \
+      --set "rows=0,la=0,policy=0" --set "rows=38" ...
+
+Each --set is a comma list of knob=value (rows -> MXD_TUNE_BAND_ROWS, la ->
+MXD_TUNE_BAND_LA, policy -> mxd_set_kernel_policy).  Inputs are bench.py's
+workload (two alternating source/output sets, resident in HBM); the time is
+HIP events around `launches` back-to-back launches on one stream, after 3
+warm-up launches, repeated `--reps` times (median reported).  Prints one JSON
+line per setting."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "mlx-data_amd"))
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def setup(workload, nsets=2):
+    """Two source/output sets of bench.py's workload, resident in HBM.
+    Returns (capi, L, stream, sets [(src, dst, imgs, n)], mode, alg_bytes, sizes, geoms, f32)."""
+    from mlx_data_amd import capi
+
+    capi.lib()
+    dev = 0
+    capi.check(capi.lib().mxd_set_device(dev))
+    B = bench.WORKLOADS[workload]["batch"]
+    sizes, geoms, f32 = bench.make_workload(capi, workload, B, 0)
+    C = bench.C
+    elem = 4 if f32 else 1
+    offs, pitches, total = [], [], 0
+    for (sw, sh) in sizes:
+        offs.append(total)
+        pitches.append((sw * C + 15) // 16 * 16)
+        total += (pitches[-1] * sh + 255) // 256 * 256
+    out_bytes = [g[4] * g[5] * C * elem for g in geoms]
+    out_offs = np.concatenate([[0], np.cumsum(out_bytes)[:-1]]).astype(np.int64)
+    rng = np.random.default_rng(1000)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    stream = capi.Stream(dev)
+    sets = []
+    for _ in range(nsets):
+        src = capi.DeviceBuffer(total, dev)
+        dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
+        src.upload(host, stream=stream)
+        entries = [dict(src=src.ptr + o, src_stride=pt, src_w=sw, src_h=sh, channels=C, resize_w=g[0], resize_h=g[1],
+                        crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6], dst=dst.ptr + int(oo),
+                        dst_stride=g[4] * C * elem) for (sw, sh), o, pt, g, oo in zip(sizes, offs, pitches, geoms,
+                                                                                     out_offs)]
+        imgs, n = capi.make_images(entries)
+        sets.append((src, dst, imgs, n))
+    mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
+    alg = sum(bench.footprint_bytes(capi, sw, sh, C, *g[:6]) for (sw, sh), g in zip(sizes, geoms)) + sum(out_bytes)
+    return capi, capi.lib(), stream, sets, mode, alg, sizes, geoms, f32
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c2", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--set", action="append", default=[])
+    args = ap.parse_args()
+    capi, L, stream, sets, mode, alg, sizes, geoms, f32 = setup(args.workload)
+    dev = 0
+    hs = ctypes.c_void_p(stream.handle)
+    e0, e1 = capi.Event(), capi.Event()
+    for spec in args.set or ["rows=0"]:
+        kv = dict(p.split("=") for p in spec.split(",") if p)
+        capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, int(kv.get("rows", 0)))
+        capi.set_tuning(capi.MXD_TUNE_BAND_LA, int(kv.get("la", 0)))
+        capi.set_kernel_policy(int(kv.get("policy", 0)))
+        for i in range(3):
+            capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, dev, hs))
+        times = []
+        for _ in range(args.reps):
+            stream.synchronize()
+            e0.record(stream)
+            for i in range(args.launches):
+                capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, dev, hs))
+            e1.record(stream)
+            stream.synchronize()
+            times.append(e0.elapsed_ms(e1) / args.launches)
+        ms = statistics.median(times)
+        print(json.dumps({"workload": args.workload, "set": spec, "ms_per_launch": round(ms, 5),
+                          "frac": round(alg / (ms * 1e-3) / 8e12, 4), "reps": [round(t, 5) for t in times],
+                          "kernel": bench.kernel_name(capi, sizes[0], geoms[0], f32, int(kv.get("policy", 0)))}),
+              flush=True)
+    capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, 0)
+    capi.set_tuning(capi.MXD_TUNE_BAND_LA, 0)
+    capi.set_kernel_policy(0)
+
+
+if __name__ == "__main__":
+    main()
