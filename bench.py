@@ -393,6 +393,10 @@ def main():
     # tuning knobs (include/mxd_amd.h mxd_tune; measurements only): band rows, groups ahead
     ap.add_argument("--tune-rows", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tune-la", type=int, default=0, help=argparse.SUPPRESS)
+    # one process, D devices: every step launches one batch slice per device
+    # (the pipeline's own split, pipeline.cpp run_host); devices from
+    # MXD_BENCH_SPLIT_DEVICES ("0,0" rehearses on one card) or range(D)
+    ap.add_argument("--split-devices", type=int, default=1)
     # timing plumbing without a GPU (tests/test_bench_dist.py): each step sleeps
     ap.add_argument("--simulate", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -426,6 +430,10 @@ def main():
     c3_sizes = [tuple(int(v) for v in t.split("x")) for t in args.c3_sizes.split(",") if t]
     sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank, c3_sizes)
     elem = 4 if f32 else 1
+    if args.split_devices > 1:
+        split_run(capi, args, ranks, sizes, geoms, f32, B)
+        ranks.close()
+        return
 
     # Sources packed in one device buffer per set (256-B aligned slots, rows
     # padded to 16 B), outputs NHWC; two sets alternate step by step.
@@ -535,6 +543,71 @@ def main():
         line["config"]["streams"] = len(streams)
         print(json.dumps(line), flush=True)
     ranks.close()
+
+
+def device_sets(capi, dev, sizes, geoms, f32, nsets, seed):
+    """nsets (src, dst, images, n) of the workload on `dev` (bench layout)."""
+    elem = 4 if f32 else 1
+    offs, pitches, total = [], [], 0
+    for (sw, sh) in sizes:
+        offs.append(total)
+        pitches.append((sw * C + 15) // 16 * 16)
+        total += (pitches[-1] * sh + 255) // 256 * 256
+    out_bytes = [g[4] * g[5] * C * elem for g in geoms]
+    out_offs = np.concatenate([[0], np.cumsum(out_bytes)[:-1]]).astype(np.int64)
+    host = np.random.default_rng(seed).integers(0, 256, total, dtype=np.uint8)
+    sets = []
+    for _ in range(nsets):
+        src = capi.DeviceBuffer(total, dev)
+        dst = capi.DeviceBuffer(int(sum(out_bytes)), dev)
+        src.upload(host)
+        entries = [dict(src=src.ptr + o, src_stride=pt, src_w=sw, src_h=sh, channels=C, resize_w=g[0], resize_h=g[1],
+                        crop_x=g[2], crop_y=g[3], crop_w=g[4], crop_h=g[5], flip=g[6], dst=dst.ptr + int(oo),
+                        dst_stride=g[4] * C * elem)
+                   for (sw, sh), o, pt, g, oo in zip(sizes, offs, pitches, geoms, out_offs)]
+        imgs, n = capi.make_images(entries)
+        sets.append((src, dst, imgs, n))
+    return sets, sum(out_bytes)
+
+
+def split_run(capi, args, ranks, sizes, geoms, f32, B):
+    """--split-devices D: one process drives D devices; every step is one
+    global batch of D x B images whose contiguous slices (B each, one per
+    device, op/Shard.cpp:11-20) are launched on each device's own HIP stream
+    from this thread (launches are asynchronous); no collective."""
+    env = os.environ.get("MXD_BENCH_SPLIT_DEVICES", "")
+    devs = [int(d) for d in env.split(",") if d] or list(range(args.split_devices))
+    devs = devs[:args.split_devices]
+    D = len(devs)
+    L = capi.lib()
+    mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
+    per = []
+    for k, d in enumerate(devs):
+        sets, _ = device_sets(capi, d, sizes, geoms, f32, 2, 2000 + k)
+        st = capi.Stream(d)
+        per.append((d, sets, st, ctypes.c_void_p(st.handle)))
+
+    def step(i):
+        for d, sets, _, hs in per:
+            _, _, imgs, n = sets[i % 2]
+            capi.check(L.mxd_resize_crop_batch(imgs, n, mode, d, hs))
+
+    def sync_all():
+        for _, _, st, _ in per:
+            st.synchronize()
+
+    for i in range(args.warmup + 2):
+        step(i)
+    wall, _ = timed_steps(ranks, step, sync_all, args.steps)
+    line = bench_line(args.workload, D, B, args.steps, args.warmup, wall, None, None, None, manifest(capi, devs[0]))
+    line["config"]["parallelism"] = (f"split{D} (one process; each step one global batch of {D} x {B} images, one "
+                                     f"contiguous slice per device on its own HIP stream; no collective)")
+    line["config"]["devices"] = devs
+    for _, sets, _, _ in per:
+        for src, dst, _, _ in sets:
+            src.free()
+            dst.free()
+    print(json.dumps(line), flush=True)
 
 
 def e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev):

@@ -43,6 +43,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define MXD_BAND_NT 1
 #endif
 constexpr int kStoreAux = MXD_BAND_NT ? 2 : 0;  // gfx950 cache-policy bits: 2 = nt
+// Cache policy of the source LDS-DMA (tuning builds: -DMXD_BAND_LOAD_AUX=2 = nt).
+#ifndef MXD_BAND_LOAD_AUX
+#define MXD_BAND_LOAD_AUX 0
+#endif
 // Progress-based priority (as wave.hip's progress_prio; tuning builds
 // -DMXD_BAND_PRIO=0): the SIMD arbiter issues oldest-first, so the workgroups
 // sharing a CU would otherwise finish in age order (C2 stamps: units of one
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
       const int c = b0 + kChunk * k + 16 * lane;
       const int voff = (row >= 0 && c < bend && !(MXD_BAND_ABLATE & 1)) ? (row - y0) * stride + c : kNoLoad;
       const uint32_t to = row >= 0 ? (uint32_t)(a * AREA + (j * NQ + k) * kChunk) : sink;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_u8*)(smem + to), 16, voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_u8*)(smem + to), 16, voff, 0, 0, MXD_BAND_LOAD_AUX);
     });
   };
 

@@ -7,12 +7,18 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <future>
 #include <map>
+#include <mutex>
 #include <numeric>
 #include <stdexcept>
+#include <thread>
 
 #include "mxd_amd.h"
 
@@ -221,10 +227,73 @@ int run_on(const Job* jobs, size_t n, int32_t dtype, int device, bool dst_device
                     : mxd_resize_crop_host(plain.data(), (int32_t)plain.size(), dtype, device);
 }
 
+// Persistent host workers per device for the slices of split batches: a
+// batch split over D devices hands D - 1 slices to the slice devices'
+// workers (started on first use, at most kWorkersPerDevice each, matching the
+// C ABI's per-device host-path contexts) instead of spawning threads per
+// batch.  Workers live for the process (never joined: no teardown-order
+// hazards at exit).
+class DeviceWorkers {
+ public:
+  static constexpr size_t kWorkersPerDevice = 4;
+  std::future<std::string> submit(int device, std::function<std::string()> fn) {
+    auto task = std::make_shared<std::packaged_task<std::string()>>(std::move(fn));
+    std::future<std::string> f = task->get_future();
+    Dev* d;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      std::unique_ptr<Dev>& slot = devs_[device];
+      if (!slot) slot = std::make_unique<Dev>();
+      d = slot.get();
+    }
+    {
+      std::lock_guard<std::mutex> lk(d->mu);
+      d->q.push_back([task] { (*task)(); });
+      // one more worker while every started one is busy (up to the cap)
+      if (d->idle == 0 && d->threads < kWorkersPerDevice) {
+        d->threads++;
+        std::thread([d] { d->loop(); }).detach();
+      }
+    }
+    d->cv.notify_one();
+    return f;
+  }
+
+ private:
+  struct Dev {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    size_t threads = 0, idle = 0;
+    void loop() {
+      for (;;) {
+        std::function<void()> t;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          idle++;
+          cv.wait(lk, [&] { return !q.empty(); });
+          idle--;
+          t = std::move(q.front());
+          q.pop_front();
+        }
+        t();
+      }
+    }
+  };
+  std::mutex mu_;
+  std::map<int, std::unique_ptr<Dev>> devs_;
+};
+
+DeviceWorkers& device_workers() {
+  static DeviceWorkers* w = new DeviceWorkers();  // leaked on purpose: outlives static teardown
+  return *w;
+}
+
 // Runs the jobs into host destinations (one fused launch per device and
-// source kind).  Several devices: contiguous slices [k n / D, (k + 1) n / D),
-// slice 0 on the calling thread, the others on their own threads; the first
-// failing slice's message wins.
+// source kind).  Several devices: contiguous slices [k n / D, (k + 1) n / D)
+// (op/Shard.cpp:11-20's contiguous split; the order of the batch is kept),
+// slice 0 on the calling thread, the others on their devices' persistent
+// workers; the first failing slice's message wins.
 void run_host(const std::vector<Job>& jobs, int32_t dtype) {
   if (jobs.empty()) return;
   const std::vector<int> devs = devices();
@@ -236,18 +305,26 @@ void run_host(const std::vector<Job>& jobs, int32_t dtype) {
     check(run_on(jobs.data(), n, dtype, devs[first % devs.size()], false));
     return;
   }
-  std::vector<std::string> err(k);
-  auto slice = [&](size_t s) {
+  auto slice = [&jobs, n, k, dtype, &devs, first](size_t s) -> std::string {
     const size_t b = s * n / k, e = (s + 1) * n / k;
     if (run_on(jobs.data() + b, e - b, dtype, devs[(first + s) % devs.size()], false) != MXD_OK)
-      err[s] = mxd_last_error();  // thread-local: read on the failing thread
+      return mxd_last_error();  // thread-local: read on the failing thread
+    return std::string();
   };
-  std::vector<std::thread> workers;
-  for (size_t s = 1; s < k; s++) workers.emplace_back(slice, s);
-  slice(0);
-  for (auto& w : workers) w.join();
-  for (const auto& e : err)
-    if (!e.empty()) throw std::runtime_error(e);
+  std::vector<std::future<std::string>> pending;
+  for (size_t s = 1; s < k; s++)
+    pending.push_back(device_workers().submit(devs[(first + s) % devs.size()], [&slice, s] { return slice(s); }));
+  std::string err;
+  try {
+    err = slice(0);
+  } catch (const std::exception& ex) {  // still wait: the slices read `jobs`
+    err = ex.what();
+  }
+  for (auto& f : pending) {
+    std::string e = f.get();  // every slice done before `jobs` goes out of scope
+    if (err.empty()) err = std::move(e);
+  }
+  if (!err.empty()) throw std::runtime_error(err);
 }
 
 int32_t out_dtype(DType t) { return t == DType::Float ? MXD_F32_DIV255 : MXD_U8; }

@@ -154,3 +154,45 @@ def test_batch_split_over_devices_matches_single_device():
     bad = dx.buffer_from_vector(samples[:4]).image_resize("image", 32, 32)
     with pytest.raises(RuntimeError, match="invalid device 99"):
         bad.batch(4)[0]
+
+
+def test_batch_split_over_every_visible_device():
+    """One batch split over range(device_count()) (op/Shard.cpp:11-20's
+    contiguous slices, one per device, on persistent per-device workers):
+    byte-identical to the one-device batch.  Needs two or more devices."""
+    from mlx_data_amd import capi
+
+    n = capi.device_count()
+    if n < 2:
+        pytest.skip("one device visible")
+    samples = c2_samples(2 * n + 1, seed=41)
+
+    def run(devs):
+        dx.set_devices(devs)
+        d = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 256)
+             .image_center_crop("image", 224, 224).image_to_float("image"))
+        return d.batch(len(samples))[0]["image"]
+
+    one = run([0])
+    every = run(list(range(n)))
+    assert np.array_equal(one.view(np.uint32), every.view(np.uint32))
+
+
+def test_split_batches_under_prefetch_reuse_workers():
+    """Many split batches from prefetch threads at once (slices 1.. on the
+    per-device workers, at most four per device): every image equals its
+    one-device form (prefetch workers interleave their pulls, so batches are
+    compared image by image, keyed by a per-sample index)."""
+    samples = [dict(s, idx=np.int64(i)) for i, s in enumerate(c2_samples(24, seed=42))]
+    dx.set_devices([0])
+    want = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 256)
+            .image_center_crop("image", 224, 224).batch(24))[0]["image"]
+    dx.set_devices([0, 0, 0])
+    s = (dx.buffer_from_vector(samples).to_stream().image_resize_smallest_side("image", 256)
+         .image_center_crop("image", 224, 224).batch(6).prefetch(4, 4))
+    seen = []
+    for b in s:
+        for k, i in enumerate(b["idx"].tolist()):
+            assert np.array_equal(b["image"][k], want[i]), i
+            seen.append(i)
+    assert sorted(seen) == list(range(24))
