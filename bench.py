@@ -24,7 +24,9 @@ the max-over-ranks time); `value` = images of all ranks / max-over-ranks wall.
 `--workload c4` (configs[3], device part: 128 ImageNet-shape images per GPU ->
 256 -> 224 f32) and `--workload c5` (configs[4]: 128 4K frames -> 512 ->
 random_crop 448 + hflip, u8) are the other device-resident configurations;
-DESIGN.md quotes them.
+`--workload c6` / `c7` (32 x 12 MP 4032x3024 / 24 MP 6000x4000 photos -> 256 ->
+224 f32: 11.8:1 and 15.6:1 downscales) measure large ratios.  DESIGN.md
+quotes them.
 
 Extra fields:
   roofline      HBM roofline of the fused kernel: algorithmic bytes per launch
@@ -80,6 +82,12 @@ WORKLOADS = {
     "c5": dict(batch=128, f32=False,
                desc="C5: 128 x 3840x2160 RGB u8 in HBM -> resize_smallest_side 512 -> random_crop 448 -> "
                     "random_h_flip 0.5 (seeded), u8"),
+    "c6": dict(batch=32, f32=True,
+               desc="C6: 32 x 4032x3024 RGB u8 (12 MP) in HBM -> resize_smallest_side 256 -> center_crop 224 -> "
+                    "f32/255 (11.8:1 downscale)"),
+    "c7": dict(batch=32, f32=True,
+               desc="C7: 32 x 6000x4000 RGB u8 (24 MP) in HBM -> resize_smallest_side 256 -> center_crop 224 -> "
+                    "f32/255 (15.6:1 downscale)"),
 }
 C3_SIZES = [(640, 480), (1280, 720), (1280, 960), (1920, 1080), (2560, 1440), (3840, 2160)]
 C4_SIZES = [(500, 375), (375, 500), (500, 333)]
@@ -105,6 +113,10 @@ def make_workload(capi, name, batch, rank, c3_sizes=None):
     elif name == "c4":
         rng = np.random.default_rng(2)
         sizes = [C4_SIZES[i] for i in rng.integers(0, len(C4_SIZES), batch)]
+    elif name == "c6":
+        sizes = [(4032, 3024)] * batch
+    elif name == "c7":
+        sizes = [(6000, 4000)] * batch
     else:
         sizes = [(3840, 2160)] * batch
     rng = np.random.default_rng(3 + rank)
@@ -130,10 +142,12 @@ def kernel_name(capi, size, g, f32, policy):
     prev = capi.set_kernel_policy(policy)
     try:
         b = capi.describe_band_plan(e, dt)
-        if b["band"]:
-            return "resample_band (taps {taps}, rows/group {db}, window {nq} KiB, strips {nstrips}, ahead {la})".format(**b)
-        w = capi.describe_plan(e, dt)
-        return "resample_wave" if w["wave"] else "resample_tiles"
+        band = "resample_band (taps {taps}, rows/group {db}, window {nq} KiB, strips {nstrips}, ahead {la})".format(**b)
+        if b["band"] and policy & capi.MXD_POLICY_PREFER_BAND:
+            return band
+        if capi.describe_plan(e, dt)["wave"]:
+            return "resample_wave"
+        return band if b["band"] else "resample_tiles"
     finally:
         capi.set_kernel_policy(prev)
 
@@ -448,10 +462,11 @@ def main():
     host = np.empty(total, np.uint8)
     if args.workload == "c2":
         host[:] = rng.integers(0, 256, total, dtype=np.uint8)
-    else:  # one random 4K frame; every image is a slice of it (timing is data-independent)
+    else:  # one random 4K frame, repeated through every image (timing is data-independent)
         base = rng.integers(0, 256, 2160 * 3840 * C, dtype=np.uint8)
         for (sw, sh), o, pt in zip(sizes, offs, pitches):
-            host[o:o + pt * sh] = base[:pt * sh]
+            n = pt * sh
+            host[o:o + n] = np.resize(base, n)
     stream = capi.Stream(dev)
     streams = [stream] + [capi.Stream(dev) for _ in range(max(1, args.streams) - 1)]
     mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8

@@ -119,10 +119,13 @@ int mxd_resize_crop_batch(const mxd_image* images, int32_t n, int32_t out_dtype,
 
 /* Kernel policy: a process-wide switch between kernels that compute
  * bit-identical results (for tests and tuning; default 0 = automatic choice:
- * the band kernel -- one workgroup streams an image band's source rows into
- * LDS by LDS-DMA -- wherever its classes fit, else a wave kernel, else the
- * general kernel).  MXD_POLICY_NO_BAND: never the band kernel (any of the
- * wave-kernel bits below implies it).  MXD_POLICY_NO_SCATTER: wave kernels gather every
+ * a wave kernel -- one wave streams an image band's row pieces -- wherever
+ * its tap buckets fit (every measured configuration C2..C5 runs fastest
+ * there), else the band kernel -- persistent workgroups stream image bands'
+ * source rows into LDS by LDS-DMA, any downscale ratio up to 32 taps per
+ * axis -- else the general kernel).  MXD_POLICY_PREFER_BAND: the band kernel
+ * first wherever its classes fit; MXD_POLICY_NO_BAND: never the band kernel
+ * (any of the wave-kernel bits below implies it).  MXD_POLICY_NO_SCATTER: wave kernels gather every
  * output row's taps instead of following a scatter schedule; MXD_POLICY_NO_WAVE: every image takes the
  * general workgroup-tile kernel; MXD_POLICY_NARROW: wave kernels keep the
  * narrow per-lane window (no wide RGB strips, no byte lanes);
@@ -144,15 +147,18 @@ enum mxd_policy {
   MXD_POLICY_NO_BYTES = 16,
   MXD_POLICY_BYTES = 32,
   MXD_POLICY_NO_ZERO_COPY = 64,
-  MXD_POLICY_NO_BAND = 128
+  MXD_POLICY_NO_BAND = 128,
+  MXD_POLICY_PREFER_BAND = 256
 };
 int mxd_set_kernel_policy(int32_t policy);
 
 /* Tuning knobs (process-wide, for measurements; 0 = automatic).  Returns the
  * previous value, or -1 for an unknown knob.
  * MXD_TUNE_BAND_ROWS: output rows per band-kernel unit;
- * MXD_TUNE_BAND_LA: row groups the band kernel keeps in flight per unit. */
-enum mxd_tune { MXD_TUNE_BAND_ROWS = 0, MXD_TUNE_BAND_LA = 1, MXD_TUNE_COUNT = 2 };
+ * MXD_TUNE_BAND_LA: row groups the band kernel keeps in flight per unit;
+ * MXD_TUNE_BAND_GRID: band-kernel workgroups (0: as many as the device holds
+ * at once, each running a stream of units; 1: one per unit; n > 1: n). */
+enum mxd_tune { MXD_TUNE_BAND_ROWS = 0, MXD_TUNE_BAND_LA = 1, MXD_TUNE_BAND_GRID = 2, MXD_TUNE_COUNT = 3 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 
 /* The wave-kernel plan of one image on `device`, i.e. what runs when the

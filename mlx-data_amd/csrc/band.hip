@@ -78,6 +78,12 @@ __device__ __forceinline__ void band_prio(int done, int total) {
 #define MXD_BAND_BRANCHLESS 1
 #endif
 
+// Tuning builds: -DMXD_BAND_PPW_ALIGN=32 rounds each wave's pixel run up to
+// whole 128-byte lines of f32 RGB output.
+#ifndef MXD_BAND_PPW_ALIGN
+#define MXD_BAND_PPW_ALIGN 1
+#endif
+
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
 
 // Diagnostic builds only (-DMXD_BAND_STAMPS=1, tools/band_stamps.sh; never
@@ -164,29 +170,46 @@ __device__ __forceinline__ void store_pixel(__amdgpu_buffer_rsrc_t rs, int voff,
   }
 }
 
-template <int C, bool F32, int NQ, int T, int S, int DB>
-__global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __restrict__ imgs, int nimgs, int nunits,
-                                                             int per_img, int la) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int DS = DB > 4 ? DB : 4;     // row slots per area (>= 4: NQ KiB of floats fit)
-  constexpr int AREA = DS * NQ * kChunk;  // bytes per ring area
-  constexpr int KW = (DB * NQ + kWaves - 1) / kWaves;  // LDS-DMA instructions per wave and group
-  constexpr int SW = store_instrs<C, F32>();
+// What the cursors of the stream need of one unit (wave-uniform: SGPRs).
+struct Unit {
+  __amdgpu_buffer_rsrc_t src, dst;
+  kint* sched;  // the band's first group
+  int ng;       // groups (0: no unit -- past the last one)
+  int b0, bend, y0, stride;  // source window of the strip (LDS-DMA)
+  int dstride, oy0;          // output rows
+  int vboff;                 // vertical-row float index of source pixel 0, channel 0 (minus first tap * C)
+};
+
+// The horizontal pass's per-lane state of one unit, and the raw table words
+// it is made from (loaded ahead; unpacked when the unit becomes current).
+template <int T>
+struct Lanes {
+  float wx[T];
+  int vb;     // vertical-row float index of the pixel's tap 0, channel 0
+  int scol;   // output byte column, kNoLoad for lanes without a pixel
+};
+template <int T>
+constexpr int raw_words() {
+  return (kTapHeader + T + 3) / 4;  // 16-byte table loads per lane
+}
+
+template <int C, bool F32>
+__device__ __forceinline__ Unit load_unit(const ImgDev* imgs, kint* unit_img, int per_img, int u, int nunits,
+                                          int* npx_out, int* ox0_out, int* xs_out, cgfloat** xtab_out, int* crop_w_out,
+                                          int* flip_out) {
   constexpr int ELEM = F32 ? 4 : 1;
-  constexpr int NX = 4 * NQ;  // source bytes per thread and row
-
-  const int tid = threadIdx.x;
-  const int lane = tid & (kLanes - 1);
-  const int wave = RFL(tid >> 6);
-  const int unit = RFL(xcd_remap(blockIdx.x, gridDim.x));
-  if (unit >= nunits) return;  // the whole workgroup
-#if MXD_BAND_STAMPS
-  unsigned long long seg[kStampSegs] = {};
-  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
-  MXD_STAMP(t_setup0);
-#endif
-
-  const ImgDev& im = per_img > 0 ? imgs[unit / per_img] : find_image(imgs, nimgs, unit);
+  Unit U;
+  if (u >= nunits) {
+    U.src = U.dst = __builtin_amdgcn_make_buffer_rsrc((void*)nullptr, (short)0, 0, 0x00020000);
+    U.sched = nullptr;
+    U.ng = 0;
+    U.b0 = U.bend = U.y0 = U.stride = U.dstride = U.oy0 = U.vboff = 0;
+    *npx_out = *ox0_out = *xs_out = *crop_w_out = *flip_out = 0;
+    *xtab_out = nullptr;
+    return U;
+  }
+  const int ii = per_img > 0 ? u / per_img : unit_img[u];
+  const ImgDev& im = imgs[ii];
   const int nstrips = RFL(im.nstrips);
   const int crop_w = RFL(im.crop_w);
   const int crop_h = RFL(im.crop_h);
@@ -196,105 +219,169 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
   const int strip_cols = RFL(im.tx);
   const int xs = kTapHeader + RFL(im.xwidth);
   cgfloat* xtab = MXD_GLOBAL_PTR(const float, im.xtab);
-  const int local = unit - RFL(im.tile_begin);
+  const int local = u - RFL(im.tile_begin);
   const int band = local / nstrips;
   const int strip = local - band * nstrips;
-  const int oy0 = band * band_rows;
-  const int nrows = min(band_rows, crop_h - oy0);
   const int ox0 = strip * strip_cols;
   const int npx = min(strip_cols, crop_w - ox0);
+  // the strip's first and last source pixel, by scalar loads (a vector load
+  // here would make the wave wait for the LDS-DMA in flight)
+  kint* xti = uniform_ptr<kint*>(im.xtab);
+  const int xa = flip ? crop_w - (ox0 + npx) : ox0;
+  const int xb = flip ? crop_w - 1 - ox0 : ox0 + npx - 1;
+  const int lo = xti[xa * xs];
+  const int hi = xti[xb * xs] + xti[xb * xs + 1] - 1;
+  const int sx0 = RFL(im.src_x0);
+  U.y0 = RFL(im.src_y0);
+  U.stride = RFL((int)im.src_stride);
+  const int rows = RFL(im.src_h), srcw = RFL(im.src_w);
+  U.src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.src), (short)0,
+                                            src_records(shift, rows, U.stride, (srcw - sx0) * C), 0x00020000);
+  U.b0 = ((lo - sx0) * C + shift) & ~15;  // window start: 16-byte boundary past the aligned base
+  U.bend = (hi + 1 - sx0) * C + shift;    // one past the strip's last source byte
+  U.vboff = -sx0 * C + shift - U.b0;
+  U.dstride = RFL((int)im.dst_stride);
+  U.dst = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.dst), (short)0,
+                                            (crop_h - 1) * U.dstride + crop_w * C * ELEM, 0x00020000);
+  U.oy0 = band * band_rows;
+  kint* hdr = uniform_ptr<kint*>(im.ytab) + band * RFL(im.ywidth);
+  U.ng = hdr[0];
+  U.sched = hdr + E;
+  *npx_out = npx;
+  *ox0_out = ox0;
+  *xs_out = xs;
+  *xtab_out = xtab;
+  *crop_w_out = crop_w;
+  *flip_out = flip;
+  return U;
+}
 
-  // Source: one descriptor over the stored region, rows addressed through the
-  // range-checked voffset (rows and columns outside it read zeros).
-  int lo, hi;
-  strip_span(xtab, xs, crop_w, flip, ox0, ox0 + npx, &lo, &hi);
-  lo = RFL(lo);
-  hi = RFL(hi);
-  const int sx0 = RFL(im.src_x0), y0 = RFL(im.src_y0);
-  const int stride = RFL((int)im.src_stride), rows = RFL(im.src_h), srcw = RFL(im.src_w);
-  const __amdgpu_buffer_rsrc_t src =
-      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.src), (short)0,
-                                        src_records(shift, rows, stride, (srcw - sx0) * C), 0x00020000);
-  const int b0 = ((lo - sx0) * C + shift) & ~15;  // window start: 16-byte boundary past the aligned base
-  const int bend = (hi + 1 - sx0) * C + shift;    // one past the strip's last source byte
+template <int C, bool F32, int NQ, int T, int S, int DB>
+__global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __restrict__ imgs,
+                                                             const int* __restrict__ unit_img_p, int nunits,
+                                                             int per_img, int la) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int DS = DB > 4 ? DB : 4;     // row slots per area (>= 4: NQ KiB of floats fit)
+  constexpr int AREA = DS * NQ * kChunk;  // bytes per ring area
+  constexpr int KW = (DB * NQ + kWaves - 1) / kWaves;  // LDS-DMA instructions per wave and group
+  constexpr int SW = store_instrs<C, F32>();
+  constexpr int LW = raw_words<T>();      // table loads per lane when a unit is loaded ahead
+  constexpr int ELEM = F32 ? 4 : 1;
+  constexpr int NX = 4 * NQ;              // source bytes per thread and row
+  constexpr int GW = (1 + DB) * E;        // schedule words per group
 
-  // Destination: the image's output rows.
-  const int dstride = RFL((int)im.dst_stride);
-  const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr<void*>(im.dst), (short)0, (crop_h - 1) * dstride + crop_w * C * ELEM, 0x00020000);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kLanes - 1);
+  const int wave = RFL(tid >> 6);
+  const int G = gridDim.x;
+  int ucur = RFL(xcd_remap(blockIdx.x, G));
+  if (ucur >= nunits) return;  // the whole workgroup
+  const int nmine = (nunits - ucur + G - 1) / G;  // units of this workgroup's stream
+  int kdone = 0;                                  // of them finished (progress priority)
+  kint* unit_img = uniform_ptr<kint*>(unit_img_p);
+#if MXD_BAND_STAMPS
+  unsigned long long seg[kStampSegs] = {};
+  const unsigned long long t_real0 = __builtin_amdgcn_s_memrealtime();
+  MXD_STAMP(t_setup0);
+#endif
 
-  // Schedule of this band: [P, -, -, -] then entries [group][DB][E] =
-  // source row (-1: none), S weights (slot s = output row g - P + s).
-  kint* sched = uniform_ptr<kint*>(im.ytab) + band * RFL(im.ywidth);
-  const int P = sched[0];
-  const int ngroups = P + nrows;
-  kint* ent = sched + E;
-
-  // Horizontal pass: thread = one output pixel of the strip row (pixels in
-  // contiguous runs per wave, so each wave's stores are one contiguous run).
-  const int ppw = (npx + kWaves - 1) / kWaves;
-  const int px = wave * ppw + lane;
-  const bool hact = lane < ppw && px < npx;
-  float wx[T];
-  int vb;  // float index (in the vertical row) of tap 0, channel 0
-  {
-    const int ox = ox0 + min(px, npx - 1);
+  // A unit's horizontal lanes: thread = one output pixel of the strip row
+  // (pixels in contiguous runs per wave, so each wave's stores are one
+  // contiguous run).  Issues the LW table loads of the lane's pixel.
+  using u32x4v = u32x4;
+  auto lane_loads = [&](int npx, int ox0, int xs, cgfloat* xtab, int crop_w, int flip, u32x4v (&raw)[LW],
+                        int* scol) {
+    const int ppw = ((npx + kWaves - 1) / kWaves + MXD_BAND_PPW_ALIGN - 1) / MXD_BAND_PPW_ALIGN * MXD_BAND_PPW_ALIGN;
+    const int px = wave * ppw + lane;
+    const bool hact = lane < ppw && px < npx;
+    const int ox = ox0 + min(px, max(npx, 1) - 1);
     const int xc = flip ? crop_w - 1 - ox : ox;
-    cgfloat* xe = xtab + xc * xs;
-    vb = (__float_as_int(xe[0]) - sx0) * C + shift - b0;
+    const __amdgpu_buffer_rsrc_t xt =
+        __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>((const void*)xtab), (short)0, crop_w * xs * 4, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < T; k++) wx[k] = xe[kTapHeader + k];  // zero padded past the tap count
+    for (int i = 0; i < LW; i++) raw[i] = __builtin_amdgcn_raw_buffer_load_b128(xt, xc * xs * 4 + 16 * i, 0, 0);
+    *scol = hact ? (ox0 + px) * C * ELEM : kNoLoad;
+  };
+  auto unpack = [&](const u32x4v (&raw)[LW], int vboff, Lanes<T>& L) {
+    float w[4 * LW];
+#pragma unroll
+    for (int i = 0; i < LW; i++) {
+      // every loaded word stays live until here: a dead one's register would
+      // be reused while its load is in flight, which costs a wait at the load
+      asm volatile("" ::"v"(raw[i]));
+      w[4 * i] = __uint_as_float(raw[i].x);
+      w[4 * i + 1] = __uint_as_float(raw[i].y);
+      w[4 * i + 2] = __uint_as_float(raw[i].z);
+      w[4 * i + 3] = __uint_as_float(raw[i].w);
+    }
+    L.vb = __float_as_int(w[0]) * C + vboff;
+#pragma unroll
+    for (int k = 0; k < T; k++) L.wx[k] = w[kTapHeader + k];  // zero padded past the tap count
+  };
+
+  // Current unit c (horizontal and vertical passes; its groups are steps
+  // [cstart, cstart + c.ng) of the stream) and the next one n (loaded ahead
+  // when the LDS-DMA cursor reaches it).
+  Unit c, n;
+  Lanes<T> cl;
+  u32x4v nraw[LW];
+  int nscol = kNoLoad;
+  {
+    int npx, ox0, xs, crop_w, flip;
+    cgfloat* xtab;
+    c = load_unit<C, F32>(imgs, unit_img, per_img, ucur, nunits, &npx, &ox0, &xs, &xtab, &crop_w, &flip);
+    u32x4v raw[LW];
+    lane_loads(npx, ox0, xs, xtab, crop_w, flip, raw, &cl.scol);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): table loads done before the ring starts counting
+    unpack(raw, c.vboff, cl);
   }
-  const int scol = (ox0 + px) * C * ELEM;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): table loads done before the ring starts counting
+  n = c;
+  n.ng = 0;
 
   const int rg = la + 1;
   const uint32_t sink = (uint32_t)(rg * AREA);  // 1 KiB for loads of absent rows
 
   // LDS-DMA of a group's rows into area a: item i = wave + 4 m is row slot
-  // i / NQ, 1-KiB piece i % NQ; lane = 16 bytes of the piece.  dma_rows reads
-  // this wave's source rows of group g (the schedule holds one all-absent
-  // group after the last, so the loads need no guard).
-  auto dma_rows = [&](int g, int (&dr)[KW]) {
-    const int gl = min(g, ngroups);
+  // i / NQ, 1-KiB piece i % NQ; lane = 16 bytes of the piece.
+  auto dma_rows = [&](const Unit& U, int l, int (&dr)[KW]) {
     static_for<KW>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
       const int j = (wave + kWaves * m) / NQ;
-      dr[m] = j < DB ? ent[(gl * DB + j) * E] : -1;
+      dr[m] = (j < DB && l < U.ng) ? U.sched[l * GW + (1 + j) * E] : -1;
     });
   };
-  auto issue = [&](const int (&dr)[KW], int a) {
+  auto issue = [&](const Unit& U, const int (&dr)[KW], int a) {
     static_for<KW>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
       const int i = wave + kWaves * m;
       const int j = i / NQ, k = i - (i / NQ) * NQ;
       const int row = dr[m];
-      const int c = b0 + kChunk * k + 16 * lane;
-      const int voff = (row >= 0 && c < bend && !(MXD_BAND_ABLATE & 1)) ? (row - y0) * stride + c : kNoLoad;
+      const int cb = U.b0 + kChunk * k + 16 * lane;
+      const int voff = (row >= 0 && cb < U.bend && !(MXD_BAND_ABLATE & 1)) ? (row - U.y0) * U.stride + cb : kNoLoad;
       const uint32_t to = row >= 0 ? (uint32_t)(a * AREA + (j * NQ + k) * kChunk) : sink;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (lds_u8*)(smem + to), 16, voff, 0, 0, MXD_BAND_LOAD_AUX);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(U.src, (lds_u8*)(smem + to), 16, voff, 0, 0, MXD_BAND_LOAD_AUX);
     });
   };
 
+  // acc[s] = open output row (oldest + s); a completed row leaves slot 0 and
+  // the slots shift down.
   float acc[S][NX];
 #pragma unroll
   for (int s = 0; s < S; s++)
 #pragma unroll
     for (int i = 0; i < NX; i++) acc[s][i] = 0.0f;
 
-  // Vertical pass of group g (accumulator slot SL = g mod S) from area a:
-  // thread t converts dwords t, t + 256, ... of each row slot.  Row slots
-  // and their schedule entries are read in batches of up to 4 before any use,
-  // and (MXD_BAND_BRANCHLESS) every slot is converted and FMA'd into every
+  // Vertical pass of one group (entries eg) from area a: thread t converts
+  // dwords t, t + 256, ... of each row slot.  Row slots and their schedule
+  // entries are read in batches of up to 4 before any use, and
+  // (MXD_BAND_BRANCHLESS) every slot is converted and FMA'd into every
   // accumulator unconditionally: absent rows and unused slots carry weight 0,
   // and fma(0, x, acc) == acc for the finite x a byte converts to (a zero may
   // change sign, which the encode cannot see), so the batch is one branch-free
   // block the compiler can schedule.
-  auto vpass = [&](auto slc, int g, int a) {
-    constexpr int SL = decltype(slc)::value;
+  auto vpass = [&](kint* eg, int a) {
     constexpr int JB = DB < 4 ? DB : 4;
     const uint32_t* rb = reinterpret_cast<const uint32_t*>(smem + a * AREA);
-    kint* eg = ent + g * DB * E;
     static_for<(DB + JB - 1) / JB>([&](auto bc) {
       constexpr int j0 = decltype(bc)::value * JB;
       constexpr int JN = DB - j0 < JB ? DB - j0 : JB;
@@ -311,7 +398,7 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
         const int* e = ev + j * E;
         if (MXD_BAND_BRANCHLESS || e[0] >= 0) {
           if constexpr ((MXD_BAND_ABLATE & 8) != 0) {
-            acc[SL][0] += __uint_as_float(d[j][0] & 0x3fffffffu);
+            acc[0][0] += __uint_as_float(d[j][0] & 0x3fffffffu);
             return;
           }
           float x[NX];
@@ -322,7 +409,7 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
             const float w = __int_as_float(e[1 + s]);
             if (MXD_BAND_BRANCHLESS || s == 0 || w != 0.0f) {
 #pragma unroll
-              for (int i = 0; i < NX; i++) acc[(SL + s) % S][i] = __builtin_fmaf(w, x[i], acc[(SL + s) % S][i]);
+              for (int i = 0; i < NX; i++) acc[s][i] = __builtin_fmaf(w, x[i], acc[s][i]);
             }
           });
         }
@@ -330,105 +417,145 @@ __global__ __launch_bounds__(kThreads, 2) void resample_band(const ImgDev* __res
     });
   };
 
-  // Finished vertical row (slot SL) -> area a as f32 in byte order.  The
-  // stores are inline asm: hipcc would otherwise wait vmcnt(0) before them
-  // (an LDS store after in-flight LDS-DMA it cannot prove disjoint), which
-  // drains the ring; the areas in flight are never this one (band.h).
-  auto vwrite = [&](auto slc, int a) {
-    constexpr int SL = decltype(slc)::value;
+  // Completed vertical row (slot 0) -> area a as f32 in byte order, then the
+  // slots shift.  The stores are inline asm: hipcc would otherwise wait
+  // vmcnt(0) before them (an LDS store after in-flight LDS-DMA it cannot prove
+  // disjoint), which drains the ring; the areas in flight are never this one.
+  auto vwrite = [&](int a) {
     const uint32_t addr = (uint32_t)(uintptr_t)(smem + a * AREA) + 16u * tid;
 #pragma unroll
     for (int k = 0; k < NQ; k++) {
-      const f32x4 v = {acc[SL][4 * k], acc[SL][4 * k + 1], acc[SL][4 * k + 2], acc[SL][4 * k + 3]};
+      const f32x4 v = {acc[0][4 * k], acc[0][4 * k + 1], acc[0][4 * k + 2], acc[0][4 * k + 3]};
       asm volatile("ds_write_b128 %0, %1" ::"v"(addr + (uint32_t)(k * kChunk * 4)), "v"(v) : "memory");
     }
 #pragma unroll
-    for (int i = 0; i < NX; i++) acc[SL][i] = 0.0f;
+    for (int s = 0; s + 1 < S; s++)
+#pragma unroll
+      for (int i = 0; i < NX; i++) acc[s][i] = acc[s + 1][i];
+#pragma unroll
+    for (int i = 0; i < NX; i++) acc[S - 1][i] = 0.0f;
   };
 
-  // Horizontal pass of output row y from the vertical row in area a; run
-  // every step (out = false: a prologue or first step, whose area holds no
-  // vertical row -- the result goes nowhere), so it shares a block with the
-  // vertical pass and every wave issues the same stores each step.
-  auto hpass = [&](int a, int y, bool out) {
-    const float* vf = reinterpret_cast<const float*>(smem + a * AREA) + vb;
+  // Horizontal pass of output row y of the current unit from the vertical
+  // row in area a.
+  auto hpass = [&](int a, int y) {
+    const float* vf = reinterpret_cast<const float*>(smem + a * AREA) + cl.vb;
     float q[C];
 #pragma unroll
-    for (int c = 0; c < C; c++) {
+    for (int ch = 0; ch < C; ch++) {
       float h = 0.0f;
       if constexpr ((MXD_BAND_ABLATE & 4) != 0) {
-        h = vf[c];
+        h = vf[ch];
       } else {
 #pragma unroll
-        for (int k = 0; k < T; k++) h = __builtin_fmaf(wx[k], vf[k * C + c], h);
+        for (int k = 0; k < T; k++) h = __builtin_fmaf(cl.wx[k], vf[k * C + ch], h);
       }
-      q[c] = encode(h);
+      q[ch] = encode(h);
     }
-    store_pixel<C, F32>(dst, hact && out && !(MXD_BAND_ABLATE & 2) ? y * dstride + scol : kNoLoad, q);
+    store_pixel<C, F32>(c.dst, cl.scol != kNoLoad && !(MXD_BAND_ABLATE & 2) ? y * c.dstride + cl.scol : kNoLoad, q);
   };
 
   for (int g = 0; g < la; g++) {
     int dr[KW];
-    dma_rows(g, dr);
-    issue(dr, g);
+    dma_rows(c, g, dr);
+    issue(c, dr, g);
   }
-  int acur = 0, aprev = rg - 1;  // areas of groups g and g - 1
-  bool done = false;
+  int acur = 0, aprev = rg - 1;  // areas of groups t and t - 1
+  int cstart = 0;                // stream step of the current unit's group 0
+  int vrows = 0;                 // output rows the vertical pass completed in its unit
+  int hrow = -1;                 // output row the next step's horizontal pass writes (-1: none)
+  int tx_loads = -(1 << 20);     // step that loaded a unit's tables ahead (its LW loads)
 #if MXD_BAND_STAMPS
   MXD_STAMP(t_loop0);
   MXD_SEG(0, t_setup0, t_loop0);
 #endif
-  for (int g0 = 0;; g0 += S) {
-    static_for<S>([&](auto sc) {
-      const int g = g0 + decltype(sc)::value;
-      if (done || g > ngroups) {
-        done = true;
-        return;
-      }
-      if ((g & 7) == 0) band_prio(g, ngroups);
-      int dr[KW];
-      dma_rows(g + la, dr);
-      // Vector-memory ops this wave issued after group g's LDS-DMA: the DMA
-      // of the la - 1 groups after it, and the stores of the steps since.
-      MXD_STAMP(ta);
-      wait_vmcnt((la - 1) * KW + SW * min(g, la - 1));
-      MXD_STAMP(tb);
-      barrier_lds();  // group g's rows and output row g - 1 - P's vertical row visible
-      MXD_STAMP(tc);
-      hpass(aprev, oy0 + g - 1 - P, g > P);
-      MXD_STAMP(td);
-      vpass(sc, g, acur);  // g == ngroups: the all-absent group, weights 0
-      MXD_STAMP(te);
-      barrier_lds();  // area acur's rows and area aprev's vertical row consumed
-      MXD_STAMP(tf);
-      if (g < ngroups && g >= P) vwrite(sc, acur);
-      issue(dr, aprev);  // group g + la: (g + la) mod (la + 1) == (g - 1) mod (la + 1)
+  for (int t = 0;; t++) {
+    const int cend = cstart + c.ng;
+    const int tcross = cend - la;  // the step whose LDS-DMA starts the next unit
+    if ((t & 7) == 0) band_prio(kdone * c.ng + t - cstart, nmine * c.ng);
+    int npx = 0, ox0 = 0, xs = 0, crop_w = 0, flip = 0;
+    cgfloat* xtab = nullptr;
+    if (t == tcross)
+      n = load_unit<C, F32>(imgs, unit_img, per_img, ucur + G, nunits, &npx, &ox0, &xs, &xtab, &crop_w, &flip);
+    const int gd = t + la;  // the group this step's LDS-DMA brings
+    const bool dcur = gd < cend;
+    int dr[KW];
+    if (dcur)
+      dma_rows(c, gd - cstart, dr);
+    else
+      dma_rows(n, gd - cend, dr);
+    // Vector-memory ops this wave issued after group t's LDS-DMA: the DMA of
+    // the la - 1 groups after it, the stores of the steps since, and a
+    // unit's table loads issued in those steps.
+    MXD_STAMP(ta);
+    wait_vmcnt((la - 1) * KW + SW * min(t, la - 1) + (tx_loads > t - la && tx_loads < t ? LW : 0));
+    MXD_STAMP(tb);
+    barrier_lds();  // group t's rows and the previous step's vertical row visible
+    MXD_STAMP(tc);
+    if (hrow >= 0) {
+      hpass(aprev, c.oy0 + hrow);
+    } else {
+      const float z[C] = {};
+      store_pixel<C, F32>(c.dst, kNoLoad, z);  // every step issues SW stores (the counts above)
+    }
+    MXD_STAMP(td);
+    const bool vcur = t < cend;  // else: group 0 of the next unit
+    kint* vg = vcur ? c.sched + (t - cstart) * GW : n.sched;
+    const bool vany = vcur || n.ng > 0;
+    int flags = 0;
+    if (vany) {
+      flags = vg[0];
+      vpass(vg + E, acur);
+    }
+    MXD_STAMP(te);
+    barrier_lds();  // area acur's rows and area aprev's vertical row consumed
+    MXD_STAMP(tf);
+    const bool done = (flags & kBandRowDone) != 0;
+    if (done) vwrite(acur);
+    const int vr = vcur ? vrows : 0;
+    hrow = done ? vr : -1;
+    vrows = vr + (done ? 1 : 0);
+    if (t == tcross && n.ng > 0) {
+      lane_loads(npx, ox0, xs, xtab, crop_w, flip, nraw, &nscol);
+      tx_loads = t;
+    }
+    issue(dcur ? c : n, dr, aprev);  // group t + la: (t + la) mod (la + 1) == (t - 1) mod (la + 1)
 #if MXD_BAND_STAMPS
-      MXD_STAMP(tg);
-      MXD_SEG(1, ta, tb);
-      MXD_SEG(2, tb, tc);
-      MXD_SEG(3, tc, td);
-      MXD_SEG(4, td, te);
-      MXD_SEG(5, te, tf);
-      MXD_SEG(6, tf, tg);
-      seg[7] += 1;
+    MXD_STAMP(tg);
+    MXD_SEG(1, ta, tb);
+    MXD_SEG(2, tb, tc);
+    MXD_SEG(3, tc, td);
+    MXD_SEG(4, td, te);
+    MXD_SEG(5, te, tf);
+    MXD_SEG(6, tf, tg);
+    seg[7] += 1;
 #endif
-      aprev = acur;
-      acur = acur + 1 == rg ? 0 : acur + 1;
-    });
-    if (done) break;
+    aprev = acur;
+    acur = acur + 1 == rg ? 0 : acur + 1;
+    if (t >= cend) {
+      // the current unit's last row went out this step: the next one takes over
+      if (n.ng <= 0) break;
+      c = n;
+      cl.scol = nscol;
+      unpack(nraw, c.vboff, cl);
+      cstart = cend;
+      ucur += G;
+      kdone++;
+      n.ng = 0;
+    }
   }
   // no LDS-DMA may land after the workgroup's LDS is reassigned
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if MXD_BAND_STAMPS
   seg[8] = t_real0;
   seg[9] = __builtin_amdgcn_s_memrealtime();
-  if (wave == 0 && lane == 0 && unit < kMaxStamped)
-    for (int k = 0; k < kStampSegs; k++) g_band_stamps[kStampSegs * unit + k] = seg[k];
+  const int sid = RFL(xcd_remap(blockIdx.x, G));
+  if (wave == 0 && lane == 0 && sid < kMaxStamped)
+    for (int k = 0; k < kStampSegs; k++) g_band_stamps[kStampSegs * sid + k] = seg[k];
 #endif
 }
 
-using BandKernel = void (*)(const ImgDev*, int, int, int, int);
+using BandKernel = void (*)(const ImgDev*, const int*, int, int, int);
 
 constexpr int kNumClasses = sizeof(kBandClasses) / sizeof(kBandClasses[0]);
 
@@ -504,11 +631,12 @@ int band_capacity(const BandCfg& cfg, int device) {
   return blocks * cus;
 }
 
-int launch_band(const BandCfg& cfg, const ImgDev* imgs, void* stream) {
+int launch_band(const BandCfg& cfg, const ImgDev* imgs, const int32_t* unit_img, void* stream) {
   const BandKernel k = select_kernel(cfg);
   if (!k) return -2;
-  hipLaunchKernelGGL(k, dim3(cfg.nunits), dim3(kThreads), band_lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
-                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.la);
+  if (cfg.grid < 1 || cfg.grid > cfg.nunits || (cfg.per_img <= 0 && !unit_img)) return -3;
+  hipLaunchKernelGGL(k, dim3(cfg.grid), dim3(kThreads), band_lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
+                     imgs, unit_img, cfg.nunits, cfg.per_img, cfg.la);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -37,10 +37,10 @@ struct BandPlan {
   int32_t taps = 0, db = 0, s = 0;
   int32_t nq = 0;        // KiB of source window per strip row
   int32_t nstrips = 0, tx = 0;
-  int32_t prologue = 0;  // P: groups before a band's first output row
+  int32_t prologue = 0;  // groups before the one completing a band's first output row (at crop row 0)
   int32_t dmax = 0;      // most source rows new for one output row
   int32_t la = 0;        // groups loaded ahead
-  double rows_per_out = 0;  // mean source rows per output row (sizing la)
+  double rows_per_out = 0;  // mean source rows per output row
 };
 
 // Scatter shape of crop rows [off, off+len): dmax, and whether the taps are
@@ -52,20 +52,20 @@ bool band_vertical_shape(const AxisView& yt, int32_t off, int32_t len, int32_t* 
 // lookahead (tuning).
 BandPlan band_plan_image(const AxisView& xt, const AxisView& yt, const BandImage& im, int32_t la_override = 0);
 
-// Accumulator slots a scatter schedule with db rows per group needs for crop
-// rows [off, off+len), bands starting at any row (cached per table window).
-int32_t band_slots(const AxisView& yt, int32_t off, int32_t len, int32_t db);
-
-// Prologue groups of a band for class db: every output row's taps fit in
-// P + 1 groups.
-int32_t band_prologue(const AxisView& yt, int32_t off, int32_t len, int32_t db);
+// Accumulator slots (open output rows a source row's weights reach) the
+// schedule of crop rows [off, off+len) needs, bands starting at any row
+// (cached per table window).
+int32_t band_slots(const AxisView& yt, int32_t off, int32_t len);
 
 // Schedule words for crop rows [crop_y, crop_y + crop_h) in bands of ty rows:
-// per band `band_words` words = header [P, 0, 0, 0], then (P + ty + 1) groups
-// of db entries {source row or -1, s weights, zero padded to 4 words}; the
-// last group is all absent (the kernel reads one group past the band).
-// Returns false if some source row's weights do not fit the s slots.
+// per band `band_words` words = header [groups, 0, 0, 0], then the groups,
+// each a header [flags, 0, 0, 0] (kBandRowDone: completes the oldest open
+// output row) and db entries {source row or -1, s weights, zero padded to 4
+// words}.  The rows new for an output row fill ceil(new / db) groups (at
+// least one), the last completing it; a band has at least min_groups groups
+// (empty ones appended).  Returns false if some source row's weights do not
+// fit the s slots.
 bool band_schedule(const AxisView& yt, int32_t crop_y, int32_t crop_h, int32_t ty, int32_t db, int32_t s,
-                   int32_t prologue, std::vector<int32_t>* words, int32_t* band_words);
+                   int32_t min_groups, std::vector<int32_t>* words, int32_t* band_words);
 
 }  // namespace mxd

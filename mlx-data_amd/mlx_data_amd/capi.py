@@ -46,9 +46,11 @@ MXD_POLICY_NO_BYTES = 16
 MXD_POLICY_BYTES = 32
 MXD_POLICY_NO_ZERO_COPY = 64
 MXD_POLICY_NO_BAND = 128
+MXD_POLICY_PREFER_BAND = 256
 
 MXD_TUNE_BAND_ROWS = 0
 MXD_TUNE_BAND_LA = 1
+MXD_TUNE_BAND_GRID = 2
 
 
 class MxdImage(ctypes.Structure):

@@ -8,8 +8,9 @@ unpinned about stbir itself is listed in DESIGN.md §3.
 
 Full-size workloads: C2 (1280x960 -> 256 -> 224), C3's six sizes, C4's
 ImageNet shapes, C5 (4K -> 512, random 448 crops, mirrored), Caltech
-upsampling, and arbitrary windows; each on the default (band) kernel, the wave
-kernels (MXD_POLICY_NO_BAND) and the general kernel (MXD_POLICY_NO_WAVE)."""
+upsampling, arbitrary windows and 12 / 24 MP photos; each on the default
+choice, the band kernel (MXD_POLICY_PREFER_BAND), the wave kernels
+(MXD_POLICY_NO_BAND) and the general kernel (MXD_POLICY_NO_WAVE)."""
 import numpy as np
 import pytest
 
@@ -19,7 +20,8 @@ from mlx_data_amd import capi
 
 pytestmark = pytest.mark.gpu
 
-POLICIES = [("band", capi.MXD_POLICY_AUTO), ("wave", capi.MXD_POLICY_NO_BAND), ("general", capi.MXD_POLICY_NO_WAVE)]
+POLICIES = [("default", capi.MXD_POLICY_AUTO), ("band", capi.MXD_POLICY_PREFER_BAND),
+            ("wave", capi.MXD_POLICY_NO_BAND), ("general", capi.MXD_POLICY_NO_WAVE)]
 
 
 def _cases():
@@ -45,6 +47,8 @@ def _cases():
         geoms.append((rw, rh, int(rng.integers(0, rw - cw + 1)), int(rng.integers(0, rh - ch + 1)), cw, ch,
                       int(rng.integers(0, 2))))
     out["windows"] = (imgs, geoms)
+    imgs = [synth(3024, 4032, 3, 90), synth(4000, 6000, 3, 91)]
+    out["photos_12_24mp"] = (imgs, [center_geom(i) for i in imgs])
     return out
 
 

@@ -22,6 +22,7 @@ kv = dict(p.split("=") for p in (sys.argv[3] if len(sys.argv) > 3 else "").split
 capi, L, stream, sets, mode, alg, sizes, geoms, f32 = band_sweep.setup(w)
 capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, int(kv.get("rows", 0)))
 capi.set_tuning(capi.MXD_TUNE_BAND_LA, int(kv.get("la", 0)))
+capi.set_tuning(capi.MXD_TUNE_BAND_GRID, int(kv.get("grid", 0)))
 hs = ctypes.c_void_p(stream.handle)
 for i in range(launches):
     capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, 0, hs))

@@ -4,8 +4,10 @@ process on one box (A/B without box-to-box spread).
   python tools/band_sweep.py [--workload c2] [--launches 20] \
       --set "rows=0,la=0,policy=0" --set "rows=38" ...
 
+Settings are measured round-robin (rep 1 of every setting, then rep 2, ...)
+after a --warm-s warm-up, so clock / cache drift does not favour any of them.
 Each --set is a comma list of knob=value (rows -> MXD_TUNE_BAND_ROWS, la ->
-MXD_TUNE_BAND_LA, policy -> mxd_set_kernel_policy).  Inputs are bench.py's
+MXD_TUNE_BAND_LA, grid -> MXD_TUNE_BAND_GRID, policy -> mxd_set_kernel_policy).  Inputs are bench.py's
 workload (two alternating source/output sets, resident in HBM); the time is
 HIP events around `launches` back-to-back launches on one stream, after 3
 warm-up launches, repeated `--reps` times (median reported).  Prints one JSON
@@ -16,6 +18,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -70,34 +73,59 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--set", action="append", default=[])
+    ap.add_argument("--warm-s", type=float, default=1.0)
     args = ap.parse_args()
     capi, L, stream, sets, mode, alg, sizes, geoms, f32 = setup(args.workload)
     dev = 0
     hs = ctypes.c_void_p(stream.handle)
     e0, e1 = capi.Event(), capi.Event()
-    for spec in args.set or ["rows=0"]:
+    specs = args.set or ["rows=0"]
+
+    def apply(spec):
         kv = dict(p.split("=") for p in spec.split(",") if p)
         capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, int(kv.get("rows", 0)))
         capi.set_tuning(capi.MXD_TUNE_BAND_LA, int(kv.get("la", 0)))
+        capi.set_tuning(capi.MXD_TUNE_BAND_GRID, int(kv.get("grid", 0)))
         capi.set_kernel_policy(int(kv.get("policy", 0)))
-        for i in range(3):
+        return kv
+
+    # Warm-up (clocks, caches, plans of every setting) before any timing;
+    # then the reps go round-robin over the settings, so drift during the
+    # run spreads over all of them instead of biasing the first.
+    for spec in specs:
+        apply(spec)
+        for i in range(10):
             capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, dev, hs))
-        times = []
-        for _ in range(args.reps):
+    apply(specs[0])
+    stream.synchronize()
+    t_end = time.time() + args.warm_s
+    while time.time() < t_end:
+        for i in range(20):
+            capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, dev, hs))
+        stream.synchronize()
+    times = {spec: [] for spec in specs}
+    for _ in range(args.reps):
+        for spec in specs:
+            apply(spec)
+            for i in range(3):
+                capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, dev, hs))
             stream.synchronize()
             e0.record(stream)
             for i in range(args.launches):
                 capi.check(L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, dev, hs))
             e1.record(stream)
             stream.synchronize()
-            times.append(e0.elapsed_ms(e1) / args.launches)
-        ms = statistics.median(times)
+            times[spec].append(e0.elapsed_ms(e1) / args.launches)
+    for spec in specs:
+        kv = apply(spec)
+        ms = statistics.median(times[spec])
         print(json.dumps({"workload": args.workload, "set": spec, "ms_per_launch": round(ms, 5),
-                          "frac": round(alg / (ms * 1e-3) / 8e12, 4), "reps": [round(t, 5) for t in times],
+                          "frac": round(alg / (ms * 1e-3) / 8e12, 4), "reps": [round(t, 5) for t in times[spec]],
                           "kernel": bench.kernel_name(capi, sizes[0], geoms[0], f32, int(kv.get("policy", 0)))}),
               flush=True)
     capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, 0)
     capi.set_tuning(capi.MXD_TUNE_BAND_LA, 0)
+    capi.set_tuning(capi.MXD_TUNE_BAND_GRID, 0)
     capi.set_kernel_policy(0)
 
 
