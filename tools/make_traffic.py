@@ -1,7 +1,7 @@
 """profiles/traffic.json from one measurement session's PMC summaries.
 
 Usage: python tools/make_traffic.py TAG PREFIX
-Reads gpurun_out/TAG_<w>pmc_p*/ (tools/r02_measure.sh) through
+Reads gpurun_out/TAG_<w>pmc_p*/ (tools/r03_measure.sh) through
 tools/pmc_traffic.py's corrections for every workload w, writes
 gpurun_out/TAG_<w>_pmc.json and gpurun_out/TAG_traffic.json; the latter is
 committed as profiles/traffic.json, with the per-workload summaries under
@@ -15,11 +15,11 @@ import sys
 tag, prefix = sys.argv[1], sys.argv[2]
 here = os.path.dirname(os.path.abspath(__file__))
 out = {}
-for w in ("c2", "c3", "c4", "c5"):
+for w in ("c2", "c3", "c4", "c5", "c6", "c7"):
     if not os.path.isdir(f"gpurun_out/{tag}_{w}pmc_p1"):
         continue
     dst = f"gpurun_out/{tag}_{w}_pmc.json"
-    subprocess.run([sys.executable, os.path.join(here, "pmc_traffic.py"), f"{tag}_{w}pmc", dst], check=True,
+    subprocess.run([sys.executable, os.path.join(here, "pmc_traffic.py"), f"{tag}_{w}pmc", dst, "resample_"], check=True,
                    stdout=subprocess.DEVNULL)
     rec = json.load(open(dst))
     if "hbm_bytes_per_launch" not in rec:

@@ -2,7 +2,7 @@
 
 Usage: python tools/pmc_traffic.py TAG OUT.json [kernel-substring]
 
-Reads gpurun_out/TAG_p*/run_counter_collection.csv (tools/gpu_pmc3.sh) and
+Reads gpurun_out/TAG_p*/run_counter_collection.csv (tools/r03_measure.sh) and
 applies the gfx950 corrections of MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE counts half the bytes of a
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
