@@ -407,6 +407,7 @@ def main():
     # tuning knobs (include/mxd_amd.h mxd_tune; measurements only): band rows, groups ahead
     ap.add_argument("--tune-rows", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tune-la", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--tune-desc", type=int, default=0, help=argparse.SUPPRESS)
     # one process, D devices: every step launches one batch slice per device
     # (the pipeline's own split, pipeline.cpp run_host); devices from
     # MXD_BENCH_SPLIT_DEVICES ("0,0" rehearses on one card) or range(D)
@@ -441,6 +442,8 @@ def main():
         capi.set_tuning(capi.MXD_TUNE_BAND_ROWS, args.tune_rows)
     if args.tune_la:
         capi.set_tuning(capi.MXD_TUNE_BAND_LA, args.tune_la)
+    if args.tune_desc:
+        capi.set_tuning(capi.MXD_TUNE_DESC, args.tune_desc)
     c3_sizes = [tuple(int(v) for v in t.split("x")) for t in args.c3_sizes.split(",") if t]
     sizes, geoms, f32 = make_workload(capi, args.workload, B, ranks.rank, c3_sizes)
     elem = 4 if f32 else 1

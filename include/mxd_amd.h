@@ -157,8 +157,17 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_BAND_ROWS: output rows per band-kernel unit;
  * MXD_TUNE_BAND_LA: row groups the band kernel keeps in flight per unit;
  * MXD_TUNE_BAND_GRID: band-kernel workgroups (0: as many as the device holds
- * at once, each running a stream of units; 1: one per unit; n > 1: n). */
-enum mxd_tune { MXD_TUNE_BAND_ROWS = 0, MXD_TUNE_BAND_LA = 1, MXD_TUNE_BAND_GRID = 2, MXD_TUNE_COUNT = 3 };
+ * at once, each running a stream of units; 1: one per unit; n > 1: n);
+ * MXD_TUNE_DESC: how a batch's new descriptor array reaches the kernels (1:
+ * copy stream + cross-stream wait; 2: copy on the launch stream; 3: kernels
+ * read the page-locked slot in place; 4: as 3, non-coherent allocation). */
+enum mxd_tune {
+  MXD_TUNE_BAND_ROWS = 0,
+  MXD_TUNE_BAND_LA = 1,
+  MXD_TUNE_BAND_GRID = 2,
+  MXD_TUNE_DESC = 3,
+  MXD_TUNE_COUNT = 4
+};
 int mxd_set_tuning(int32_t knob, int32_t value);
 
 /* The wave-kernel plan of one image on `device`, i.e. what runs when the

@@ -1,0 +1,661 @@
+// hostpath.cpp -- host-resident batches (capi_internal.h): sources staged
+// through page-locked memory (or read in place over PCIe), results copied out
+// or written to device destinations, JPEG batches finished on the device.
+#include "capi_internal.h"
+
+#include <sched.h>
+
+namespace mxd {
+namespace capi {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Host-resident path.  Each call borrows a context from its device's pool
+// (at most kCtxPerDevice, so pinned / device memory is bounded no matter how
+// many threads call), and runs the batch in chunks over the context's two
+// slots: while the GPU copies in, computes and copies out chunk k on one
+// slot's stream, the calling thread stages chunk k+1 into the other slot's
+// pinned buffer and copies chunk k-1's results out.
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* pin_in = nullptr;
+  size_t pin_in_cap = 0;
+  uint8_t* pin_out = nullptr;
+  size_t pin_out_cap = 0;
+  uint8_t* dev_in = nullptr;
+  size_t dev_in_cap = 0;
+  uint8_t* dev_out = nullptr;
+  size_t dev_out_cap = 0;
+  uint8_t* dev_mid = nullptr;  // JPEG chunks: IDCT samples + decoded RGB images
+  size_t dev_mid_cap = 0;
+};
+
+struct HostCtx {
+  Slot slot[2];
+};
+
+int grow_pinned(uint8_t** p, size_t* cap, size_t need) {
+  if (need <= *cap) return MXD_OK;
+  if (*p) MXD_HIP(hipHostFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  const size_t c = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+  MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(p), c, hipHostMallocDefault));
+  *cap = c;
+  return MXD_OK;
+}
+
+int grow_device(uint8_t** p, size_t* cap, size_t need) {
+  if (need <= *cap) return MXD_OK;
+  if (*p) MXD_HIP(hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  const size_t c = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+  MXD_HIP(hipMalloc(reinterpret_cast<void**>(p), c));
+  *cap = c;
+  return MXD_OK;
+}
+
+void free_slot_buffers(Slot& s) {
+  if (s.pin_in) (void)hipHostFree(s.pin_in);
+  if (s.pin_out) (void)hipHostFree(s.pin_out);
+  if (s.dev_in) (void)hipFree(s.dev_in);
+  if (s.dev_out) (void)hipFree(s.dev_out);
+  if (s.dev_mid) (void)hipFree(s.dev_mid);
+  s.pin_in = s.pin_out = s.dev_in = s.dev_out = s.dev_mid = nullptr;
+  s.pin_in_cap = s.pin_out_cap = s.dev_in_cap = s.dev_out_cap = s.dev_mid_cap = 0;
+}
+
+// Concurrent host-path calls per device (each context holds its staging
+// buffers): enough for the 16 prefetch workers of the largest measured
+// pipeline, which 4 contexts serialised.
+constexpr int kCtxPerDevice = 16;
+
+// Host-side byte moves of the host path (footprint staging into pinned
+// memory, copy-out of results) are bound by one core's memory bandwidth;
+// they are split over helper threads, fewer when several host-path calls run
+// at once (prefetch workers already spread the work).
+std::atomic<int> g_host_calls{0};
+
+template <class F>
+void parallel_items(int32_t first, int32_t end, int64_t bytes, F&& f) {
+  const int32_t n = end - first;
+  static const int hw = [] {  // the cores this process may run on (a container's share, not the machine)
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) return std::max(1, CPU_COUNT(&set));
+    return std::max(1, (int)std::thread::hardware_concurrency());
+  }();
+  int t = std::min<int64_t>({8, hw / std::max(1, g_host_calls.load()), n, bytes >> 20});
+  if (t <= 1) {
+    for (int32_t i = first; i < end; i++) f(i);
+    return;
+  }
+  std::atomic<int32_t> next{first};
+  auto work = [&] {
+    for (int32_t i; (i = next.fetch_add(1)) < end;) f(i);
+  };
+  std::vector<std::thread> ts;
+  for (int k = 1; k < t; k++) ts.emplace_back(work);
+  work();
+  for (auto& th : ts) th.join();
+}
+
+class HostPool {
+ public:
+  HostCtx* acquire(int32_t device) {
+    std::unique_lock<std::mutex> lk(mu_);
+    Dev& d = devs_[device];
+    cv_.wait(lk, [&] { return !d.idle.empty() || (int)d.all.size() < kCtxPerDevice; });
+    if (!d.idle.empty()) {
+      HostCtx* c = d.idle.back();
+      d.idle.pop_back();
+      return c;
+    }
+    d.all.push_back(std::make_unique<HostCtx>());
+    return d.all.back().get();
+  }
+  void release(int32_t device, HostCtx* c) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      devs_[device].idle.push_back(c);
+    }
+    cv_.notify_one();
+  }
+  // Frees the buffers of every idle context (streams stay).
+  void trim() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& kv : devs_) {
+      DeviceGuard g(kv.first);
+      for (HostCtx* c : kv.second.idle)
+        for (Slot& s : c->slot) free_slot_buffers(s);
+    }
+  }
+
+ private:
+  struct Dev {
+    std::vector<std::unique_ptr<HostCtx>> all;
+    std::vector<HostCtx*> idle;
+  };
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int32_t, Dev> devs_;
+};
+
+HostPool& host_pool() {
+  static HostPool* p = new HostPool();
+  return *p;
+}
+
+// Borrowed context, returned to the pool on scope exit.
+struct CtxLease {
+  int32_t device;
+  HostCtx* ctx;
+  explicit CtxLease(int32_t d) : device(d), ctx(host_pool().acquire(d)) {}
+  ~CtxLease() { host_pool().release(device, ctx); }
+};
+
+int init_slot(Slot& s) {
+  if (!s.stream) MXD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  if (!s.done) MXD_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  return MXD_OK;
+}
+
+// Source footprint of an image's crop window (rows [y_lo, y_hi], pixels
+// [x_lo, x_hi]): taps are monotone, so the window's ends bound it.
+void footprint(const DevTable& xt, const DevTable& yt, const mxd_image& im, int32_t* x_lo, int32_t* x_hi,
+               int32_t* y_lo, int32_t* y_hi) {
+  const int32_t xa = im.crop_x, xb = im.crop_x + im.crop_w - 1;
+  const int32_t ya = im.crop_y, yb = im.crop_y + im.crop_h - 1;
+  *x_lo = xt.first[xa];
+  *x_hi = xt.first[xb] + xt.count[xb] - 1;
+  *y_lo = yt.first[ya];
+  *y_hi = yt.first[yb] + yt.count[yb] - 1;
+}
+
+}  // namespace
+
+// The host path: host sources (footprints staged through pinned memory),
+// results to host (dst_device false: D2H + copy-out) or straight into device
+// destinations (dst_device true).
+// Page-locked host memory of this HIP runtime (hipHostMalloc'd or
+// registered): the DMA engines can read / write it in place.
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not an error here
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// The device-side address of page-locked host memory (kernels read it over
+// PCIe), or null when the runtime gives none.
+const uint8_t* host_device_ptr(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return static_cast<const uint8_t*>(a.devicePointer);
+}
+
+// Chunk tables of a JPEG chunk (device-side finish, jpegdev.h): where the
+// coefficients, descriptors and quantisation tables sit in the staged input,
+// and the decoded images in the slot's dev_mid buffer.
+struct JpegChunk {
+  std::vector<mxd::JpegPlaneDev> planes;
+  std::vector<mxd::JpegImgDev> imgs;
+  std::vector<uint16_t> qtabs;
+  int64_t planes_off = 0, imgs_off = 0, q_off = 0, end = 0;  // in the staged input
+  int64_t samples = 0, rgb_off = 0, mid_bytes = 0;             // in dev_mid
+  int64_t nblocks = 0, max_quad_rows = 0;
+};
+
+const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
+
+int64_t rgb_pitch(int32_t w) { return (((int64_t)w * 3 + 63) & ~(int64_t)63) + 64; }
+
+// Lays out the chunk [first, end) of a JPEG batch whose coefficients are staged
+// at in_off[i]; the tables follow at `tables_at`.
+void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const std::vector<int64_t>& in_off,
+                int64_t tables_at, JpegChunk* out) {
+  JpegChunk& c = *out;
+  c = JpegChunk();
+  auto up = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
+  for (int32_t i = first; i < end; i++) {
+    const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
+    mxd::JpegImgDev m{};
+    m.ncomp = info.ncomp == 1 ? 1 : 3;
+    m.rgb = info.color_space == 2 ? 1 : 0;
+    m.width = info.width;
+    m.height = info.height;
+    m.pitch = (int32_t)rgb_pitch(info.width);
+    m.quads = (info.width + 3) / 4;
+    for (int k = 0; k < m.ncomp; k++) {
+      const mxd::jpeg::CoefPlane& cp = info.comp[k];
+      mxd::JpegPlaneDev p{};
+      p.coef = (in_off[i] + cp.off * 2) / 2;
+      p.out = c.samples;
+      p.first_block = c.nblocks;
+      p.bw = cp.bw;
+      p.bh = cp.bh;
+      p.qtab = (int32_t)c.qtabs.size();
+      p.coded = cp.coded ? 1 : 0;
+      c.qtabs.insert(c.qtabs.end(), cp.q, cp.q + 64);
+      c.planes.push_back(p);
+      m.plane[k] = c.samples;
+      m.stride[k] = cp.bw * 8;
+      m.dw[k] = cp.dw;
+      m.dh[k] = cp.dh;
+      m.hx[k] = info.max_h / cp.h;
+      m.vx[k] = info.max_v / cp.v;
+      // jpeg.cpp upsample_row's choice
+      const bool h2 = cp.h * 2 == info.max_h, v2 = cp.v * 2 == info.max_v;
+      const bool hf = cp.h == info.max_h, vf = cp.v == info.max_v;
+      m.mode[k] = hf && vf                ? mxd::kUpFull
+                  : h2 && vf              ? (cp.dw > 2 ? mxd::kUpH2V1 : mxd::kUpRep)
+                  : hf && v2              ? mxd::kUpH1V2
+                  : h2 && v2 && cp.dw > 2 ? mxd::kUpH2V2
+                                          : mxd::kUpRep;
+      c.samples += up((int64_t)cp.bw * 8 * cp.bh * 8, 256);
+      c.nblocks += (int64_t)cp.bw * cp.bh;
+    }
+    m.out = c.mid_bytes;  // relative to rgb_off, fixed below
+    c.mid_bytes += up((int64_t)m.pitch * m.height, 256);
+    c.max_quad_rows = std::max<int64_t>(c.max_quad_rows, (int64_t)m.height * m.quads);
+    c.imgs.push_back(m);
+  }
+  c.rgb_off = c.samples;
+  c.mid_bytes += c.samples;
+  c.planes_off = up(tables_at, 256);
+  c.imgs_off = up(c.planes_off + (int64_t)(c.planes.size() * sizeof(mxd::JpegPlaneDev)), 256);
+  c.q_off = up(c.imgs_off + (int64_t)(c.imgs.size() * sizeof(mxd::JpegImgDev)), 256);
+  c.end = c.q_off + (int64_t)(c.qtabs.size() * sizeof(uint16_t));
+}
+
+// jpeg != nullptr: images[i] is jpeg[i] as an mxd_image (3 channels, the
+// window as the source); its "source" is the image's coefficients, staged
+// whole, and the chunk's kernels first decode them into dev_mid.
+int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device,
+              const mxd_jpeg_image* jpeg) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (out_dtype != MXD_U8 && out_dtype != MXD_F32_DIV255) return fail(MXD_ERR_INVALID, "mxd: bad out_dtype");
+  if (n == 0) return MXD_OK;
+  const int64_t elem = out_dtype == MXD_F32_DIV255 ? 4 : 1;
+  for (int32_t i = 0; i < n; i++)
+    if (int rc = validate(images[i], i)) return rc;
+  if (int rc = check_device(device)) return rc;
+  DeviceGuard g(device);
+  g_host_calls.fetch_add(1);
+  struct CallCount {
+    ~CallCount() { g_host_calls.fetch_sub(1); }
+  } call_count;
+  // Per image: the staged footprint (columns from x0, 16-byte aligned so both
+  // kernel families read it as they would the whole image) and its offsets.
+  struct Stage {
+    int32_t x0, y0, rows;
+    int64_t pitch, copy, in_off, out_off, out_row;
+    int64_t in_size;              // staged bytes (footprint rows, or a JPEG's coefficients)
+    bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
+    const uint8_t* src_dev;       // zero copy: the kernel reads the page-locked source in place
+    uint8_t* dst_dev;             // zero copy: the kernel writes the page-locked destination in place
+  };
+  std::vector<Stage> st(n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_image& im = images[i];
+    if (jpeg) {
+      Stage& s = st[i];
+      const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jpeg[i].coefs));
+      s.x0 = s.y0 = 0;
+      s.rows = im.src_h;
+      s.pitch = s.copy = 0;
+      s.in_size = info.coef_count * 2;
+      s.out_row = (int64_t)im.crop_w * im.channels * elem;
+      s.src_pinned = false;
+      s.src_dev = nullptr;
+      s.dst_pinned = !dst_device && host_pinned(im.dst);
+      s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
+                      ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
+      if (!dst_device && im.dst_stride < s.out_row)
+        return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+      continue;
+    }
+    const DevTable *xt = nullptr, *yt = nullptr;
+    if (int rc = tables().get(device, im.src_w, im.resize_w, &xt)) return rc;
+    if (int rc = tables().get(device, im.src_h, im.resize_h, &yt)) return rc;
+    int32_t xl, xh, yl, yh;
+    footprint(*xt, *yt, im, &xl, &xh, &yl, &yh);
+    const int32_t c = im.channels;
+    const int32_t m = 16 / std::gcd(c, 16);  // x0 * c is a multiple of 16
+    Stage& s = st[i];
+    s.x0 = xl - xl % m;
+    s.y0 = yl;
+    s.rows = yh - yl + 1;
+    const int64_t want = (int64_t)(xh + 1 - s.x0) * c + 32;  // + the kernels' read-ahead inside a row
+    s.copy = std::min<int64_t>((int64_t)(im.src_w - s.x0) * c, want);
+    s.pitch = (want + 15) & ~(int64_t)15;
+    s.in_size = s.pitch * s.rows;
+    s.out_row = (int64_t)im.crop_w * c * elem;
+    s.src_pinned = host_pinned(im.src);
+    // Page-locked sources are read in place by the kernel (PCIe reads): 2-D
+    // DMA of short footprint rows measured 3.4x slower than one contiguous
+    // copy of the same bytes (tools/pcie_probe.py).
+    s.src_dev = s.src_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY) ? host_device_ptr(im.src) : nullptr;
+    s.dst_pinned = !dst_device && host_pinned(im.dst);
+    s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
+                    ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
+    if (!dst_device && im.dst_stride < s.out_row)
+      return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+  }
+  // Chunks of about kChunk staged bytes (at least one image each).
+  constexpr int64_t kChunk = 24 << 20;
+  // (and at most 65535 images: the JPEG colour kernel puts one image per grid row)
+  constexpr int32_t kChunkImages = 65535;
+  std::vector<std::pair<int32_t, int32_t>> chunks;  // [first, end)
+  for (int32_t i = 0; i < n;) {
+    int32_t j = i;
+    int64_t bytes = 0;
+    while (j < n && j - i < kChunkImages && (j == i || bytes + st[j].in_size <= kChunk)) {
+      bytes += st[j].in_size;
+      j++;
+    }
+    chunks.push_back({i, j});
+    i = j;
+  }
+  CtxLease lease(device);
+  HostCtx& ctx = *lease.ctx;
+  // On every exit (an error return included) the context goes back to the
+  // pool idle: no kernel of this call may still read its slot buffers or
+  // write the caller's destinations once the call has returned.
+  struct Drain {
+    HostCtx& c;
+    ~Drain() {
+      for (Slot& sl : c.slot)
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+    }
+  } drain{ctx};
+  for (Slot& sl : ctx.slot)
+    if (int rc = init_slot(sl)) return rc;
+  int pending[2] = {-1, -1};  // chunk in flight on each slot
+  auto copy_out = [&](int k) -> int {
+    Slot& sl = ctx.slot[k & 1];
+    MXD_HIP(hipEventSynchronize(sl.done));
+    pending[k & 1] = -1;
+    if (dst_device) return MXD_OK;  // the kernel wrote the destinations
+    int64_t bytes = 0;
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) bytes += st[i].out_row * images[i].crop_h;
+    parallel_items(chunks[k].first, chunks[k].second, bytes, [&](int32_t i) {
+      if (st[i].dst_pinned) return;  // DMA'd straight into place
+      const mxd_image& im = images[i];
+      uint8_t* d = static_cast<uint8_t*>(im.dst);
+      const uint8_t* src = sl.pin_out + st[i].out_off;
+      if (im.dst_stride == st[i].out_row) {
+        std::memcpy(d, src, (size_t)st[i].out_row * im.crop_h);
+      } else {
+        for (int32_t r = 0; r < im.crop_h; r++)
+          std::memcpy(d + (size_t)r * im.dst_stride, src + (size_t)r * st[i].out_row, st[i].out_row);
+      }
+    });
+    return MXD_OK;
+  };
+  for (int k = 0; k < (int)chunks.size(); k++) {
+    Slot& sl = ctx.slot[k & 1];
+    if (pending[k & 1] >= 0)
+      if (int rc = copy_out(pending[k & 1])) return rc;
+    // Staged images first (one H2D / D2H each way covers them), directly
+    // DMA'd ones after them.
+    int64_t in_bytes = 0, out_bytes = 0;
+    for (int pass = 0; pass < 2; pass++)
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+        if (st[i].src_pinned == (pass == 1) && !st[i].src_dev) {
+          st[i].in_off = in_bytes;
+          in_bytes += (st[i].in_size + 255) & ~(int64_t)255;
+        }
+    int64_t in_staged = 0, out_staged = 0;
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+      if (!st[i].src_pinned) in_staged = std::max(in_staged, st[i].in_off + st[i].in_size);
+    JpegChunk jc;
+    if (jpeg) {
+      std::vector<int64_t> off(n, 0);
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++) off[i] = st[i].in_off;
+      jpeg_chunk(jpeg, chunks[k].first, chunks[k].second, off, in_bytes, &jc);
+      in_bytes = in_staged = jc.end;  // coefficients, then the chunk's tables, in one copy
+      if (int rc = grow_device(&sl.dev_mid, &sl.dev_mid_cap, jc.mid_bytes)) return rc;
+    }
+    for (int pass = 0; pass < 2; pass++)
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+        if (st[i].dst_pinned == (pass == 1) && !st[i].dst_dev) {
+          st[i].out_off = out_bytes;
+          // page-locked destinations back to back (one copy per contiguous run)
+          const int64_t b = st[i].out_row * images[i].crop_h;
+          out_bytes += pass == 1 && (st[i].out_row & 3) == 0 ? b : (b + 255) & ~(int64_t)255;
+        }
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
+      if (!st[i].dst_pinned) out_staged = std::max(out_staged, st[i].out_off + st[i].out_row * images[i].crop_h);
+    if (int rc = grow_pinned(&sl.pin_in, &sl.pin_in_cap, in_bytes)) return rc;
+    if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, in_bytes)) return rc;
+    if (!dst_device) {
+      if (int rc = grow_pinned(&sl.pin_out, &sl.pin_out_cap, out_bytes)) return rc;
+      if (int rc = grow_device(&sl.dev_out, &sl.dev_out_cap, out_bytes)) return rc;
+    }
+    // Zero copy through the staging buffers too: the kernel reads staged
+    // footprints from the page-locked slot buffer and writes results into its
+    // page-locked output buffer (no H2D / D2H DMA step in between).
+    const bool zc = !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY) && !jpeg;
+    const uint8_t* pin_in_dev = zc ? host_device_ptr(sl.pin_in) : nullptr;
+    uint8_t* pin_out_dev = zc && !dst_device && sl.pin_out ? const_cast<uint8_t*>(host_device_ptr(sl.pin_out)) : nullptr;
+    const int32_t cn = chunks[k].second - chunks[k].first;
+    std::vector<mxd_image> dev_imgs(images + chunks[k].first, images + chunks[k].second);
+    std::vector<Stored> where(cn);
+    parallel_items(chunks[k].first, chunks[k].second, in_staged, [&](int32_t i) {
+      const mxd_image& im = images[i];
+      const Stage& s = st[i];
+      if (jpeg) {
+        std::memcpy(sl.pin_in + s.in_off, mxd::jpeg::coef_info(coefs_of(jpeg[i].coefs)).coef, s.in_size);
+        return;
+      }
+      if (s.src_pinned) return;
+      uint8_t* stage = sl.pin_in + s.in_off;
+      const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
+      for (int32_t r = 0; r < s.rows; r++) std::memcpy(stage + r * s.pitch, from + (int64_t)r * im.src_stride, s.copy);
+    });
+    if (jpeg) {
+      std::memcpy(sl.pin_in + jc.planes_off, jc.planes.data(), jc.planes.size() * sizeof(mxd::JpegPlaneDev));
+      for (auto& m : jc.imgs) m.out += jc.rgb_off;
+      std::memcpy(sl.pin_in + jc.imgs_off, jc.imgs.data(), jc.imgs.size() * sizeof(mxd::JpegImgDev));
+      std::memcpy(sl.pin_in + jc.q_off, jc.qtabs.data(), jc.qtabs.size() * sizeof(uint16_t));
+    }
+    for (int32_t j = 0; j < cn; j++) {
+      const int32_t i = chunks[k].first + j;
+      const mxd_image& im = images[i];
+      const Stage& s = st[i];
+      if (jpeg) {
+        const mxd::JpegImgDev& m = jc.imgs[j];
+        const uint8_t* win = sl.dev_mid + m.out + (int64_t)jpeg[i].win_y * m.pitch + (int64_t)jpeg[i].win_x * 3;
+        where[j] = Stored{win, m.pitch, 0, 0, im.src_h};
+        dev_imgs[j].src = win;
+        dev_imgs[j].src_stride = m.pitch;
+        if (!dst_device && !s.dst_dev) {
+          dev_imgs[j].dst = sl.dev_out + s.out_off;
+          dev_imgs[j].dst_stride = s.out_row;
+        } else if (s.dst_dev) {
+          dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
+        }
+        continue;
+      }
+      if (s.src_dev) {
+        // zero copy: the footprint rows in place in the page-locked source
+        const uint8_t* base = s.src_dev + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
+        where[j] = Stored{base, im.src_stride, s.x0, s.y0, s.rows};
+        dev_imgs[j].src = base;
+      } else {
+        const uint8_t* in = pin_in_dev ? pin_in_dev : sl.dev_in;
+        where[j] = Stored{in + s.in_off, s.pitch, s.x0, s.y0, s.rows};
+        dev_imgs[j].src = in + s.in_off;  // checked by validate() only; `where` says what is stored
+      }
+      dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
+      if (!dst_device && !s.dst_dev) {
+        dev_imgs[j].dst = (pin_out_dev ? pin_out_dev : sl.dev_out) + s.out_off;
+        dev_imgs[j].dst_stride = s.out_row;
+      } else if (s.dst_dev) {
+        dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
+      }
+    }
+    if (in_staged > 0 && !pin_in_dev)
+      MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
+    if (jpeg) {
+      mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
+                            reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
+                            reinterpret_cast<const mxd::JpegPlaneDev*>(sl.dev_in + jc.planes_off),
+                            (int32_t)jc.planes.size(), jc.nblocks, sl.dev_mid, sl.stream);
+      mxd::launch_jpeg_color(sl.dev_mid, reinterpret_cast<const mxd::JpegImgDev*>(sl.dev_in + jc.imgs_off), cn,
+                             jc.max_quad_rows, sl.dev_mid, sl.stream);
+      MXD_HIP(hipGetLastError());
+    }
+    for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+      const Stage& s = st[i];
+      if (!s.src_pinned || s.src_dev) continue;
+      const mxd_image& im = images[i];
+      const uint8_t* from = im.src + (int64_t)s.y0 * im.src_stride + (int64_t)s.x0 * im.channels;
+      MXD_HIP(hipMemcpy2DAsync(sl.dev_in + s.in_off, s.pitch, from, im.src_stride, s.copy, s.rows,
+                               hipMemcpyHostToDevice, sl.stream));
+    }
+    if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
+    if (!dst_device) {
+      if (out_staged > 0 && !pin_out_dev)
+        MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_staged, hipMemcpyDeviceToHost, sl.stream));
+      // Page-locked destinations: straight from the device.  Images packed
+      // back to back both here and in the destination (a batch tensor) go as
+      // one copy; strided ones as 2-D copies.
+      for (int32_t i = chunks[k].first; i < chunks[k].second;) {
+        const Stage& s = st[i];
+        if (!s.dst_pinned || s.dst_dev) {
+          i++;
+          continue;
+        }
+        const int64_t bytes_i = s.out_row * images[i].crop_h;
+        if (images[i].dst_stride != s.out_row) {
+          MXD_HIP(hipMemcpy2DAsync(images[i].dst, images[i].dst_stride, sl.dev_out + s.out_off, s.out_row, s.out_row,
+                                   images[i].crop_h, hipMemcpyDeviceToHost, sl.stream));
+          i++;
+          continue;
+        }
+        int32_t j = i + 1;
+        int64_t run = bytes_i;
+        while (j < chunks[k].second && st[j].dst_pinned && images[j].dst_stride == st[j].out_row &&
+               static_cast<uint8_t*>(images[j].dst) == static_cast<uint8_t*>(images[i].dst) + run &&
+               st[j].out_off == s.out_off + run) {
+          run += st[j].out_row * images[j].crop_h;
+          j++;
+        }
+        MXD_HIP(hipMemcpyAsync(images[i].dst, sl.dev_out + s.out_off, run, hipMemcpyDeviceToHost, sl.stream));
+        i = j;
+      }
+    }
+    MXD_HIP(hipEventRecord(sl.done, sl.stream));
+    pending[k & 1] = k;
+    // results of the previous chunk, while this one runs
+    const int prev = pending[(k + 1) & 1];
+    if (prev >= 0)
+      if (int rc = copy_out(prev)) return rc;
+  }
+  for (int k = 0; k < 2; k++)
+    if (pending[k] >= 0)
+      if (int rc = copy_out(pending[k])) return rc;
+  return MXD_OK;
+}
+int jpeg_path(const mxd_jpeg_image* jimg, int32_t n, int32_t out_dtype, int32_t device, bool dst_device) {
+  if (n < 0 || (n > 0 && !jimg)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  std::vector<mxd_image> imgs(n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_jpeg_image& j = jimg[i];
+    const std::string at = " (image " + std::to_string(i) + ")";
+    if (!j.coefs) return fail(MXD_ERR_INVALID, "mxd: null coefs" + at);
+    const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(j.coefs));
+    if (!info.device_ok)
+      return fail(MXD_ERR_UNSUPPORTED, "mxd: CMYK / YCCK JPEGs finish on the host (mxd_jpeg_coefs_finish)" + at);
+    if (j.win_w <= 0 || j.win_h <= 0)
+      return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
+    if (j.win_x < 0 || j.win_y < 0 || (int64_t)j.win_x + j.win_w > info.width ||
+        (int64_t)j.win_y + j.win_h > info.height)
+      return fail(MXD_ERR_INVALID, "mxd: source window outside the image" + at);
+    mxd_image& m = imgs[i];
+    m.src = reinterpret_cast<const uint8_t*>(j.coefs);  // validated, never read: host_path decodes the coefficients
+    m.src_stride = (int64_t)j.win_w * 3;
+    m.src_w = j.win_w;
+    m.src_h = j.win_h;
+    m.channels = 3;
+    m.resize_w = j.resize_w;
+    m.resize_h = j.resize_h;
+    m.crop_x = j.crop_x;
+    m.crop_y = j.crop_y;
+    m.crop_w = j.crop_w;
+    m.crop_h = j.crop_h;
+    m.flip = j.flip;
+    m.dst = j.dst;
+    m.dst_stride = j.dst_stride;
+  }
+  return host_path(imgs.data(), n, out_dtype, device, dst_device, jimg);
+}
+
+void host_trim() { host_pool().trim(); }
+
+// Pixel maps of host images through a borrowed context (mxd_pixmap_host).
+int pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device) {
+  if (n < 0 || (n > 0 && !images)) return fail(MXD_ERR_INVALID, "mxd: bad image array");
+  if (n == 0) return MXD_OK;
+  for (int32_t i = 0; i < n; i++)
+    if (int rc = pix_validate(images[i], op, i)) return rc;
+  if (int rc = check_device(device)) return rc;
+  DeviceGuard g(device);
+  CtxLease lease(device);
+  Slot& ctx = lease.ctx->slot[0];
+  if (int rc = init_slot(ctx)) return rc;
+  std::vector<size_t> in_off(n), out_off(n);
+  std::vector<int64_t> in_pitch(n), out_pitch(n);
+  size_t in_bytes = 0, out_bytes = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_pixmap& im = images[i];
+    const int64_t oc = op == MXD_AFFINE ? im.channels : 1;
+    in_pitch[i] = ((int64_t)im.src_w * im.channels + 15) & ~(int64_t)15;
+    out_pitch[i] = ((int64_t)im.dst_w * oc + 15) & ~(int64_t)15;
+    in_off[i] = in_bytes;
+    in_bytes += ((size_t)in_pitch[i] * im.src_h + 255) & ~(size_t)255;
+    out_off[i] = out_bytes;
+    out_bytes += ((size_t)out_pitch[i] * im.dst_h + 255) & ~(size_t)255;
+  }
+  if (int rc = grow_pinned(&ctx.pin_in, &ctx.pin_in_cap, in_bytes)) return rc;
+  if (int rc = grow_pinned(&ctx.pin_out, &ctx.pin_out_cap, out_bytes)) return rc;
+  if (int rc = grow_device(&ctx.dev_in, &ctx.dev_in_cap, in_bytes)) return rc;
+  if (int rc = grow_device(&ctx.dev_out, &ctx.dev_out_cap, out_bytes)) return rc;
+  std::vector<mxd_pixmap> dev_imgs(images, images + n);
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_pixmap& im = images[i];
+    const size_t row = (size_t)im.src_w * im.channels;
+    uint8_t* stage = ctx.pin_in + in_off[i];
+    for (int32_t r = 0; r < im.src_h; r++)
+      std::memcpy(stage + (size_t)r * in_pitch[i], im.src + (size_t)r * im.src_stride, row);
+    dev_imgs[i].src = ctx.dev_in + in_off[i];
+    dev_imgs[i].src_stride = in_pitch[i];
+    dev_imgs[i].dst = ctx.dev_out + out_off[i];
+    dev_imgs[i].dst_stride = out_pitch[i];
+  }
+  MXD_HIP(hipMemcpyAsync(ctx.dev_in, ctx.pin_in, in_bytes, hipMemcpyHostToDevice, ctx.stream));
+  if (int rc = run_pixmap(dev_imgs.data(), n, op, device, ctx.stream)) return rc;
+  MXD_HIP(hipMemcpyAsync(ctx.pin_out, ctx.dev_out, out_bytes, hipMemcpyDeviceToHost, ctx.stream));
+  MXD_HIP(hipStreamSynchronize(ctx.stream));
+  for (int32_t i = 0; i < n; i++) {
+    const mxd_pixmap& im = images[i];
+    const size_t row = (size_t)im.dst_w * (op == MXD_AFFINE ? im.channels : 1);
+    uint8_t* d = static_cast<uint8_t*>(im.dst);
+    const uint8_t* s = ctx.pin_out + out_off[i];
+    for (int32_t r = 0; r < im.dst_h; r++) std::memcpy(d + (size_t)r * im.dst_stride, s + (size_t)r * out_pitch[i], row);
+  }
+  return MXD_OK;
+}
+
+
+}  // namespace capi
+}  // namespace mxd

@@ -138,6 +138,8 @@ void build_huff(Huff& h, const uint8_t* bits /* [17], bits[0] unused */, const u
   h.present = true;
 }
 
+inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v + ((-1) << s) + 1 : v; }
+
 // Entropy-coded segment reader: stops at a marker; bits needed past it are
 // zeros and set `insufficient` (jdhuff.c jpeg_fill_bit_buffer).
 struct Bits {
@@ -231,6 +233,103 @@ struct Bits {
     consume(l);
     return h.vals[(code + h.valoffset[l]) & 0xff];
   }
+  // Codes longer than the lookahead (and short ones whose value bits did not
+  // fit the AC fast table), on a bit buffer held by the caller.
+  static int decode_slow(const Huff& h, uint64_t& b, int& n) {
+    const int e = h.look[b >> (64 - kLook)];
+    if (e) {
+      b <<= e >> 8;
+      n -= e >> 8;
+      return e & 0xff;
+    }
+    int l = kLook + 1;
+    int32_t code = (int32_t)(b >> (64 - l));
+    while (code > h.maxcode[l]) {
+      if (++l > 16) {
+        // jdhuff.c jpeg_huff_decode: corrupt data, return a zero
+        b <<= 16;
+        n -= 16;
+        return 0;
+      }
+      code = (int32_t)(b >> (64 - l));
+    }
+    b <<= l;
+    n -= l;
+    return h.vals[(code + h.valoffset[l]) & 0xff];
+  }
+
+  // One block of a sequential scan (DC difference + AC run/levels, into blk,
+  // which the caller zeroed), with the bit buffer in registers: refilled to
+  // >= 57 bits whenever fewer than 32 remain (a symbol and its value bits
+  // take <= 27), 8 bytes at a time where they hold no 0xFF.  Bits past the
+  // end of the segment are zeros and mark the data insufficient, as in
+  // consume(); the flag is only read between MCUs.
+  void block_seq(const Huff& hd, const Huff& ha, int& pred, int16_t* blk) {
+    uint64_t b = buf;
+    int n = cnt;
+    auto refill = [&]() {
+      if (!at_marker && end - p >= 8 && n >= 0) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        const uint64_t x = ~w;
+        if (((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) == 0) {
+          const int k = (64 - n) >> 3;
+          b |= (__builtin_bswap64(w) >> (64 - 8 * k)) << (64 - n - 8 * k);
+          p += k;
+          n += 8 * k;
+          return;
+        }
+      }
+      if (n < 0) return;  // past the end: only zeros follow
+      buf = b;
+      cnt = n;
+      fill();
+      b = buf;
+      n = cnt;
+    };
+    if (n < 32) refill();
+    int s = decode_slow(hd, b, n);
+    if (s) {
+      const int v = (int)(b >> (64 - s));
+      b <<= s;
+      n -= s;
+      s = extend(v, s);
+    }
+    pred += s;
+    blk[0] = (int16_t)pred;
+    for (int k = 1; k < 64; k++) {
+      if (n < 32) refill();
+      const FastAC f = ha.fac[b >> (64 - kLook)];
+      if (f.len) {
+        b <<= f.len;
+        n -= f.len;
+        if (f.run == kEob) break;
+        k += f.run;
+        blk[kNatural[k]] = f.val;
+        continue;
+      }
+      const int rs = decode_slow(ha, b, n);
+      const int r = rs >> 4, sz = rs & 15;
+      if (sz) {
+        k += r;
+        const int v = (int)(b >> (64 - sz));
+        b <<= sz;
+        n -= sz;
+        blk[kNatural[k]] = (int16_t)extend(v, sz);
+      } else {
+        if (r != 15) break;
+        k += 15;
+      }
+    }
+    if (n < 0) {
+      insufficient = true;
+      n = 0;
+      b = 0;
+    }
+    buf = b;
+    cnt = n;
+  }
+
   // Next marker from p: p at its 0xFF, returns its code; 0xD9 (EOI) at the
   // end of the data, as libjpeg's sources insert a fake EOI there.
   int find_marker() {
@@ -275,7 +374,6 @@ struct Bits {
   }
 };
 
-inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v + ((-1) << s) + 1 : v; }
 
 // ---------------------------------------------------------------- IDCT
 constexpr int kConstBits = 13;
@@ -770,38 +868,10 @@ struct Decoder {
       }
       int16_t local[64];
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
+        // deferred blocks are zero from the allocation (each is written once)
         int16_t* blk = defer ? cblk(c, bx, by) : local;
-        std::memset(blk, 0, 64 * sizeof(int16_t));
-        if (!skip) {
-          const Huff& hd = dc[c.dc_tbl];
-          const Huff& ha = ac[c.ac_tbl];
-          int s = bits.decode(hd);
-          if (s) s = extend(bits.get(s), s);
-          s += c.dc_pred;
-          c.dc_pred = s;
-          blk[0] = (int16_t)s;
-          for (int k = 1; k < 64; k++) {
-            if (bits.cnt < 16) bits.fill();
-            const FastAC f = ha.fac[bits.peek(kLook)];
-            if (f.len) {
-              bits.consume(f.len);
-              if (f.run == kEob) break;
-              k += f.run;
-              blk[kNatural[k]] = f.val;
-              continue;
-            }
-            int rs = bits.decode(ha);
-            const int r = rs >> 4;
-            s = rs & 15;
-            if (s) {
-              k += r;
-              blk[kNatural[k]] = (int16_t)extend(bits.get(s), s);
-            } else {
-              if (r != 15) break;
-              k += 15;
-            }
-          }
-        }
+        if (!defer) std::memset(blk, 0, 64 * sizeof(int16_t));
+        if (!skip) bits.block_seq(dc[c.dc_tbl], ac[c.ac_tbl], c.dc_pred, blk);
         if (!defer) idct_block(blk, c.q, c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
       });
       return;

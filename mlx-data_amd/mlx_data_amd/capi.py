@@ -51,6 +51,7 @@ MXD_POLICY_PREFER_BAND = 256
 MXD_TUNE_BAND_ROWS = 0
 MXD_TUNE_BAND_LA = 1
 MXD_TUNE_BAND_GRID = 2
+MXD_TUNE_DESC = 3
 
 
 class MxdImage(ctypes.Structure):

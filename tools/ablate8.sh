@@ -24,7 +24,7 @@ if [ "$1" = build ]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
       ${FLAGS[$m]} -c csrc/wave.hip -o build/wave_abl$m.o || exit 1
     /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave_abl$m.o build/pixmap.o \
-      build/capi.o build/taps.o build/jpeg.o -o ../tools/abl/libmxd_amd_$m.so || exit 1
+      build/capi.o build/plan.o build/batch.o build/hostpath.o build/taps.o build/jpeg.o -o ../tools/abl/libmxd_amd_$m.so || exit 1
   done
   exit 0
 fi

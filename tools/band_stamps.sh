@@ -9,7 +9,7 @@ if [ "$1" = build ]; then
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
     -DMXD_BAND_STAMPS=1 ${STAMP_FLAGS:-} -c csrc/band.hip -o build/band_stamps.o || exit 1
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave.o build/band_stamps.o \
-    build/band_plan.o build/pixmap.o build/capi.o build/taps.o build/jpeg.o build/jpegdev.o \
+    build/band_plan.o build/pixmap.o build/capi.o build/plan.o build/batch.o build/hostpath.o build/taps.o build/jpeg.o build/jpegdev.o \
     -o ../tools/libmxd_amd_bstamps.so || exit 1
   exit 0
 fi

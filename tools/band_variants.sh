@@ -11,7 +11,7 @@ if [ "$1" = build ]; then
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
     $3 -c csrc/band.hip -o build/band_$NAME.o || exit 1
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave.o build/band_$NAME.o \
-    build/band_plan.o build/pixmap.o build/capi.o build/taps.o build/jpeg.o build/jpegdev.o \
+    build/band_plan.o build/pixmap.o build/capi.o build/plan.o build/batch.o build/hostpath.o build/taps.o build/jpeg.o build/jpegdev.o \
     -o ../tools/libmxd_amd_band_$NAME.so || exit 1
   exit 0
 fi

@@ -20,6 +20,8 @@ Variants per worker count:
 Datasets (synthetic stand-ins, seeded smooth noise, Pillow q=90 JPEGs):
   c1  300x200 / 200x300 (Caltech-101-like), batch 32
   c4  500x375 / 375x500 / 500x333 (ImageNet-like), batch 128
+Each surface point iterates the file list as many times as it takes to run
+>= --min-seconds (default 5 s) with >= --min-batches (16) batches per worker.
 Prints one JSON line per (dataset, variant, workers)."""
 import argparse
 import ctypes
@@ -66,7 +68,7 @@ def make_files(root, name, n):
     return files
 
 
-def run_surface(files, batch, workers, variant):
+def run_surface(files, batch, workers, variant, repeat=1):
     from mlx_data_amd import data as dx
 
     hostdec = variant.endswith("_hostdec")
@@ -74,13 +76,13 @@ def run_surface(files, batch, workers, variant):
     prev = dx.device_decode()
     dx.set_device_decode(not hostdec)
     try:
-        return _run_surface(dx, files, batch, workers, variant)
+        return _run_surface(dx, files, batch, workers, variant, repeat)
     finally:
         dx.set_device_decode(prev)
 
 
-def _run_surface(dx, files, batch, workers, variant):
-    samples = [dict(image=f.encode("ascii"), label=i) for i, f in enumerate(files)]
+def _run_surface(dx, files, batch, workers, variant, repeat=1):
+    samples = [dict(image=f.encode("ascii"), label=i) for i, f in enumerate(files)] * repeat
     d = (dx.buffer_from_vector(samples).shuffle().to_stream().load_image("image")
          .image_resize_smallest_side("image", 256).image_center_crop("image", 224, 224))
     if variant == "ref_form":
@@ -144,6 +146,8 @@ def main():
     ap.add_argument("--workers", default="1,8,16")
     ap.add_argument("--variants", default="ref_form,fused,device,cpu")
     ap.add_argument("--cpu-images", type=int, default=512, help="files the CPU restatement runs over")
+    ap.add_argument("--min-seconds", type=float, default=5.0, help="least duration of a timed surface run")
+    ap.add_argument("--min-batches", type=int, default=16, help="least batches per worker of a timed surface run")
     args = ap.parse_args()
     workers = [int(w) for w in args.workers.split(",")]
     variants = args.variants.split(",")
@@ -159,9 +163,13 @@ def main():
                         n, dt = run_cpu(fl[:args.cpu_images], B, w)
                     else:
                         # warm-up with every worker busy twice over: tap tables, host-path
-                        # contexts and the recycled batch buffers reach their steady state
-                        run_surface(fl[:min(len(fl), 2 * B * w)], B, w, v)
-                        n, dt = run_surface(fl, B, w, v)
+                        # contexts and the recycled batch buffers reach their steady state;
+                        # its rate sizes the timed run: the file list repeated until the run
+                        # lasts >= --min-seconds and gives every worker >= --min-batches
+                        nw, tw = run_surface(fl[:min(len(fl), 2 * B * w)], B, w, v)
+                        want = max(args.min_seconds * nw / tw, args.min_batches * B * w)
+                        repeat = max(1, int(np.ceil(want / len(fl))))
+                        n, dt = run_surface(fl, B, w, v, repeat)
                     print(json.dumps(dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
                                           images_per_s=round(n / dt, 1), batch=B)), flush=True)
 

@@ -10,7 +10,7 @@ if [ "$1" = build ]; then
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
     -DMXD_STAMPS=1 ${STAMP_FLAGS:-} -c csrc/wave.hip -o build/wave_stamps.o || exit 1
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave_stamps.o build/pixmap.o \
-    build/capi.o build/taps.o build/jpeg.o build/jpegdev.o -o ../tools/libmxd_amd_stamps.so || exit 1
+    build/capi.o build/plan.o build/batch.o build/hostpath.o build/taps.o build/jpeg.o build/jpegdev.o -o ../tools/libmxd_amd_stamps.so || exit 1
   exit 0
 fi
 shift
