@@ -506,11 +506,16 @@ def main():
     wall, _ = timed_steps(ranks, step, sync_all, args.steps)
     # Per-launch kernel time for the roofline: the same launches back to back
     # on ONE stream, bracketed by HIP events on that stream (the kernel's own).
+    # host_ms: the submitting thread's time per call (planning, descriptor
+    # upload, launch); when it reaches the per-launch time the loop is
+    # host-bound.
     e0, e1 = capi.Event(), capi.Event()
     sync_all()
     e0.record(stream)
+    t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, 1)
+    host_ms = (time.perf_counter() - t0) * 1e3 / max(1, args.steps)
     e1.record(stream)
     stream.synchronize()
     kernel_ms = e0.elapsed_ms(e1) / args.steps
@@ -518,14 +523,16 @@ def main():
     # The same launches with descriptor caching off: every batch uploads its
     # descriptor array (what a batch of fresh pointers costs); reported, not
     # the headline.
-    fresh_ms = None
+    fresh_ms = fresh_host_ms = None
     if args.steps > 0:
         prev = capi.set_kernel_policy(args.policy | capi.MXD_POLICY_NO_DESC_CACHE)
         k = max(10, args.steps // 2)
         stream.synchronize()
         e0.record(stream)
+        t0 = time.perf_counter()
         for i in range(k):
             step(i, 1)
+        fresh_host_ms = (time.perf_counter() - t0) * 1e3 / k
         e1.record(stream)
         stream.synchronize()
         fresh_ms = e0.elapsed_ms(e1) / k
@@ -540,6 +547,8 @@ def main():
                 "kernel_ms_per_launch": round(kernel_ms, 5),
                 "sustained_gbs": round(alg_bytes / (wall / max(1, args.steps)) / 1e9, 1) if args.steps else None,
                 "ms_per_launch_fresh_descriptors": round(fresh_ms, 5) if fresh_ms else None,
+                "host_ms_per_call": round(host_ms, 5) if args.steps else None,
+                "host_ms_per_call_fresh": round(fresh_host_ms, 5) if fresh_host_ms else None,
                 "kernel": kernel_name(capi, sizes[0], geoms[0], f32, args.policy),
                 "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
                 "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None}

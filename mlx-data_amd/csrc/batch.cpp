@@ -70,20 +70,18 @@ int32_t strip_chunks(const DevTable& xt, int32_t crop_x, int32_t crop_w, int32_t
 }
 
 int validate(const mxd_image& im, int32_t i) {
-  const std::string at = " (image " + std::to_string(i) + ")";
-  if (!im.src || !im.dst) return fail(MXD_ERR_INVALID, "mxd: null src/dst pointer" + at);
-  if (im.src_w <= 0 || im.src_h <= 0)
-    return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
-  if (im.channels <= 0 || im.channels > 4)
-    return fail(MXD_ERR_INVALID, "verifyImage: channels must be 0 <= c <= 4" + at);
+  // the message is built only on failure (this runs for every image of every batch)
+  auto at = [i](const char* msg) { return fail(MXD_ERR_INVALID, std::string(msg) + " (image " + std::to_string(i) + ")"); };
+  if (!im.src || !im.dst) return at("mxd: null src/dst pointer");
+  if (im.src_w <= 0 || im.src_h <= 0) return at("image: cannot create image with 0 or negative dimension");
+  if (im.channels <= 0 || im.channels > 4) return at("verifyImage: channels must be 0 <= c <= 4");
   if (im.resize_w <= 0 || im.resize_h <= 0 || im.crop_w <= 0 || im.crop_h <= 0)
-    return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
+    return at("image: cannot create image with 0 or negative dimension");
   if (im.crop_x < 0 || im.crop_y < 0 || im.crop_x >= im.resize_w || im.crop_y >= im.resize_h)
-    return fail(MXD_ERR_INVALID, "Array: sub: offset out of bound" + at);
+    return at("Array: sub: offset out of bound");
   if (im.crop_x + im.crop_w > im.resize_w || im.crop_y + im.crop_h > im.resize_h)
-    return fail(MXD_ERR_INVALID, "Array: sub: shape out of bound" + at);
-  if (im.src_stride < (int64_t)im.src_w * im.channels)
-    return fail(MXD_ERR_INVALID, "mxd: src_stride smaller than a row" + at);
+    return at("Array: sub: shape out of bound");
+  if (im.src_stride < (int64_t)im.src_w * im.channels) return at("mxd: src_stride smaller than a row");
   return MXD_OK;
 }
 

@@ -359,6 +359,25 @@ void plan_band(const mxd_image& im, const Stored& st, int32_t f32, ImgPlan& p) {
   p.band = p.bp.ok;
 }
 
+constexpr int32_t kMaxScatterDepth = 16;  // deepest scatter schedule (wave.hip select_scatter)
+
+// The scatter kernel for a vertical shape: the smallest instantiated tap
+// bucket >= xw and schedule depth >= sh.dmax (a deeper schedule runs the same
+// rows with bubble iterations, so any downscale ratio up to 16:1 reaches a
+// kernel instead of the general path).
+bool scatter_kernel_for(int32_t c, int32_t f32, int32_t xw, const ScatterShape& sh, int32_t q, int32_t shift,
+                        int32_t pp, int32_t* taps, int32_t* dmax) {
+  if (sh.s <= 0) return false;
+  for (int32_t t = mxd::wave_taps_bucket(xw); t > 0; t = mxd::wave_taps_bucket(t + 1))
+    for (int32_t d = sh.dmax; d <= kMaxScatterDepth; d++)
+      if (mxd::wave_has_kernel(mxd::WaveCfg{c, f32, t, 0, 0, 2, sh.s, d, q, shift, pp})) {
+        *taps = t;
+        *dmax = d;
+        return true;
+      }
+  return false;
+}
+
 // Chooses the wave kernel of one image (p.wave = false: the general kernel):
 // over the lane widths available for its channel count, the one that cuts
 // the crop into the fewest strips (narrow strips read more halo and more,
@@ -372,7 +391,6 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
   // else gather.
   const ScatterShape sh =
       (g_policy.load() & MXD_POLICY_NO_SCATTER) ? ScatterShape{} : scatter_shape(*p.yt, im.crop_y, im.crop_h);
-  const int32_t xb = mxd::wave_taps_bucket(p.xt->width);
   const int32_t gb = mxd::wave_taps_bucket(std::max(p.xt->width, p.yt->width));
   const int32_t dp = mxd::wave_default_p(c);
   const int32_t policy = g_policy.load();
@@ -388,12 +406,12 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
     cand.q = q;
     cand.pp = pp;
     cand.shift = shift;
-    if (sh.s > 0 && xb > 0 &&
-        mxd::wave_has_kernel(mxd::WaveCfg{c, f32, xb, 0, 0, 2, sh.s, sh.dmax, q, shift, pp})) {
+    int32_t tb = 0, td = 0;
+    if (scatter_kernel_for(c, f32, p.xt->width, sh, q, shift, pp, &tb, &td)) {
       cand.kind = 2;
-      cand.bucket = xb;
+      cand.bucket = tb;
       cand.s = sh.s;
-      cand.dmax = sh.dmax;
+      cand.dmax = td;
       cand.p = sh.p;
     } else if (gb > 0 && mxd::wave_has_kernel(mxd::WaveCfg{c, f32, gb, 0, 0, 0, 0, 0, q, shift, pp})) {
       cand.kind = 0;
@@ -409,11 +427,11 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
   // output pixels per lane (measured: 720p -> 224 with two strips 4 % faster;
   // with more strips -- their narrower 341-pixel window -- or a single 224-column
   // strip (C4) pixel lanes were 2-10 % faster; profiles/r02/bytes_ab.txt).
-  if (c == 3 && sh.s > 0 && xb > 0 && !(policy & (MXD_POLICY_NO_BYTES | MXD_POLICY_NARROW))) {
-    int32_t ns = 0, tx = 0, q = 0;
+  if (c == 3 && sh.s > 0 && !(policy & (MXD_POLICY_NO_BYTES | MXD_POLICY_NARROW))) {
+    int32_t ns = 0, tx = 0, q = 0, bt = 0, bd = 0;
     if (wave_strips_bytes(*p.xt, im, st, &ns, &tx, &q) &&
         ((policy & MXD_POLICY_BYTES) || !p.wave || p.kind != 2 || (ns <= p.nstrips && q <= 2)) &&
-        mxd::wave_has_kernel(mxd::WaveCfg{c, f32, xb, 0, 0, 2, sh.s, sh.dmax, q, 0, 16})) {
+        scatter_kernel_for(c, f32, p.xt->width, sh, q, 0, 16, &bt, &bd)) {
       p.wave = true;
       p.nstrips = ns;
       p.tx = tx;
@@ -421,9 +439,9 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
       p.pp = 16;
       p.shift = 0;
       p.kind = 2;
-      p.bucket = xb;
+      p.bucket = bt;
       p.s = sh.s;
-      p.dmax = sh.dmax;
+      p.dmax = bd;
       p.p = sh.p;
     }
   }

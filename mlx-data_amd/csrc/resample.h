@@ -8,11 +8,11 @@ namespace mxd {
 
 // One entry of a per-axis tap table in device memory: the first input index
 // and tap count stored as int bits, then `width` f32 weights, zero padded to
-// at least kMinTabWidth so the wave kernel can read T <= kMinTabWidth
-// weights of any entry unconditionally (wave.hip reads up to 17, band.hip
-// up to its largest class, 25).
+// at least kMinTabWidth so the wave and band kernels can read T <=
+// kMinTabWidth weights of any entry unconditionally (both read up to their
+// largest tap bucket / class, 32).
 constexpr int kTapHeader = 2;
-constexpr int kMinTabWidth = 26;
+constexpr int kMinTabWidth = 32;
 
 // Per-image parameters, resolved by the host (geometry already validated).
 // Each image is cut into nbands x nstrips tiles of ty output rows x tx output
@@ -76,8 +76,16 @@ constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; 
 #ifndef MXD_RING
 #define MXD_RING 6
 #endif
+// Past DMAX 9 (large downscale ratios) a ring of DMAX slots would hold 12-16
+// rows of registers: the ring is the smallest size in [MXD_RING, 2 MXD_RING]
+// that divides two groups (the block then stays S = 2 groups long).
 constexpr int scatter_ring_slots(int dmax) {
-  return MXD_RING % dmax == 0 ? MXD_RING : (2 * dmax <= MXD_RING ? 2 * dmax : dmax);
+  if (MXD_RING % dmax == 0) return MXD_RING;
+  if (2 * dmax <= MXD_RING) return 2 * dmax;
+  if (dmax > 9)
+    for (int r = MXD_RING; r <= 2 * MXD_RING; r++)
+      if ((2 * dmax) % r == 0) return r;
+  return dmax;
 }
 constexpr int scatter_block_groups(int s, int dmax) {
   return scatter_ring_slots(dmax) / scatter_gcd(scatter_ring_slots(dmax), s * dmax) * s;

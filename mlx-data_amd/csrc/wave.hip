@@ -646,6 +646,10 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   MXD_SCATTER(2, 2, 3, 2, 4)    // 375 / 333 -> 256 (C4)
   MXD_SCATTER(2, 2, 3, 4, 8)
   MXD_SCATTER(3, 1, 2, 4, 4)    // upsampling (200 -> 256)
+  MXD_SCATTER(2, 12, 24, 1, 8)  // 8.5..12:1 (12 MP -> 256, C6)
+  MXD_SCATTER(2, 12, 24, 1, 4)
+  MXD_SCATTER(2, 16, 32, 1, 8)  // 12..16:1 (24 MP -> 256, C7)
+  MXD_SCATTER(2, 16, 32, 1, 4)
   // byte lanes: 1 KiB windows (341 RGB pixels) per strip row
   MXD_SCATTER_B(2, 4, 8, 2)     // 960 -> 256 (C2: 3 strips of 75)
   MXD_SCATTER_B(2, 4, 8, 1)
@@ -688,7 +692,7 @@ constexpr int plane_floats() {
 }  // namespace
 
 int wave_taps_bucket(int taps) {
-  static const int kB[] = {2, 3, 4, 6, 8, 10, 12, 17};
+  static const int kB[] = {2, 3, 4, 6, 8, 10, 12, 17, 24, 32};
   for (int b : kB)
     if (taps <= b) return b;
   return -1;

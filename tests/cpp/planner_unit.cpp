@@ -76,7 +76,8 @@ static void test_band_rows() {
     }
 }
 
-// plan_wave: C2 takes a scatter wave kernel; a 12 MP photo has no wave bucket.
+// plan_wave: C2 takes a scatter wave kernel; a 12 MP photo takes the 24-tap
+// bucket with a depth-12 schedule, a 48 MP one (31:1) none.
 static void test_plan_wave() {
   const mxd_image c2 = center(1280, 960, 256, 224, true);
   ImgPlan p = plan(c2);
@@ -88,7 +89,11 @@ static void test_plan_wave() {
   const mxd_image big = center(4032, 3024, 256, 224, true);
   ImgPlan q = plan(big);
   plan_wave(big, whole(big), 1, MXD_F32_DIV255, q);
-  CHECK(!q.wave);
+  CHECK(q.wave && q.kind == 2 && q.bucket == 24 && q.dmax == 12 && q.s == 2);
+  const mxd_image huge = center(8000, 6000, 256, 224, true);
+  ImgPlan h = plan(huge);
+  plan_wave(huge, whole(huge), 1, MXD_F32_DIV255, h);
+  CHECK(!h.wave);
   // an odd row stride leaves the wave kernels (4-byte aligned rows only)
   mxd_image odd = c2;
   odd.src_stride = 1280 * 3 + 1;

@@ -145,3 +145,25 @@ def test_byte_lanes_stay_inside_the_row():
     assert p["wave"] == 1 and p["p"] != 16
     # the same crop with 16-byte padded rows fits
     assert _plan(dict(right, src_stride=1504), forced)["p"] == 16
+
+
+def test_every_downscale_ratio_up_to_16_has_a_wave_kernel():
+    """No cliff to the general kernel: RGB
+    resize_smallest_side 256 -> center_crop 224 from every smaller side 257 ..
+    4096 (up to 16:1) plans a wave scatter kernel whose tap bucket covers the
+    horizontal taps and whose schedule depth covers the vertical shape (a
+    deeper schedule runs bubble iterations); 12 MP and 24 MP photos take the
+    24 / 32-tap buckets."""
+    for side in list(range(257, 1200, 7)) + list(range(1200, 4097, 53)):
+        w = side * 4 // 3
+        rw, rh = capi.resize_smallest_side_dims(w, side, 256)
+        cx, cy = capi.center_crop_origin(rw, rh, 224, 224)
+        e = _entry(w, side, (w * 3 + 15) // 16 * 16, rw, rh, cx=cx, cy=cy)
+        p = _plan(e)
+        first, cnt, _ = capi.axis_taps(w, rw)
+        assert p["wave"] == 1 and p["kind"] == 2, (side, p)
+        assert p["taps"] >= cnt.max(), (side, p)
+    p = _plan(_entry(4032, 3024, 4032 * 3, 341, 256, cx=58, cy=16))
+    assert (p["taps"], p["dmax"], p["p"], p["nstrips"]) == (24, 12, 8, 6)
+    p = _plan(_entry(6000, 4000, 6000 * 3, 384, 256, cx=80, cy=16))
+    assert (p["taps"], p["dmax"]) == (32, 16)

@@ -136,18 +136,21 @@ def test_tuning_knobs_keep_bytes(rows, la, grid):
 def test_large_downscale(h, w):
     """12 MP, 24 MP and 48 MP photos -> 256 -> 224 (11.8:1 .. 31:1; 24 .. 64
     taps per axis; an output row's new source rows span several groups):
-    band kernel against the general kernel (the wave kernels have no bucket
-    above 17) and the kernel-order oracle, bit for bit."""
+    the default choice (the wave kernels' 24 / 32-tap scatter buckets up to
+    16:1), the band kernel, the wave kernels at both lane widths and the
+    general kernel against the kernel-order oracle, bit for bit."""
     img = synth(h, w, 3, 11)
     g = center_geom(img)
     if max(h, w) <= 6000:
         _assert_band_planned([img], [g], True)
-    band = run_device([img], [g], f32=True)[0]
-    gen = _with(capi.MXD_POLICY_NO_WAVE, lambda: run_device([img], [g], f32=True))[0]
-    assert np.array_equal(band.view(np.uint32), gen.view(np.uint32))
-    want = O.resize_crop_vfirst(img, g)
+        p = capi.describe_plan(_entry(img, g, True), capi.MXD_F32_DIV255)
+        assert p["wave"] == 1 and p["kind"] == 2, p
     lut = (np.arange(256, dtype=np.uint8).astype("float32") / 255).view(np.uint32)
-    assert np.array_equal(band.view(np.uint32), lut[want])
+    want = lut[O.resize_crop_vfirst(img, g)]
+    for pol in (capi.MXD_POLICY_AUTO, capi.MXD_POLICY_PREFER_BAND, capi.MXD_POLICY_NO_BAND,
+                capi.MXD_POLICY_NARROW, capi.MXD_POLICY_NO_WAVE):
+        got = _with(pol, lambda: run_device([img], [g], f32=True))[0]
+        assert np.array_equal(got.view(np.uint32), want), pol
 
 
 def test_constant_frames_exact():

@@ -10,7 +10,8 @@ Full-size workloads: C2 (1280x960 -> 256 -> 224), C3's six sizes, C4's
 ImageNet shapes, C5 (4K -> 512, random 448 crops, mirrored), Caltech
 upsampling, arbitrary windows and 12 / 24 MP photos; each on the default
 choice, the band kernel (MXD_POLICY_PREFER_BAND), the wave kernels
-(MXD_POLICY_NO_BAND) and the general kernel (MXD_POLICY_NO_WAVE)."""
+(MXD_POLICY_NO_BAND), the 256-pixel-window wave kernels (MXD_POLICY_NARROW)
+and the general kernel (MXD_POLICY_NO_WAVE)."""
 import numpy as np
 import pytest
 
@@ -21,7 +22,8 @@ from mlx_data_amd import capi
 pytestmark = pytest.mark.gpu
 
 POLICIES = [("default", capi.MXD_POLICY_AUTO), ("band", capi.MXD_POLICY_PREFER_BAND),
-            ("wave", capi.MXD_POLICY_NO_BAND), ("general", capi.MXD_POLICY_NO_WAVE)]
+            ("wave", capi.MXD_POLICY_NO_BAND), ("narrow", capi.MXD_POLICY_NARROW),
+            ("general", capi.MXD_POLICY_NO_WAVE)]
 
 
 def _cases():
