@@ -160,7 +160,8 @@ int mxd_set_kernel_policy(int32_t policy);
  * at once, each running a stream of units; 1: one per unit; n > 1: n);
  * MXD_TUNE_DESC: how a batch's new descriptor array reaches the kernels (1:
  * copy stream + cross-stream wait; 2: copy on the launch stream; 3: kernels
- * read the page-locked slot in place; 4: as 3, non-coherent allocation). */
+ * read the page-locked slot in place; 4 (the default): as 3, non-coherent
+ * allocation). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,

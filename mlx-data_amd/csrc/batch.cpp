@@ -153,10 +153,15 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   }
   std::memcpy(c.host, descs.data(), bytes);
   c.count = n;
-  // Upload modes (MXD_TUNE_DESC; measurements): 1 = copy stream + cross-stream
-  // wait, 2 = copy on the launch stream, 3 / 4 = the kernels read the pinned
-  // slot in place (coherent / non-coherent allocation).
-  const int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 1;
+  // Upload modes (MXD_TUNE_DESC): 1 = copy stream + cross-stream wait, 2 =
+  // copy on the launch stream, 3 / 4 = the kernels read the pinned slot in
+  // place (coherent / non-coherent allocation).  Default 4: no copy and no
+  // cross-stream wait; the first wave of each XCD to read a line brings it
+  // over PCIe into that XCD's L2 (kernel-start acquires invalidate the lines
+  // of a previous use of the slot).  Fresh batches cost C2 +3.9 % / C4 +5 %
+  // over cached descriptors, against +6.5 % / +31 % with mode 1
+  // (profiles/r03/desc_host.jsonl).
+  const int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 4;
   if (mode >= 3) {
     const bool nc = mode == 4;
     if (!c.zc || c.zc_nc != nc || n > c.cap) {

@@ -79,7 +79,12 @@ constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; 
 // Past DMAX 9 (large downscale ratios) a ring of DMAX slots would hold 12-16
 // rows of registers: the ring is the smallest size in [MXD_RING, 2 MXD_RING]
 // that divides two groups (the block then stays S = 2 groups long).
+// Tuning builds: -DMXD_RING_FIXED=<n> uses n slots at every DMAX >= 2.
+#ifndef MXD_RING_FIXED
+#define MXD_RING_FIXED 0
+#endif
 constexpr int scatter_ring_slots(int dmax) {
+  if (MXD_RING_FIXED > 0 && dmax >= 2) return MXD_RING_FIXED;
   if (MXD_RING % dmax == 0) return MXD_RING;
   if (2 * dmax <= MXD_RING) return 2 * dmax;
   if (dmax > 9)

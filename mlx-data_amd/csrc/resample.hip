@@ -19,10 +19,12 @@
 //            or the exact f32 q/255.0f with 16-byte (f32) / 4-byte (u8) stores.
 // Arithmetic is in byte units (v = sum w*p), f32 accumulation with FMA.
 // 4 channels with ALPHA (stb_image_resize2's STBIR_RGBA, the layout
-// core::image::resize passes for c = 4, ImageTransform.cpp:49-58): colours are
-// weighted by alpha (p * a / 255) before both passes and divided by the
-// filtered alpha (times 255) after them, unless that alpha is below
-// stbir's tiny threshold; alpha itself is filtered as is.
+// core::image::resize passes for c = 4, ImageTransform.cpp:49-58) follow
+// stbir's float operations instead: every byte decoded to [0, 1] (b * 1/255),
+// colours multiplied by their decoded alpha, both passes, colours multiplied
+// by 1 / filtered alpha unless that alpha is below stbir's tiny threshold,
+// then encoded as (uint8)trunc(clamp(v * 255 + 0.5)) with an unfused multiply
+// and add -- bit-exact to oracle/stbir_oracle.c orc_resize_crop_vfirst_rgba.
 // Workgroup ids are remapped so that tiles of the same image run on the same
 // XCD (blocks b, b+8, ... share an XCD): the vertical halo of adjacent bands
 // then hits that XCD's L2.
@@ -72,12 +74,18 @@ struct Chunk<16, ALPHA> {
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const float a = (float)(d[i] >> 24);
-      const float m = ALPHA ? a * kInv255 : 1.0f;
-      acc[4 * i + 0] = __builtin_fmaf(w, (float)(d[i] & 0xffu) * m, acc[4 * i + 0]);
-      acc[4 * i + 1] = __builtin_fmaf(w, (float)((d[i] >> 8) & 0xffu) * m, acc[4 * i + 1]);
-      acc[4 * i + 2] = __builtin_fmaf(w, (float)((d[i] >> 16) & 0xffu) * m, acc[4 * i + 2]);
-      acc[4 * i + 3] = __builtin_fmaf(w, a, acc[4 * i + 3]);
+      if constexpr (ALPHA) {
+        const float a = (float)(d[i] >> 24) * kInv255;
+        acc[4 * i + 0] = __builtin_fmaf(w, (float)(d[i] & 0xffu) * kInv255 * a, acc[4 * i + 0]);
+        acc[4 * i + 1] = __builtin_fmaf(w, (float)((d[i] >> 8) & 0xffu) * kInv255 * a, acc[4 * i + 1]);
+        acc[4 * i + 2] = __builtin_fmaf(w, (float)((d[i] >> 16) & 0xffu) * kInv255 * a, acc[4 * i + 2]);
+        acc[4 * i + 3] = __builtin_fmaf(w, a, acc[4 * i + 3]);
+      } else {
+        acc[4 * i + 0] = __builtin_fmaf(w, (float)(d[i] & 0xffu), acc[4 * i + 0]);
+        acc[4 * i + 1] = __builtin_fmaf(w, (float)((d[i] >> 8) & 0xffu), acc[4 * i + 1]);
+        acc[4 * i + 2] = __builtin_fmaf(w, (float)((d[i] >> 16) & 0xffu), acc[4 * i + 2]);
+        acc[4 * i + 3] = __builtin_fmaf(w, (float)(d[i] >> 24), acc[4 * i + 3]);
+      }
     }
   }
 };
@@ -88,7 +96,10 @@ struct Chunk<1, ALPHA> {
   float v;
   __device__ __forceinline__ void load(const uint8_t* p, int c = 3) {
     v = (float)*p;
-    if (ALPHA && c < 3) v *= (float)p[3 - c] * kInv255;
+    if constexpr (ALPHA) {
+      v = v * kInv255;
+      if (c < 3) v = v * ((float)p[3 - c] * kInv255);
+    }
   }
   __device__ __forceinline__ void fma_into(float* acc, float w) const { acc[0] = __builtin_fmaf(w, v, acc[0]); }
 };
@@ -240,14 +251,20 @@ __global__ __launch_bounds__(kThreads) void resample_tiles(const ImgDev* __restr
       }
       if constexpr (ALPHA) {
         // the thread's 4 elements are one RGBA pixel (tiles start on a pixel)
-        if (res[3] * kInv255 >= kTinyAlpha) {
-          const float ia = 255.0f / res[3];
+        if (res[3] >= kTinyAlpha) {
+          const float ia = 1.0f / res[3];
 #pragma unroll
-          for (int j = 0; j < 3; j++) res[j] *= ia;
+          for (int j = 0; j < 3; j++) res[j] = res[j] * ia;
         }
-      }
+        {
+#pragma clang fp contract(off)  // v * 255, then + 0.5 (built with -ffp-contract=on: the pragma holds)
 #pragma unroll
-      for (int j = 0; j < 4; j++) res[j] = encode(res[j]);
+          for (int j = 0; j < 4; j++) res[j] = encode(res[j] * 255.0f);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) res[j] = encode(res[j]);
+      }
       const int64_t row = (int64_t)(oy + g) * im.dst_stride;
       const int o0 = tile.ox0 * C + 4 * q;
       if constexpr (F32) {

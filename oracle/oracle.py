@@ -79,7 +79,7 @@ def resize(img, dw, dh, rgba_weighted=None):
 
 def resize_crop_vfirst(img, g):
     """Kernel-order restatement (orc_resize_crop_vfirst): the geometry tuple
-    g = (rw, rh, cx, cy, cw, ch, flip) of a (H, W, C <= 3) uint8 image, summed
+    g = (rw, rh, cx, cy, cw, ch, flip) of a (H, W, C <= 4) uint8 image, summed
     vertical-first in byte units with fmaf chains in tap order -- what the HIP
     kernels must reproduce bit for bit."""
     rw, rh, cx, cy, cw, ch, flip = g
@@ -89,6 +89,21 @@ def resize_crop_vfirst(img, g):
     if lib().orc_resize_crop_vfirst(_ptr(img), w, h, c, ctypes.c_int64(w * c), _ptr(out), rw, rh, cx, cy, cw, ch,
                                     int(bool(flip))):
         raise ValueError("orc_resize_crop_vfirst failed")
+    return out
+
+
+def resize_crop_vfirst_rgba(img, g):
+    """Kernel-order restatement of the STBIR_RGBA form (orc_resize_crop_vfirst_rgba):
+    a (H, W, 4) uint8 image, decoded, alpha-weighted, vertical pass first, in
+    stbir's float operations -- what the general HIP kernel reproduces bit for bit."""
+    rw, rh, cx, cy, cw, ch, flip = g
+    img = np.ascontiguousarray(img)
+    h, w, c = img.shape
+    assert c == 4
+    out = np.empty((ch, cw, 4), np.uint8)
+    if lib().orc_resize_crop_vfirst_rgba(_ptr(img), w, h, ctypes.c_int64(w * 4), _ptr(out), rw, rh, cx, cy, cw, ch,
+                                         int(bool(flip))):
+        raise ValueError("orc_resize_crop_vfirst_rgba failed")
     return out
 
 

@@ -345,13 +345,14 @@ int orc_resize_u8(const uint8_t* src, int w, int h, int c, uint8_t* dst, int dw,
  * (uint8)trunc(clamp(v + 0.5, 0, 255)).  This is the order the HIP kernels
  * sum in (mlx-data_amd/csrc/band.hip, wave.hip), so they must match it bit for
  * bit; it differs from the stbir-order restatement above only by f32
- * rounding (+-1).  channels 1..3 (no alpha weighting).  Writes the crop
+ * rounding (+-1).  channels 1..4 (no alpha weighting; the STBIR_RGBA form is
+ * orc_resize_crop_vfirst_rgba below).  Writes the crop
  * window (cx, cy, cw, ch) of the (dw x dh) resize of the (w x h, row stride
  * `stride` bytes) source, mirrored when flip, as ch x cw x c bytes.
  */
 int orc_resize_crop_vfirst(const uint8_t* src, int w, int h, int c, int64_t stride, uint8_t* dst, int dw, int dh,
                            int cx, int cy, int cw, int ch, int flip) {
-  if (w <= 0 || h <= 0 || dw <= 0 || dh <= 0 || c < 1 || c > 3) return -1;
+  if (w <= 0 || h <= 0 || dw <= 0 || dh <= 0 || c < 1 || c > 4) return -1;
   if (cx < 0 || cy < 0 || cw <= 0 || ch <= 0 || cx + cw > dw || cy + ch > dh) return -1;
   const int cwx = orc_axis_width(w, dw), cwy = orc_axis_width(h, dh);
   int* x0 = (int*)malloc(sizeof(int) * (size_t)dw * 2);
@@ -387,6 +388,89 @@ int orc_resize_crop_vfirst(const uint8_t* src, int w, int h, int c, int64_t stri
         float hsum = 0.0f;
         for (int k = 0; k <= xb - xa; k++) hsum = fmaf(cfx[k], vrow[(xa + k) * c + k2], hsum);
         float f = hsum + 0.5f;
+        if (f < 0.0f) f = 0.0f;
+        if (f > 255.0f) f = 255.0f;
+        d[x * c + k2] = (uint8_t)f;
+      }
+    }
+  }
+  rc = 0;
+out:
+  free(x0);
+  free(y0);
+  free(wx);
+  free(wy);
+  free(vrow);
+  return rc;
+}
+
+/*
+ * Kernel-order restatement of the STBIR_RGBA (alpha-weighted, c = 4) resize ->
+ * crop -> hflip, in stbir's float operations (a
+ * restatement: parity unpinned): every byte decoded as b * (1/255), colours
+ * multiplied by their decoded alpha, the vertical pass then the horizontal pass
+ * (fmaf chains in tap order from 0, shared tap tables), colours multiplied by
+ * 1 / filtered alpha unless it is below stbir's small float, encoded as
+ * (uint8)trunc(clamp(v * 255 + 0.5)) with the multiply and add unfused (this
+ * file is built with -ffp-contract=off).  The order of the general HIP kernel
+ * (mlx-data_amd/csrc/resample.hip, ALPHA), which must match it bit for bit; it
+ * differs from orc_resize_u8_layout (stbir's horizontal-first order) only by f32
+ * rounding.
+ */
+int orc_resize_crop_vfirst_rgba(const uint8_t* src, int w, int h, int64_t stride, uint8_t* dst, int dw, int dh, int cx,
+                                int cy, int cw, int ch, int flip) {
+  const int c = 4;
+  if (w <= 0 || h <= 0 || dw <= 0 || dh <= 0) return -1;
+  if (cx < 0 || cy < 0 || cw <= 0 || ch <= 0 || cx + cw > dw || cy + ch > dh) return -1;
+  const int cwx = orc_axis_width(w, dw), cwy = orc_axis_width(h, dh);
+  int* x0 = (int*)malloc(sizeof(int) * (size_t)dw * 2);
+  int* y0 = (int*)malloc(sizeof(int) * (size_t)dh * 2);
+  float* wx = (float*)malloc(sizeof(float) * (size_t)dw * cwx);
+  float* wy = (float*)malloc(sizeof(float) * (size_t)dh * cwy);
+  float* vrow = (float*)malloc(sizeof(float) * (size_t)w * c);
+  int rc = -1;
+  if (!x0 || !y0 || !wx || !wy || !vrow) goto out;
+  if (orc_axis_coeffs(w, dw, cwx, x0, x0 + dw, wx)) goto out;
+  if (orc_axis_coeffs(h, dh, cwy, y0, y0 + dh, wy)) goto out;
+  const float inv255 = 1.0f / 255.0f;
+  int xlo = x0[cx], xhi = x0[dw + cx];
+  for (int ox = cx; ox < cx + cw; ox++) {
+    if (x0[ox] < xlo) xlo = x0[ox];
+    if (x0[dw + ox] > xhi) xhi = x0[dw + ox];
+  }
+  for (int r = 0; r < ch; r++) {
+    const int oy = cy + r;
+    const int a = y0[oy], b = y0[dh + oy];
+    const float* cf = wy + (size_t)oy * cwy;
+    for (int px = xlo; px <= xhi; px++)
+      for (int k2 = 0; k2 < c; k2++) {
+        float v = 0.0f;
+        for (int k = 0; k <= b - a; k++) {
+          const uint8_t* p = src + (size_t)(a + k) * stride + (size_t)px * c;
+          const float al = (float)p[3] * inv255;
+          const float x = k2 < 3 ? (float)p[k2] * inv255 * al : al;
+          v = fmaf(cf[k], x, v);
+        }
+        vrow[px * c + k2] = v;
+      }
+    uint8_t* d = dst + (size_t)r * cw * c;
+    for (int x = 0; x < cw; x++) {
+      const int ox = cx + (flip ? cw - 1 - x : x);
+      const int xa = x0[ox], xb = x0[dw + ox];
+      const float* cfx = wx + (size_t)ox * cwx;
+      float px4[4];
+      for (int k2 = 0; k2 < c; k2++) {
+        float hsum = 0.0f;
+        for (int k = 0; k <= xb - xa; k++) hsum = fmaf(cfx[k], vrow[(xa + k) * c + k2], hsum);
+        px4[k2] = hsum;
+      }
+      if (px4[3] >= 7.52316384526264e-37f) { /* stbir's small float, 1 / 2^120 */
+        const float ia = 1.0f / px4[3];
+        for (int k2 = 0; k2 < 3; k2++) px4[k2] = px4[k2] * ia;
+      }
+      for (int k2 = 0; k2 < c; k2++) {
+        float f = px4[k2] * 255.0f;
+        f = f + 0.5f;
         if (f < 0.0f) f = 0.0f;
         if (f > 255.0f) f = 255.0f;
         d[x * c + k2] = (uint8_t)f;

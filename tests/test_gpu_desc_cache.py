@@ -57,3 +57,56 @@ def test_slot_reuse_under_back_to_back_launches():
             d.free()
     for b in src:
         b.free()
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_fresh_descriptor_arrays_every_launch(mode):
+    """Every launch carries a new descriptor array (its own output buffers),
+    40 launches back to back on one stream through 4 slots, under each upload
+    mode (MXD_TUNE_DESC; 4 = the default, the kernels read a non-coherent
+    page-locked slot in place): a launch that read a stale or half-written
+    slot would write another launch's geometry into its buffers, or nothing."""
+    imgs = [synth(200 + 30 * i, 260 + 20 * i, 3, 70 + i) for i in range(3)]
+    pitch = [(im.shape[1] * 3 + 15) // 16 * 16 for im in imgs]
+    src = [capi.DeviceBuffer(p * im.shape[0], 0) for p, im in zip(pitch, imgs)]
+    for b, p, im in zip(src, pitch, imgs):
+        host = np.zeros((im.shape[0], p), np.uint8)
+        host[:, :im.shape[1] * 3] = im.reshape(im.shape[0], -1)
+        b.upload(host)
+    want = {}
+    launches = []
+    for k in range(40):
+        g = k % 5
+        entries, outs = [], []
+        for i, im in enumerate(imgs):
+            h, w = im.shape[:2]
+            rw, rh = O.smallest_side_dims(w, h, 64 + 16 * g)
+            cw, ch = 40, 32
+            cx, cy = (rw - cw) * g // 5, (rh - ch) * (4 - g) // 5
+            key = (g, i)
+            if key not in want:
+                want[key] = O.crop(O.resize(im, rw, rh), cx, cy, cw, ch)
+            d = capi.DeviceBuffer(cw * ch * 3, 0)
+            d.memset(0)
+            outs.append((d, key))
+            entries.append(dict(src=src[i].ptr, src_stride=pitch[i], src_w=w, src_h=h, channels=3, resize_w=rw,
+                                resize_h=rh, crop_x=cx, crop_y=cy, crop_w=cw, crop_h=ch, flip=0, dst=d.ptr,
+                                dst_stride=cw * 3))
+        arr, n = capi.make_images(entries)
+        launches.append((arr, n, outs))
+    capi.check(capi.lib().mxd_stream_synchronize(ctypes.c_void_p(None)))
+    prev = capi.set_tuning(capi.MXD_TUNE_DESC, mode)
+    try:
+        stream = capi.Stream(0)
+        for arr, n, _ in launches:
+            capi.resize_crop_batch(arr, n, capi.MXD_U8, 0, stream.handle)
+        stream.synchronize()
+    finally:
+        capi.set_tuning(capi.MXD_TUNE_DESC, prev)
+    for _, _, outs in launches:
+        for d, key in outs:
+            got = d.download(want[key].shape, np.uint8)
+            assert np.abs(got.astype(int) - want[key].astype(int)).max() <= 1, key
+            d.free()
+    for b in src:
+        b.free()

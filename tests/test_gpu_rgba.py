@@ -3,9 +3,11 @@ c = 4 = STBIR_RGBA at core/image/ImageTransform.cpp:49-58).
 
 A resize is alpha-weighted: colours are premultiplied by alpha for filtering
 and divided by the filtered alpha after it.  This follows SURVEY.md Appendix
-A item 9, restated in the oracle (oracle/stbir_oracle.c
-orc_resize_u8_layout) -- stb is absent, so the weighting itself is parity
-unpinned; the GPU must match the restatement within +-1 (< 0.5 % of channels).
+A item 9, restated in the oracle in stbir's float operations -- stb is absent,
+so the weighting itself is parity unpinned.  The GPU is bit-exact to the
+kernel-order restatement (orc_resize_crop_vfirst_rgba: decode, weight,
+vertical then horizontal pass, x 1/alpha, unfused v * 255 + 0.5) and within
++-1 of stbir's horizontal-first order (orc_resize_u8_layout).
 A crop or flip without a resize is array::sub / hflip in the reference (no
 stbir): bit-exact copies, transparent pixels keep their colour."""
 import numpy as np
@@ -27,16 +29,16 @@ def rgba(h, w, seed, holes=True):
     return img
 
 
-@pytest.mark.parametrize("f32", [False, True])
-def test_rgba_resize_alpha_weighted(f32):
-    imgs = [rgba(200, 300, 1), rgba(375, 500, 2), rgba(960, 1280, 3), rgba(61, 47, 4)]
+@pytest.mark.parametrize("f32,src_align", [(False, 16), (True, 16), (False, 1), (True, 1)])
+def test_rgba_resize_alpha_weighted(f32, src_align):
+    imgs = [rgba(200, 300, 1), rgba(375, 500, 2), rgba(960, 1280, 3), rgba(61, 47, 4), rgba(90, 70, 5)]
     geoms = []
-    for im in imgs:
+    for k, im in enumerate(imgs):
         h, w = im.shape[:2]
-        tw, th = O.smallest_side_dims(w, h, 64)
+        tw, th = O.smallest_side_dims(w, h, 64 if k < 4 else 160)  # the last one upsamples
         cw, ch = min(tw, 56), min(th, 56)
-        geoms.append((tw, th, (tw - cw) // 2, (th - ch) // 2, cw, ch, 0))
-    outs = run_device(imgs, geoms, f32=f32, rgba_weighted=1)
+        geoms.append((tw, th, (tw - cw) // 2, (th - ch) // 2, cw, ch, k % 2))
+    outs = run_device(imgs, geoms, f32=f32, rgba_weighted=1, src_align=src_align)
     lut = (np.arange(256, dtype=np.uint8).astype("float32") / 255).view(np.uint32)
     for im, g, o in zip(imgs, geoms, outs):
         ref = oracle_out(im, g)
@@ -44,6 +46,7 @@ def test_rgba_resize_alpha_weighted(f32):
             q = np.round(o * 255).astype(np.uint8)
             assert np.array_equal(o.view(np.uint32), lut[q])
             o = q
+        assert np.array_equal(o, O.resize_crop_vfirst_rgba(im, g)), g
         m, frac = compare(o, ref)
         assert m <= 1 and frac < 5e-3, (g, m, frac)
         # colour under zero alpha is not the unweighted colour
