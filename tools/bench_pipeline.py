@@ -118,7 +118,7 @@ def _cpu_batch(args):
     return crops
 
 
-def run_cpu(files, batch, workers):
+def run_cpu(files, batch, workers, min_seconds=0.0):
     """The reference's CPU path restated on `workers` processes (the reference
     runs it on a C++ thread pool; processes keep Python's GIL out of the
     measurement): decode + resize + crop per batch in a worker, the batch's
@@ -132,10 +132,13 @@ def run_cpu(files, batch, workers):
         list(ex.map(_cpu_batch, [(c[:2],) for c in chunks[:workers]]))  # warm the workers
         t0 = time.perf_counter()
         n = 0
-        for crops in ex.map(_cpu_batch, [(c,) for c in chunks]):
-            x = crops.astype("float32") / 255
-            n += len(x)
-        dt = time.perf_counter() - t0
+        while True:  # whole passes over the files until >= min_seconds
+            for crops in ex.map(_cpu_batch, [(c,) for c in chunks]):
+                x = crops.astype("float32") / 255
+                n += len(x)
+            dt = time.perf_counter() - t0
+            if dt >= min_seconds:
+                break
     return n, dt
 
 
@@ -160,7 +163,7 @@ def main():
                 B = DATASETS[name]["batch"]
                 for w in workers:
                     if v == "cpu":
-                        n, dt = run_cpu(fl[:args.cpu_images], B, w)
+                        n, dt = run_cpu(fl[:args.cpu_images], B, w, args.min_seconds)
                     else:
                         # warm-up with every worker busy twice over: tap tables, host-path
                         # contexts and the recycled batch buffers reach their steady state;
@@ -170,6 +173,13 @@ def main():
                         want = max(args.min_seconds * nw / tw, args.min_batches * B * w)
                         repeat = max(1, int(np.ceil(want / len(fl))))
                         n, dt = run_surface(fl, B, w, v, repeat)
+                        # the warm-up's rate underestimates the steady one: rerun
+                        # longer until the timed run itself lasts >= --min-seconds
+                        for _ in range(3):
+                            if dt >= args.min_seconds:
+                                break
+                            repeat = max(repeat + 1, int(np.ceil(repeat * 1.25 * args.min_seconds / dt)))
+                            n, dt = run_surface(fl, B, w, v, repeat)
                     print(json.dumps(dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
                                           images_per_s=round(n / dt, 1), batch=B)), flush=True)
 
