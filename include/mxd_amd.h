@@ -161,13 +161,16 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_DESC: how a batch's new descriptor array reaches the kernels (1:
  * copy stream + cross-stream wait; 2: copy on the launch stream; 3: kernels
  * read the page-locked slot in place; 4 (the default): as 3, non-coherent
- * allocation). */
+ * allocation);
+ * MXD_TUNE_STREAMS: streams the launches of a mixed batch (one per kernel
+ * shape) spread over (1: all on the caller's stream; default 2, at most 4). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
   MXD_TUNE_BAND_GRID = 2,
   MXD_TUNE_DESC = 3,
-  MXD_TUNE_COUNT = 4
+  MXD_TUNE_STREAMS = 4,
+  MXD_TUNE_COUNT = 5
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 

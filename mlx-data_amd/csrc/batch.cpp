@@ -535,7 +535,12 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   for (size_t g = 0; g < groups.size(); g++) launches.push_back({groups[g].units, 1, (int32_t)g});
   if (!slow.empty()) launches.push_back({tiles, 2, -1});
   std::stable_sort(launches.begin(), launches.end(), [](const Launch& a, const Launch& b) { return a.units > b.units; });
-  const int nfork = std::min<int>((int)launches.size() - 1, Workspace::kHelpers);
+  // Streams: the caller's and one helper by default.  C3's six launches
+  // measured 0.465 ms on one stream, 0.429 on two and 0.455 on four
+  // (profiles/r03/c3_sizing.jsonl); MXD_TUNE_STREAMS overrides.
+  const int32_t knob_streams = g_tune[MXD_TUNE_STREAMS].load();
+  const int32_t nstreams = knob_streams > 0 ? knob_streams : 2;
+  const int nfork = std::min<int>({(int)launches.size() - 1, nstreams - 1, Workspace::kHelpers});
   if (nfork > 0) {
     if (!ws->fork) {
       MXD_HIP(hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming));

@@ -52,6 +52,7 @@ MXD_TUNE_BAND_ROWS = 0
 MXD_TUNE_BAND_LA = 1
 MXD_TUNE_BAND_GRID = 2
 MXD_TUNE_DESC = 3
+MXD_TUNE_STREAMS = 4
 
 
 class MxdImage(ctypes.Structure):

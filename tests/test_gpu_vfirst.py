@@ -73,3 +73,17 @@ def test_kernels_bit_exact_to_vfirst_oracle(case):
             diff = int((a != w).sum())
             assert diff == 0, (name, case, g, diff)
             assert np.array_equal(f.view(np.uint32), lut[w]), (name, case, g)
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3, 4])
+def test_mixed_batch_launch_layouts_keep_bytes(streams):
+    """C3's six shapes in one batch with its six launches over 1 .. 4 streams
+    (MXD_TUNE_STREAMS; default 2) -- bit-exact to the kernel-order oracle."""
+    imgs, geoms = CASES["c3"]
+    ps = capi.set_tuning(capi.MXD_TUNE_STREAMS, streams)
+    try:
+        outs = run_device(imgs, geoms)
+    finally:
+        capi.set_tuning(capi.MXD_TUNE_STREAMS, ps)
+    for img, g, o in zip(imgs, geoms, outs):
+        assert np.array_equal(o, O.resize_crop_vfirst(img, g)), g
