@@ -197,7 +197,7 @@ def _pool_rate(threads, total, work):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(sample_per_thread=24):
+def cpu_baseline(sample_per_thread=96):
     """Reference-algorithm CPU restatement (oracle C code, GIL released) on C2
     shapes, at 1, 8 and all of this rank's cores, plus Pillow BILINEAR."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -652,11 +652,17 @@ def e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev):
     imgs, n = capi.make_images(entries)
     mode = capi.MXD_F32_DIV255 if f32 else capi.MXD_U8
     capi.resize_crop_host(imgs, n, mode, dev)
-    k = max(3, args.steps // 10)
-    ta = time.perf_counter()
-    for _ in range(k):
-        capi.resize_crop_host(imgs, n, mode, dev)
-    tb = time.perf_counter()
+
+    def timed(call, min_s=1.0):
+        # whole calls until >= min_s (host-side rates scatter run to run; a
+        # handful of calls measured 10-16 k img/s for the same C2 code)
+        k, t0 = 0, time.perf_counter()
+        while k < 3 or time.perf_counter() - t0 < min_s:
+            call()
+            k += 1
+        return k, time.perf_counter() - t0
+
+    k, dt_pageable = timed(lambda: capi.resize_crop_host(imgs, n, mode, dev))
     B = len(sizes)
     # The same call with the host images and the host batch in page-locked
     # memory (what a decoder writing into pinned buffers hands over): the
@@ -672,17 +678,14 @@ def e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev):
                     for e in entries]
         pimgs, pn = capi.make_images(pentries)
         capi.resize_crop_host(pimgs, pn, mode, dev)
-        tc = time.perf_counter()
-        for _ in range(k):
-            capi.resize_crop_host(pimgs, pn, mode, dev)
-        td = time.perf_counter()
+        kp, dt_pinned = timed(lambda: capi.resize_crop_host(pimgs, pn, mode, dev))
         hout = np.ctypeslib.as_array((ctypes.c_uint8 * outs.nbytes).from_address(pin_out.value))
         same = bool(np.array_equal(hout, outs.view(np.uint8)))
     finally:
         capi.check(L.mxd_free_pinned(pin_in))
         capi.check(L.mxd_free_pinned(pin_out))
-    return {"value": round(B * k / (tb - ta), 1), "unit": "images/s", "steps": k,
-            "pinned_value": round(B * k / (td - tc), 1), "pinned_matches_pageable": same,
+    return {"value": round(B * k / dt_pageable, 1), "unit": "images/s", "steps": k, "seconds": round(dt_pageable, 3),
+            "pinned_value": round(B * kp / dt_pinned, 1), "pinned_steps": kp, "pinned_matches_pageable": same,
             "note": "mxd_resize_crop_host: each image's source footprint staged into page-locked memory by "
                     "helper threads and read by the fused kernel over PCIe, results written over PCIe into "
                     "page-locked staging and copied out; chunks overlapped over two slots; synchronous per call. "

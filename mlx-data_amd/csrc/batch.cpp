@@ -160,7 +160,9 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   // over PCIe into that XCD's L2 (kernel-start acquires invalidate the lines
   // of a previous use of the slot).  Fresh batches cost C2 +3.9 % / C4 +5 %
   // over cached descriptors, against +6.5 % / +31 % with mode 1
-  // (profiles/r03/desc_host.jsonl).
+  // (profiles/r03/desc_host.jsonl).  A copy kernel on the launch stream
+  // bringing the slot into HBM (mode 5 of profiles/r03/desc_host_b.jsonl)
+  // measured no better than 4 and was dropped.
   const int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 4;
   if (mode >= 3) {
     const bool nc = mode == 4;

@@ -83,8 +83,12 @@ constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; 
 #ifndef MXD_RING_FIXED
 #define MXD_RING_FIXED 0
 #endif
+// DMAX 5 (1080p / 4K -> 512, C5) takes 4 slots: its RGB u8 kernel then fits
+// 124 VGPRs (4 waves per SIMD instead of 3 at 5 slots), C5 0.3244 -> 0.3204 ms
+// per launch (profiles/r03/ring_variants.jsonl, variant ring4).
 constexpr int scatter_ring_slots(int dmax) {
   if (MXD_RING_FIXED > 0 && dmax >= 2) return MXD_RING_FIXED;
+  if (dmax == 5 && MXD_RING == 6) return 4;
   if (MXD_RING % dmax == 0) return MXD_RING;
   if (2 * dmax <= MXD_RING) return 2 * dmax;
   if (dmax > 9)

@@ -4,7 +4,8 @@
 # line, rocprofv3 kernel stats of the default bench command (C2) and of the
 # C4 / C6 single-stream runs, PMC FETCH/WRITE/SQ passes per workload (single
 # stream, kernel-trace only, each pass its own run), profiles/traffic.json
-# inputs, and optionally the operator-surface pipeline bench.
+# inputs, and optionally the operator-surface pipeline bench.  rocprof stats
+# of C3 / C5 / C6 / C7 are single-stream runs of 20 launches.
 #   tools/r03_measure.sh TAG [skip-pipeline] [skip-pmc] [skip-tests]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -35,8 +36,10 @@ run prof_1stream 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpu
 cut -c1-220 gpurun_out/${TAG}_prof1/run_kernel_stats.csv
 run prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c4 -o run -- python3 bench.py --workload c4 --streams 1 --no-cpu --no-e2e
 cut -c1-220 gpurun_out/${TAG}_prof_c4/run_kernel_stats.csv
-run prof_c6 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c6 -o run -- python3 bench.py --workload c6 --streams 1 --no-cpu --no-e2e
-cut -c1-220 gpurun_out/${TAG}_prof_c6/run_kernel_stats.csv
+for w in c3 c5 c6 c7; do
+  run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_$w -o run -- python3 bench.py --workload $w --streams 1 --steps 20 --warmup 3 --no-cpu --no-e2e
+  cut -c1-220 gpurun_out/${TAG}_prof_$w/run_kernel_stats.csv
+done
 if [ "${3:-}" != "skip-pmc" ]; then
 for w in c2 c3 c4 c5 c6 c7; do
   i=0
