@@ -127,3 +127,51 @@ def test_zero_copy_equals_dma(f32):
     finally:
         for p in pins:
             p.free()
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_zero_copy_bottom_right_crops_of_page_aligned_buffers(f32):
+    """a zero-copy source read in place must never be read past its
+    last pixel.  Images whose bytes end exactly at a page boundary of their
+    page-locked buffer (1024x768x3 = 576 pages; 768x1024x3), cropped at the
+    bottom-right corner (the footprint reaches the last stored byte) with and
+    without a mirror, and sources that start 1-3 bytes past a 4-byte boundary
+    so the same end falls mid-dword: bytes equal the kernel-order oracle."""
+    import oracle as O
+
+    elem = 4 if f32 else 1
+    cases = []
+    for (h, w) in [(768, 1024), (1024, 768)]:
+        for flip in (0, 1):
+            for shift in (0, 1, 3):
+                cases.append((h, w, flip, shift))
+    pins = []
+    try:
+        entries, outs = [], []
+        for k, (h, w, flip, shift) in enumerate(cases):
+            im = synth(h, w, 3, 40 + k)
+            nbytes = h * w * 3
+            ps = Pinned(nbytes + shift)
+            pins.append(ps)
+            src = ps.a[shift:shift + nbytes]
+            src[:] = im.reshape(-1)
+            rw, rh = capi.resize_smallest_side_dims(w, h, 256)
+            g = (rw, rh, rw - 224, rh - 224, 224, 224, flip)
+            row = 224 * 3 * elem
+            dst = np.zeros((224, row), np.uint8)
+            outs.append((dst, im, g))
+            entries.append(dict(src=ps.p.value + shift, src_stride=w * 3, src_w=w, src_h=h, channels=3, resize_w=rw,
+                                resize_h=rh, crop_x=g[2], crop_y=g[3], crop_w=224, crop_h=224, flip=flip,
+                                dst=dst.ctypes.data, dst_stride=row))
+        arr, n = capi.make_images(entries)
+        capi.resize_crop_host(arr, n, capi.MXD_F32_DIV255 if f32 else capi.MXD_U8, 0)
+        lut = (np.arange(256, dtype=np.uint8).astype("float32") / 255).view(np.uint32)
+        for dst, im, g in outs:
+            want = O.resize_crop_vfirst(im, g)
+            if f32:
+                assert np.array_equal(dst.view(np.uint32).reshape(224, 224, 3), lut[want]), g
+            else:
+                assert np.array_equal(dst.reshape(224, 224, 3), want), g
+    finally:
+        for p in pins:
+            p.free()
