@@ -562,7 +562,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const BandGroup& g = bgroups[launches[k].group];
       rc = mxd::launch_band(g.cfg, dev + g.first, g.table >= 0 ? tables_dev + g.table : nullptr, s);
     } else if (launches[k].kind == 1) {
-      const Group& g = groups[launches[k].group];
+      Group& g = groups[launches[k].group];
+      g.cfg.prio = launches.size() == 1 ? 1 : 0;
       rc = mxd::launch_wave(g.cfg, dev + wbase + g.first, s);
     } else {
       rc = mxd::launch_resample(cfg, dev + wbase + nw, s);

@@ -62,6 +62,7 @@ struct WaveCfg {
   int32_t q, shift;
   int32_t p;  // source pixels per lane (wave_default_p, or 8 for wide RGB windows; RGB 16 = byte lanes)
   int32_t per_img = 0;  // units of every image when all images of the launch have the same count, else 0
+  int32_t prio = 1;     // progress-based wave priority (off for the concurrent launches of a mixed batch)
 };
 
 // Scatter schedule geometry, shared by the kernel and the host builder:

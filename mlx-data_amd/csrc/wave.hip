@@ -57,9 +57,10 @@ namespace {
 
 using namespace dev;
 
-// Waves per workgroup (tuning builds: -DMXD_WAVES=<1|2|4|8>).
+// Waves per workgroup (tuning builds: -DMXD_WAVES=<1|2|4|8>).  8 measured
+// 0.2-2.6 % faster than 4 on C2..C7 (profiles/r03/wave_variants.jsonl).
 #ifndef MXD_WAVES
-#define MXD_WAVES 4
+#define MXD_WAVES 8
 #endif
 constexpr int kWaves = MXD_WAVES;
 constexpr int kLanes = 64;
@@ -100,12 +101,16 @@ constexpr int kPad = 32;  // floats after each plane: padded taps read zeros the
 // finishes its band in ~95 us and its last in ~141 us (C2, tools/stamps.sh):
 // the launch then drains for ~60 us with ever fewer waves feeding HBM.  Each
 // wave lowers its s_setprio level as it completes quarters of its band, so
-// waves that are behind win the arbiter and the band ends line up.
+// waves that are behind win the arbiter and the band ends line up.  Only for
+// a batch that is one launch (`on`): launches of a mixed batch run
+// concurrently, and there the priorities of one launch's waves starve the
+// others' (C3 0.440 -> 0.423 ms without them, profiles/r03/wave_variants.jsonl).
 #ifndef MXD_PRIO
 #define MXD_PRIO 1
 #endif
 
-__device__ __forceinline__ void progress_prio(int done, int total) {
+__device__ __forceinline__ void progress_prio(bool on, int done, int total) {
+  if (!on) return;
   if constexpr (MXD_PRIO != 0) {
     const int level = 3 - (4 * done) / (total + 1);  // 3 at the start .. 0 in the last quarter
     switch (level) {
@@ -347,7 +352,7 @@ struct HStrip {
 // called with the V sums of every completed output row y.
 template <class L, int S, int DMAX, bool SHIFT, class OnRow, class Start>
 __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const Src<L, SHIFT>& src, OnRow&& on_row,
-                                             Start&& start, bool sync = false) {
+                                             Start&& start, bool prio, bool sync = false) {
   constexpr int C = L::VC;
   constexpr int R = scatter_ring_slots(DMAX);
   constexpr int LA = R - 1;  // iterations loaded ahead
@@ -402,7 +407,7 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
       if constexpr (MXD_SYNC_STRIPS != 0)
         if (sync) __builtin_amdgcn_s_barrier();
     });
-    progress_prio(gb + BG, ngroups);
+    progress_prio(prio, gb + BG, ngroups);
   }
 }
 
@@ -413,10 +418,10 @@ constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; 
 // One unit (image, band, strip) by the calling wave; planes = its LDS rows.
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
 __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int nimgs, int per_img, int unit,
-                                         float* __restrict__ planes, int lane) {
+                                         float* __restrict__ planes, int lane, bool prio) {
   using L = Lay<C, P>;
   constexpr int VC = L::VC, VP = L::VP;
-  progress_prio(0, 1);
+  progress_prio(prio, 0, 1);
 #if MXD_STAMPS
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -540,7 +545,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
     load_rows(RA, oy0, true);
     start();
     for (int y = oy0;; y += 2) {
-      progress_prio(y - oy0, oy1 - oy0);
+      progress_prio(prio, y - oy0, oy1 - oy0);
       load_rows(RB, min(y + 1, crop_h - 1), y + 1 < oy1);
       step(RA, y);
       if (y + 1 >= oy1) break;
@@ -551,7 +556,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start,
+    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio,
                                     nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0);
   }
 #if MXD_STAMPS
@@ -564,7 +569,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
 
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
 __global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES) void resample_wave(
-    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img) {
+    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = Lay<C, P>;
   constexpr int PL = L::PL;
@@ -576,10 +581,12 @@ __global__ __launch_bounds__(kWaves* kLanes, lane_bytes(C, P) > 16 ? MXD_MIN_WAV
 #pragma unroll
     for (int i = 0; i < L::PAD; i += kLanes)
       if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
-  if (unit < nunits) run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT>(imgs, nimgs, per_img, unit, planes, lane);
+  if (unit < nunits)
+    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT>(imgs, nimgs, per_img, unit, planes, lane,
+                                                    __builtin_amdgcn_readfirstlane(prio) != 0);
 }
 
-using WaveKernel = void (*)(const ImgDev*, int, int, int);
+using WaveKernel = void (*)(const ImgDev*, int, int, int, int);
 
 constexpr int default_p(int c) { return c == 1 ? 16 : c == 2 ? 8 : 4; }
 
@@ -738,7 +745,7 @@ int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
   if (!k) return -2;
   const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
-                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img);
+                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.prio);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
