@@ -116,6 +116,9 @@ int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);
 bool wave_has_kernel(const WaveCfg& cfg);
 // Waves of this configuration the device runs at once (occupancy x CUs), 0 if unknown.
 int wave_capacity(const WaveCfg& cfg, int device);
+// Diagnostics: the occupancy API's blocks per CU, the kernel's VGPRs and LDS
+// bytes per block; returns waves per block (-1: no kernel / error).
+int wave_kernel_info(const WaveCfg& cfg, int device, int* api_blocks, int* vgprs, int* lds);
 int launch_copy(const void* src, void* dst, size_t bytes, void* stream);
 
 // Dynamic LDS bytes the kernel needs for cfg.

@@ -749,6 +749,20 @@ int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int wave_kernel_info(const WaveCfg& cfg, int device, int* api_blocks, int* vgprs, int* lds) {
+  const WaveKernel k = select_kernel(cfg);
+  if (!k) return -1;
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k)) != hipSuccess) return -1;
+  *vgprs = a.numRegs;
+  *lds = lds_bytes(cfg);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(api_blocks, reinterpret_cast<const void*>(k), kWaves * kLanes,
+                                                   *lds) != hipSuccess)
+    return -1;
+  (void)device;
+  return kWaves;
+}
+
 int wave_capacity(const WaveCfg& cfg, int device) {
   const WaveKernel k = select_kernel(cfg);
   if (!k) return 0;

@@ -90,6 +90,12 @@ def main():
         capi.set_tuning(capi.MXD_TUNE_DESC, int(kv.get("desc", 0)))
         capi.set_tuning(capi.MXD_TUNE_STREAMS, int(kv.get("streams", 0)))
         capi.set_kernel_policy(int(kv.get("policy", 0)))
+        # wrows: the wave kernels' band height, read from the environment by
+        # tuning builds only (-DMXD_TUNING_ENV; tools/variants.sh build tenv)
+        if int(kv.get("wrows", 0)) > 0:
+            os.environ["MXD_BAND_ROWS"] = kv["wrows"]
+        else:
+            os.environ.pop("MXD_BAND_ROWS", None)
         return kv
 
     # Warm-up (clocks, caches, plans of every setting) before any timing;
