@@ -161,7 +161,8 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_DESC: how a batch's new descriptor array reaches the kernels (1:
  * copy stream + cross-stream wait; 2: copy on the launch stream; 3: kernels
  * read the page-locked slot in place; 4 (the default): as 3, non-coherent
- * allocation);
+ * allocation; 6: the host stores the array into device memory through a
+ * large PCI BAR, falling back to 4 without one);
  * MXD_TUNE_STREAMS: streams the launches of a mixed batch (one per kernel
  * shape) spread over (1: all on the caller's stream; default 2, at most 4). */
 enum mxd_tune {

@@ -1,6 +1,9 @@
 // batch.cpp -- run_batch (capi_internal.h): per-stream descriptor
 // workspaces and the fused launches of one batch (band, wave and general
 // kernels, forked over helper streams when a batch needs several).
+#include <atomic>
+#include <deque>
+
 #include "capi_internal.h"
 
 namespace mxd {
@@ -9,13 +12,19 @@ namespace {
 
 struct Workspace {
   std::mutex mu;
-  // Descriptor slots: each launch reads its descriptors from one slot's
-  // device copy.  A batch whose descriptors a slot holds reuses it; a new one
-  // takes the least recently used slot once the launches that read it are
-  // done, and uploads on a copy stream while the previous launch computes.
-  // Launches wait for their slot's upload, so consecutive batches never
-  // serialize behind an H2D copy.
-  static constexpr int kSlots = 4;
+  // Descriptor slots: each launch reads its descriptors from one slot.  A
+  // batch whose descriptors a slot holds reuses it; a new one takes the least
+  // recently used slot once the launches that read it are done.
+  // Reuse is fenced without an event per launch (an event between kernels
+  // costs the GPU a few microseconds): batches are numbered in stream order,
+  // every slot remembers the last batch that read it, and one event is
+  // recorded every kFenceEvery batches; reusing a slot waits on the first
+  // fence recorded after its last batch (recording one then if none is).
+  // With 8 slots the fence a reuse needs was recorded >= 4 batches earlier
+  // and has normally completed.
+  static constexpr int kSlots = 8;
+  static constexpr uint64_t kFenceEvery = 4;
+  static constexpr size_t kMaxFences = 8;
   struct Slot {
     ImgDev* host = nullptr;  // pinned
     ImgDev* dev = nullptr;
@@ -23,12 +32,19 @@ struct Workspace {
     bool zc_nc = false;            // zc allocated non-coherent
     const ImgDev* launch = nullptr;  // what the batch's kernels read (dev or zc)
     size_t cap = 0, count = 0;
-    hipEvent_t copied = nullptr, used = nullptr;
-    uint64_t last_use = 0;
-    bool unrecorded_hits = false;  // launched from since `used` was last recorded
+    hipEvent_t copied = nullptr;   // mode 1: the copy-stream upload landed
+    uint64_t last_use = 0;         // LRU clock
+    uint64_t last_batch = 0;       // the last batch that read it (0: none)
   } slot[kSlots];
   int cur = -1;
   uint64_t clock = 0;
+  uint64_t batch = 0;  // batches launched on this stream
+  struct Fence {
+    hipEvent_t ev;
+    uint64_t covers;  // every batch <= covers has finished once ev has
+  };
+  std::deque<Fence> fences;
+  std::vector<hipEvent_t> spare;
   hipStream_t copy = nullptr;
   // Fork/join helpers: the launches of a mixed batch (one per kernel shape)
   // run concurrently on these streams, so one launch's tail overlaps the
@@ -37,6 +53,38 @@ struct Workspace {
   hipStream_t helper[kHelpers] = {};
   hipEvent_t fork = nullptr, join[kHelpers] = {};
 };
+
+// Records a fence covering every batch launched so far on the stream.
+int record_fence(Workspace* ws, hipStream_t s) {
+  hipEvent_t ev = nullptr;
+  if (!ws->spare.empty()) {
+    ev = ws->spare.back();
+    ws->spare.pop_back();
+  } else {
+    MXD_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  MXD_HIP(hipEventRecord(ev, s));
+  ws->fences.push_back({ev, ws->batch});
+  while (ws->fences.size() > Workspace::kMaxFences) {
+    // a later fence covers everything the oldest did
+    ws->spare.push_back(ws->fences.front().ev);
+    ws->fences.pop_front();
+  }
+  return MXD_OK;
+}
+
+// Blocks until batch `b` of the stream has finished.
+int wait_batch(Workspace* ws, uint64_t b, hipStream_t s) {
+  if (b == 0) return MXD_OK;
+  for (const Workspace::Fence& f : ws->fences)
+    if (f.covers >= b) {
+      MXD_HIP(hipEventSynchronize(f.ev));
+      return MXD_OK;
+    }
+  if (int rc = record_fence(ws, s)) return rc;
+  MXD_HIP(hipEventSynchronize(ws->fences.back().ev));
+  return MXD_OK;
+}
 
 class WorkspacePool {
  public:
@@ -85,6 +133,20 @@ int validate(const mxd_image& im, int32_t i) {
   return MXD_OK;
 }
 
+// Whether the host can store into the device's memory directly (large PCI
+// BAR: the whole HBM mapped for the CPU), cached per device.
+bool large_bar(int32_t device) {
+  static std::mutex mu;
+  static std::map<int32_t, bool> known;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = known.find(device);
+  if (it != known.end()) return it->second;
+  hipDeviceProp_t prop{};
+  const bool ok = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.isLargeBar != 0;
+  known[device] = ok;
+  return ok;
+}
+
 // Uploads descs to the stream's workspace (skipped when unchanged) and returns
 // the device copy.
 int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream, ImgDev** dev_out,
@@ -106,10 +168,8 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
       if (c.count == n && c.host && std::memcmp(c.host, descs.data(), bytes) == 0) {
         ws->cur = k;
         c.last_use = ++ws->clock;
-        if (hipEventQuery(c.copied) != hipSuccess) MXD_HIP(hipStreamWaitEvent(s, c.copied, 0));
-        // No per-launch event (it costs ~2.5 us between kernels): the slot's
-        // readers are fenced when it is next overwritten (below).
-        c.unrecorded_hits = true;
+        c.last_batch = ws->batch + 1;  // the batch about to launch
+        if (c.copied && hipEventQuery(c.copied) != hipSuccess) MXD_HIP(hipStreamWaitEvent(s, c.copied, 0));
         *dev_out = const_cast<ImgDev*>(c.launch);
         if (hit) *hit = true;
         return MXD_OK;
@@ -123,22 +183,11 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   ws->cur = victim;
   ws->slot[victim].last_use = ++ws->clock;
   Workspace::Slot& c = ws->slot[ws->cur];
-  if (!c.copied) {
-    MXD_HIP(hipEventCreateWithFlags(&c.copied, hipEventDisableTiming));
-    MXD_HIP(hipEventCreateWithFlags(&c.used, hipEventDisableTiming));
-  } else {
-    // Launched from by cache hits since `used` was recorded: fence them now
-    // (after every launch enqueued so far).  Only a working-set change evicts
-    // such a slot; a stream of fresh batches never has hits.
-    if (c.unrecorded_hits) {
-      MXD_HIP(hipEventRecord(c.used, s));
-      c.unrecorded_hits = false;
-    }
-    // Host-side wait: the launches that read this slot are done.  (Ordering
-    // the upload after them on the GPU instead, with a wait of the copy
-    // stream on the compute stream, measured ms-long stalls.)
-    MXD_HIP(hipEventSynchronize(c.used));
-  }
+  // Host-side wait: the launches that read this slot are done.  (Ordering
+  // the upload after them on the GPU instead, with a wait of the copy stream
+  // on the compute stream, measured ms-long stalls.)
+  if (int rc = wait_batch(ws, c.last_batch, s)) return rc;
+  c.last_batch = ws->batch + 1;
   if (n > c.cap) {
     if (c.dev) MXD_HIP(hipFree(c.dev));
     if (c.host) MXD_HIP(hipHostFree(c.host));
@@ -155,16 +204,28 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   c.count = n;
   // Upload modes (MXD_TUNE_DESC): 1 = copy stream + cross-stream wait, 2 =
   // copy on the launch stream, 3 / 4 = the kernels read the pinned slot in
-  // place (coherent / non-coherent allocation).  Default 4: no copy and no
+  // place (coherent / non-coherent allocation), 6 = the host stores into the
+  // device slot through a large PCI BAR.  Default 4: no copy and no
   // cross-stream wait; the first wave of each XCD to read a line brings it
   // over PCIe into that XCD's L2 (kernel-start acquires invalidate the lines
-  // of a previous use of the slot).  Fresh batches cost C2 +3.9 % / C4 +5 %
-  // over cached descriptors, against +6.5 % / +31 % with mode 1
-  // (profiles/r03/desc_host.jsonl).  A copy kernel on the launch stream
-  // bringing the slot into HBM (mode 5 of profiles/r03/desc_host_b.jsonl)
-  // measured no better than 4 and was dropped.
-  const int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 4;
-  if (mode >= 3) {
+  // of a previous use of the slot).  With slot reuse fenced every 4 batches
+  // instead of by an event per launch, fresh batches cost C2 +1.0 % / C4
+  // +1.6 % over cached descriptors (mode 6: +1.1 % / within noise; mode 1
+  // +2.2 % / +6 %), against +3.9 % / +5 % with an event per launch
+  // (profiles/r03/desc_host_c.jsonl, desc_host.jsonl).  A copy kernel on the
+  // launch stream bringing the slot into HBM (mode 5 of
+  // profiles/r03/desc_host_b.jsonl) measured no better and was dropped.
+  int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 4;
+  if (mode == 6 && !large_bar(device)) mode = 4;
+  if (mode == 6) {
+    // the host stores the array straight into the device slot through the
+    // large PCI BAR (~1 us for 13 KB); the fence drains the write-combining
+    // buffers before the launch's doorbell, and the kernel-start acquire
+    // drops the slot's lines from the L2s.  Kernels read HBM, no PCIe trip.
+    std::memcpy(c.dev, descs.data(), bytes);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    c.launch = c.dev;
+  } else if (mode >= 3) {
     const bool nc = mode == 4;
     if (!c.zc || c.zc_nc != nc || n > c.cap) {
       if (c.zc) MXD_HIP(hipHostFree(c.zc));
@@ -178,6 +239,7 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
     MXD_HIP(hipMemcpyAsync(c.dev, c.host, bytes, hipMemcpyHostToDevice, s));
     c.launch = c.dev;
   } else {
+    if (!c.copied) MXD_HIP(hipEventCreateWithFlags(&c.copied, hipEventDisableTiming));
     MXD_HIP(hipMemcpyAsync(c.dev, c.host, bytes, hipMemcpyHostToDevice, ws->copy));
     MXD_HIP(hipEventRecord(c.copied, ws->copy));
     MXD_HIP(hipStreamWaitEvent(s, c.copied, 0));
@@ -187,9 +249,11 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   return MXD_OK;
 }
 
-// After the launches of a batch: the slot is free again once they finish.
+// After the launches of a batch: count it, and every kFenceEvery batches
+// record a fence for slot reuse.
 int release_descs(Workspace* ws, void* stream) {
-  MXD_HIP(hipEventRecord(ws->slot[ws->cur].used, reinterpret_cast<hipStream_t>(stream)));
+  ws->batch++;
+  if (ws->batch % Workspace::kFenceEvery == 0) return record_fence(ws, reinterpret_cast<hipStream_t>(stream));
   return MXD_OK;
 }
 
@@ -576,7 +640,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
     MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
   }
-  return hit ? MXD_OK : release_descs(ws, stream);
+  return release_descs(ws, stream);
 }
 
 

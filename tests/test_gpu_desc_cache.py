@@ -59,7 +59,7 @@ def test_slot_reuse_under_back_to_back_launches():
         b.free()
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6])
 def test_fresh_descriptor_arrays_every_launch(mode):
     """Every launch carries a new descriptor array (its own output buffers),
     40 launches back to back on one stream through 4 slots, under each upload
