@@ -38,7 +38,8 @@ struct Workspace {
   } slot[kSlots];
   int cur = -1;
   uint64_t clock = 0;
-  uint64_t batch = 0;  // batches launched on this stream
+  uint64_t batch = 0;    // batches launched on this stream
+  uint64_t written = 0;  // of them, batches that wrote a slot
   struct Fence {
     hipEvent_t ev;
     uint64_t covers;  // every batch <= covers has finished once ev has
@@ -249,11 +250,13 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   return MXD_OK;
 }
 
-// After the launches of a batch: count it, and every kFenceEvery batches
-// record a fence for slot reuse.
-int release_descs(Workspace* ws, void* stream) {
+// After the launches of a batch: count it, and every kFenceEvery batches that
+// wrote a slot record a fence for slot reuse (a loop of cache hits records
+// none: an eviction after it records its fence on demand).
+int release_descs(Workspace* ws, void* stream, bool hit) {
   ws->batch++;
-  if (ws->batch % Workspace::kFenceEvery == 0) return record_fence(ws, reinterpret_cast<hipStream_t>(stream));
+  if (!hit && ++ws->written % Workspace::kFenceEvery == 0)
+    return record_fence(ws, reinterpret_cast<hipStream_t>(stream));
   return MXD_OK;
 }
 
@@ -640,7 +643,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
     MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
   }
-  return release_descs(ws, stream);
+  return release_descs(ws, stream, hit);
 }
 
 
