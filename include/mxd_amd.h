@@ -160,8 +160,8 @@ int mxd_set_kernel_policy(int32_t policy);
  * at once, each running a stream of units; 1: one per unit; n > 1: n);
  * MXD_TUNE_DESC: how a batch's new descriptor array reaches the kernels (1:
  * copy stream + cross-stream wait; 2: copy on the launch stream; 3: kernels
- * read the page-locked slot in place; 4 (the default): as 3, non-coherent
- * allocation; 6: the host stores the array into device memory through a
+ * read the page-locked slot in place; 4: as 3, non-coherent allocation; 6
+ * (the default): the host stores the array into device memory through the
  * large PCI BAR, falling back to 4 without one);
  * MXD_TUNE_STREAMS: streams the launches of a mixed batch (one per kernel
  * shape) spread over (1: all on the caller's stream; default 2, at most 4). */

@@ -206,17 +206,17 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   // Upload modes (MXD_TUNE_DESC): 1 = copy stream + cross-stream wait, 2 =
   // copy on the launch stream, 3 / 4 = the kernels read the pinned slot in
   // place (coherent / non-coherent allocation), 6 = the host stores into the
-  // device slot through a large PCI BAR.  Default 4: no copy and no
-  // cross-stream wait; the first wave of each XCD to read a line brings it
-  // over PCIe into that XCD's L2 (kernel-start acquires invalidate the lines
-  // of a previous use of the slot).  With slot reuse fenced every 4 batches
-  // instead of by an event per launch, fresh batches cost C2 +1.0 % / C4
-  // +1.6 % over cached descriptors (mode 6: +1.1 % / within noise; mode 1
-  // +2.2 % / +6 %), against +3.9 % / +5 % with an event per launch
-  // (profiles/r03/desc_host_c.jsonl, desc_host.jsonl).  A copy kernel on the
-  // launch stream bringing the slot into HBM (mode 5 of
-  // profiles/r03/desc_host_b.jsonl) measured no better and was dropped.
-  int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 4;
+  // device slot through the large PCI BAR.  Default 6 (4 without a large
+  // BAR): no copy, no cross-stream wait, and the kernels read their
+  // descriptors from HBM like a cached batch.  With slot reuse fenced every 4
+  // written batches, fresh batches cost C2 +0.2-1.5 % and C4 -3..+1.5 % over
+  // cached descriptors in mode 6, C2 +1.3 % and C4 +3..18 % in mode 4
+  // (profiles/r03/desc_host_d.jsonl, three repetitions), against +3.9 % / +5 %
+  // with an event per launch (desc_host.jsonl) and +6.5 % / +31 % for the
+  // round-2 copy stream.  A copy kernel on the launch stream bringing the slot
+  // into HBM (mode 5 of profiles/r03/desc_host_b.jsonl) measured no better and
+  // was dropped.
+  int32_t mode = g_tune[MXD_TUNE_DESC].load() > 0 ? g_tune[MXD_TUNE_DESC].load() : 6;
   if (mode == 6 && !large_bar(device)) mode = 4;
   if (mode == 6) {
     // the host stores the array straight into the device slot through the
