@@ -527,7 +527,7 @@ def main():
     if args.steps > 0:
         prev = capi.set_kernel_policy(args.policy | capi.MXD_POLICY_NO_DESC_CACHE)
         k = max(10, args.steps // 2)
-        for i in range(12):  # untimed: every descriptor slot allocated and written once
+        for i in range(40):  # untimed: every descriptor slot allocated and written (twice)
             step(i, 1)
         stream.synchronize()
         e0.record(stream)

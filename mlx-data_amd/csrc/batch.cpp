@@ -20,10 +20,10 @@ struct Workspace {
   // every slot remembers the last batch that read it, and one event is
   // recorded every kFenceEvery batches; reusing a slot waits on the first
   // fence recorded after its last batch (recording one then if none is).
-  // With 8 slots the fence a reuse needs was recorded >= 4 batches earlier
+  // With 16 slots the fence a reuse needs was recorded >= 8 batches earlier
   // and has normally completed.
-  static constexpr int kSlots = 8;
-  static constexpr uint64_t kFenceEvery = 4;
+  static constexpr int kSlots = 16;
+  static constexpr uint64_t kFenceEvery = 8;
   static constexpr size_t kMaxFences = 8;
   struct Slot {
     ImgDev* host = nullptr;  // pinned
@@ -209,9 +209,11 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   // device slot through the large PCI BAR.  Default 6 (4 without a large
   // BAR): no copy, no cross-stream wait, and the kernels read their
   // descriptors from HBM like a cached batch.  With slot reuse fenced every 4
-  // written batches, fresh batches cost C2 +0.2-1.5 % and C4 -3..+1.5 % over
-  // cached descriptors in mode 6, C2 +1.3 % and C4 +3..18 % in mode 4
-  // (profiles/r03/desc_host_d.jsonl, three repetitions), against +3.9 % / +5 %
+  // written batches (8 slots), fresh batches cost C2 +0.2-1.5 % and C4
+  // -3..+1.5 % over cached descriptors in mode 6, C2 +1.3 % and C4 +3..18 %
+  // in mode 4 (profiles/r03/desc_host_d.jsonl, three repetitions); with 16
+  // slots fenced every 8, C2 -1.5..0 % and C4 -3..+4.6 %
+  // (profiles/r03/fresh_slots16.jsonl); against +3.9 % / +5 %
   // with an event per launch (desc_host.jsonl) and +6.5 % / +31 % for the
   // round-2 copy stream.  A copy kernel on the launch stream bringing the slot
   // into HBM (mode 5 of profiles/r03/desc_host_b.jsonl) measured no better and
