@@ -400,6 +400,12 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
     int32_t ns = 0, tx = 0, q = 0;
     if (!wave_strips(*p.xt, im, pp, &ns, &tx, &q)) continue;
     if (p.wave && ns >= p.nstrips) continue;
+    // A crop the wide lanes take in one strip that narrow lanes take in two
+    // (ImageNet shapes, 480p) keeps the narrow kernel: at 64-78 VGPRs it runs
+    // 8 waves per SIMD where the wide one-strip kernels (132-146 VGPRs) run 2-3
+    // -- C4 0.0237 -> 0.0229 ms per launch, C3 unchanged
+    // (profiles/r03/onestrip.jsonl).
+    if (p.wave && p.nstrips == 2 && ns == 1 && pp == 8) continue;
     ImgPlan cand = p;
     cand.nstrips = ns;
     cand.tx = tx;

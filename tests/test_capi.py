@@ -118,8 +118,9 @@ def test_rgb_scatter_lane_layouts():
     per lane, 1-KiB windows) when they need no more strips than pixel lanes at
     <= 2 output pixels per lane -- 720p -> 224, two strips -- and pixel lanes
     otherwise: C2's 960 -> 256 takes two 512-pixel strips with pixel lanes,
-    three with byte lanes; ImageNet shapes (C4) one strip either way, q = 4
-    (profiles/r02/bytes_ab.txt).  MXD_POLICY_NO_BYTES keeps pixel lanes,
+    three with byte lanes; ImageNet shapes (C4) two 256-pixel strips (one
+    wide strip would run at 2-3 waves per SIMD, profiles/r03/onestrip.jsonl),
+    one 1-KiB byte-lane strip when forced (profiles/r02/bytes_ab.txt).  MXD_POLICY_NO_BYTES keeps pixel lanes,
     MXD_POLICY_BYTES takes byte lanes wherever a kernel exists."""
     p = _plan(_entry())
     assert (p["wave"], p["kind"], p["taps"], p["s"], p["dmax"]) == (1, 2, 8, 2, 4)
@@ -130,7 +131,8 @@ def test_rgb_scatter_lane_layouts():
     assert (_plan(hd)["p"], _plan(hd)["nstrips"]) == (16, 2)
     assert _plan(hd, capi.MXD_POLICY_NO_BYTES)["p"] == 8
     c4 = _entry(500, 375, 1500, 341, 256)
-    assert (_plan(c4)["p"], _plan(c4)["nstrips"], _plan(c4)["q"]) == (8, 1, 4)
+    # one wide strip or two narrow ones: the narrow kernel (8 waves per SIMD)
+    assert (_plan(c4)["p"], _plan(c4)["nstrips"], _plan(c4)["q"]) == (4, 2, 2)
     assert (_plan(c4, capi.MXD_POLICY_BYTES)["p"], _plan(c4, capi.MXD_POLICY_BYTES)["q"]) == (16, 4)
 
 
