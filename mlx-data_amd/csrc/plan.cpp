@@ -429,14 +429,16 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
     p = cand;
   }
   // RGB scatter: byte lanes (one 1-KiB contiguous load per wave and row)
-  // when they cut the crop into no more strips than pixel lanes do, at <= 2
-  // output pixels per lane (measured: 720p -> 224 with two strips 4 % faster;
-  // with more strips -- their narrower 341-pixel window -- or a single 224-column
-  // strip (C4) pixel lanes were 2-10 % faster; profiles/r02/bytes_ab.txt).
+  // instead of wide pixel lanes when they cut the crop into no more strips,
+  // at <= 2 output pixels per lane (measured: 720p -> 224 with two strips 4 %
+  // faster; with more strips -- their narrower 341-pixel window -- or a single
+  // 224-column strip (C4) pixel lanes were 2-10 % faster;
+  // profiles/r02/bytes_ab.txt).  Never instead of the narrow kernel (480p:
+  // 0.0908 vs 0.0977 ms, profiles/r03/c3_layouts.jsonl).
   if (c == 3 && sh.s > 0 && !(policy & (MXD_POLICY_NO_BYTES | MXD_POLICY_NARROW))) {
     int32_t ns = 0, tx = 0, q = 0, bt = 0, bd = 0;
     if (wave_strips_bytes(*p.xt, im, st, &ns, &tx, &q) &&
-        ((policy & MXD_POLICY_BYTES) || !p.wave || p.kind != 2 || (ns <= p.nstrips && q <= 2)) &&
+        ((policy & MXD_POLICY_BYTES) || !p.wave || p.kind != 2 || (p.pp == 8 && ns <= p.nstrips && q <= 2)) &&
         scatter_kernel_for(c, f32, p.xt->width, sh, q, 0, 16, &bt, &bd)) {
       p.wave = true;
       p.nstrips = ns;
