@@ -632,7 +632,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       rc = mxd::launch_band(g.cfg, dev + g.first, g.table >= 0 ? tables_dev + g.table : nullptr, s);
     } else if (launches[k].kind == 1) {
       Group& g = groups[launches[k].group];
-      g.cfg.prio = launches.size() == 1 ? 1 : 0;
+      g.cfg.prio = nfork == 0 ? 1 : 0;  // priorities only where launches never overlap
       rc = mxd::launch_wave(g.cfg, dev + wbase + g.first, s);
     } else {
       rc = mxd::launch_resample(cfg, dev + wbase + nw, s);

@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 
 
-def setup(workload, nsets=2, c3_sizes=None):
+def setup(workload, nsets=2, c3_sizes=None, batch=0):
     """Two source/output sets of bench.py's workload, resident in HBM.
     Returns (capi, L, stream, sets [(src, dst, imgs, n)], mode, alg_bytes, sizes, geoms, f32)."""
     from mlx_data_amd import capi
@@ -38,7 +38,7 @@ def setup(workload, nsets=2, c3_sizes=None):
     capi.lib()
     dev = 0
     capi.check(capi.lib().mxd_set_device(dev))
-    B = bench.WORKLOADS[workload]["batch"]
+    B = batch or bench.WORKLOADS[workload]["batch"]
     sizes, geoms, f32 = bench.make_workload(capi, workload, B, 0, c3_sizes)
     C = bench.C
     elem = 4 if f32 else 1
@@ -76,9 +76,10 @@ def main():
     ap.add_argument("--set", action="append", default=[])
     ap.add_argument("--warm-s", type=float, default=1.0)
     ap.add_argument("--c3-sizes", default="", help="C3 only: WxH,... pool (default bench.C3_SIZES)")
+    ap.add_argument("--batch", type=int, default=0, help="images per launch (default: the workload's)")
     args = ap.parse_args()
     c3 = [tuple(int(v) for v in t.split("x")) for t in args.c3_sizes.split(",") if t] or None
-    capi, L, stream, sets, mode, alg, sizes, geoms, f32 = setup(args.workload, c3_sizes=c3)
+    capi, L, stream, sets, mode, alg, sizes, geoms, f32 = setup(args.workload, c3_sizes=c3, batch=args.batch)
     dev = 0
     hs = ctypes.c_void_p(stream.handle)
     e0, e1 = capi.Event(), capi.Event()
