@@ -84,6 +84,9 @@ constexpr int kLanes = 64;
 #ifndef MXD_MIN_WAVES
 #define MXD_MIN_WAVES 3
 #endif
+#ifndef MXD_SPLIT_LANES
+#define MXD_SPLIT_LANES 1
+#endif
 #ifndef MXD_MIN_WAVES_WIDE
 #define MXD_MIN_WAVES_WIDE 2
 #endif
@@ -166,6 +169,14 @@ struct Lay {
   static constexpr int PL = WPX + PAD;          // floats per plane
   static constexpr int HS = B ? C : 1;          // floats between adjacent pixels of a plane
   static constexpr int CS = B ? 1 : PL;         // floats between the channels of a pixel
+  // Split RGB lanes (default; tuning builds -DMXD_SPLIT_LANES=0 interleave): at
+  // P = 8 lane l owns pixels 4l..4l+3 and 256+4l..256+4l+3, loaded by two
+  // dwordx3 loads that each cover one contiguous 768-byte half of the window,
+  // instead of a dwordx4 and a dwordx2 interleaved over all of it.  Same bytes;
+  // C3 0.468 -> 0.451 ms per launch, C2 / C5 / C6 / C7 unchanged
+  // (profiles/r03/split.jsonl).
+  static constexpr bool SPLIT = MXD_SPLIT_LANES != 0 && C == 3 && P == 8;
+  static constexpr int HALF = kLanes * 4 * C;   // bytes per window half (SPLIT)
 };
 
 // One f32 output store (vector memory; nontemporal unless MXD_NT_STORE == 0).
@@ -215,15 +226,34 @@ __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_
 template <class L, bool SHIFT>
 struct Src {
   Rsrc live, dead;
-  int stride, voff, sh, y0;
+  int stride, voff, voff2, sh, y0;  // voff2: the second window half (L::SPLIT)
 
   __device__ __forceinline__ Raw<L::ND> load(int r) const {
     constexpr int ND = L::ND;
     const bool ok = r >= 0 && !(MXD_ABLATE & 1);
     const Rsrc rs = ok ? live : dead;
+    const uint32_t roff = ok ? (uint32_t)((r - y0) * stride) : 0u;
     // unsigned: a row above the region wraps to a huge (out-of-range) offset
-    const int off = (int)((uint32_t)voff + (ok ? (uint32_t)((r - y0) * stride) : 0u));
+    const int off = (int)((uint32_t)voff + roff);
     Raw<ND> x;
+    if constexpr (L::SPLIT) {
+      const int off2 = (int)((uint32_t)voff2 + roff);
+      constexpr int NH = ND / 2;
+      if constexpr (!SHIFT) {
+        load_dwords<NH>(rs, off, 0, x.d);
+        load_dwords<NH>(rs, off2, 0, x.d + NH);
+      } else {
+        uint32_t w[NH + 1], v[NH + 1];
+        load_dwords<NH + 1>(rs, off, 0, w);
+        load_dwords<NH + 1>(rs, off2, 0, v);
+#pragma unroll
+        for (int j = 0; j < NH; j++) {
+          x.d[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+          x.d[NH + j] = __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh);
+        }
+      }
+      return x;
+    }
     if constexpr (!SHIFT) {
       load_dwords<ND>(rs, off, 0, x.d);
     } else {
@@ -273,7 +303,7 @@ __device__ __forceinline__ void write_planes(float* planes, const float (&acc)[L
   for (int c = 0; c < C; c++)
 #pragma unroll
     for (int p = 0; p < P; p += 4)
-      *reinterpret_cast<f32x4*>(planes + c * L::PL + P * lane + p) =
+      *reinterpret_cast<f32x4*>(planes + c * L::PL + (L::SPLIT ? (p / 4) * 4 * kLanes + 4 * lane : P * lane + p)) =
           f32x4{acc[c][p], acc[c][p + 1], acc[c][p + 2], acc[c][p + 3]};
 }
 
@@ -485,7 +515,12 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
       // window start, bytes past the 4-byte aligned base of the stored region
       const int fbyte = (wp0 - sx0) * C + shift;
       src.sh = fbyte & 3;
-      src.voff = P * lane < npx ? (fbyte & ~3) + L::LB * lane : kNoLoad;
+      if constexpr (L::SPLIT) {
+        src.voff = 4 * lane < npx ? (fbyte & ~3) + 4 * C * lane : kNoLoad;
+        src.voff2 = 4 * kLanes + 4 * lane < npx ? (fbyte & ~3) + L::HALF + 4 * C * lane : kNoLoad;
+      } else {
+        src.voff = P * lane < npx ? (fbyte & ~3) + L::LB * lane : kNoLoad;
+      }
       hbase = wp0;
     }
   }
