@@ -526,7 +526,7 @@ def main():
     fresh_ms = fresh_host_ms = None
     if args.steps > 0:
         prev = capi.set_kernel_policy(args.policy | capi.MXD_POLICY_NO_DESC_CACHE)
-        k = max(10, args.steps // 2)
+        k = max(10, args.steps, int(20.0 / max(kernel_ms, 1e-3)))  # >= ~20 ms of launches (small kernels scatter)
         for i in range(40):  # untimed: every descriptor slot allocated and written (twice)
             step(i, 1)
         stream.synchronize()
