@@ -3,6 +3,9 @@
 // or written to device destinations, JPEG batches finished on the device.
 #include "capi_internal.h"
 
+#include <deque>
+#include <functional>
+
 #include <sched.h>
 
 namespace mxd {
@@ -78,6 +81,77 @@ constexpr int kCtxPerDevice = 16;
 // at once (prefetch workers already spread the work).
 std::atomic<int> g_host_calls{0};
 
+// Persistent helper threads for parallel_items (MXD_HOST_HELPERS=1, the
+// default; 0 spawns threads per call as before): a chunk's staging used to
+// start and join up to 7 std::threads, ~20 us each, for every ~24 MB chunk.
+#ifndef MXD_HOST_HELPERS
+#define MXD_HOST_HELPERS 1
+#endif
+
+class Helpers {
+ public:
+  static Helpers& get() {
+    static Helpers* h = new Helpers();  // leaked on purpose: its threads live until exit
+    return *h;
+  }
+  // Runs `work` on the calling thread and on up to `extra` helpers; returns
+  // once every helper that took part has finished it (helpers that had not
+  // started by then never will).
+  void run(int extra, const std::function<void()>& work) {
+    auto job = std::make_shared<Job>();
+    job->work = &work;
+    job->pending = extra;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while ((int)threads_.size() < std::min(extra, kMaxHelpers)) threads_.emplace_back([this] { loop(); });
+      for (int k = 0; k < extra; k++) queue_.push_back(job);
+    }
+    cv_.notify_all();
+    work();
+    int unclaimed = 0;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto it = queue_.begin(); it != queue_.end();)
+        if (*it == job) {
+          it = queue_.erase(it);
+          unclaimed++;
+        } else {
+          ++it;
+        }
+    }
+    std::unique_lock<std::mutex> lk(job->mu);
+    job->pending -= unclaimed;
+    job->cv.wait(lk, [&] { return job->pending == 0; });
+  }
+
+ private:
+  static constexpr int kMaxHelpers = 16;
+  struct Job {
+    const std::function<void()>* work = nullptr;
+    int pending = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+  };
+  void loop() {
+    for (;;) {
+      std::shared_ptr<Job> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !queue_.empty(); });
+        job = queue_.front();
+        queue_.pop_front();
+      }
+      (*job->work)();
+      std::lock_guard<std::mutex> lk(job->mu);
+      if (--job->pending == 0) job->cv.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::shared_ptr<Job>> queue_;
+  std::vector<std::thread> threads_;
+};
+
 template <class F>
 void parallel_items(int32_t first, int32_t end, int64_t bytes, F&& f) {
   const int32_t n = end - first;
@@ -96,10 +170,15 @@ void parallel_items(int32_t first, int32_t end, int64_t bytes, F&& f) {
   auto work = [&] {
     for (int32_t i; (i = next.fetch_add(1)) < end;) f(i);
   };
-  std::vector<std::thread> ts;
-  for (int k = 1; k < t; k++) ts.emplace_back(work);
-  work();
-  for (auto& th : ts) th.join();
+  if constexpr (MXD_HOST_HELPERS != 0) {
+    const std::function<void()> fn = work;
+    Helpers::get().run(t - 1, fn);
+  } else {
+    std::vector<std::thread> ts;
+    for (int k = 1; k < t; k++) ts.emplace_back(work);
+    work();
+    for (auto& th : ts) th.join();
+  }
 }
 
 class HostPool {
