@@ -26,7 +26,7 @@ struct Workspace {
   static constexpr uint64_t kFenceEvery = 8;
   static constexpr size_t kMaxFences = 8;
   struct Slot {
-    ImgDev* host = nullptr;  // pinned
+    ImgDev* host = nullptr;  // pageable copy (cache key; copy modes' source)
     ImgDev* dev = nullptr;
     ImgDev* zc = nullptr;          // pinned, read by the kernels in place (zero-copy modes)
     bool zc_nc = false;            // zc allocated non-coherent
@@ -191,14 +191,21 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   c.last_batch = ws->batch + 1;
   if (n > c.cap) {
     if (c.dev) MXD_HIP(hipFree(c.dev));
-    if (c.host) MXD_HIP(hipHostFree(c.host));
+    std::free(c.host);
     if (c.zc) MXD_HIP(hipHostFree(c.zc));
     c.dev = nullptr;
     c.host = nullptr;
     c.zc = nullptr;
     const size_t cap = std::max<size_t>(n, 64);
     MXD_HIP(hipMalloc(reinterpret_cast<void**>(&c.dev), sizeof(ImgDev) * cap));
-    MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&c.host), sizeof(ImgDev) * cap, hipHostMallocDefault));
+    // the host copy only answers "does a slot hold these descriptors" (and is
+    // the source of the copy modes 1 / 2): pageable, so 16 slots per stream
+    // cost no page-locked allocations
+    c.host = static_cast<ImgDev*>(std::malloc(sizeof(ImgDev) * cap));
+    if (!c.host) {
+      c.cap = c.count = 0;
+      return fail(MXD_ERR_NOMEM, "mxd: out of host memory for descriptors");
+    }
     c.cap = cap;
   }
   std::memcpy(c.host, descs.data(), bytes);
