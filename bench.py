@@ -320,6 +320,57 @@ def timed_steps(ranks, step, sync, steps):
     return ranks.max(t1 - t0), t1 - t0
 
 
+HEADLINE_WINDOWS = 3
+LAUNCH_WINDOWS = 3
+MIN_WINDOW_LAUNCHES = 100
+MIN_WINDOW_MS = 20.0
+
+
+def launch_windows(capi, stream, launch, sync):
+    """Average time per launch, back to back on `stream`, from HIP events
+    recorded on that stream: LAUNCH_WINDOWS windows of >= MIN_WINDOW_LAUNCHES
+    launches and >= MIN_WINDOW_MS each (sized from a 10-launch pilot).
+    Returns (median ms per launch, median host ms per call, every window's ms
+    per launch)."""
+    e0, e1 = capi.Event(), capi.Event()
+
+    def window(k):
+        sync()
+        e0.record(stream)
+        t0 = time.perf_counter()
+        for i in range(k):
+            launch(i)
+        host = (time.perf_counter() - t0) * 1e3 / k
+        e1.record(stream)
+        stream.synchronize()
+        return e0.elapsed_ms(e1) / k, host
+
+    pilot, _ = window(10)
+    k = max(MIN_WINDOW_LAUNCHES, int(MIN_WINDOW_MS / max(pilot, 1e-4)) + 1)
+    k += k % 2  # whole alternations of the input/output sets
+    runs = [window(k) for _ in range(LAUNCH_WINDOWS)]
+    ks = sorted(r[0] for r in runs)
+    hs = sorted(r[1] for r in runs)
+    return ks[len(ks) // 2], hs[len(hs) // 2], [round(v, 5) for v in (r[0] for r in runs)]
+
+
+def marketing_name(arch):
+    """The agent's "Marketing Name" from rocminfo (a child process), or None."""
+    try:
+        out = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=30).stdout
+    except (OSError, subprocess.SubprocessError):
+        return None
+    want = arch.split(":")[0]
+    name = None
+    for line in out.splitlines():
+        line = line.strip()
+        if line.startswith("Name:"):
+            name = line.split(":", 1)[1].strip()
+        elif line.startswith("Marketing Name:") and name and want and name.startswith(want):
+            return line.split(":", 1)[1].strip() or None
+    return None
+
+
 def manifest(capi, dev):
     """Run manifest: device, ROCm, host cores, decoder."""
     m = {"host_cores": host_cores(), "jpeg": "native (libjpeg-turbo ISLOW semantics, mxd_jpeg_decode)"}
@@ -328,6 +379,7 @@ def manifest(capi, dev):
         m.update(gpu=name, arch=arch, compute_units=cus)
     except Exception:  # noqa: BLE001  (a manifest never fails the bench)
         pass
+    m["gpu_marketing_name"] = marketing_name(m.get("arch", ""))
     try:
         with open("/opt/rocm/.info/version") as f:
             m["rocm"] = f.read().strip()
@@ -503,41 +555,29 @@ def main():
 
     for i in range(args.warmup + len(streams)):
         step(i)
-    wall, _ = timed_steps(ranks, step, sync_all, args.steps)
+    # The headline: the K requested steps, timed as three windows of exactly K
+    # steps each (barrier + device sync on both sides of every window); the
+    # median window is `value` / `ms_per_step` (a window of 20 C2 steps lasts
+    # ~3 ms, so a single one scatters by a few per cent).
+    walls = sorted(timed_steps(ranks, step, sync_all, args.steps)[0] for _ in range(HEADLINE_WINDOWS))
+    wall = walls[len(walls) // 2]
     # Per-launch kernel time for the roofline: the same launches back to back
-    # on ONE stream, bracketed by HIP events on that stream (the kernel's own).
-    # host_ms: the submitting thread's time per call (planning, descriptor
-    # upload, launch); when it reaches the per-launch time the loop is
-    # host-bound.
-    e0, e1 = capi.Event(), capi.Event()
-    sync_all()
-    e0.record(stream)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, 1)
-    host_ms = (time.perf_counter() - t0) * 1e3 / max(1, args.steps)
-    e1.record(stream)
-    stream.synchronize()
-    kernel_ms = e0.elapsed_ms(e1) / args.steps
+    # on ONE stream, bracketed by HIP events on that stream (the kernel's own),
+    # over windows of >= 100 launches and >= 20 ms each, independent of
+    # --steps; the median of three windows.  host_ms: the submitting thread's
+    # time per call (planning, descriptor upload, launch); when it reaches the
+    # per-launch time the loop is host-bound.
+    kernel_ms, host_ms, kernel_windows = launch_windows(capi, stream, lambda i: step(i, 1), sync_all)
 
     # The same launches with descriptor caching off: every batch uploads its
     # descriptor array (what a batch of fresh pointers costs); reported, not
-    # the headline.
+    # the headline.  Same windows.
     fresh_ms = fresh_host_ms = None
     if args.steps > 0:
         prev = capi.set_kernel_policy(args.policy | capi.MXD_POLICY_NO_DESC_CACHE)
-        k = max(10, args.steps, int(20.0 / max(kernel_ms, 1e-3)))  # >= ~20 ms of launches (small kernels scatter)
         for i in range(40):  # untimed: every descriptor slot allocated and written (twice)
             step(i, 1)
-        stream.synchronize()
-        e0.record(stream)
-        t0 = time.perf_counter()
-        for i in range(k):
-            step(i, 1)
-        fresh_host_ms = (time.perf_counter() - t0) * 1e3 / k
-        e1.record(stream)
-        stream.synchronize()
-        fresh_ms = e0.elapsed_ms(e1) / k
+        fresh_ms, fresh_host_ms, _ = launch_windows(capi, stream, lambda i: step(i, 1), sync_all)
         capi.set_kernel_policy(prev)
 
     alg_bytes = sum(footprint_bytes(capi, sw, sh, C, *g[:6]) for (sw, sh), g in zip(sizes, geoms)) + sum(out_bytes)
@@ -547,7 +587,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.workload),
                 "alg_bytes_per_launch": int(alg_bytes), "alg_bytes_per_image": round(alg_bytes / B, 1),
                 "kernel_ms_per_launch": round(kernel_ms, 5),
+                "kernel_ms_windows": kernel_windows,
                 "sustained_gbs": round(alg_bytes / (wall / max(1, args.steps)) / 1e9, 1) if args.steps else None,
+                "headline_window_ms": [round(w * 1e3, 4) for w in walls],
                 "ms_per_launch_fresh_descriptors": round(fresh_ms, 5) if fresh_ms else None,
                 "host_ms_per_call": round(host_ms, 5) if args.steps else None,
                 "host_ms_per_call_fresh": round(fresh_host_ms, 5) if fresh_host_ms else None,

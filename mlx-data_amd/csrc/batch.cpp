@@ -190,6 +190,10 @@ int upload_descs(const std::vector<ImgDev>& descs, int32_t device, void* stream,
   if (int rc = wait_batch(ws, c.last_batch, s)) return rc;
   c.last_batch = ws->batch + 1;
   if (n > c.cap) {
+    // empty first: a failed allocation below leaves an empty slot (cap 0),
+    // never a stale capacity over null buffers
+    c.cap = c.count = 0;
+    c.launch = nullptr;
     if (c.dev) MXD_HIP(hipFree(c.dev));
     std::free(c.host);
     if (c.zc) MXD_HIP(hipHostFree(c.zc));
@@ -630,6 +634,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventRecord(ws->fork, reinterpret_cast<hipStream_t>(stream)));
     for (int h = 0; h < nfork; h++) MXD_HIP(hipStreamWaitEvent(ws->helper[h], ws->fork, 0));
   }
+  int launch_rc = MXD_OK;
   for (size_t k = 0; k < launches.size(); k++) {
     const int lane = nfork > 0 ? (int)(k % (size_t)(nfork + 1)) : 0;
     void* s = lane == 0 ? stream : reinterpret_cast<void*>(ws->helper[lane - 1]);
@@ -644,15 +649,23 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     } else {
       rc = mxd::launch_resample(cfg, dev + wbase + nw, s);
     }
-    if (rc)
-      return fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
-                                      " rc=" + std::to_string(rc));
+    if (rc) {
+      launch_rc = fail(MXD_ERR_DEVICE, std::string("resample launch failed: ") + hipGetErrorString(hipGetLastError()) +
+                                           " rc=" + std::to_string(rc));
+      break;
+    }
   }
+  // Every helper stream that may hold kernels of this batch joins the
+  // caller's stream and the batch is counted -- on a failed launch too, so the
+  // slot's fence covers the kernels already queued and a caller syncing its
+  // own stream waits for their writes.
   for (int h = 0; h < nfork; h++) {
-    MXD_HIP(hipEventRecord(ws->join[h], ws->helper[h]));
-    MXD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0));
+    if (hipEventRecord(ws->join[h], ws->helper[h]) != hipSuccess ||
+        hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ws->join[h], 0) != hipSuccess)
+      if (launch_rc == MXD_OK) launch_rc = fail(MXD_ERR_DEVICE, "mxd: joining helper streams failed");
   }
-  return release_descs(ws, stream, hit);
+  const int rel = release_descs(ws, stream, hit);
+  return launch_rc != MXD_OK ? launch_rc : rel;
 }
 
 

@@ -177,7 +177,16 @@ int mxd_device_properties(int32_t device, char* name, size_t name_len, char* arc
     std::strncpy(dst, src, n - 1);
     dst[n - 1] = 0;
   };
-  put(name, name_len, p.name);
+  // hipDeviceProp_t::name came back empty on some boxes:
+  // then hipDeviceGetName, then the architecture and CU count.
+  std::string nm = p.name;
+  if (nm.empty()) {
+    char buf[256] = {0};
+    if (hipDeviceGetName(buf, sizeof buf - 1, device) == hipSuccess) nm = buf;
+  }
+  if (nm.empty()) nm = std::string(p.gcnArchName).substr(0, std::string(p.gcnArchName).find(':')) + " (" +
+                       std::to_string(p.multiProcessorCount) + " CUs)";
+  put(name, name_len, nm.c_str());
   put(arch, arch_len, p.gcnArchName);
   if (cus) *cus = p.multiProcessorCount;
   return MXD_OK;

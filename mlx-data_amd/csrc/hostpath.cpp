@@ -102,8 +102,11 @@ class Helpers {
     job->work = &work;
     job->pending = extra;
     {
+      // the pool grows to the helpers every call in flight asks for (capped),
+      // so concurrent calls (prefetch workers, split devices) each get theirs
       std::lock_guard<std::mutex> lk(mu_);
-      while ((int)threads_.size() < std::min(extra, kMaxHelpers)) threads_.emplace_back([this] { loop(); });
+      outstanding_ += extra;
+      while ((int)threads_.size() < std::min(outstanding_, kMaxHelpers)) threads_.emplace_back([this] { loop(); });
       for (int k = 0; k < extra; k++) queue_.push_back(job);
     }
     cv_.notify_all();
@@ -111,6 +114,7 @@ class Helpers {
     int unclaimed = 0;
     {
       std::lock_guard<std::mutex> lk(mu_);
+      outstanding_ -= extra;
       for (auto it = queue_.begin(); it != queue_.end();)
         if (*it == job) {
           it = queue_.erase(it);
@@ -150,6 +154,7 @@ class Helpers {
   std::condition_variable cv_;
   std::deque<std::shared_ptr<Job>> queue_;
   std::vector<std::thread> threads_;
+  int outstanding_ = 0;  // helpers asked for by the calls in flight
 };
 
 template <class F>

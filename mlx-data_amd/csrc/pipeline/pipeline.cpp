@@ -1135,20 +1135,22 @@ Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<
 }
 
 // ------------------------------------------------------------------ pool
-ThreadPool::ThreadPool(int n) {
+ThreadPool::ThreadPool(int n) : st_(std::make_shared<State>()) {
   n = std::max(n, 1);
   for (int i = 0; i < n; i++) {
-    workers_.emplace_back([this] {
+    workers_.emplace_back([st = st_] {
       for (;;) {
         std::packaged_task<Sample()> task;
         {
-          std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [this] { return stop_ || !tasks_.empty(); });
-          if (stop_ && tasks_.empty()) return;
-          task = std::move(tasks_.front());
-          tasks_.pop();
+          std::unique_lock<std::mutex> lk(st->mu);
+          st->cv.wait(lk, [&] { return st->stop || !st->tasks.empty(); });
+          if (st->stop && st->tasks.empty()) return;
+          task = std::move(st->tasks.front());
+          st->tasks.pop();
         }
         task();
+        // `task` is released here, possibly destroying this pool (see the
+        // class comment): only `st` is touched afterwards
       }
     });
   }
@@ -1156,22 +1158,35 @@ ThreadPool::ThreadPool(int n) {
 
 ThreadPool::~ThreadPool() {
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
+    std::lock_guard<std::mutex> lk(st_->mu);
+    st_->stop = true;
   }
-  cv_.notify_all();
-  for (auto& w : workers_) w.join();
+  st_->cv.notify_all();
+  const auto self = std::this_thread::get_id();
+  for (auto& w : workers_) {
+    if (w.get_id() == self)
+      w.detach();  // destroyed from its own worker: it exits once this returns
+    else
+      w.join();
+  }
+}
+
+bool ThreadPool::on_worker() const {
+  const auto self = std::this_thread::get_id();
+  for (const auto& w : workers_)
+    if (w.get_id() == self) return true;
+  return false;
 }
 
 std::future<Sample> ThreadPool::enqueue(std::function<Sample()> fn) {
   std::packaged_task<Sample()> task(std::move(fn));
   auto fut = task.get_future();
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (stop_) throw std::runtime_error("ThreadPool: enqueue on stopped pool");
-    tasks_.push(std::move(task));
+    std::lock_guard<std::mutex> lk(st_->mu);
+    if (st_->stop) throw std::runtime_error("ThreadPool: enqueue on stopped pool");
+    st_->tasks.push(std::move(task));
   }
-  cv_.notify_one();
+  st_->cv.notify_one();
   return fut;
 }
 
@@ -1278,6 +1293,10 @@ Prefetch::Prefetch(std::shared_ptr<Stream> s, int prefetch_size, int num_threads
 
 Prefetch::~Prefetch() {
   std::lock_guard<std::mutex> lk(mu_);
+  // Destroyed from one of its own workers (ThreadPool): the outstanding tasks
+  // hold their upstream, not this node, so they are left to the pool's other
+  // workers instead of waited for here (with one worker that would deadlock).
+  if (pool_->on_worker()) return;
   while (!cache_.empty()) {
     cache_.front().wait();
     cache_.pop();
@@ -1317,6 +1336,7 @@ OrderedPrefetch::OrderedPrefetch(std::shared_ptr<Buffer> b, int prefetch_size, i
 
 OrderedPrefetch::~OrderedPrefetch() {
   std::lock_guard<std::mutex> lk(mu_);
+  if (pool_->on_worker()) return;  // as in ~Prefetch
   for (auto& f : cache_)
     if (f.valid()) f.wait();
   cache_.clear();

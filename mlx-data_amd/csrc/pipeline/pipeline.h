@@ -315,18 +315,28 @@ Sample merge_batch(const std::vector<Sample>& samples, const std::unordered_map<
                    const std::unordered_map<std::string, int>& dims, const DeviceOut& out = {});
 
 // ---------------------------------------------------------------- threads
+// Workers share the queue state with the pool, so the pool may be destroyed
+// from one of its own workers: a finished task's result can hold the last
+// reference to the pipeline that owns the pool (an exception carrying a
+// Python traceback, released on the worker).  That worker is detached
+// instead of joined and leaves its loop through the shared state.
 class ThreadPool {
  public:
   explicit ThreadPool(int n);
   ~ThreadPool();
   std::future<Sample> enqueue(std::function<Sample()> fn);
+  // Whether the calling thread is one of this pool's workers.
+  bool on_worker() const;
 
  private:
+  struct State {
+    std::queue<std::packaged_task<Sample()>> tasks;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool stop = false;
+  };
+  std::shared_ptr<State> st_;
   std::vector<std::thread> workers_;
-  std::queue<std::packaged_task<Sample()>> tasks_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stop_ = false;
 };
 
 // ---------------------------------------------------------------- buffers
