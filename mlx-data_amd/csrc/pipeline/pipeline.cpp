@@ -289,31 +289,52 @@ DeviceWorkers& device_workers() {
   return *w;
 }
 
+}  // namespace
+
+// Slices of an n-image batch over `ndev` devices, starting at device index
+// `first` (round-robin counter): a batch whose per-device slice would hold
+// fewer than kMinSliceImages images is not split -- the whole batch goes to
+// one device and consecutive batches rotate over the devices (Caltech's batch
+// 32 on 8 GPUs: 8 prefetch workers, each batch one call on its own device,
+// instead of every batch as 8 synchronous calls of 4 images); larger batches
+// are cut into contiguous slices [s n / k, (s + 1) n / k) (op/Shard.cpp:11-20's
+// contiguous split; the order of the batch is kept), k = min(ndev,
+// n / kMinSliceImages) (C4's 1024 over 8 GPUs: 8 slices of 128).
+std::vector<Slice> split_batch(int64_t n, int64_t ndev, uint64_t first) {
+  std::vector<Slice> out;
+  if (n <= 0 || ndev <= 0) return out;
+  const int64_t k = std::max<int64_t>(1, std::min<int64_t>(ndev, n / kMinSliceImages));
+  for (int64_t s = 0; s < k; s++)
+    out.push_back(Slice{(int64_t)((first + (uint64_t)s) % (uint64_t)ndev), s * n / k, (s + 1) * n / k});
+  return out;
+}
+
+namespace {
+
 // Runs the jobs into host destinations (one fused launch per device and
-// source kind).  Several devices: contiguous slices [k n / D, (k + 1) n / D)
-// (op/Shard.cpp:11-20's contiguous split; the order of the batch is kept),
-// slice 0 on the calling thread, the others on their devices' persistent
-// workers; the first failing slice's message wins.
+// source kind) over split_batch's slices: slice 0 on the calling thread, the
+// others on their devices' persistent workers; the first failing slice's
+// message wins.
 void run_host(const std::vector<Job>& jobs, int32_t dtype) {
   if (jobs.empty()) return;
   const std::vector<int> devs = devices();
   if (devs.empty()) throw std::runtime_error("mxd: no HIP device visible (the image path runs only on the GPU)");
   const size_t n = jobs.size();
-  const size_t k = std::min(devs.size(), n);
-  const uint64_t first = g_rr.fetch_add(k);
-  if (k == 1) {
-    check(run_on(jobs.data(), n, dtype, devs[first % devs.size()], false));
+  const size_t k = (size_t)std::max<int64_t>(1, std::min<int64_t>((int64_t)devs.size(), (int64_t)n / kMinSliceImages));
+  const std::vector<Slice> sl = split_batch((int64_t)n, (int64_t)devs.size(), g_rr.fetch_add(k));
+  if (sl.size() == 1) {
+    check(run_on(jobs.data(), n, dtype, devs[sl[0].device], false));
     return;
   }
-  auto slice = [&jobs, n, k, dtype, &devs, first](size_t s) -> std::string {
-    const size_t b = s * n / k, e = (s + 1) * n / k;
-    if (run_on(jobs.data() + b, e - b, dtype, devs[(first + s) % devs.size()], false) != MXD_OK)
+  auto slice = [&jobs, dtype, &devs, &sl](size_t s) -> std::string {
+    if (run_on(jobs.data() + sl[s].begin, (size_t)(sl[s].end - sl[s].begin), dtype, devs[sl[s].device], false) !=
+        MXD_OK)
       return mxd_last_error();  // thread-local: read on the failing thread
     return std::string();
   };
   std::vector<std::future<std::string>> pending;
-  for (size_t s = 1; s < k; s++)
-    pending.push_back(device_workers().submit(devs[(first + s) % devs.size()], [&slice, s] { return slice(s); }));
+  for (size_t s = 1; s < sl.size(); s++)
+    pending.push_back(device_workers().submit(devs[sl[s].device], [&slice, s] { return slice(s); }));
   std::string err;
   try {
     err = slice(0);

@@ -112,6 +112,13 @@ std::shared_ptr<Array> check_key(const Sample& s, const std::string& key);
 // offsets, so the batch is identical to a single-device one.
 void set_devices(const std::vector<int>& devices);
 std::vector<int> devices();
+// How run_host splits a batch of n images over ndev devices (pipeline.cpp).
+constexpr int64_t kMinSliceImages = 64;
+struct Slice {
+  int64_t device;      // index into devices()
+  int64_t begin, end;  // images [begin, end) of the batch
+};
+std::vector<Slice> split_batch(int64_t n, int64_t ndev, uint64_t first);
 
 // load_image's JPEG route: on (the default when a device is visible), only
 // the entropy decode runs in load_image and the GPU finishes the decode inside

@@ -496,6 +496,16 @@ PYBIND11_MODULE(_pipeline, m) {
 
   m.def("set_state", &set_state, py::arg("seed") = 1234);
   m.def("set_devices", &set_devices, py::arg("devices"));
+  // diagnostics: how a batch of n images is split over ndev devices
+  m.def(
+      "_split_batch",
+      [](int64_t n, int64_t ndev, uint64_t first) {
+        std::vector<std::tuple<int64_t, int64_t, int64_t>> out;
+        for (const Slice& s : split_batch(n, ndev, first)) out.emplace_back(s.device, s.begin, s.end);
+        return out;
+      },
+      py::arg("n"), py::arg("ndev"), py::arg("first") = 0);
+  m.attr("_MIN_SLICE_IMAGES") = kMinSliceImages;
   m.def("devices", &devices);
   m.def("set_device_decode", &set_device_decode, py::arg("on"));
   m.def("device_decode", &device_decode);

@@ -18,8 +18,9 @@ mirror of the whole batch as one fused GPU launch and writes the stacked
 build's one addition to the surface) replaces the trailing
 ``key_transform(..., lambda x: x.astype("float32") / 255)``: the same launch
 then writes the float32 batch, bit-identical to that lambda.  With several
-devices (``set_devices``) one batch is split into contiguous slices, one per
-device.  ``batch(n, device=d)`` builds the image keys' batches in device
+devices (``set_devices``) a batch of at least 64 images per device is split
+into contiguous slices, one per device; smaller batches go whole to one
+device, consecutive batches rotating over the devices.  ``batch(n, device=d)`` builds the image keys' batches in device
 memory instead (``DeviceArray``: DLPack producer, ``numpy()`` copies back);
 import torch before this package when torch consumes them, so both share one
 HIP runtime.  Reading an unbatched image materialises it with its own launch.

@@ -6,8 +6,10 @@
   of its trailing ``key_transform(lambda x: x.astype("float32") / 255)``.
 - batch with mixed channel counts pads the channel dim like array::batch
   (Array.cpp:465-498, BatchShape::add), pending or materialised (ADVICE r1).
-- one batch split over several devices: contiguous slices in one host
-  thread each, identical to the single-device batch (VERDICT r1 missing 2).
+- one batch split over several devices: contiguous slices of >= 64 images
+  in one host thread each, identical to the single-device batch (VERDICT r1
+  missing 2); smaller batches go whole to one device, rotating (VERDICT r3
+  weak 6).
 """
 import numpy as np
 import pytest
@@ -130,20 +132,30 @@ def test_mixed_channel_resized_batch():
         assert (got[k, :, :, c:] == 0).all()
 
 
+def small_samples(n, seed=0):
+    """n small images of mixed shapes (split tests need >= 64 images a slice)."""
+    shapes = [(48, 64), (75, 100), (100, 75), (60, 90), (97, 131)]
+    return [dict(image=synth(*shapes[i % len(shapes)], 3, seed + i), idx=np.int64(i)) for i in range(n)]
+
+
 def test_batch_split_over_devices_matches_single_device():
-    """set_devices([0, 0, 0]): three slices from three host threads onto the
+    """set_devices([0, 0, 0]) with a 200-image batch: three slices (>= 64
+    images each, pipeline.cpp split_batch) from three host threads onto the
     same card; the batch equals the one-device batch byte for byte, and a
     failing slice surfaces its message."""
-    samples = c2_samples(11, seed=40)
+    from mlx_data_amd import _pipeline
+
+    samples = small_samples(200, seed=40)
+    assert len(_pipeline._split_batch(200, 3)) == 3
 
     def run(devs):
         dx.set_devices(devs)
-        d = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 256)
-             .image_random_crop("image", 224, 224).image_random_h_flip("image", 0.5))
+        d = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 72)
+             .image_random_crop("image", 64, 64).image_random_h_flip("image", 0.5))
         dx.set_state(7)
-        u = d.batch(11)[0]["image"]
+        u = d.batch(200)[0]["image"]
         dx.set_state(7)
-        return u, d.image_to_float("image").batch(11)[0]["image"]
+        return u, d.image_to_float("image").batch(200)[0]["image"]
 
     u1, f1 = run([0])
     u3, f3 = run([0, 0, 0])
@@ -151,9 +163,34 @@ def test_batch_split_over_devices_matches_single_device():
     assert np.array_equal(f1.view(np.uint32), LUT[u1].view(np.uint32))
     # a failing slice (device 99 does not exist) surfaces its message
     dx.set_devices([0, 99])
-    bad = dx.buffer_from_vector(samples[:4]).image_resize("image", 32, 32)
+    bad = dx.buffer_from_vector(samples[:128]).image_resize("image", 32, 32)
     with pytest.raises(RuntimeError, match="invalid device 99"):
-        bad.batch(4)[0]
+        bad.batch(128)[0]
+
+
+def test_small_batches_route_whole_to_one_device():
+    """Caltech's shape on eight devices: batch 32 under prefetch(8, 8) with
+    set_devices([0] * 8).  A 32-image batch is below the 64-image slice
+    threshold, so each batch is one call on one device, consecutive batches
+    rotating over the devices (split_batch) -- and every
+    image equals its one-device form (prefetch interleaves the pulls, so
+    batches are compared image by image, keyed by a per-sample index)."""
+    from mlx_data_amd import _pipeline
+
+    assert _pipeline._split_batch(32, 8, 5) == [(5, 0, 32)]
+    samples = small_samples(256, seed=43)
+    dx.set_devices([0])
+    want = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 72)
+            .image_center_crop("image", 64, 64).image_to_float("image").batch(256))[0]["image"]
+    dx.set_devices([0] * 8)
+    s = (dx.buffer_from_vector(samples).to_stream().image_resize_smallest_side("image", 72)
+         .image_center_crop("image", 64, 64).image_to_float("image").batch(32).prefetch(8, 8))
+    seen = []
+    for b in s:
+        for k, i in enumerate(b["idx"].tolist()):
+            assert np.array_equal(b["image"][k].view(np.uint32), want[i].view(np.uint32)), i
+            seen.append(i)
+    assert sorted(seen) == list(range(256))
 
 
 def test_batch_split_over_every_visible_device():
@@ -165,12 +202,12 @@ def test_batch_split_over_every_visible_device():
     n = capi.device_count()
     if n < 2:
         pytest.skip("one device visible")
-    samples = c2_samples(2 * n + 1, seed=41)
+    samples = small_samples(64 * n + 1, seed=41)
 
     def run(devs):
         dx.set_devices(devs)
-        d = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 256)
-             .image_center_crop("image", 224, 224).image_to_float("image"))
+        d = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 72)
+             .image_center_crop("image", 64, 64).image_to_float("image"))
         return d.batch(len(samples))[0]["image"]
 
     one = run([0])
@@ -179,20 +216,20 @@ def test_batch_split_over_every_visible_device():
 
 
 def test_split_batches_under_prefetch_reuse_workers():
-    """Many split batches from prefetch threads at once (slices 1.. on the
-    per-device workers, at most four per device): every image equals its
-    one-device form (prefetch workers interleave their pulls, so batches are
-    compared image by image, keyed by a per-sample index)."""
-    samples = [dict(s, idx=np.int64(i)) for i, s in enumerate(c2_samples(24, seed=42))]
+    """Many split batches from prefetch threads at once (128-image batches
+    over [0, 0, 0]: two slices each, slice 1 on the per-device workers, at most
+    four per device): every image equals its one-device form (compared image
+    by image, keyed by a per-sample index)."""
+    samples = small_samples(768, seed=42)
     dx.set_devices([0])
-    want = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 256)
-            .image_center_crop("image", 224, 224).batch(24))[0]["image"]
+    want = (dx.buffer_from_vector(samples).image_resize_smallest_side("image", 72)
+            .image_center_crop("image", 64, 64).batch(768))[0]["image"]
     dx.set_devices([0, 0, 0])
-    s = (dx.buffer_from_vector(samples).to_stream().image_resize_smallest_side("image", 256)
-         .image_center_crop("image", 224, 224).batch(6).prefetch(4, 4))
+    s = (dx.buffer_from_vector(samples).to_stream().image_resize_smallest_side("image", 72)
+         .image_center_crop("image", 64, 64).batch(128).prefetch(4, 4))
     seen = []
     for b in s:
         for k, i in enumerate(b["idx"].tolist()):
             assert np.array_equal(b["image"][k], want[i]), i
             seen.append(i)
-    assert sorted(seen) == list(range(24))
+    assert sorted(seen) == list(range(768))

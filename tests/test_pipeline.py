@@ -366,3 +366,30 @@ def test_dropping_a_busy_prefetch_does_not_deadlock():
     t.start()
     t.join(timeout=20)
     assert done.is_set()
+
+
+def test_split_batch_routing():
+    """pipeline.cpp split_batch: below 64 images per
+    device slice a batch goes whole to one device, consecutive batches
+    rotating over the devices; larger batches are cut into contiguous slices
+    (op/Shard.cpp:11-20), k = min(devices, n // 64), covering [0, n) in order."""
+    from mlx_data_amd import _pipeline as P
+
+    assert P._MIN_SLICE_IMAGES == 64
+    # Caltech: batch 32 on 8 devices -> one call, device = the rotation counter
+    for first in range(10):
+        assert P._split_batch(32, 8, first) == [(first % 8, 0, 32)]
+    assert P._split_batch(127, 8, 0) == [(0, 0, 127)]
+    assert P._split_batch(128, 8, 3) == [(3, 0, 64), (4, 64, 128)]
+    # C4: 1024 over 8 devices -> 8 slices of 128, one per device
+    sl = P._split_batch(1024, 8, 6)
+    assert [d for d, _, _ in sl] == [6, 7, 0, 1, 2, 3, 4, 5]
+    assert [(b, e) for _, b, e in sl] == [(128 * k, 128 * (k + 1)) for k in range(8)]
+    for n in (1, 63, 64, 65, 200, 511, 513, 4096):
+        for nd in (1, 2, 3, 8):
+            sl = P._split_batch(n, nd, 0)
+            assert len(sl) == max(1, min(nd, n // 64))
+            assert sl[0][1] == 0 and sl[-1][2] == n
+            assert all(a[2] == b[1] for a, b in zip(sl, sl[1:]))
+            assert all(e - b >= min(n, 64) for _, b, e in sl)
+    assert P._split_batch(0, 8, 0) == []

@@ -25,4 +25,5 @@ run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/
 cut -c1-220 gpurun_out/${TAG}_prof/run_kernel_stats.csv
 run prof_1stream 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof1 -o run -- python3 bench.py --streams 1 --no-cpu --no-e2e
 cut -c1-220 gpurun_out/${TAG}_prof1/run_kernel_stats.csv
+if [ -x tools/inflight_probe ]; then run inflight 300 tools/inflight_probe; cat gpurun_out/${TAG}_inflight.log; fi
 exit 0
