@@ -356,10 +356,14 @@ def launch_windows(capi, stream, launch, sync):
 
 def marketing_name(arch):
     """The agent's "Marketing Name" from rocminfo (a child process), or None."""
-    try:
-        out = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=30).stdout
-    except (OSError, subprocess.SubprocessError):
-        return None
+    out = ""
+    for exe in ("rocminfo", "/opt/rocm/bin/rocminfo"):
+        try:
+            out = subprocess.run([exe], capture_output=True, text=True, timeout=30).stdout
+        except (OSError, subprocess.SubprocessError):
+            continue
+        if out:
+            break
     want = arch.split(":")[0]
     name = None
     for line in out.splitlines():

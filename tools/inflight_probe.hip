@@ -41,13 +41,21 @@ typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
 using Rsrc = __amdgpu_buffer_rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int kRows = 960, kStride = 3840, kImgs = 256;
-constexpr int kFy0 = 56, kFy1 = 900, kFb0 = 640, kNeed = 2532;  // footprint rows / bytes
-constexpr int kOutRows = 224, kOutRow = 2688;                      // f32 output row bytes
-constexpr int kStrips = 2, kWin = 1284, kHalf = 768, kStripStep = 1248;
 constexpr int kNoLoad = 0x7ffffff0;
 constexpr int kWaves = 8;
+constexpr int kHalf = 768;  // bytes one dwordx3-per-lane wave instruction covers
 constexpr int kSlot = 2 * kHalf;  // LDS bytes per ring slot (one row, two halves)
+
+// Source / output geometry of one workload shape.
+struct Geo {
+  const char* name;
+  int imgs, rows, stride;  // images of rows x stride bytes
+  int fy0, fy1, fb0;       // footprint rows [fy0, fy1), first footprint byte
+  int strips, win, step;   // strips per row, window bytes per strip (<= 2 kHalf), strip step bytes
+  float ratio;             // source rows per output row
+  int out_px, out_elem;    // output pixels per strip row, bytes per channel (4 f32, 1 u8)
+  double bytes;            // algorithmic bytes per launch
+};
 
 __device__ __forceinline__ void wait_vm(int n) {
 #define VMC(k)                                              \
@@ -82,7 +90,9 @@ __device__ __forceinline__ void consume(const Row& r, float (&acc)[2][24], float
 
 template <int MODE, int D>
 __global__ __launch_bounds__(kWaves * 64) void probe(const uint8_t* __restrict__ base, float* __restrict__ out,
-                                                     int nbands) {
+                                                     int nbands, Geo g) {
+  const int kStrips = g.strips, kRows = g.rows, kStride = g.stride, kImgs = g.imgs, kFy0 = g.fy0, kFy1 = g.fy1;
+  const int kOutRows = 224, kOutRow = 224 * 3 * g.out_elem;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wave);
@@ -93,12 +103,12 @@ __global__ __launch_bounds__(kWaves * 64) void probe(const uint8_t* __restrict__
   const int band = rest / kStrips, strip = rest - band * kStrips;
   const uint8_t* p = base + (size_t)img * kRows * kStride;
   const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, kRows * kStride, 0x00020000);
-  const int b0 = kFb0 + strip * kStripStep;
-  const int va = b0 + 12 * lane;
-  const int vb = 12 * lane + kHalf < kWin ? b0 + kHalf + 12 * lane : kNoLoad;
+  const int b0 = g.fb0 + strip * g.step;
+  const int va = 12 * lane < g.win ? b0 + 12 * lane : kNoLoad;
+  const int vb = 12 * lane + kHalf < g.win ? b0 + kHalf + 12 * lane : kNoLoad;
   const int oy0 = band * kOutRows / nbands, oy1 = (band + 1) * kOutRows / nbands;
-  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
-  char* o = reinterpret_cast<char*>(out) + (size_t)img * kOutRows * kOutRow + strip * (112 * 12);
+  const int r0 = kFy0 + (int)(oy0 * g.ratio), r1 = min(kFy1, kFy0 + (int)(oy1 * g.ratio) + 4);
+  char* o = reinterpret_cast<char*>(out) + (size_t)img * kOutRows * kOutRow + strip * (g.out_px * 3 * g.out_elem);
   char* ring = smem + wave * (D * kSlot);  // MODE 1: this wave's slots
   float acc[2][24];
 #pragma unroll
@@ -140,17 +150,22 @@ __global__ __launch_bounds__(kWaves * 64) void probe(const uint8_t* __restrict__
       if constexpr (MODE == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before refilling
       issue(d, row + d + D);
       consume(r, acc, 0.25f, 0.125f);
-      const int want = (int)((row + d - r0) / 3.768f) + oy0;
+      const int want = (int)((row + d - r0) / g.ratio) + oy0;
       if (want > oy && oy < oy1) {
         char* orow = o + (size_t)oy * kOutRow;
         float sum[3] = {0.0f, 0.0f, 0.0f};  // every accumulator feeds the stores (none is dead code)
 #pragma unroll
         for (int i = 0; i < 24; i++) sum[i % 3] += acc[0][i];
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
+        for (int q = 0; q < 4; q++) {
           const int px = lane + 64 * q;
-          if (px < 112)
-            __builtin_nontemporal_store(f32x3{sum[0] + q, sum[1], sum[2]}, reinterpret_cast<f32x3*>(orow + 12 * px));
+          if (px < g.out_px) {
+            if (g.out_elem == 4) {
+              __builtin_nontemporal_store(f32x3{sum[0] + q, sum[1], sum[2]}, reinterpret_cast<f32x3*>(orow + 12 * px));
+            } else {  // u8: three byte stores per pixel, like the product kernel
+              orow[3 * px] = (char)sum[0], orow[3 * px + 1] = (char)sum[1], orow[3 * px + 2] = (char)(sum[2] + q);
+            }
+          }
         }
 #pragma unroll
         for (int i = 0; i < 24; i++) acc[0][i] = acc[1][i], acc[1][i] = 0.0f;
@@ -187,7 +202,9 @@ double timeit(const char* name, double bytes, const std::function<void()>& f) {
 }
 
 template <int MODE, int D>
-void run(const uint8_t* const* srcs, float* const* outs, double bytes, int cus) {
+void run(const uint8_t* const* srcs, float* const* outs, const Geo& g, int cus) {
+  const double bytes = g.bytes;
+  const int kImgs = g.imgs, kStrips = g.strips;
   const int lds_need = MODE == 1 ? kWaves * D * kSlot : 0;
   for (int wgs : {1, 2, 3, 4}) {  // workgroups (of 8 waves) per CU
     const int lds = 160 * 1024 / wgs - 64;
@@ -202,18 +219,32 @@ void run(const uint8_t* const* srcs, float* const* outs, double bytes, int cus) 
     if (nbands < 1) nbands = 1;
     const int units = kImgs * kStrips * nbands;
     char name[128];
-    snprintf(name, sizeof name, "%s D=%-2d  %d WG/CU (%2d waves/CU) bands=%d", MODE ? "lds" : "reg", D, wgs,
-             wgs * kWaves, nbands);
+    snprintf(name, sizeof name, "%-12s %s D=%-2d %d WG/CU (%2d waves/CU) bands=%d", g.name, MODE ? "lds" : "reg", D,
+             wgs, wgs * kWaves, nbands);
     CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     timeit(name, bytes, [&] {
       hipLaunchKernelGGL(k, dim3((units + kWaves - 1) / kWaves), dim3(kWaves * 64), lds, 0, srcs[g_iter & 1],
-                         outs[g_iter & 1], nbands);
+                         outs[g_iter & 1], nbands, g);
     });
   }
 }
 
-int main() {
-  const size_t sbytes = (size_t)kImgs * kRows * kStride, obytes = (size_t)kImgs * kOutRows * kOutRow;
+int main(int argc, char** argv) {
+  // C2: 256 x 1280x960 -> 341x256 -> 224 f32: footprint 844 rows x 844 px,
+  // two strips of 1284 B (P = 8 split lanes), 3.768 source rows per output row.
+  const Geo c2{"c2", 256, 960, 3840, 56, 900, 640, 2, 1284, 1248, 3.768f, 112, 4,
+               256.0 * (844.0 * 844 * 3 + 224.0 * 224 * 12)};
+  // C3's 480p shape: 512 x 640x480 -> 341x256 -> 224 u8: footprint ~424 x 424 px,
+  // narrow lanes (P = 4): two strips of 636 B; 1.875 source rows per output row.
+  const Geo p480{"480p-2strip", 512, 480, 1920, 28, 452, 174, 2, 636, 636, 1.875f, 112, 1,
+                 512.0 * (424.0 * 424 * 3 + 224.0 * 224 * 3)};
+  // the same shape read as one 1272-B strip per row (wide lanes, 4 pixels per lane out)
+  const Geo p480w{"480p-1strip", 512, 480, 1920, 28, 452, 174, 1, 1272, 0, 1.875f, 224, 1,
+                  512.0 * (424.0 * 424 * 3 + 224.0 * 224 * 3)};
+  const bool only480 = argc > 1 && argv[1][0] == '4';
+  const size_t sbytes = (size_t)512 * 480 * 1920 > (size_t)256 * 960 * 3840 ? (size_t)512 * 480 * 1920
+                                                                            : (size_t)256 * 960 * 3840;
+  const size_t obytes = (size_t)256 * 224 * 224 * 12;
   uint8_t *s0, *s1;
   float *o0, *o1;
   CHECK(hipMalloc(&s0, sbytes));
@@ -226,22 +257,22 @@ int main() {
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const uint8_t* srcs[2] = {s0, s1};
   float* outs[2] = {o0, o1};
-  // footprint reads (2 strips x 1284 B of 844 rows, with the 4-row band halo
-  // ignored) + f32 writes: the algorithmic bytes of C2 (2,739,120 B / image)
-  const double bytes = (double)kImgs * (844.0 * 844 * 3 + 224.0 * 224 * 12);
-  printf("# %d CUs; algorithmic bytes per launch %.0f\n", cus, bytes);
-  run<0, 2>(srcs, outs, bytes, cus);
-  run<0, 3>(srcs, outs, bytes, cus);
-  run<0, 4>(srcs, outs, bytes, cus);
-  run<0, 6>(srcs, outs, bytes, cus);
-  run<0, 8>(srcs, outs, bytes, cus);
-  run<0, 12>(srcs, outs, bytes, cus);
-  run<1, 2>(srcs, outs, bytes, cus);
-  run<1, 3>(srcs, outs, bytes, cus);
-  run<1, 4>(srcs, outs, bytes, cus);
-  run<1, 6>(srcs, outs, bytes, cus);
-  run<1, 8>(srcs, outs, bytes, cus);
-  run<1, 12>(srcs, outs, bytes, cus);
-  run<1, 16>(srcs, outs, bytes, cus);
+  printf("# %d CUs\n", cus);
+  for (const Geo* g : {&p480, &p480w, &c2}) {
+    if (only480 && g == &c2) continue;
+    printf("# %s: algorithmic bytes per launch %.0f\n", g->name, g->bytes);
+    run<0, 2>(srcs, outs, *g, cus);
+    run<0, 3>(srcs, outs, *g, cus);
+    run<0, 4>(srcs, outs, *g, cus);
+    run<0, 6>(srcs, outs, *g, cus);
+    run<0, 8>(srcs, outs, *g, cus);
+    run<0, 12>(srcs, outs, *g, cus);
+    run<1, 2>(srcs, outs, *g, cus);
+    run<1, 4>(srcs, outs, *g, cus);
+    run<1, 6>(srcs, outs, *g, cus);
+    run<1, 8>(srcs, outs, *g, cus);
+    run<1, 12>(srcs, outs, *g, cus);
+    run<1, 16>(srcs, outs, *g, cus);
+  }
   return 0;
 }
