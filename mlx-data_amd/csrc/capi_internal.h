@@ -168,6 +168,7 @@ struct ImgPlan {
 // s = 0: taps not monotone (not a geometry the scatter kernel handles).
 struct ScatterShape {
   int32_t s = 0, dmax = 0, p = 0;
+  int32_t lane_bytes = 0;  // of the kernel that runs it (its ring: resample.h scatter_ring_slots)
 };
 ScatterShape scatter_shape(const DevTable& t, int32_t off, int32_t len);
 

@@ -65,7 +65,7 @@ class SchedCache {
   int get(int32_t device, const DevTable& yt, int32_t src_h, int32_t resize_h, int32_t crop_y, int32_t crop_h,
           int32_t ty, const ScatterShape& sh, const DevSched** out) {
     std::lock_guard<std::mutex> lock(mu_);
-    const auto key = std::make_tuple(device, src_h, resize_h, crop_y, crop_h, ty, sh.s, sh.dmax, sh.p);
+    const auto key = std::make_tuple(device, src_h, resize_h, crop_y, crop_h, ty, sh.s, sh.dmax, sh.p, sh.lane_bytes);
     auto it = map_.find(key);
     if (it != map_.end()) {
       *out = it->second.get();
@@ -87,7 +87,8 @@ class SchedCache {
   static bool build(const DevTable& yt, int32_t crop_y, int32_t crop_h, int32_t ty, const ScatterShape& sh,
                     std::vector<int32_t>* words, DevSched* d) {
     const int32_t S = sh.s, D = sh.dmax, P = sh.p;
-    const int32_t la = mxd::scatter_ring_slots(D) - 1, bg = mxd::scatter_block_groups(S, D);
+    const int32_t la = mxd::scatter_ring_slots(D, sh.lane_bytes) - 1,
+                  bg = mxd::scatter_block_groups(S, D, sh.lane_bytes);
     const int32_t E = mxd::scatter_entry_words(S);
     const int32_t nb = (crop_h + ty - 1) / ty;
     const int32_t gmax = (P + ty + bg - 1) / bg * bg;
@@ -130,7 +131,7 @@ class SchedCache {
   }
 
   std::mutex mu_;
-  std::map<std::tuple<int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t>,
+  std::map<std::tuple<int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t>,
            std::unique_ptr<DevSched>>
       map_;
 };
