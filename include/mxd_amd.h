@@ -164,14 +164,18 @@ int mxd_set_kernel_policy(int32_t policy);
  * (the default): the host stores the array into device memory through the
  * large PCI BAR, falling back to 4 without one);
  * MXD_TUNE_STREAMS: streams the launches of a mixed batch (one per kernel
- * shape) spread over (1: all on the caller's stream; default 2, at most 4). */
+ * shape) spread over (1: all on the caller's stream; default 2, at most 4);
+ * MXD_TUNE_HUFF_BITS: shortest subsequence (bits, a multiple of 32) of the
+ * device entropy decode (default 512; tests force short ones so many
+ * subsequences must synchronise). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
   MXD_TUNE_BAND_GRID = 2,
   MXD_TUNE_DESC = 3,
   MXD_TUNE_STREAMS = 4,
-  MXD_TUNE_COUNT = 5
+  MXD_TUNE_HUFF_BITS = 5,
+  MXD_TUNE_COUNT = 6
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 
@@ -282,6 +286,18 @@ typedef struct mxd_jpeg_coefs mxd_jpeg_coefs;
 /* Entropy-decodes `data` (which may be freed afterwards) into *out; release
  * with mxd_jpeg_coefs_free.  MXD_ERR_INVALID with libjpeg's message. */
 int mxd_jpeg_coefs_decode(const uint8_t* data, size_t size, mxd_jpeg_coefs** out);
+/* The same with the Huffman decode optionally left to the GPU
+ * (device_entropy != 0): a baseline / extended-sequential file whose one scan
+ * carries every component (grey, YCbCr or RGB), complete up to a marker after
+ * its entropy-coded data, with its restart markers in sequence, is only
+ * parsed here; mxd_jpeg_resize_crop_host / _to_device then decode its
+ * segments on the device (csrc/jpeghuff.hip), mxd_jpeg_coefs_finish on the
+ * host.  Any other file is entropy-decoded here, as by mxd_jpeg_coefs_decode.
+ * The bytes are copied (`data` may be freed after the call); every route
+ * gives mxd_jpeg_decode's bytes. */
+int mxd_jpeg_coefs_parse(const uint8_t* data, size_t size, int32_t device_entropy, mxd_jpeg_coefs** out);
+/* *pending = 1 when the coefficients will come from the device entropy decode. */
+int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending);
 int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs);
 
 /* Image size; *device_ok = 1 when the GPU can finish it (grey, YCbCr or RGB;

@@ -441,6 +441,21 @@ int mxd_jpeg_coefs_decode(const uint8_t* data, size_t size, mxd_jpeg_coefs** out
   return MXD_OK;
 }
 
+int mxd_jpeg_coefs_parse(const uint8_t* data, size_t size, int32_t device_entropy, mxd_jpeg_coefs** out) {
+  if (!data || !out) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  std::string err;
+  mxd::jpeg::Coefs* c = mxd::jpeg::parse_coefs(data, size, device_entropy != 0, &err);
+  if (!c) return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
+  *out = reinterpret_cast<mxd_jpeg_coefs*>(c);
+  return MXD_OK;
+}
+
+int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending) {
+  if (!coefs || !pending) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  *pending = mxd::jpeg::coef_info(coefs_of(coefs)).entropy_pending ? 1 : 0;
+  return MXD_OK;
+}
+
 int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs) {
   mxd::jpeg::free_coefs(reinterpret_cast<mxd::jpeg::Coefs*>(coefs));
   return MXD_OK;

@@ -30,6 +30,7 @@
 #include "band_plan.h"
 #include "jpeg.h"
 #include "jpegdev.h"
+#include "jpeghuff.h"
 #include "pixmap.h"
 #include "resample.h"
 #include "taps.h"

@@ -295,6 +295,24 @@ struct JpegChunk {
   int64_t planes_off = 0, imgs_off = 0, q_off = 0, end = 0;  // in the staged input
   int64_t samples = 0, rgb_off = 0, mid_bytes = 0;             // in dev_mid
   int64_t nblocks = 0, max_quad_rows = 0;
+  // Device entropy decode of the chunk's pending images (jpeghuff.h): their
+  // unstuffed segments (words_off..), tables, image / segment / job records in
+  // the staged input; their coefficients in dev_in past the staged bytes
+  // ([coef_off, dev_end), written by the decode, never copied).
+  std::vector<mxd::HuffDev> htabs;
+  std::vector<mxd::HuffImgDev> himgs;
+  std::vector<mxd::HuffSegDev> hsegs;
+  std::vector<mxd::HuffJobDev> hjobs;
+  struct Raw {
+    const uint8_t *b, *e;  // raw segment bytes
+    int64_t at;            // staged byte offset (relative to words_off)
+  };
+  std::vector<Raw> raw;              // per hsegs entry
+  std::vector<int32_t> seg_first;    // per chunk image: its first hsegs entry (-1: not pending)
+  std::vector<int32_t> seg_count;    // and their number
+  int64_t words_off = 0, words_bytes = 0, htabs_off = 0, himgs_off = 0, hsegs_off = 0, hjobs_off = 0;
+  int64_t coef_off = 0, dev_end = 0;
+  int32_t huff_threads = 0;
 };
 
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
@@ -308,6 +326,80 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
   JpegChunk& c = *out;
   c = JpegChunk();
   auto up = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
+  int64_t coef_rel = 0;  // pending images' coefficients, relative to coef_off
+  std::vector<int64_t> pend_rel(end - first, -1);
+  c.seg_first.assign(end - first, -1);
+  c.seg_count.assign(end - first, 0);
+  for (int32_t i = first; i < end; i++) {
+    const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
+    if (!info.entropy_pending) continue;
+    const mxd::jpeg::EntropyScan es = mxd::jpeg::entropy_scan(coefs_of(jimg[i].coefs));
+    pend_rel[i - first] = coef_rel;
+    mxd::HuffImgDev h{};
+    h.coef = coef_rel / 2;  // coef_off added below
+    for (int k = 0; k < info.ncomp && k < 3; k++) {
+      h.plane[k] = info.comp[k].off;
+      h.bw[k] = info.comp[k].bw;
+      h.comp_h[k] = (int8_t)info.comp[k].h;
+      h.comp_v[k] = (int8_t)info.comp[k].v;
+    }
+    h.tables = (int32_t)c.htabs.size();
+    h.ntables = es.ntables;
+    h.bpm = es.bpm;
+    h.mcux = es.mcux;
+    h.interleaved = es.interleaved;
+    h.rst_mcus = es.restart_interval > 0 ? es.restart_interval : (int32_t)std::min<int64_t>(es.mcus, INT32_MAX);
+    h.mcus = es.mcus;
+    for (int j = 0; j < es.bpm; j++) {
+      h.blk_comp[j] = (int8_t)es.blk_comp[j];
+      h.blk_dc[j] = (int8_t)es.blk_dc[j];
+      h.blk_ac[j] = (int8_t)es.blk_ac[j];
+      h.blk_dx[j] = (int8_t)es.blk_dx[j];
+      h.blk_dy[j] = (int8_t)es.blk_dy[j];
+    }
+    for (int t = 0; t < es.ntables; t++) {
+      c.htabs.emplace_back();
+      mxd::jpeg::device_table(coefs_of(jimg[i].coefs), es.table_class[t], es.table_id[t], &c.htabs.back());
+    }
+    // subsequence length: every segment in <= kHuffThreads subsequences, at
+    // least kHuffMinBits bits (MXD_TUNE_HUFF_BITS overrides the minimum)
+    int64_t max_bits = 0;
+    for (int sgi = 0; sgi < es.nseg; sgi++) max_bits = std::max(max_bits, 8 * (es.seg_end[sgi] - es.seg_begin[sgi]));
+    const int32_t knob = g_tune[MXD_TUNE_HUFF_BITS].load();
+    const int64_t min_bits = knob > 0 ? knob : kHuffMinBits;
+    const int32_t sub_bits =
+        (int32_t)up(std::max<int64_t>(min_bits, (max_bits + mxd::kHuffThreads - 1) / mxd::kHuffThreads), 32);
+    c.seg_first[i - first] = (int32_t)c.hsegs.size();
+    c.seg_count[i - first] = es.nseg;
+    const int32_t img_index = (int32_t)c.himgs.size();
+    int32_t job_sub = mxd::kHuffThreads + 1;
+    for (int sgi = 0; sgi < es.nseg; sgi++) {
+      const int64_t raw = es.seg_end[sgi] - es.seg_begin[sgi];
+      mxd::HuffSegDev sd{};
+      sd.word = c.words_bytes / 4;
+      sd.bits = 0;  // set once unstuffed
+      sd.img = img_index;
+      sd.mcu0 = (int64_t)sgi * h.rst_mcus;
+      sd.mcus = (int32_t)std::min<int64_t>(h.rst_mcus, es.mcus - sd.mcu0);
+      sd.sub_bits = sub_bits;
+      c.raw.push_back({es.data + es.seg_begin[sgi], es.data + es.seg_end[sgi], c.words_bytes});
+      c.words_bytes += up(raw + 4, 16);  // zero padding past the data (a partial last word)
+      // jobs: consecutive segments of one image, <= kHuffThreads subsequences
+      // (planned from the raw size; unstuffing only shortens a segment)
+      const int32_t nsub = (int32_t)std::max<int64_t>(1, (8 * raw + sub_bits - 1) / sub_bits);
+      if (job_sub + nsub > mxd::kHuffThreads) {
+        c.hjobs.push_back(mxd::HuffJobDev{(int32_t)c.hsegs.size(), 0, 0, 0});
+        job_sub = 0;
+      }
+      c.hjobs.back().nseg++;
+      c.hjobs.back().nsub += nsub;
+      job_sub += nsub;
+      c.huff_threads = std::max(c.huff_threads, c.hjobs.back().nsub);
+      c.hsegs.push_back(sd);
+    }
+    c.himgs.push_back(h);
+    coef_rel += up(info.coef_count * 2, 256);
+  }
   for (int32_t i = first; i < end; i++) {
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
     mxd::JpegImgDev m{};
@@ -320,7 +412,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     for (int k = 0; k < m.ncomp; k++) {
       const mxd::jpeg::CoefPlane& cp = info.comp[k];
       mxd::JpegPlaneDev p{};
-      p.coef = (in_off[i] + cp.off * 2) / 2;
+      // host-decoded coefficients: staged at in_off[i]; pending: in the
+      // device-only region (coef_off added below)
+      p.coef = pend_rel[i - first] >= 0 ? (pend_rel[i - first] + cp.off * 2) / 2 : (in_off[i] + cp.off * 2) / 2;
       p.out = c.samples;
       p.first_block = c.nblocks;
       p.bw = cp.bw;
@@ -353,10 +447,25 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
   }
   c.rgb_off = c.samples;
   c.mid_bytes += c.samples;
-  c.planes_off = up(tables_at, 256);
+  c.words_off = up(tables_at, 256);
+  c.htabs_off = up(c.words_off + c.words_bytes, 256);
+  c.himgs_off = up(c.htabs_off + (int64_t)(c.htabs.size() * sizeof(mxd::HuffDev)), 256);
+  c.hsegs_off = up(c.himgs_off + (int64_t)(c.himgs.size() * sizeof(mxd::HuffImgDev)), 256);
+  c.hjobs_off = up(c.hsegs_off + (int64_t)(c.hsegs.size() * sizeof(mxd::HuffSegDev)), 256);
+  c.planes_off = up(c.hjobs_off + (int64_t)(c.hjobs.size() * sizeof(mxd::HuffJobDev)), 256);
   c.imgs_off = up(c.planes_off + (int64_t)(c.planes.size() * sizeof(mxd::JpegPlaneDev)), 256);
   c.q_off = up(c.imgs_off + (int64_t)(c.imgs.size() * sizeof(mxd::JpegImgDev)), 256);
   c.end = c.q_off + (int64_t)(c.qtabs.size() * sizeof(uint16_t));
+  c.coef_off = up(c.end, 256);
+  c.dev_end = c.coef_off + coef_rel;
+  for (mxd::HuffImgDev& h : c.himgs) h.coef += c.coef_off / 2;
+  for (size_t k = 0, pi = 0; k < (size_t)(end - first); k++) {
+    const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[first + k].coefs));
+    const int np = info.ncomp == 1 ? 1 : 3;
+    if (pend_rel[k] >= 0)
+      for (int q = 0; q < np; q++) c.planes[pi + q].coef += c.coef_off / 2;
+    pi += np;
+  }
 }
 
 // jpeg != nullptr: images[i] is jpeg[i] as an mxd_image (3 channels, the
@@ -383,6 +492,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     int64_t pitch, copy, in_off, out_off, out_row;
     int64_t in_size;              // staged bytes (footprint rows, or a JPEG's coefficients)
     bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
+    bool pending = false;         // JPEG whose entropy decode runs on the device (nothing staged at in_off)
     const uint8_t* src_dev;       // zero copy: the kernel reads the page-locked source in place
     uint8_t* dst_dev;             // zero copy: the kernel writes the page-locked destination in place
   };
@@ -395,7 +505,8 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       s.x0 = s.y0 = 0;
       s.rows = im.src_h;
       s.pitch = s.copy = 0;
-      s.in_size = info.coef_count * 2;
+      s.in_size = info.coef_count * 2;  // chunk sizing (device memory); staged only when decoded on the host
+      s.pending = info.entropy_pending;
       s.out_row = (int64_t)im.crop_w * im.channels * elem;
       s.src_pinned = false;
       s.src_dev = nullptr;
@@ -493,19 +604,21 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     int64_t in_bytes = 0, out_bytes = 0;
     for (int pass = 0; pass < 2; pass++)
       for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
-        if (st[i].src_pinned == (pass == 1) && !st[i].src_dev) {
+        if (st[i].src_pinned == (pass == 1) && !st[i].src_dev && !st[i].pending) {
           st[i].in_off = in_bytes;
           in_bytes += (st[i].in_size + 255) & ~(int64_t)255;
         }
     int64_t in_staged = 0, out_staged = 0;
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
-      if (!st[i].src_pinned) in_staged = std::max(in_staged, st[i].in_off + st[i].in_size);
+      if (!st[i].src_pinned && !st[i].pending) in_staged = std::max(in_staged, st[i].in_off + st[i].in_size);
     JpegChunk jc;
+    int64_t dev_in_bytes = 0;
     if (jpeg) {
       std::vector<int64_t> off(n, 0);
       for (int32_t i = chunks[k].first; i < chunks[k].second; i++) off[i] = st[i].in_off;
       jpeg_chunk(jpeg, chunks[k].first, chunks[k].second, off, in_bytes, &jc);
       in_bytes = in_staged = jc.end;  // coefficients, then the chunk's tables, in one copy
+      dev_in_bytes = jc.dev_end;      // + the device-decoded coefficients
       if (int rc = grow_device(&sl.dev_mid, &sl.dev_mid_cap, jc.mid_bytes)) return rc;
     }
     for (int pass = 0; pass < 2; pass++)
@@ -519,7 +632,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
       if (!st[i].dst_pinned) out_staged = std::max(out_staged, st[i].out_off + st[i].out_row * images[i].crop_h);
     if (int rc = grow_pinned(&sl.pin_in, &sl.pin_in_cap, in_bytes)) return rc;
-    if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, in_bytes)) return rc;
+    if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, std::max(in_bytes, dev_in_bytes))) return rc;
     if (!dst_device) {
       if (int rc = grow_pinned(&sl.pin_out, &sl.pin_out_cap, out_bytes)) return rc;
       if (int rc = grow_device(&sl.dev_out, &sl.dev_out_cap, out_bytes)) return rc;
@@ -537,6 +650,18 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const mxd_image& im = images[i];
       const Stage& s = st[i];
       if (jpeg) {
+        if (s.pending) {
+          // the image's entropy-coded segments, unstuffed, zero padded
+          const int32_t f = jc.seg_first[i - chunks[k].first];
+          for (int32_t q = f; q < f + jc.seg_count[i - chunks[k].first]; q++) {
+            const JpegChunk::Raw& r = jc.raw[q];
+            uint8_t* to = sl.pin_in + jc.words_off + r.at;
+            const int64_t n = mxd::jpeg::unstuff(r.b, r.e, to);
+            std::memset(to + n, 0, (size_t)(((r.e - r.b + 4 + 15) & ~(int64_t)15) - n));
+            jc.hsegs[q].bits = (int32_t)std::min<int64_t>(8 * n, INT32_MAX);
+          }
+          return;
+        }
         std::memcpy(sl.pin_in + s.in_off, mxd::jpeg::coef_info(coefs_of(jpeg[i].coefs)).coef, s.in_size);
         return;
       }
@@ -546,6 +671,12 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       for (int32_t r = 0; r < s.rows; r++) std::memcpy(stage + r * s.pitch, from + (int64_t)r * im.src_stride, s.copy);
     });
     if (jpeg) {
+      if (!jc.hjobs.empty()) {
+        std::memcpy(sl.pin_in + jc.htabs_off, jc.htabs.data(), jc.htabs.size() * sizeof(mxd::HuffDev));
+        std::memcpy(sl.pin_in + jc.himgs_off, jc.himgs.data(), jc.himgs.size() * sizeof(mxd::HuffImgDev));
+        std::memcpy(sl.pin_in + jc.hsegs_off, jc.hsegs.data(), jc.hsegs.size() * sizeof(mxd::HuffSegDev));
+        std::memcpy(sl.pin_in + jc.hjobs_off, jc.hjobs.data(), jc.hjobs.size() * sizeof(mxd::HuffJobDev));
+      }
       std::memcpy(sl.pin_in + jc.planes_off, jc.planes.data(), jc.planes.size() * sizeof(mxd::JpegPlaneDev));
       for (auto& m : jc.imgs) m.out += jc.rgb_off;
       std::memcpy(sl.pin_in + jc.imgs_off, jc.imgs.data(), jc.imgs.size() * sizeof(mxd::JpegImgDev));
@@ -590,6 +721,15 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (in_staged > 0 && !pin_in_dev)
       MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
     if (jpeg) {
+      if (!jc.hjobs.empty() &&
+          mxd::launch_jpeg_huff(reinterpret_cast<const uint32_t*>(sl.dev_in + jc.words_off),
+                                reinterpret_cast<const mxd::HuffDev*>(sl.dev_in + jc.htabs_off),
+                                reinterpret_cast<const mxd::HuffImgDev*>(sl.dev_in + jc.himgs_off),
+                                reinterpret_cast<const mxd::HuffSegDev*>(sl.dev_in + jc.hsegs_off),
+                                reinterpret_cast<const mxd::HuffJobDev*>(sl.dev_in + jc.hjobs_off),
+                                (int32_t)jc.hjobs.size(), jc.huff_threads, reinterpret_cast<int16_t*>(sl.dev_in),
+                                sl.stream))
+        return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
       mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
                             reinterpret_cast<const mxd::JpegPlaneDev*>(sl.dev_in + jc.planes_off),

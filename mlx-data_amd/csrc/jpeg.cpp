@@ -24,6 +24,8 @@
 // 8-bit libjpeg API rejects or does not produce them either).
 #include "jpeg.h"
 
+#include "jpeghuff.h"
+
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -46,6 +48,9 @@ struct Error {
 };
 
 [[noreturn]] void fail(const std::string& m) { throw Error{m}; }
+
+// parse_coefs: the file is not one the device entropy decode covers.
+struct NotDevice {};
 
 std::string hex2(int v) {
   static const char* d = "0123456789abcdef";
@@ -75,6 +80,7 @@ struct FastAC {
 
 struct Huff {
   bool present = false;
+  int nvals = 0;
   uint16_t look[1 << kLook];  // (length << 8) | symbol, 0 = longer code
   int32_t maxcode[18];
   int32_t valoffset[18];
@@ -122,6 +128,7 @@ void build_huff(Huff& h, const uint8_t* bits /* [17], bits[0] unused */, const u
       for (int ctr = 1 << (kLook - l); ctr > 0; ctr--) h.look[lookbits + ctr - 1] = (uint16_t)((l << 8) | vals[p]);
     }
   std::memcpy(h.vals, vals, n);
+  h.nvals = n;
   for (int i = 0; i < (1 << kLook); i++) {
     FastAC f{0, 0, 0};
     if (const int e = h.look[i]) {
@@ -656,7 +663,18 @@ struct Decoder {
   // defer: keep the coefficients of sequential scans too (decode_coefs) and
   // run no IDCT while parsing.
   bool defer = false;
+  // device_entropy (parse_coefs): the first sequential scan is not decoded
+  // but its entropy-coded segments recorded (pending); a file the device
+  // decode does not cover throws NotDevice and is decoded on the host.
+  bool device_entropy = false;
+  bool pending = false;
+  int scans = 0;
+  std::vector<int64_t> seg_begin, seg_end;
+  int scan_ns = 0;
+  int scan_comp[4] = {0, 0, 0, 0};  // frame index of each scan component (SOS order)
+  int64_t scan_mcus = 0;
   std::vector<int16_t> coefbuf;  // every component's bw*bh blocks of 64, natural order
+  int64_t coef_total = 0;        // its size (also while the entropy decode is pending)
 
   int16_t* cblk(const Component& c, int bx, int by) {
     return coefbuf.data() + c.off + ((int64_t)by * c.bw + bx) * 64;
@@ -731,6 +749,7 @@ struct Decoder {
     if (width <= 0 || height <= 0 || ncomp <= 0 || ncomp > 4) fail("Empty JPEG image (DNL not supported)");
     if (len != 8 + 3 * ncomp) fail("Bogus marker length");
     progressive = marker == 0xC2;
+    if (progressive && device_entropy) throw NotDevice{};
     for (int i = 0; i < ncomp; i++) {
       Component& c = comp[i];
       c.id = u8();
@@ -755,9 +774,10 @@ struct Decoder {
       c.bh = mcuy * c.v;
       c.off = total;
       total += (int64_t)c.bw * c.bh * 64;
-      if (!progressive && !defer) c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
+      if (!progressive && !defer && !device_entropy) c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
     }
-    if (progressive || defer) coefbuf.assign((size_t)total, 0);
+    coef_total = total;
+    if ((progressive || defer) && !device_entropy) coefbuf.assign((size_t)total, 0);
     frame = true;
   }
 
@@ -805,6 +825,11 @@ struct Decoder {
     }
     const int ss = u8(), se = u8(), a = u8();
     const int ah = a >> 4, al = a & 15;
+    if (device_entropy) {
+      record_scan(sc, ns);
+      any_scan = true;
+      return;
+    }
     if (progressive) {
       if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || ah > 13 || al > 13)
         fail("Invalid progressive parameters");
@@ -820,6 +845,64 @@ struct Decoder {
     decode_scan(bits, sc, ns, ss, se, ah, al);
     // resume marker parsing where the entropy data ended
     pos = (size_t)(bits.p - data);
+  }
+
+  // jdhuff.c jpeg_make_d_derived_tbl: DC symbols (difference categories)
+  // above 15 are a bogus table.
+  void check_dc_table(const Huff& h) const {
+    for (int i = 0; i < h.nvals; i++)
+      if (h.vals[i] > 15) fail("Bogus Huffman table definition");
+  }
+
+  // Device entropy decode: the scan's segments are recorded, not decoded.
+  // Covered: the first and only scan of a sequential file, carrying every
+  // component of a grey (1) or YCbCr / RGB (3) image, its entropy-coded data
+  // ending at a marker, restart markers RST0..7 in sequence, one per interval.
+  void record_scan(Component** sc, int ns) {
+    if (scans++ > 0 || progressive || ns != ncomp || (ncomp != 1 && ncomp != 3)) throw NotDevice{};
+    int bpm = 0;
+    for (int i = 0; i < ns; i++) {
+      if (!dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present) fail("Huffman table was not defined");
+      check_dc_table(dc[sc[i]->dc_tbl]);
+      std::memcpy(sc[i]->q, quant(*sc[i]), sizeof sc[i]->q);  // latched at the scan
+      sc[i]->coded = true;
+      scan_comp[i] = (int)(sc[i] - comp);
+      bpm += ns == 1 ? 1 : sc[i]->h * sc[i]->v;
+    }
+    if (bpm > 10) throw NotDevice{};  // libjpeg: "Sampling factors too large for interleaved scan"
+    scan_ns = ns;
+    scan_mcus = ns == 1 ? (int64_t)sc[0]->wib * sc[0]->hib : (int64_t)mcux * mcuy;
+    // segments: split the entropy-coded data at its restart markers
+    const int64_t nseg = restart_interval ? (scan_mcus + restart_interval - 1) / restart_interval : 1;
+    size_t p = pos, b = pos;
+    int next_rst = 0;
+    for (;;) {
+      const uint8_t* f = static_cast<const uint8_t*>(std::memchr(data + p, 0xFF, size - p));
+      if (!f || (size_t)(f - data) + 1 >= size) throw NotDevice{};  // no marker after the data: truncated
+      p = (size_t)(f - data);
+      const uint8_t m = data[p + 1];
+      if (m == 0x00) {
+        p += 2;
+        continue;
+      }
+      if (m == 0xFF) {
+        p += 1;
+        continue;
+      }
+      seg_begin.push_back((int64_t)b);
+      seg_end.push_back((int64_t)p);
+      if (m >= 0xD0 && m <= 0xD7) {
+        if (!restart_interval || m != 0xD0 + next_rst || (int64_t)seg_begin.size() >= nseg) throw NotDevice{};
+        next_rst = (next_rst + 1) & 7;
+        p += 2;
+        b = p;
+        continue;
+      }
+      break;  // the marker after the scan
+    }
+    if ((int64_t)seg_begin.size() != nseg) throw NotDevice{};
+    pos = seg_end.back();  // marker parsing resumes at the marker
+    pending = true;
   }
 
   template <class F>
@@ -863,6 +946,7 @@ struct Decoder {
     if (!progressive) {
       for (int i = 0; i < ns; i++) {
         if (!dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present) fail("Huffman table was not defined");
+        check_dc_table(dc[sc[i]->dc_tbl]);
         std::memcpy(sc[i]->q, quant(*sc[i]), sizeof sc[i]->q);  // latched at the scan
         sc[i]->coded = true;
       }
@@ -1171,6 +1255,7 @@ int Decoder::color_space() const {
 
 struct Coefs {
   Decoder d;
+  std::vector<uint8_t> file;  // parse_coefs with a pending entropy decode: the file, for the segments
   Coefs(const uint8_t* data, size_t size) : d(data, size) {}
 };
 
@@ -1200,7 +1285,105 @@ Coefs* decode_coefs(const uint8_t* data, size_t size, std::string* err) {
   }
 }
 
+Coefs* parse_coefs(const uint8_t* data, size_t size, bool device_entropy, std::string* err) {
+  if (!device_entropy) return decode_coefs(data, size, err);
+  try {
+    auto c = std::make_unique<Coefs>(nullptr, 0);
+    c->file.assign(data, data + size);
+    Decoder& d = c->d;
+    d.data = c->file.data();
+    d.size = size;
+    d.device_entropy = true;
+    d.parse();
+    if (!d.frame) fail("Invalid JPEG file structure: missing SOF marker");
+    if (d.color_space() < 0) fail("unhandled format");
+    if (!d.pending) throw NotDevice{};  // no scan
+    // decode_coefs' check: output() reaches it exactly for non-integral factors
+    if (d.ncomp > 1)
+      for (int i = 0; i < d.used_components(); i++)
+        if (d.max_h % d.comp[i].h != 0 || d.max_v % d.comp[i].v != 0) fail("Fractional sampling not implemented yet");
+    return c.release();
+  } catch (const NotDevice&) {
+    return decode_coefs(data, size, err);
+  } catch (const Error& e) {
+    if (err) *err = e.msg;
+    return nullptr;
+  } catch (const std::bad_alloc&) {
+    if (err) *err = "Insufficient memory";
+    return nullptr;
+  }
+}
+
 void free_coefs(Coefs* c) { delete c; }
+
+EntropyScan entropy_scan(const Coefs* c) {
+  const Decoder& d = c->d;
+  EntropyScan e{};
+  e.nseg = (int)d.seg_begin.size();
+  e.seg_begin = d.seg_begin.data();
+  e.seg_end = d.seg_end.data();
+  e.data = d.data;
+  e.mcus = d.scan_mcus;
+  e.restart_interval = d.restart_interval;
+  e.interleaved = d.scan_ns > 1 ? 1 : 0;
+  e.mcux = d.scan_ns > 1 ? d.mcux : d.comp[d.scan_comp[0]].wib;
+  // tables: distinct (class, index) pairs in first-use order
+  auto table = [&](int cls, int id) {
+    for (int t = 0; t < e.ntables; t++)
+      if (e.table_class[t] == cls && e.table_id[t] == id) return t;
+    e.table_class[e.ntables] = cls;
+    e.table_id[e.ntables] = id;
+    return e.ntables++;
+  };
+  for (int i = 0; i < d.scan_ns; i++) {
+    const int ci = d.scan_comp[i];
+    const Component& k = d.comp[ci];
+    const int nh = d.scan_ns > 1 ? k.h : 1, nv = d.scan_ns > 1 ? k.v : 1;
+    for (int v = 0; v < nv; v++)
+      for (int h = 0; h < nh; h++) {
+        e.blk_comp[e.bpm] = ci;
+        e.blk_dx[e.bpm] = h;
+        e.blk_dy[e.bpm] = v;
+        e.blk_dc[e.bpm] = table(0, k.dc_tbl);
+        e.blk_ac[e.bpm] = table(1, k.ac_tbl);
+        e.bpm++;
+      }
+  }
+  return e;
+}
+
+void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
+  const Huff& h = cls ? c->d.ac[table_id] : c->d.dc[table_id];
+  HuffDev& o = *static_cast<HuffDev*>(huff_dev);
+  std::memcpy(o.look, h.look, sizeof o.look);
+  std::memcpy(o.maxcode, h.maxcode, sizeof o.maxcode);
+  std::memcpy(o.valoffset, h.valoffset, sizeof o.valoffset);
+  std::memcpy(o.vals, h.vals, sizeof o.vals);
+  for (int i = 0; i < (1 << kLook); i++)
+    o.fac[i] = (uint32_t)(uint16_t)h.fac[i].val | ((uint32_t)h.fac[i].run << 16) | ((uint32_t)h.fac[i].len << 24);
+}
+
+// Mirrors Bits::fill's byte rules on a segment that ends at its marker's 0xFF.
+int64_t unstuff(const uint8_t* b, const uint8_t* e, uint8_t* dst) {
+  uint8_t* o = dst;
+  while (b < e) {
+    const uint8_t* f = static_cast<const uint8_t*>(std::memchr(b, 0xFF, (size_t)(e - b)));
+    if (!f) {
+      std::memcpy(o, b, (size_t)(e - b));
+      o += e - b;
+      break;
+    }
+    std::memcpy(o, b, (size_t)(f - b));
+    o += f - b;
+    if (f + 1 < e && f[1] == 0x00) {
+      *o++ = 0xFF;  // stuffed byte
+      b = f + 2;
+    } else {
+      b = f + 1;  // fill byte (0xFF 0xFF ...)
+    }
+  }
+  return (int64_t)(o - dst);
+}
 
 CoefInfo coef_info(const Coefs* c) {
   const Decoder& d = c->d;
@@ -1212,8 +1395,9 @@ CoefInfo coef_info(const Coefs* c) {
   r.color_space = d.color_space();
   r.max_h = d.max_h;
   r.max_v = d.max_v;
-  r.coef = d.coefbuf.data();
-  r.coef_count = (int64_t)d.coefbuf.size();
+  r.coef = d.pending ? nullptr : d.coefbuf.data();
+  r.coef_count = d.coef_total;
+  r.entropy_pending = d.pending;
   for (int i = 0; i < d.ncomp; i++) {
     const Component& k = d.comp[i];
     CoefPlane& p = r.comp[i];
@@ -1233,6 +1417,13 @@ CoefInfo coef_info(const Coefs* c) {
 
 bool finish(const Coefs* c, uint8_t* dst, int64_t dst_stride, std::string* err) {
   try {
+    if (c->d.pending) {
+      // the entropy decode was left to the device: run it here now
+      std::unique_ptr<Coefs> h(decode_coefs(c->file.data(), c->file.size(), err));
+      if (!h) return false;
+      h->d.output(dst, dst_stride);
+      return true;
+    }
     c->d.output(dst, dst_stride);
     return true;
   } catch (const Error& e) {

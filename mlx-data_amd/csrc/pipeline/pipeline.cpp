@@ -913,9 +913,11 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
     }
     if (!ok) throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
     if (device_decode()) {
-      // entropy decode only; the GPU finishes it in the batch launch
+      // markers only (the Huffman decode too runs on the GPU, csrc/jpeghuff.hip)
+      // when the file qualifies, else the entropy decode here; the GPU
+      // finishes it in the batch launch
       mxd_jpeg_coefs* c = nullptr;
-      if (mxd_jpeg_coefs_decode(bytes, nbytes, &c) != MXD_OK)
+      if (mxd_jpeg_coefs_parse(bytes, nbytes, 1, &c) != MXD_OK)
         throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
       auto src = std::make_shared<const JpegSource>(c);
       int32_t cw = 0, ch = 0, dev_ok = 0;

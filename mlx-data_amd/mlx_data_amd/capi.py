@@ -30,7 +30,8 @@ EXPORTS = (
     "mxd_release_host_buffers",
     "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
-    "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_free", "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
+    "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
+    "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
     "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device",
 )
 
@@ -53,6 +54,7 @@ MXD_TUNE_BAND_LA = 1
 MXD_TUNE_BAND_GRID = 2
 MXD_TUNE_DESC = 3
 MXD_TUNE_STREAMS = 4
+MXD_TUNE_HUFF_BITS = 5
 
 
 class MxdImage(ctypes.Structure):
@@ -263,14 +265,23 @@ def jpeg_decode(data):
 class JpegCoefs:
     """An entropy-decoded JPEG (mxd_jpeg_coefs_decode): the host half of the
     split decode; finish() runs the rest on the host, make_jpeg_images() hands
-    it to the GPU finish."""
+    it to the GPU finish.  device_entropy=True: mxd_jpeg_coefs_parse, the
+    Huffman decode too is left to the GPU when the file qualifies
+    (``entropy_pending``)."""
 
-    def __init__(self, data):
+    def __init__(self, data, device_entropy=False):
         buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
         h = ctypes.c_void_p()
-        check(lib().mxd_jpeg_coefs_decode(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes),
-                                          ctypes.byref(h)))
+        if device_entropy:
+            check(lib().mxd_jpeg_coefs_parse(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes), 1,
+                                             ctypes.byref(h)))
+        else:
+            check(lib().mxd_jpeg_coefs_decode(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes),
+                                              ctypes.byref(h)))
         self.handle = h.value
+        pend = ctypes.c_int32()
+        check(lib().mxd_jpeg_coefs_entropy_pending(ctypes.c_void_p(self.handle), ctypes.byref(pend)))
+        self.entropy_pending = bool(pend.value)
         w, hh, ok = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib().mxd_jpeg_coefs_info(ctypes.c_void_p(self.handle), ctypes.byref(w), ctypes.byref(hh),
                                         ctypes.byref(ok)))

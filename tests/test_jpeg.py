@@ -109,3 +109,51 @@ def test_load_image_uses_native_decoder(tmp_path):
                           bad[2:]])
     with pytest.raises(RuntimeError, match=r"load_jpeg: could not load from memory \(.*arithmetic"):
         dx.buffer_from_vector([dict(m=bad)]).load_image("m", from_memory=True)[0]
+
+
+def test_device_entropy_parse_routes_and_host_finish():
+    """mxd_jpeg_coefs_parse(device_entropy=1) (CPU half of the device entropy
+    decode, csrc/jpeghuff.h): baseline one-scan files are only parsed
+    (entropy_pending), every other file is entropy-decoded on the host; either
+    way the host finish gives the decoder's bytes (Pillow's libjpeg-turbo)."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(77)
+    for i in range(24):
+        h, w = int(rng.integers(1, 160)), int(rng.integers(1, 160))
+        grey = i % 5 == 4
+        prog = i % 4 == 1
+        kw = dict(quality=int(rng.integers(5, 101)), progressive=prog, optimize=bool(rng.random() < 0.4))
+        if not grey:
+            kw["subsampling"] = i % 3
+        if i % 3 == 2:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 5))
+        b = io.BytesIO()
+        a = _smooth(rng, h, w, 1 if grey else 3)
+        Image.fromarray(a[:, :, 0] if grey else a).save(b, "JPEG", **kw)
+        data = b.getvalue()
+        c = capi.JpegCoefs(data, device_entropy=True)
+        assert c.entropy_pending == (not prog), (i, kw)
+        assert np.array_equal(c.finish(), np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))), (i, kw)
+    # fixtures: progressive / CMYK / truncated files are decoded on the host
+    for k in [k[:-4] for k in GOLD.files if k.endswith("_jpg")]:
+        data = bytes(GOLD[f"{k}_jpg"])
+        c = capi.JpegCoefs(data, device_entropy=True)
+        if ("prog" in k and "prog0" not in k) or "cmyk" in k or "trunc" in k:
+            assert not c.entropy_pending, k
+        if c.device_ok:
+            assert np.array_equal(c.finish(), GOLD[f"{k}_rgb"]), k
+
+
+def test_device_entropy_parse_errors_match_host():
+    """The markers-only parse reports the host decode's errors (a DC table
+    with a category above 15 is libjpeg's "Bogus Huffman table definition")."""
+    data = bytearray(GOLD["sub2_prog0_jpg"].tobytes())
+    dht = data.index(b"\xff\xc4")
+    # first DHT: class/index byte, 16 counts, then the values: make a DC value 16
+    tc = data[dht + 4]
+    assert tc >> 4 == 0  # a DC table first (Pillow writes DC 0 first)
+    vals = dht + 5 + 16
+    data[vals] = 16
+    for dev in (False, True):
+        with pytest.raises(capi.MxdError, match="Bogus Huffman table definition"):
+            capi.JpegCoefs(bytes(data), device_entropy=dev)
