@@ -158,12 +158,14 @@ def test_corrupt_and_short_entropy_data(bits):
         else:
             # cut entropy bytes out of the middle of the last segment: the data
             # runs out before the last MCUs, the file still ends with EOI
-            last = max(s, bytes(d).rfind(b"\xff\xd0", s, e), bytes(d).rfind(b"\xff\xd7", s, e))
+            last = max([s] + [bytes(d).rfind(bytes([0xFF, 0xD0 + m]), s, e) + 2 for m in range(8)])
             a = last + (e - last) // 3
             b = a + (e - last) // 3
+            while d[a - 1] == 0xFF:  # never leave a dangling 0xFF (a marker) behind
+                a += 1
             while b < e and d[b - 1] == 0xFF:
                 b += 1
-            del d[a:b]
+            del d[a:max(a, b)]
         datas.append(bytes(d))
     prev = capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
     try:
