@@ -356,6 +356,10 @@ std::atomic<int> g_device_decode{-1};  // -1: not set (on when a device is visib
 
 void set_device_decode(bool on) { g_device_decode.store(on ? 1 : 0); }
 
+std::atomic<bool> g_device_entropy{true};
+void set_device_entropy(bool on) { g_device_entropy.store(on); }
+bool device_entropy() { return g_device_entropy.load(); }
+
 bool device_decode() {
   const int v = g_device_decode.load();
   return v < 0 ? !devices().empty() : v == 1;
@@ -917,7 +921,7 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
       // when the file qualifies, else the entropy decode here; the GPU
       // finishes it in the batch launch
       mxd_jpeg_coefs* c = nullptr;
-      if (mxd_jpeg_coefs_parse(bytes, nbytes, 1, &c) != MXD_OK)
+      if (mxd_jpeg_coefs_parse(bytes, nbytes, device_entropy() ? 1 : 0, &c) != MXD_OK)
         throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
       auto src = std::make_shared<const JpegSource>(c);
       int32_t cw = 0, ch = 0, dev_ok = 0;

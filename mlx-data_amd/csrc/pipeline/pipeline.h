@@ -125,6 +125,11 @@ std::vector<Slice> split_batch(int64_t n, int64_t ndev, uint64_t first);
 // the batch launch; off, load_image decodes whole on the
 // host.  Identical bytes either way.
 void set_device_decode(bool on);
+// With the device decode on: the Huffman decode too runs on the GPU for the
+// files it covers (mxd_jpeg_coefs_parse; default on).  Off: the host
+// entropy-decodes every file (round 3's split).
+void set_device_entropy(bool on);
+bool device_entropy();
 bool device_decode();
 
 // ---------------------------------------------------------------- state

@@ -508,6 +508,8 @@ PYBIND11_MODULE(_pipeline, m) {
   m.attr("_MIN_SLICE_IMAGES") = kMinSliceImages;
   m.def("devices", &devices);
   m.def("set_device_decode", &set_device_decode, py::arg("on"));
+  m.def("set_device_entropy", &set_device_entropy, py::arg("on"));
+  m.def("device_entropy", &device_entropy);
   m.def("device_decode", &device_decode);
 
   // The decoder holds a Python callable: drop it before the interpreter goes.

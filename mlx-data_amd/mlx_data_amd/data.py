@@ -27,10 +27,13 @@ HIP runtime.  Reading an unbatched image materialises it with its own launch.
 There is no CPU resize: without a visible GPU the image ops raise.
 
 ``load_image`` decodes JPEG natively (``csrc/jpeg.cpp``, the reference's
-libjpeg path, ``core/image/ImageJPEG.cpp``).  With a device visible it runs
-only the entropy decode and the batch launch finishes the decode on the GPU
-(IDCT, upsampling, colour; ``csrc/jpegdev.hip``) before resizing, with the
-same bytes; ``set_device_decode(False)`` decodes whole on the host instead.
+libjpeg path, ``core/image/ImageJPEG.cpp``).  With a device visible it only
+parses the markers of a sequential file and the batch launch runs the whole
+decode on the GPU -- Huffman (``csrc/jpeghuff.hip``), IDCT, upsampling,
+colour (``csrc/jpegdev.hip``) -- before resizing, with the same bytes;
+progressive and other files are entropy-decoded on the host first.
+``set_device_entropy(False)`` keeps the Huffman decode on the host for every
+file, ``set_device_decode(False)`` decodes whole on the host.
 Other formats go to a Pillow hook that follows the reference's stb_image
 rules (``core/image/ImageSTBI.cpp``: 1/2/3 channels kept, 4 -> 3, 16-bit >> 8).
 """
@@ -40,11 +43,11 @@ import numpy as np
 
 from . import capi  # noqa: F401  (loads libmxd_amd.so before anything else binds a HIP runtime)
 from . import _pipeline  # noqa: F401
-from ._pipeline import (Buffer, DeviceArray, Stream, buffer_from_vector, device_decode, devices, set_device_decode,
-                        set_devices, set_image_decoder, set_state)
+from ._pipeline import (Buffer, DeviceArray, Stream, buffer_from_vector, device_decode, device_entropy, devices,
+                        set_device_decode, set_device_entropy, set_devices, set_image_decoder, set_state)
 
 __all__ = ["Buffer", "Stream", "DeviceArray", "buffer_from_vector", "set_state", "set_devices", "devices",
-           "set_device_decode", "device_decode"]
+           "set_device_decode", "device_decode", "set_device_entropy", "device_entropy"]
 
 
 def _decode(path, data, from_memory, info):

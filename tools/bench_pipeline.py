@@ -12,8 +12,10 @@ Variants per worker count:
   fused      image_to_float before batch: the kernel writes the f32 batch
   device     fused + batch(..., device=0): the batch stays in HBM (DLPack)
   *_hostdec  the same with set_device_decode(False): the whole JPEG decode on
-             the host (default with a device: entropy decode on the host,
-             IDCT / upsampling / colour in the batch launch)
+             the host (default with a device: the whole decode of sequential
+             files in the batch launch -- Huffman, IDCT, upsampling, colour)
+  *_hostent  the same with set_device_entropy(False): the Huffman decode on
+             the host, the rest in the batch launch (round 3's split)
   cpu        Pillow (libjpeg-turbo) decode -> oracle C stbir restatement ->
              crop per batch on a pool of that many worker processes, numpy
              /255 of each batch in the consumer
@@ -72,13 +74,16 @@ def run_surface(files, batch, workers, variant, repeat=1):
     from mlx_data_amd import data as dx
 
     hostdec = variant.endswith("_hostdec")
-    variant = variant[:-len("_hostdec")] if hostdec else variant
-    prev = dx.device_decode()
+    hostent = variant.endswith("_hostent")
+    variant = variant.rsplit("_", 1)[0] if hostdec or hostent else variant
+    prev, prev_ent = dx.device_decode(), dx.device_entropy()
     dx.set_device_decode(not hostdec)
+    dx.set_device_entropy(not hostent)
     try:
         return _run_surface(dx, files, batch, workers, variant, repeat)
     finally:
         dx.set_device_decode(prev)
+        dx.set_device_entropy(prev_ent)
 
 
 def _run_surface(dx, files, batch, workers, variant, repeat=1):
