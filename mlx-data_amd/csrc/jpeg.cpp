@@ -11,8 +11,10 @@
 //     bits were needed) the rest of the restart interval decodes as zeros
 //     (uniform grey), as jdhuff.c does for "insufficient data";
 //   * dequantize + inverse DCT: JDCT_ISLOW, 13-bit fixed point, two passes with
-//     PASS1_BITS = 2 (jidctint.c), outputs through the 1024-entry IDCT range
-//     limit table (jdmaster.c prepare_range_limit_table);
+//     PASS1_BITS = 2 (jidctint.c), outputs clamped to 0..255 as libjpeg-turbo's
+//     SIMD IDCTs do (range_limit below);
+//   * block smoothing of progressive files whose scans leave low-frequency AC
+//     coefficients inexact (jdcoefct.c decompress_smooth_data, on by default);
 //   * chroma upsampling: "fancy" triangle upsampling h2v1 / h1v2 / h2v2
 //     (jdsample.c) with edge columns special-cased and the rows above the
 //     first / below the last real row replicated (jdmainct.c context rows);
@@ -394,18 +396,18 @@ using JLONG = int64_t;  // libjpeg-turbo's JLONG (long on LP64)
 
 inline int32_t descale(JLONG x, int n) { return (int32_t)((x + ((JLONG)1 << (n - 1))) >> n); }
 
-struct RangeLimit {
-  uint8_t idct[1024];  // jdmaster.c post-IDCT table, indexed by (x & 1023)
-  RangeLimit() {
-    for (int i = 0; i < 1024; i++) {
-      if (i < 128) idct[i] = (uint8_t)(i + 128);
-      else if (i < 512) idct[i] = 255;
-      else if (i < 896) idct[i] = 0;
-      else idct[i] = (uint8_t)(i - 896);
-    }
-  }
-};
-const RangeLimit kRange;
+// Output range limit.  jidctint.c indexes jdmaster.c's post-IDCT table with
+// (x & 1023) -- out-of-range values wrap past +-384 -- while libjpeg-turbo's
+// SIMD IDCTs (the build Pillow ships; x86 AVX2 / ARM NEON builds of the
+// reference's libjpeg-turbo) narrow with signed saturation, i.e. clamp.  The
+// two agree on every value a well-formed file produces; they part on the
+// blocks truncated or corrupt data and block smoothing can drive out of
+// range, where the saturating form is what Pillow's decodes (the pinned
+// fixtures) hold.
+inline uint8_t range_limit(int32_t x) {
+  x += 128;
+  return (uint8_t)(x < 0 ? 0 : x > 255 ? 255 : x);
+}
 
 // jidctint.c jpeg_idct_islow: dequantize + 8x8 inverse DCT into out (stride).
 void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) {
@@ -461,12 +463,11 @@ void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) 
     wp[24] = descale(tmp13 + tmp0, s);
     wp[32] = descale(tmp13 - tmp0, s);
   }
-  const uint8_t* rl = kRange.idct;
   for (int r = 0; r < 8; r++) {
     const int32_t* wp = ws + 8 * r;
     uint8_t* op = out + (size_t)r * stride;
     if (wp[1] == 0 && wp[2] == 0 && wp[3] == 0 && wp[4] == 0 && wp[5] == 0 && wp[6] == 0 && wp[7] == 0) {
-      const uint8_t v = rl[descale(wp[0], kPass1Bits + 3) & 1023];
+      const uint8_t v = range_limit(descale(wp[0], kPass1Bits + 3));
       for (int c = 0; c < 8; c++) op[c] = v;
       continue;
     }
@@ -501,14 +502,14 @@ void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) 
     tmp2 += z2 + z3;
     tmp3 += z1 + z4;
     constexpr int s = kConstBits + kPass1Bits + 3;
-    op[0] = rl[descale(tmp10 + tmp3, s) & 1023];
-    op[7] = rl[descale(tmp10 - tmp3, s) & 1023];
-    op[1] = rl[descale(tmp11 + tmp2, s) & 1023];
-    op[6] = rl[descale(tmp11 - tmp2, s) & 1023];
-    op[2] = rl[descale(tmp12 + tmp1, s) & 1023];
-    op[5] = rl[descale(tmp12 - tmp1, s) & 1023];
-    op[3] = rl[descale(tmp13 + tmp0, s) & 1023];
-    op[4] = rl[descale(tmp13 - tmp0, s) & 1023];
+    op[0] = range_limit(descale(tmp10 + tmp3, s));
+    op[7] = range_limit(descale(tmp10 - tmp3, s));
+    op[1] = range_limit(descale(tmp11 + tmp2, s));
+    op[6] = range_limit(descale(tmp11 - tmp2, s));
+    op[2] = range_limit(descale(tmp12 + tmp1, s));
+    op[5] = range_limit(descale(tmp12 - tmp1, s));
+    op[3] = range_limit(descale(tmp13 + tmp0, s));
+    op[4] = range_limit(descale(tmp13 - tmp0, s));
   }
 }
 
@@ -573,7 +574,7 @@ __attribute__((target_clones("avx2", "default"))) bool idct_islow32(const int16_
     for (int c = 0; c < 8; c++) wt[c * 8 + r] = ws[r * 8 + c];
   idct_1d8<kConstBits + kPass1Bits + 3>(wt, o);  // o[c * 8 + r]: column c of row r
   for (int i = 0; i < 64; i++) {
-    const int32_t v = (((o[i] + 512) & 1023) - 512) + 128;
+    const int32_t v = o[i] + 128;
     o[i] = v < 0 ? 0 : v > 255 ? 255 : v;
   }
   for (int r = 0; r < 8; r++)
@@ -675,6 +676,15 @@ struct Decoder {
   int64_t scan_mcus = 0;
   std::vector<int16_t> coefbuf;  // every component's bw*bh blocks of 64, natural order
   int64_t coef_total = 0;        // its size (also while the entropy decode is pending)
+  // Progression status of the first 10 zigzag coefficients (jdphuff.c
+  // start_pass_phuff_decoder's coef_bits): [ci] the Al of the component's
+  // latest scan of each (-1: none yet), [4 + ci] the values before that scan.
+  int coef_bits[8][10];
+  int input_scans = 0;
+  // iMCU row of the last MCU that started with data left (jdcoefct.c
+  // consume_data's last_good_iMCU_row): rows past it use the progression
+  // status from before the last scan when smoothing
+  int64_t last_good_imcu = INT64_MAX;
 
   int16_t* cblk(const Component& c, int bx, int by) {
     return coefbuf.data() + c.off + ((int64_t)by * c.bw + bx) * 64;
@@ -778,6 +788,8 @@ struct Decoder {
     }
     coef_total = total;
     if ((progressive || defer) && !device_entropy) coefbuf.assign((size_t)total, 0);
+    for (auto& row : coef_bits)
+      for (int& b : row) b = -1;
     frame = true;
   }
 
@@ -833,6 +845,14 @@ struct Decoder {
     if (progressive) {
       if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || ah > 13 || al > 13)
         fail("Invalid progressive parameters");
+      // progression status, updated when the scan starts (whatever its data holds)
+      input_scans++;
+      for (int i = 0; i < ns; i++) {
+        const int ci = (int)(sc[i] - comp);
+        for (int k = std::min(ss, 1); k <= std::min(std::max(se, 9), 9); k++)
+          coef_bits[4 + ci][k] = input_scans > 1 ? coef_bits[ci][k] : 0;
+        for (int k = ss; k <= std::min(se, 9); k++) coef_bits[ci][k] = al;
+      }
     } else if (ss != 0 || se != 63 || ah != 0 || al != 0) {
       // libjpeg only warns here; sequential decoding ignores the fields
     }
@@ -926,6 +946,7 @@ struct Decoder {
       for (int by = 0; by < c.hib; by++)
         for (int bx = 0; bx < c.wib; bx++) {
           restart_check();
+          if (!bits.insufficient) last_good_imcu = by / c.v;
           decode_block(c, bx, by, bits.insufficient);
         }
     } else {
@@ -933,6 +954,7 @@ struct Decoder {
         for (int mx = 0; mx < mcux; mx++) {
           restart_check();
           const bool skip = bits.insufficient;
+          if (!skip) last_good_imcu = my;
           for (int i = 0; i < ns; i++) {
             Component& c = *sc[i];
             for (int v = 0; v < c.v; v++)
@@ -1172,6 +1194,136 @@ struct Decoder {
       std::memcpy(comp[i].q, quant(comp[i]), sizeof comp[i].q);
       comp[i].coded = true;
     }
+    smooth_blocks();
+  }
+
+  // ---- block smoothing (libjpeg's do_block_smoothing, on by default and
+  // reached through jpeg_start_decompress, ImageJPEG.cpp:100-101)
+  //
+  // A progressive file whose scans leave some of the first nine AC
+  // coefficients inexact (truncated files, or files that never send them)
+  // gets them estimated from the DC values of the 5x5 block neighbourhood,
+  // as libjpeg-turbo's jdcoefct.c decompress_smooth_data does (its 5x5
+  // extension of ITU T.81 Annex K.8): an estimate replaces a coefficient
+  // only while it is still zero, limited to the bits below its Al; with no
+  // AC data at all for a component the DC itself is re-estimated too and
+  // four more coefficients are filled.  Pinned by Pillow's libjpeg-turbo
+  // decodes of truncated progressive files (tests/golden/jpeg.npz, prog_trunc*).
+
+  // jdcoefct.c smoothing_ok: DC known for every component, the ten
+  // quantisers nonzero, and some of the nine AC coefficients inexact.
+  bool smoothing_ok() const {
+    static const int kPos[10] = {0, 1, 8, 16, 9, 2, 3, 10, 17, 24};
+    bool useful = false;
+    for (int ci = 0; ci < ncomp; ci++) {
+      for (int k = 0; k < 10; k++)
+        if (comp[ci].q[kPos[k]] == 0) return false;
+      if (coef_bits[ci][0] < 0) return false;
+      for (int k = 1; k < 10; k++)
+        if (coef_bits[ci][k] != 0) useful = true;
+    }
+    return useful;
+  }
+
+  static int smooth_pred(int64_t num, int64_t q, int al, bool limit) {
+    int pred = (int)(((q << 7) + (num >= 0 ? num : -num)) / (q << 8));
+    if (limit && al > 0 && pred >= (1 << al)) pred = (1 << al) - 1;
+    return num >= 0 ? pred : -pred;
+  }
+
+  void smooth_blocks() {
+    if (coefbuf.empty() || !smoothing_ok()) return;
+    std::vector<int16_t> out(coefbuf);
+    for (int ci = 0; ci < ncomp; ci++) {
+      const Component& c = comp[ci];
+      int prev[10];
+      for (int k = 0; k < 10; k++) prev[k] = input_scans > 1 ? coef_bits[4 + ci][k] : -1;
+      const int64_t Q00 = c.q[0], Q01 = c.q[1], Q10 = c.q[8], Q20 = c.q[16], Q11 = c.q[9], Q02 = c.q[2],
+                    Q03 = c.q[3], Q12 = c.q[10], Q21 = c.q[17], Q30 = c.q[24];
+      auto dc = [&](int row, int col) { return (int)coefbuf[c.off + ((int64_t)row * c.bw + col) * 64]; };
+      const int last_col = c.wib - 1;
+      for (int m = 0; m < mcuy; m++) {
+        // block rows of this iMCU row (the last one: the rows of the component proper)
+        int block_rows = c.v;
+        if (m == mcuy - 1 && c.hib % c.v) block_rows = c.hib % c.v;
+        const int64_t image_rows = (int64_t)block_rows * mcuy;
+        const int* bits = m > last_good_imcu ? prev : coef_bits[ci];
+        bool change_dc = true;
+        for (int k = 1; k < 10; k++) change_dc = change_dc && bits[k] == -1;
+        for (int br = 0; br < block_rows; br++) {
+          const int r = m * c.v + br;
+          const int64_t ir = (int64_t)m * block_rows + br;
+          const int rp = ir > 0 ? r - 1 : r, rpp = ir > 1 ? r - 2 : rp;
+          const int rn = ir < image_rows - 1 ? r + 1 : r, rnn = ir < image_rows - 2 ? r + 2 : rn;
+          const int rows[5] = {rpp, rp, r, rn, rnn};
+          // D[i][j]: DC of row i, column block - 2 + j clamped to the component's blocks
+          int D[5][5];
+          for (int b = 0; b <= last_col; b++) {
+            for (int i = 0; i < 5; i++)
+              for (int j = 0; j < 5; j++) D[i][j] = dc(rows[i], std::min(std::max(b - 2 + j, 0), last_col));
+            const int DC01 = D[0][0], DC02 = D[0][1], DC03 = D[0][2], DC04 = D[0][3], DC05 = D[0][4];
+            const int DC06 = D[1][0], DC07 = D[1][1], DC08 = D[1][2], DC09 = D[1][3], DC10 = D[1][4];
+            const int DC11 = D[2][0], DC12 = D[2][1], DC13 = D[2][2], DC14 = D[2][3], DC15 = D[2][4];
+            const int DC16 = D[3][0], DC17 = D[3][1], DC18 = D[3][2], DC19 = D[3][3], DC20 = D[3][4];
+            const int DC21 = D[4][0], DC22 = D[4][1], DC23 = D[4][2], DC24 = D[4][3], DC25 = D[4][4];
+            int16_t* w = out.data() + c.off + ((int64_t)r * c.bw + b) * 64;
+            if (bits[1] != 0 && w[1] == 0)
+              w[1] = (int16_t)smooth_pred(
+                  Q00 * (change_dc ? (-DC01 - DC02 + DC04 + DC05 - 3 * DC06 + 13 * DC07 - 13 * DC09 + 3 * DC10 -
+                                      3 * DC11 + 38 * DC12 - 38 * DC14 + 3 * DC15 - 3 * DC16 + 13 * DC17 -
+                                      13 * DC19 + 3 * DC20 - DC21 - DC22 + DC24 + DC25)
+                                   : (-7 * DC11 + 50 * DC12 - 50 * DC14 + 7 * DC15)),
+                  Q01, bits[1], true);
+            if (bits[2] != 0 && w[8] == 0)
+              w[8] = (int16_t)smooth_pred(
+                  Q00 * (change_dc ? (-DC01 - 3 * DC02 - 3 * DC03 - 3 * DC04 - DC05 - DC06 + 13 * DC07 +
+                                      38 * DC08 + 13 * DC09 - DC10 + DC16 - 13 * DC17 - 38 * DC18 - 13 * DC19 +
+                                      DC20 + DC21 + 3 * DC22 + 3 * DC23 + 3 * DC24 + DC25)
+                                   : (-7 * DC03 + 50 * DC08 - 50 * DC18 + 7 * DC23)),
+                  Q10, bits[2], true);
+            if (bits[3] != 0 && w[16] == 0)
+              w[16] = (int16_t)smooth_pred(
+                  Q00 * (change_dc ? (DC03 + 2 * DC07 + 7 * DC08 + 2 * DC09 - 5 * DC12 - 14 * DC13 - 5 * DC14 +
+                                      2 * DC17 + 7 * DC18 + 2 * DC19 + DC23)
+                                   : (-DC03 + 13 * DC08 - 24 * DC13 + 13 * DC18 - DC23)),
+                  Q20, bits[3], true);
+            if (bits[4] != 0 && w[9] == 0)
+              w[9] = (int16_t)smooth_pred(
+                  Q00 * (change_dc ? (-DC01 + DC05 + 9 * DC07 - 9 * DC09 - 9 * DC17 + 9 * DC19 + DC21 - DC25)
+                                   : (DC10 + DC16 - 10 * DC17 + 10 * DC19 - DC02 - DC20 + DC22 - DC24 + DC04 -
+                                      DC06 + 10 * DC07 - 10 * DC09)),
+                  Q11, bits[4], true);
+            if (bits[5] != 0 && w[2] == 0)
+              w[2] = (int16_t)smooth_pred(
+                  Q00 * (change_dc ? (2 * DC07 - 5 * DC08 + 2 * DC09 + DC11 + 7 * DC12 - 14 * DC13 + 7 * DC14 +
+                                      DC15 + 2 * DC17 - 5 * DC18 + 2 * DC19)
+                                   : (-DC11 + 13 * DC12 - 24 * DC13 + 13 * DC14 - DC15)),
+                  Q02, bits[5], true);
+            if (change_dc) {
+              if (bits[6] != 0 && w[3] == 0)
+                w[3] = (int16_t)smooth_pred(Q00 * (DC07 - DC09 + 2 * DC12 - 2 * DC14 + DC17 - DC19), Q03, bits[6],
+                                            true);
+              if (bits[7] != 0 && w[10] == 0)
+                w[10] = (int16_t)smooth_pred(Q00 * (DC07 - 3 * DC08 + DC09 - DC17 + 3 * DC18 - DC19), Q12,
+                                             bits[7], true);
+              if (bits[8] != 0 && w[17] == 0)
+                w[17] = (int16_t)smooth_pred(Q00 * (DC07 - DC09 - 3 * DC12 + 3 * DC14 + DC17 - DC19), Q21,
+                                             bits[8], true);
+              if (bits[9] != 0 && w[24] == 0)
+                w[24] = (int16_t)smooth_pred(Q00 * (DC07 + 2 * DC08 + DC09 - DC17 - 2 * DC18 - DC19), Q30,
+                                             bits[9], true);
+              w[0] = (int16_t)smooth_pred(
+                  Q00 * (-2 * DC01 - 6 * DC02 - 8 * DC03 - 6 * DC04 - 2 * DC05 - 6 * DC06 + 6 * DC07 + 42 * DC08 +
+                         6 * DC09 - 6 * DC10 - 8 * DC11 + 42 * DC12 + 152 * DC13 + 42 * DC14 - 8 * DC15 -
+                         6 * DC16 + 6 * DC17 + 42 * DC18 + 6 * DC19 - 6 * DC20 - 2 * DC21 - 6 * DC22 - 8 * DC23 -
+                         6 * DC24 - 2 * DC25),
+                  Q00, 0, false);
+            }
+          }
+        }
+      }
+    }
+    coefbuf.swap(out);
   }
 
   // Components output() reads: grey -> 1; CMYK -> 3 (K is dropped).
@@ -1186,9 +1338,10 @@ struct Decoder {
     store.assign((size_t)c.bw * 8 * c.bh * 8, 0);
     if (c.coded)
       for (int by = 0; by < c.bh; by++)
-        for (int bx = 0; bx < c.bw; bx++)
+        for (int bx = 0; bx < c.bw; bx++) {
           idct_block(coefbuf.data() + c.off + ((int64_t)by * c.bw + bx) * 64, c.q,
                      store.data() + (size_t)by * 8 * c.bw * 8 + (size_t)bx * 8, c.bw * 8);
+        }
     return store.data();
   }
 

@@ -3,8 +3,9 @@
 // jpeg_idct: one thread per 8x8 block: dequantise, jidctint.c ISLOW (13-bit
 //   constants, PASS1_BITS 2, 64-bit intermediates like libjpeg-turbo's JLONG;
 //   its all-zero-AC shortcuts are exact, so the plain transform gives the same
-//   bytes), the post-IDCT range limit as arithmetic (wrap to 10 bits, +128,
-//   clamp), eight 8-byte row stores into the component's sample plane.
+//   bytes), the output range limit of libjpeg-turbo's SIMD IDCTs (+128,
+//   clamp; jpeg.cpp range_limit), eight 8-byte row stores into the
+//   component's sample plane.
 // jpeg_color: one thread per four horizontal output pixels of one image:
 //   each component's sample by jdsample.c's rule for its sampling factors
 //   (fancy triangle upsampling h2v1 / h1v2 / h2v2 with jpeg.cpp's edge cases,
@@ -28,7 +29,7 @@ constexpr i64 F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 73
 __device__ __forceinline__ i64 descale(i64 x, int n) { return (x + ((i64)1 << (n - 1))) >> n; }
 
 __device__ __forceinline__ uint32_t range_limit(i64 x) {
-  const int v = (int)((x + 512) & 1023) - 512 + 128;
+  const i64 v = x + 128;
   return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v);
 }
 

@@ -6,8 +6,12 @@ out, grey replicated to 3 channels, CMYK -> the first three raw channels).
 Cases: 4:4:4 / 4:2:2 / 4:2:0 chroma, greyscale, progressive (spectral
 selection + successive approximation), optimised Huffman tables, restart
 markers (every block, every MCU row), an RGB JPEG (Adobe transform 0), an
-Adobe CMYK JPEG, odd / tiny sizes, and a baseline file truncated inside a
-restart interval (libjpeg's insufficient-data rule).
+Adobe CMYK JPEG, odd / tiny sizes, a baseline file truncated inside a
+restart interval (libjpeg's insufficient-data rule), and progressive files
+truncated after 1-3 whole scans or inside a DC / AC scan (`prog_trunc_*`:
+libjpeg's block smoothing, jdcoefct.c decompress_smooth_data, which
+jpeg_start_decompress applies by default; Pillow's decoder appends the EOI
+that libjpeg's memory source fakes for the reference).
 
     python tests/golden/make_jpeg_golden.py
 """
@@ -64,6 +68,34 @@ def main():
     full = encode(big, quality=90, subsampling=2, restart_marker_blocks=2)
     ImageFile.LOAD_TRUNCATED_IMAGES = True
     cases["truncated_rst"] = full[: len(full) * 6 // 10]
+    # progressive files cut at scan boundaries and inside scans (block smoothing)
+    trng = np.random.default_rng(77)
+    for name, (h, w, c, kw, cut) in {
+        "prog_trunc_s1": (61, 83, 3, dict(subsampling=2), ("scan", 1)),
+        "prog_trunc_s2": (61, 83, 3, dict(subsampling=2), ("scan", 2)),
+        "prog_trunc_s3": (61, 83, 3, dict(subsampling=1), ("scan", 3)),
+        "prog_trunc_dc_mid": (90, 70, 3, dict(subsampling=0), ("mid", 1)),
+        "prog_trunc_ac_mid": (97, 120, 3, dict(subsampling=2), ("mid", 2)),
+        "prog_trunc_ac_mid2": (75, 64, 3, dict(subsampling=1), ("mid", 4)),
+        "prog_trunc_grey_mid": (70, 50, 1, {}, ("mid", 2)),
+        "prog_trunc_w10": (40, 10, 3, dict(subsampling=1), ("scan", 2)),
+    }.items():
+        a = smooth(trng, h, w, c)
+        data = encode(a if c == 3 else a[:, :, 0], quality=75, progressive=True, **kw)
+        sos = [i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] == 0xDA]
+        if cut[0] == "scan":
+            cases[name] = data[: sos[cut[1]]]  # the first cut[1] scans, whole
+        else:
+            # inside scan cut[1] (1-based): halfway through its entropy-coded data
+            p = sos[cut[1] - 1]
+            s = p + 2 + int.from_bytes(data[p + 2:p + 4], "big")
+            e = s
+            while not (data[e] == 0xFF and data[e + 1] != 0 and not 0xD0 <= data[e + 1] <= 0xD7):
+                e += 1
+            m = (s + e) // 2
+            while data[m - 1] == 0xFF:
+                m += 1
+            cases[name] = data[:m]
     out = {"libjpeg_version": np.array(features.version("libjpeg_turbo") or "", dtype="U16")}
     for k, data in cases.items():
         out[f"{k}_jpg"] = np.frombuffer(data, np.uint8)

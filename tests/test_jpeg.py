@@ -6,8 +6,9 @@ upsampling, RGB out, grey replicated, CMYK -> first three raw channels).
 Pinned two ways: the committed fixtures (tests/golden/jpeg.npz, encoded and
 decoded by Pillow's bundled libjpeg-turbo; generator make_jpeg_golden.py) and,
 on hosts with Pillow, a seeded sweep decoded live by Pillow.  Bit-exact
-everywhere.  Not reproduced: libjpeg's block smoothing of progressive files
-whose later scans are missing (truncated progressive data)."""
+everywhere, including libjpeg's block smoothing of progressive files whose
+scans leave low-frequency coefficients inexact (truncated progressive data;
+fixtures `prog_trunc_*` and a live sweep of files cut at and inside scans)."""
 import io
 import os
 
@@ -65,6 +66,54 @@ def test_live_pillow_sweep(seed):
         data = b.getvalue()
         want = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
         assert np.array_equal(capi.jpeg_decode(data), want), (h, w, kw)
+
+
+def _cut_progressive(data, rng):
+    """Cuts a progressive file after a whole scan or inside a scan's entropy-coded data."""
+    sos = [i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] == 0xDA]
+    k = int(rng.integers(1, len(sos)))
+    if rng.random() < 0.4:
+        return data[:sos[k]]
+    p = sos[k - 1]
+    s = p + 2 + int.from_bytes(data[p + 2:p + 4], "big")
+    e = s
+    while not (data[e] == 0xFF and data[e + 1] != 0 and not 0xD0 <= data[e + 1] <= 0xD7):
+        e += 1
+    if e - s < 3:
+        return data[:sos[k]]
+    m = int(rng.integers(s + 1, e))
+    while data[m - 1] == 0xFF:
+        m += 1
+    return data[:m]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_truncated_progressive_block_smoothing(seed):
+    """Progressive files cut after / inside a scan: libjpeg-turbo estimates
+    the missing low-frequency AC coefficients (and, with no AC data at all,
+    the DC) from the 5x5 DC neighbourhood, rows past the last complete iMCU
+    row with the progression status from before the cut scan; Pillow appends
+    the EOI libjpeg's memory source fakes for the reference."""
+    Image = pytest.importorskip("PIL.Image")
+    ImageFile = pytest.importorskip("PIL.ImageFile")
+    rng = np.random.default_rng(500 + seed)
+    prev = ImageFile.LOAD_TRUNCATED_IMAGES
+    ImageFile.LOAD_TRUNCATED_IMAGES = True
+    try:
+        for i in range(10):
+            h, w = int(rng.integers(1, 130)), int(rng.integers(1, 130))
+            grey = i % 5 == 4
+            kw = dict(quality=int(rng.integers(10, 96)), progressive=True)
+            if not grey:
+                kw["subsampling"] = i % 3
+            b = io.BytesIO()
+            a = _smooth(rng, h, w, 1 if grey else 3)
+            Image.fromarray(a[:, :, 0] if grey else a).save(b, "JPEG", **kw)
+            data = _cut_progressive(b.getvalue(), rng)
+            want = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+            assert np.array_equal(capi.jpeg_decode(data), want), (i, h, w, kw, len(data))
+    finally:
+        ImageFile.LOAD_TRUNCATED_IMAGES = prev
 
 
 def _segment(marker, payload):
