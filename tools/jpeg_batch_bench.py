@@ -54,6 +54,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--datasets", default="c4,c1")
+    ap.add_argument("--huff-bits", default="0", help="device entropy: subsequence lengths to time (0: default)")
     args = ap.parse_args()
     from mlx_data_amd import capi
 
@@ -62,8 +63,10 @@ def main():
     for name in args.datasets.split(","):
         datas = files(name, args.batch)
         line = dict(dataset=name, batch=args.batch, mean_file_bytes=round(float(np.mean([len(d) for d in datas])), 1))
-        for dev in (True, False):
-            tag = "device_entropy" if dev else "host_entropy"
+        runs = [(True, int(b)) for b in args.huff_bits.split(",")] + [(False, 0)]
+        for dev, bits in runs:
+            capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
+            tag = ("device_entropy" + (f"_bits{bits}" if bits else "")) if dev else "host_entropy"
             line[f"{tag}_host_us_per_image"] = round(per_image(lambda d: capi.JpegCoefs(d, dev).close(), datas), 1)
             coefs = [capi.JpegCoefs(d, dev) for d in datas]
             assert all(c.entropy_pending == dev for c in coefs)
@@ -88,6 +91,7 @@ def main():
             dst.free()
             for c in coefs:
                 c.close()
+        capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, 0)
         print(json.dumps(line), flush=True)
 
 
