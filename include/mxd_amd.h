@@ -167,7 +167,10 @@ int mxd_set_kernel_policy(int32_t policy);
  * shape) spread over (1: all on the caller's stream; default 2, at most 4);
  * MXD_TUNE_HUFF_BITS: shortest subsequence (bits, a multiple of 32) of the
  * device entropy decode (default 512; tests force short ones so many
- * subsequences must synchronise). */
+ * subsequences must synchronise);
+ * MXD_TUNE_HUFF_GLOBAL: 1 = the device entropy decode reads every job's
+ * entropy-coded words from device memory (default: from LDS for the jobs
+ * whose words fit it). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -175,7 +178,8 @@ enum mxd_tune {
   MXD_TUNE_DESC = 3,
   MXD_TUNE_STREAMS = 4,
   MXD_TUNE_HUFF_BITS = 5,
-  MXD_TUNE_COUNT = 6
+  MXD_TUNE_HUFF_GLOBAL = 6,
+  MXD_TUNE_COUNT = 7
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 
@@ -223,9 +227,13 @@ int mxd_event_elapsed_ms(float* ms, void* start, void* stop);
 
 /* Host image in, host result out; synchronous.  `images[i].src` and
  * `images[i].dst` are HOST pointers here.  Only each image's source footprint
- * (the rows and columns its crop window's taps touch) is staged into pinned
- * memory and copied to the device; the batch runs in chunks whose host
- * staging, H2D, kernel, D2H and copy-out overlap across two streams.  Calls
+ * (the rows and columns its crop window's taps touch) is read, zero copy:
+ * page-locked sources and destinations are read and written in place by the
+ * kernel over PCIe; pageable sources are staged into the call's page-locked
+ * buffers by helper threads (the kernel reads them there) and pageable
+ * destinations written into page-locked buffers and copied out (no H2D / D2H
+ * DMA step; MXD_POLICY_NO_ZERO_COPY restores the DMA form).  The batch runs in
+ * chunks over two slots so staging, kernel and copy-out overlap.  Calls
  * borrow one of a bounded number of per-device contexts (threads beyond that
  * wait), so pinned and device memory stay bounded.  This is the path the C++
  * pipeline ops use when samples live in host memory (mlx-data's default). */

@@ -313,6 +313,7 @@ struct JpegChunk {
   int64_t words_off = 0, words_bytes = 0, htabs_off = 0, himgs_off = 0, hsegs_off = 0, hjobs_off = 0;
   int64_t coef_off = 0, dev_end = 0;
   int32_t huff_threads = 0;
+  int64_t huff_lds = 0;  // the largest job's dynamic LDS (its words included when they fit)
 };
 
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
@@ -372,7 +373,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     c.seg_first[i - first] = (int32_t)c.hsegs.size();
     c.seg_count[i - first] = es.nseg;
     const int32_t img_index = (int32_t)c.himgs.size();
-    int32_t job_sub = mxd::kHuffThreads + 1;
+    const size_t first_job = c.hjobs.size();
+    c.hjobs.push_back(mxd::HuffJobDev{(int32_t)c.hsegs.size(), 0, 0, 0, 0, {0, 0, 0}});  // the image's first job
+    int32_t job_sub = 0;
     for (int sgi = 0; sgi < es.nseg; sgi++) {
       const int64_t raw = es.seg_end[sgi] - es.seg_begin[sgi];
       mxd::HuffSegDev sd{};
@@ -387,18 +390,30 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       // jobs: consecutive segments of one image, <= kHuffThreads subsequences
       // (planned from the raw size; unstuffing only shortens a segment)
       const int32_t nsub = (int32_t)std::max<int64_t>(1, (8 * raw + sub_bits - 1) / sub_bits);
-      if (job_sub + nsub > mxd::kHuffThreads) {
-        c.hjobs.push_back(mxd::HuffJobDev{(int32_t)c.hsegs.size(), 0, 0, 0});
+      const int64_t seg16 = up(raw + 4, 16) / 16;  // its staged words, 16-byte units
+      if (c.hjobs.back().nseg > 0 &&
+          (job_sub + nsub > mxd::kHuffThreads ||
+           mxd::jpeg_huff_lds_bytes(es.ntables, c.hjobs.back().nseg + 1, 4 * (c.hjobs.back().words16 + seg16)) >
+               mxd::jpeg_huff_lds_budget())) {
+        c.hjobs.push_back(mxd::HuffJobDev{(int32_t)c.hsegs.size(), 0, 0, 0, 0, {0, 0, 0}});
         job_sub = 0;
       }
       c.hjobs.back().nseg++;
       c.hjobs.back().nsub += nsub;
+      c.hjobs.back().words16 += (int32_t)seg16;
       job_sub += nsub;
       c.huff_threads = std::max(c.huff_threads, c.hjobs.back().nsub);
       c.hsegs.push_back(sd);
     }
     c.himgs.push_back(h);
     coef_rel += up(info.coef_count * 2, 256);
+    // per job: its words from LDS when they fit (MXD_TUNE_HUFF_GLOBAL: never);
+    // the launch's dynamic LDS is the largest job's
+    for (size_t q = first_job; q < c.hjobs.size(); q++) {
+      const int64_t with = mxd::jpeg_huff_lds_bytes(es.ntables, c.hjobs[q].nseg, 4 * (int64_t)c.hjobs[q].words16);
+      c.hjobs[q].lds = with <= mxd::jpeg_huff_lds_budget() && g_tune[MXD_TUNE_HUFF_GLOBAL].load() == 0 ? 1 : 0;
+      c.huff_lds = std::max(c.huff_lds, c.hjobs[q].lds ? with : mxd::jpeg_huff_lds_bytes(es.ntables, c.hjobs[q].nseg, 0));
+    }
   }
   for (int32_t i = first; i < end; i++) {
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
@@ -727,8 +742,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                 reinterpret_cast<const mxd::HuffImgDev*>(sl.dev_in + jc.himgs_off),
                                 reinterpret_cast<const mxd::HuffSegDev*>(sl.dev_in + jc.hsegs_off),
                                 reinterpret_cast<const mxd::HuffJobDev*>(sl.dev_in + jc.hjobs_off),
-                                (int32_t)jc.hjobs.size(), jc.huff_threads, reinterpret_cast<int16_t*>(sl.dev_in),
-                                sl.stream))
+                                (int32_t)jc.hjobs.size(), jc.huff_threads,
+                                jc.huff_lds,
+                                reinterpret_cast<int16_t*>(sl.dev_in), sl.stream))
         return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
       mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),

@@ -78,21 +78,34 @@ struct HuffSegDev {
   int32_t sub_bits; // bits per subsequence
 };
 
-// One workgroup of the launch: segments [seg0, seg0 + nseg), whose
-// subsequences (ceil(bits / sub_bits) each, >= 1) number nsub <= kHuffThreads.
+// One workgroup of the launch: segments [seg0, seg0 + nseg) of one image
+// (one subsequence length), whose subsequences (ceil(bits / sub_bits) each,
+// >= 1) number nsub <= kHuffThreads; their words are staged contiguously
+// from segment seg0's first word, words16 x 16 bytes, and are read from LDS
+// (lds != 0: they fit the launch's dynamic LDS) or from device memory.
 struct HuffJobDev {
-  int32_t seg0, nseg, nsub, pad;
+  int32_t seg0, nseg, nsub, words16;
+  int32_t lds, pad[3];
 };
+static_assert(sizeof(HuffJobDev) == 32, "HuffJobDev layout");
 
 // Shortest subsequence (bits): a decoder that starts mid-stream needs some
 // symbols to fall into step; the launch uses longer ones when a segment
 // would otherwise need more than kHuffThreads.
 constexpr int kHuffMinBits = 512;
 
+// Dynamic LDS a job needs (its tables and segment records, plus its words
+// when they are read from LDS), and the most a job may use.
+int64_t jpeg_huff_lds_bytes(int ntables, int nseg, int64_t words);
+int64_t jpeg_huff_lds_budget();
+
 // Enqueues the decode of `njobs` jobs (threads: the largest job's
-// subsequences); coefficient offsets in HuffImgDev are int16 elements of
-// `coef`, segment words index `words`.  Returns 0, or -1 if the launch failed.
+// subsequences; lds_bytes: the largest job's dynamic LDS, its words included
+// when it reads them from LDS); coefficient offsets in HuffImgDev are int16
+// elements of `coef`, segment words index `words`.  Returns 0, or -1 if the
+// launch failed.
 int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImgDev* imgs, const HuffSegDev* segs,
-                     const HuffJobDev* jobs, int32_t njobs, int32_t threads, int16_t* coef, void* stream);
+                     const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, int16_t* coef,
+                     void* stream);
 
 }  // namespace mxd

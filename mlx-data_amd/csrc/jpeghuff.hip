@@ -22,7 +22,17 @@
 namespace mxd {
 namespace {
 
-constexpr int kMaxTables = 8;
+
+// Diagnostic builds only (-DMXD_HUFF_STATS=1; never in the product library):
+// per job, the synchronisation rounds and the symbols decoded in them and in
+// the write pass, read back with mxd_debug_huff_stats.
+#ifndef MXD_HUFF_STATS
+#define MXD_HUFF_STATS 0
+#endif
+#if MXD_HUFF_STATS
+constexpr int kStatJobs = 1 << 16;
+__device__ int g_huff_stats[kStatJobs * 4];
+#endif
 
 // Zig-zag -> natural order, 16 extra entries absorbing a corrupt run past 63
 // (jpeg.cpp kNatural, jutils.c jpeg_natural_order); copied into LDS.
@@ -31,10 +41,12 @@ __constant__ uint8_t kNatural[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32,
                                  29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
                                  47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
-// Bit reader over one segment's unstuffed bytes (32-bit words, big-endian
+// Bit readers over one segment's unstuffed bytes (32-bit words, big-endian
 // byte order); words past the segment read as zeros (libjpeg's zeros past
 // the data).  After refill() at least 33 bits are buffered.
-struct Reader {
+//
+// LdsReader: the job's words staged in LDS.
+struct LdsReader {
   const uint32_t* w;
   int32_t nw;
   uint64_t buf;
@@ -66,8 +78,64 @@ struct Reader {
   }
 };
 
+// GlobalReader: the job's words in device memory (jobs whose words do not
+// fit LDS), read in 16-byte chunks two chunks ahead of the one being
+// consumed, so a chunk's load latency hides behind ~256 bits of decoding
+// instead of stalling every word.  Chunks past the segment are not loaded.
+struct GlobalReader {
+  const uint4* chunks;  // the job's words (16-byte aligned)
+  int32_t w0, nw;       // the segment's first word (relative to the job's) and its words
+  int32_t last_chunk;   // the segment's last chunk
+  uint64_t buf;
+  int32_t cnt, wi;      // wi: next word, relative to the segment
+  int32_t ca;           // chunk held in A; B, C: the next two
+  uint4 A, B, C;
+
+  __device__ __forceinline__ uint4 fetch(int32_t ch) const {
+    return ch <= last_chunk ? chunks[ch] : uint4{0u, 0u, 0u, 0u};
+  }
+  __device__ __forceinline__ void refill() {
+    while (cnt <= 32) {
+      const int32_t a = w0 + wi;
+      if ((a >> 2) != ca) {  // words are consumed in order: the next chunk
+        A = B;
+        B = C;
+        ca++;
+        C = fetch(ca + 2);
+      }
+      const int i = a & 3;
+      const uint32_t v = i == 0 ? A.x : i == 1 ? A.y : i == 2 ? A.z : A.w;
+      const uint32_t x = wi < nw ? __builtin_bswap32(v) : 0u;
+      buf |= (uint64_t)x << (32 - cnt);
+      cnt += 32;
+      wi++;
+    }
+  }
+  __device__ __forceinline__ void seek(int32_t bit) {
+    wi = bit >> 5;
+    ca = (w0 + wi) >> 2;
+    A = fetch(ca);
+    B = fetch(ca + 1);
+    C = fetch(ca + 2);
+    buf = 0;
+    cnt = 0;
+    refill();
+    const int s = bit & 31;
+    buf <<= s;
+    cnt -= s;
+  }
+  __device__ __forceinline__ int32_t pos() const { return wi * 32 - cnt; }
+  __device__ __forceinline__ uint32_t take(int n) {
+    const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
+    buf <<= n;
+    cnt -= n;
+    return v;
+  }
+};
+
 // jdhuff.c jpeg_huff_decode on a buffer of >= 16 bits: a code longer than 16
 // bits (corrupt data) consumes 16 bits and decodes as 0.
+template <class Reader>
 __device__ __forceinline__ int huff_symbol(const HuffDev& t, Reader& r) {
   const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
   if (e) {
@@ -94,12 +162,18 @@ __device__ __forceinline__ int extend(uint32_t v, int s) {
   return s == 0 ? 0 : (int)v < (1 << (s - 1)) ? (int)v + ((-1) << s) + 1 : (int)v;
 }
 
-// Per-job shared state.
+// One segment of the job in LDS.
+struct SegLds {
+  int32_t word;  // first word, relative to the job's first word
+  int32_t bits;
+  int32_t mcu0, mcus;
+};
+
+// Per-job shared state (static part; the tables, segment records and, when
+// they fit, the job's words follow in dynamic LDS: jpeg_huff_lds_bytes).
 struct Shared {
-  HuffDev tab[kMaxTables];
   HuffImgDev img;
   uint8_t nat[80];
-  HuffSegDev seg[kHuffThreads];
   int32_t seg_sub0[kHuffThreads];  // first subsequence of each segment of the job
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
@@ -146,7 +220,7 @@ struct Dec {
   // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
   // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
   // value) receive the block's values.
-  template <class OnDc, class OnAc>
+  template <class Reader, class OnDc, class OnAc>
   __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
     if (r.cnt < 32) r.refill();
     if (k == 0) {
@@ -207,30 +281,161 @@ __device__ __forceinline__ int64_t block_addr(const HuffImgDev& im, int64_t g64)
   return im.coef + im.plane[c] + (by * im.bw[c] + bx) * 64;
 }
 
+// Dynamic LDS of a job: its tables, its segment records, then (job.lds)
+// its words.
+__host__ __device__ constexpr int64_t lds_tables_bytes(int ntables) { return (int64_t)ntables * sizeof(HuffDev); }
+__host__ __device__ constexpr int64_t lds_words_at(int ntables, int nseg) {
+  return (lds_tables_bytes(ntables) + (int64_t)nseg * sizeof(SegLds) + 15) / 16 * 16;
+}
+
+// One thread's subsequence: its segment (in LDS form), its index in the
+// segment and its bit range.
+struct Sub {
+  SegLds sg;
+  int j;
+  bool active, first, last;
+  int32_t start, end;
+};
+
+#if MXD_HUFF_STATS
+struct Stats {
+  int sync_syms = 0, write_syms = 0, rounds = 0;
+};
+#else
+struct Stats {};
+#endif
+
+// Passes 1-3 over the job with bit reader `rd` (LdsReader or GlobalReader):
+// synchronisation rounds, each subsequence's first block, the write pass.
+// Leaves the subsequence's per-component DC-difference sums in dcsum and the
+// blocks whose DC it decoded in [dc0, dc1).
+template <class R>
+__device__ __forceinline__ void decode_passes(R rd, Shared& sh, const HuffImgDev& im, const HuffDev* tab, const Sub& u,
+                                              int16_t* coef, int (&dcsum)[3], int64_t& dc0, int64_t& dc1,
+                                              Stats& st) {
+  const int t = threadIdx.x;
+  Dec dec{&im, tab, 0, 0};
+  const auto nop_dc = [](int) {};
+  const auto nop_ac = [](int, int) {};
+
+  // 1. synchronisation rounds (the last subsequence of a segment hands its
+  // state to nobody: it decodes only in the write pass)
+  bool need = u.active && !u.last;
+  for (int round = 0;; round++) {
+#if MXD_HUFF_STATS
+    st.rounds = round + 1;
+#endif
+    if (need) {
+      rd.seek(sh.in_pos[t]);
+      dec.b = sh.in_b[t];
+      dec.k = sh.in_k[t];
+      int done = 0;
+      for (;;) {
+        const int32_t p = rd.pos();
+        if (p >= u.end || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
+        done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
+#if MXD_HUFF_STATS
+        st.sync_syms++;
+#endif
+      }
+      sh.out_pos[t] = rd.pos();
+      sh.out_b[t] = (int8_t)dec.b;
+      sh.out_k[t] = (int8_t)dec.k;
+      sh.done[t] = done;
+      need = false;
+    }
+    __syncthreads();
+    if (t == 0) sh.flag[(round + 1) & 1] = 0;
+    if (u.active && !u.first) {
+      const int32_t p = sh.out_pos[t - 1];
+      const int8_t b = sh.out_b[t - 1], k = sh.out_k[t - 1];
+      if (p != sh.in_pos[t] || b != sh.in_b[t] || k != sh.in_k[t]) {
+        sh.in_pos[t] = p;
+        sh.in_b[t] = b;
+        sh.in_k[t] = k;
+        need = !u.last;
+        sh.flag[round & 1] = 1;
+      }
+    }
+    __syncthreads();
+    if (!sh.flag[round & 1]) break;
+  }
+
+  // 2. first block of each subsequence: the blocks completed before it in its segment
+  const int before = block_exclusive_scan(u.active && !u.last ? sh.done[t] : 0, sh.scan, nullptr);
+  __syncthreads();
+  sh.done[t] = before;  // reuse: exclusive prefix (over the whole job)
+  __syncthreads();
+  const int64_t seg_block0 = (int64_t)u.sg.mcu0 * im.bpm, seg_block1 = ((int64_t)u.sg.mcu0 + u.sg.mcus) * im.bpm;
+  int64_t g = seg_block0 + (u.active ? before - sh.done[t - u.j] : 0);
+
+  // 3. write pass
+  if (u.active) {
+    rd.seek(sh.in_pos[t]);
+    dec.b = sh.in_b[t];
+    dec.k = sh.in_k[t];
+    int16_t* blk = coef + block_addr(im, min(g, seg_block1 - 1));
+    for (;;) {
+      const int32_t p = rd.pos();
+      if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
+      const bool fin = dec.step(
+          rd,
+          [&](int diff) {
+            blk[0] = (int16_t)diff;
+            dcsum[im.blk_comp[dec.b]] += diff;
+            if (dc0 < 0) dc0 = g;
+            dc1 = g + 1;
+          },
+          [&](int kk, int v) {
+            if (v) blk[sh.nat[kk]] = (int16_t)v;
+          });
+      if (fin) {
+        g++;
+        if (g < seg_block1) blk = coef + block_addr(im, g);
+      }
+#if MXD_HUFF_STATS
+      st.write_syms++;
+#endif
+    }
+  }
+}
+
 __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __restrict__ words,
                                                           const HuffDev* __restrict__ tables,
                                                           const HuffImgDev* __restrict__ imgs,
                                                           const HuffSegDev* __restrict__ segs,
                                                           const HuffJobDev* __restrict__ jobs, int16_t* coef) {
   __shared__ Shared sh;
+  extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   const int t = threadIdx.x;
   const HuffJobDev job = jobs[blockIdx.x];
   if (t == 0) sh.img = imgs[segs[job.seg0].img];
   if (t < 80) sh.nat[t] = kNatural[t];
   __syncthreads();
   const HuffImgDev& im = sh.img;
+  HuffDev* tab = reinterpret_cast<HuffDev*>(dyn);
+  SegLds* seg = reinterpret_cast<SegLds*>(reinterpret_cast<char*>(dyn) + lds_tables_bytes(im.ntables));
+  const int64_t word0 = segs[job.seg0].word;  // the job's first word (16-byte aligned)
+  const int sub_bits = segs[job.seg0].sub_bits;
 
-  // 0. tables and segment records into LDS; zero the job's coefficient blocks
+  // 0. tables, segment records and (job.lds) words into LDS; zero the job's
+  // coefficient blocks
   {
     const uint4* src = reinterpret_cast<const uint4*>(tables + im.tables);
-    uint4* dst = reinterpret_cast<uint4*>(sh.tab);
     const int n16 = im.ntables * (int)(sizeof(HuffDev) / 16);
-    for (int i = t; i < n16; i += blockDim.x) dst[i] = src[i];
+    for (int i = t; i < n16; i += blockDim.x) dyn[i] = src[i];
+  }
+  uint32_t* lds_words = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dyn) + lds_words_at(im.ntables, job.nseg));
+  if (job.lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(words + word0);
+    uint4* dst = reinterpret_cast<uint4*>(lds_words);
+    for (int i = t; i < job.words16; i += blockDim.x) dst[i] = src[i];
   }
   int nsub_mine = 0;
   if (t < job.nseg) {
-    sh.seg[t] = segs[job.seg0 + t];
-    nsub_mine = max(1, (sh.seg[t].bits + sh.seg[t].sub_bits - 1) / sh.seg[t].sub_bits);
+    const HuffSegDev g = segs[job.seg0 + t];
+    seg[t] = SegLds{(int32_t)(g.word - word0), g.bits, (int32_t)g.mcu0, g.mcus};
+    nsub_mine = max(1, (g.bits + sub_bits - 1) / sub_bits);
   }
   int nsub = 0;
   const int sub0 = block_exclusive_scan(nsub_mine, sh.scan, &nsub);
@@ -238,7 +443,7 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   {
     const HuffSegDev& s0 = segs[job.seg0];
     const HuffSegDev& s1 = segs[job.seg0 + job.nseg - 1];
-    const int64_t b0 = s0.mcu0 * im.bpm, b1 = (s1.mcu0 + s1.mcus) * im.bpm;
+    const int64_t b0 = s0.mcu0 * im.bpm, b1 = (s1.mcu0 + (int64_t)s1.mcus) * im.bpm;
     for (int64_t g = b0 + (t >> 3); g < b1; g += blockDim.x >> 3)
       reinterpret_cast<uint4*>(coef + block_addr(im, g))[t & 7] = uint4{0, 0, 0, 0};
   }
@@ -256,110 +461,63 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     }
     si = lo;
   }
-  const HuffSegDev& sg = sh.seg[si];
-  const int j = t - sh.seg_sub0[si];                  // index inside the segment
-  const int nseg_sub = max(1, (sg.bits + sg.sub_bits - 1) / sg.sub_bits);
-  const bool active = t < nsub;
-  const bool first = j == 0, last = j == nseg_sub - 1;
-  const int32_t start = j * sg.sub_bits;
-  const int32_t end = last ? 0x7fffffff : start + sg.sub_bits;
-  Reader rd;
-  rd.w = words + sg.word;
-  rd.nw = (sg.bits + 31) >> 5;
-  Dec dec{&im, sh.tab, 0, 0};
-  if (active) {
-    sh.in_pos[t] = start;
+  Sub u;
+  u.sg = seg[si];
+  u.j = t - sh.seg_sub0[si];  // index inside the segment
+  const int nseg_sub = max(1, (u.sg.bits + sub_bits - 1) / sub_bits);
+  u.active = t < nsub;
+  u.first = u.j == 0;
+  u.last = u.j == nseg_sub - 1;
+  u.start = u.j * sub_bits;
+  u.end = u.last ? 0x7fffffff : u.start + sub_bits;
+  if (u.active) {
+    sh.in_pos[t] = u.start;
     sh.in_b[t] = 0;
     sh.in_k[t] = 0;
     sh.done[t] = 0;
   }
-  const auto nop_dc = [](int) {};
-  const auto nop_ac = [](int, int) {};
 
-  // 1. synchronisation rounds (the last subsequence of a segment hands its
-  // state to nobody: it decodes only in the write pass)
-  bool need = active && !last;
-  for (int round = 0;; round++) {
-    if (need) {
-      rd.seek(sh.in_pos[t]);
-      dec.b = sh.in_b[t];
-      dec.k = sh.in_k[t];
-      int done = 0;
-      for (;;) {
-        const int32_t p = rd.pos();
-        if (p >= end || (dec.b == 0 && dec.k == 0 && p > sg.bits)) break;
-        done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
-      }
-      sh.out_pos[t] = rd.pos();
-      sh.out_b[t] = (int8_t)dec.b;
-      sh.out_k[t] = (int8_t)dec.k;
-      sh.done[t] = done;
-      need = false;
-    }
-    __syncthreads();
-    if (t == 0) sh.flag[(round + 1) & 1] = 0;
-    if (active && !first) {
-      const int32_t p = sh.out_pos[t - 1];
-      const int8_t b = sh.out_b[t - 1], k = sh.out_k[t - 1];
-      if (p != sh.in_pos[t] || b != sh.in_b[t] || k != sh.in_k[t]) {
-        sh.in_pos[t] = p;
-        sh.in_b[t] = b;
-        sh.in_k[t] = k;
-        need = !last;
-        sh.flag[round & 1] = 1;
-      }
-    }
-    __syncthreads();
-    if (!sh.flag[round & 1]) break;
-  }
-
-  // 2. first block of each subsequence: the blocks completed before it in its segment
-  const int before = block_exclusive_scan(active && !last ? sh.done[t] : 0, sh.scan, nullptr);
-  __syncthreads();
-  sh.done[t] = before;  // reuse: exclusive prefix (over the whole job)
-  __syncthreads();
-  const int64_t seg_block0 = sg.mcu0 * im.bpm, seg_block1 = (sg.mcu0 + sg.mcus) * im.bpm;
-  int64_t g = seg_block0 + (active ? before - sh.done[t - j] : 0);
-
-  // 3. write pass
   int dcsum[3] = {0, 0, 0};
   int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
-  if (active) {
-    rd.seek(sh.in_pos[t]);
-    dec.b = sh.in_b[t];
-    dec.k = sh.in_k[t];
-    int16_t* blk = coef + block_addr(im, min(g, seg_block1 - 1));
-    for (;;) {
-      const int32_t p = rd.pos();
-      if (p >= end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > sg.bits)) break;
-      const bool fin = dec.step(
-          rd,
-          [&](int diff) {
-            blk[0] = (int16_t)diff;
-            dcsum[im.blk_comp[dec.b]] += diff;
-            if (dc0 < 0) dc0 = g;
-            dc1 = g + 1;
-          },
-          [&](int kk, int v) {
-            if (v) blk[sh.nat[kk]] = (int16_t)v;
-          });
-      if (fin) {
-        g++;
-        if (g < seg_block1) blk = coef + block_addr(im, g);
-      }
-    }
+  Stats st;
+  const int32_t nw = (u.sg.bits + 31) >> 5;
+  if (job.lds) {  // uniform over the workgroup
+    LdsReader rd;
+    rd.w = lds_words + u.sg.word;
+    rd.nw = nw;
+    decode_passes(rd, sh, im, tab, u, coef, dcsum, dc0, dc1, st);
+  } else {
+    GlobalReader rd;
+    rd.chunks = reinterpret_cast<const uint4*>(words + word0);
+    rd.w0 = u.sg.word;
+    rd.nw = nw;
+    rd.last_chunk = (u.sg.word + nw - 1) >> 2;
+    decode_passes(rd, sh, im, tab, u, coef, dcsum, dc0, dc1, st);
   }
 
   // 4. DC values: per component, the differences before this subsequence in its segment
   for (int c = 0; c < 3; c++) {
-    const int ex = block_exclusive_scan(active ? dcsum[c] : 0, sh.scan, nullptr);
+    const int ex = block_exclusive_scan(u.active ? dcsum[c] : 0, sh.scan, nullptr);
     __syncthreads();
     sh.done[t] = ex;
     __syncthreads();
-    dcsum[c] = active ? ex - sh.done[t - j] : 0;  // this subsequence's predictor start
+    dcsum[c] = u.active ? ex - sh.done[t - u.j] : 0;  // this subsequence's predictor start
     __syncthreads();
   }
-  if (active && dc0 >= 0) {
+#if MXD_HUFF_STATS
+  {
+    int sync_syms = 0, write_syms = 0;
+    const int a = block_exclusive_scan(st.sync_syms, sh.scan, &sync_syms);
+    const int b = block_exclusive_scan(st.write_syms, sh.scan, &write_syms);
+    (void)a;
+    (void)b;
+    if (blockIdx.x < kStatJobs && t < 4) {  // lanes 0..3 of wave 0 (vector stores)
+      const int v[4] = {st.rounds, nsub, sync_syms, write_syms};
+      g_huff_stats[blockIdx.x * 4 + t] = v[t];
+    }
+  }
+#endif
+  if (u.active && dc0 >= 0) {
     int pred[3] = {dcsum[0], dcsum[1], dcsum[2]};
     for (int64_t b = dc0; b < dc1; b++) {
       const int bj = (int)(b % im.bpm);
@@ -373,14 +531,37 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
 
 }  // namespace
 
+int64_t jpeg_huff_lds_budget() { return 160 * 1024 - (int64_t)sizeof(Shared) - 1024; }
+
+int64_t jpeg_huff_lds_bytes(int ntables, int nseg, int64_t words) {
+  return lds_words_at(ntables, nseg) + words * 4;
+}
+
 int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImgDev* imgs, const HuffSegDev* segs,
-                     const HuffJobDev* jobs, int32_t njobs, int32_t threads, int16_t* coef, void* stream) {
+                     const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, int16_t* coef,
+                     void* stream) {
   if (njobs <= 0) return 0;
   threads = (threads + 63) / 64 * 64;
   threads = threads < 64 ? 64 : threads > kHuffThreads ? kHuffThreads : threads;
-  hipLaunchKernelGGL(jpeg_huff, dim3(njobs), dim3(threads), 0, reinterpret_cast<hipStream_t>(stream),
-                     words, tables, imgs, segs, jobs, coef);
+  auto k = jpeg_huff;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds_bytes) != hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(k, dim3(njobs), dim3(threads), (size_t)lds_bytes, reinterpret_cast<hipStream_t>(stream), words,
+                     tables, imgs, segs, jobs, coef);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace mxd
+
+#if MXD_HUFF_STATS
+// (rounds, subsequences, sync-pass symbols, write-pass symbols) of the last
+// launch's first n jobs.
+extern "C" int mxd_debug_huff_stats(int* host, int n) {
+  if (n > mxd::kStatJobs) n = mxd::kStatJobs;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mxd::g_huff_stats), sizeof(int) * 4 * n, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif

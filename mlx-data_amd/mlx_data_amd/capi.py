@@ -55,6 +55,7 @@ MXD_TUNE_BAND_GRID = 2
 MXD_TUNE_DESC = 3
 MXD_TUNE_STREAMS = 4
 MXD_TUNE_HUFF_BITS = 5
+MXD_TUNE_HUFF_GLOBAL = 6
 
 
 class MxdImage(ctypes.Structure):

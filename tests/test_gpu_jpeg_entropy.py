@@ -20,7 +20,10 @@ to libjpeg-turbo through Pillow), at identity geometry (the decoded image):
   that runs out before the last MCU while the file still ends with EOI
   (libjpeg's insufficient-data rule: the rest of the interval stays zero);
 * batches across several jobs / images, resize + crop windows, device
-  destinations."""
+  destinations;
+* both word sources: LDS (jobs whose words fit it, the default) and device
+  memory through the prefetching reader (MXD_TUNE_HUFF_GLOBAL = 1, what
+  jobs too large for LDS use)."""
 import io
 import os
 
@@ -116,14 +119,21 @@ def test_fixtures_identity():
     assert sum(c.entropy_pending for c in coefs) >= 5  # the baseline fixtures go to the device
 
 
+@pytest.fixture(params=[0, 1], ids=["lds_words", "global_words"])
+def word_source(request):
+    prev = capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, request.param)
+    yield request.param
+    capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, prev)
+
+
 @pytest.mark.parametrize("seed", range(4))
-def test_encoded_sweep_identity(seed):
+def test_encoded_sweep_identity(seed, word_source):
     coefs = _check_identity(_sweep(seed))
     assert all(c.entropy_pending for c in coefs)  # baseline, one scan: every file qualifies
 
 
 @pytest.mark.parametrize("bits", [32, 64, 96])
-def test_short_subsequences_synchronise(bits):
+def test_short_subsequences_synchronise(bits, word_source):
     prev = capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
     try:
         _check_identity(_sweep(100 + bits, n=10, max_side=400))
@@ -140,7 +150,7 @@ def _ecs_range(d):
 
 
 @pytest.mark.parametrize("bits", [0, 64])
-def test_corrupt_and_short_entropy_data(bits):
+def test_corrupt_and_short_entropy_data(bits, word_source):
     rng = np.random.default_rng(9)
     datas = []
     for i in range(12):
@@ -208,7 +218,7 @@ def test_resize_crop_windows(f32, device_dst):
         assert np.array_equal(g, w_)
 
 
-def test_large_image_many_jobs():
+def test_large_image_many_jobs(word_source):
     """A 3000x2000 image with restart markers every block: thousands of
     segments, packed into several jobs; and a 2400x1800 one without restart
     markers (one segment of ~1024 subsequences)."""

@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--datasets", default="c4,c1")
     ap.add_argument("--huff-bits", default="0", help="device entropy: subsequence lengths to time (0: default)")
+    ap.add_argument("--huff-global", action="store_true", help="device entropy: also time words read from device memory")
     args = ap.parse_args()
     from mlx_data_amd import capi
 
@@ -63,10 +64,13 @@ def main():
     for name in args.datasets.split(","):
         datas = files(name, args.batch)
         line = dict(dataset=name, batch=args.batch, mean_file_bytes=round(float(np.mean([len(d) for d in datas])), 1))
-        runs = [(True, int(b)) for b in args.huff_bits.split(",")] + [(False, 0)]
-        for dev, bits in runs:
+        runs = [(True, int(b), 0) for b in args.huff_bits.split(",")] + ([(True, 0, 1)] if args.huff_global else [])
+        runs.append((False, 0, 0))
+        for dev, bits, glob in runs:
             capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
-            tag = ("device_entropy" + (f"_bits{bits}" if bits else "")) if dev else "host_entropy"
+            capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, glob)
+            tag = ("device_entropy" + (f"_bits{bits}" if bits else "") + ("_global" if glob else "")) if dev \
+                else "host_entropy"
             line[f"{tag}_host_us_per_image"] = round(per_image(lambda d: capi.JpegCoefs(d, dev).close(), datas), 1)
             coefs = [capi.JpegCoefs(d, dev) for d in datas]
             assert all(c.entropy_pending == dev for c in coefs)
@@ -92,6 +96,7 @@ def main():
             for c in coefs:
                 c.close()
         capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, 0)
+        capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, 0)
         print(json.dumps(line), flush=True)
 
 

@@ -14,7 +14,7 @@ if [ "$1" = build ]; then
   cd mlx-data_amd
   mkdir -p build/var_$NAME
   OBJS=""
-  for o in resample wave band band_plan pixmap capi plan batch hostpath taps jpeg jpegdev; do
+  for o in resample wave band band_plan pixmap capi plan batch hostpath taps jpeg jpegdev jpeghuff; do
     if [[ " $SRCS " == *" $o "* ]]; then
       src=csrc/$o.hip; [ -f $src ] || src=csrc/$o.cpp
       /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
