@@ -25,13 +25,22 @@ namespace {
 
 // Diagnostic builds only (-DMXD_HUFF_STATS=1; never in the product library):
 // per job, the synchronisation rounds and the symbols decoded in them and in
-// the write pass, read back with mxd_debug_huff_stats.
+// the write pass, and the durations of the phases (s_memrealtime ticks, 10 ns:
+// staging, synchronisation, write pass, DC), read back with
+// mxd_debug_huff_stats (kStatInts per job).
 #ifndef MXD_HUFF_STATS
 #define MXD_HUFF_STATS 0
 #endif
+// Tuning builds (-DMXD_HUFF_UNIFIED=1): one decode path for DC and AC symbols.
+#ifndef MXD_HUFF_UNIFIED
+#define MXD_HUFF_UNIFIED 0
+#endif
+
 #if MXD_HUFF_STATS
 constexpr int kStatJobs = 1 << 16;
-__device__ int g_huff_stats[kStatJobs * 4];
+constexpr int kStatInts = 8;
+__device__ int g_huff_stats[kStatJobs * kStatInts];
+__device__ __forceinline__ uint64_t stat_clock() { return __builtin_amdgcn_s_memrealtime(); }
 #endif
 
 // Zig-zag -> natural order, 16 extra entries absorbing a corrupt run past 63
@@ -158,6 +167,28 @@ __device__ __forceinline__ int huff_symbol(const HuffDev& t, Reader& r) {
   return t.vals[(code + t.valoffset[l]) & 0xff];
 }
 
+// A code longer than kHuffLook bits without a loop: its length is the
+// shortest l in kHuffLook+1..16 whose l-bit prefix is <= maxcode[l] (canonical
+// codes; jdhuff.c jpeg_huff_decode's search); none (corrupt data) consumes 16
+// bits and decodes as 0, as huff_symbol does.
+template <class Reader>
+__device__ __forceinline__ int huff_long(const HuffDev& t, Reader& r) {
+  const uint32_t p16 = (uint32_t)(r.buf >> 48);
+  int len = 17;
+#pragma unroll
+  for (int l = 16; l > kHuffLook; l--)
+    if ((int32_t)(p16 >> (16 - l)) <= t.maxcode[l]) len = l;
+  if (len > 16) {
+    r.buf <<= 16;
+    r.cnt -= 16;
+    return 0;
+  }
+  const int32_t code = (int32_t)(p16 >> (16 - len));
+  r.buf <<= len;
+  r.cnt -= len;
+  return t.vals[(code + t.valoffset[len]) & 0xff];
+}
+
 __device__ __forceinline__ int extend(uint32_t v, int s) {
   return s == 0 ? 0 : (int)v < (1 << (s - 1)) ? (int)v + ((-1) << s) + 1 : (int)v;
 }
@@ -220,6 +251,48 @@ struct Dec {
   // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
   // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
   // value) receive the block's values.
+#if MXD_HUFF_UNIFIED
+  // One path for DC and AC symbols (tuning builds, -DMXD_HUFF_UNIFIED=1): the
+  // block's DC or AC table is selected, one lookup gives the symbol (codes
+  // past the lookahead without a loop), the value bits follow; the lanes of a
+  // wave, whichever symbol kind each decodes, run the same instructions.
+  template <class Reader, class OnDc, class OnAc>
+  __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
+    if (r.cnt < 32) r.refill();
+    const bool dc = k == 0;
+    const HuffDev& t = tab[dc ? im->blk_dc[b] : im->blk_ac[b]];
+    const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
+    int sym;
+    if (e) {
+      r.buf <<= e >> 8;
+      r.cnt -= e >> 8;
+      sym = e & 0xff;
+    } else {
+      sym = huff_long(t, r);
+    }
+    const int run = dc ? 0 : sym >> 4, sz = dc ? sym : sym & 15;
+    const int v = extend(r.take(sz), sz);
+    bool end = false;
+    if (dc) {
+      on_dc(v);
+      k = 1;
+    } else if (sz) {
+      k += run;
+      on_ac(k, v);
+      end = ++k >= 64;
+    } else if (run == 15) {
+      k += 16;
+      end = k >= 64;
+    } else {
+      end = true;
+    }
+    if (end) {
+      k = 0;
+      b = b + 1 == im->bpm ? 0 : b + 1;
+    }
+    return end;
+  }
+#else
   template <class Reader, class OnDc, class OnAc>
   __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
     if (r.cnt < 32) r.refill();
@@ -263,6 +336,7 @@ struct Dec {
     }
     return end;
   }
+#endif
 };
 
 // Coefficient offset of block g (decode order) of the image: blocks number
@@ -300,6 +374,7 @@ struct Sub {
 #if MXD_HUFF_STATS
 struct Stats {
   int sync_syms = 0, write_syms = 0, rounds = 0;
+  uint64_t t[4] = {0, 0, 0, 0};  // thread 0: staged, synchronised, written, done
 };
 #else
 struct Stats {};
@@ -360,6 +435,9 @@ __device__ __forceinline__ void decode_passes(R rd, Shared& sh, const HuffImgDev
     __syncthreads();
     if (!sh.flag[round & 1]) break;
   }
+#if MXD_HUFF_STATS
+  st.t[1] = stat_clock();
+#endif
 
   // 2. first block of each subsequence: the blocks completed before it in its segment
   const int before = block_exclusive_scan(u.active && !u.last ? sh.done[t] : 0, sh.scan, nullptr);
@@ -407,6 +485,9 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
                                                           const HuffJobDev* __restrict__ jobs, int16_t* coef) {
   __shared__ Shared sh;
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
+#if MXD_HUFF_STATS
+  const uint64_t t_kernel = stat_clock();
+#endif
   const int t = threadIdx.x;
   const HuffJobDev job = jobs[blockIdx.x];
   if (t == 0) sh.img = imgs[segs[job.seg0].img];
@@ -449,6 +530,9 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   }
   if (t == 0) sh.flag[0] = sh.flag[1] = 0;
   __syncthreads();
+#if MXD_HUFF_STATS
+  const uint64_t t_start = stat_clock();
+#endif
 
   // this thread's subsequence: its segment (binary search of seg_sub0) and bit range
   int si = 0;
@@ -480,6 +564,9 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   int dcsum[3] = {0, 0, 0};
   int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
   Stats st;
+#if MXD_HUFF_STATS
+  st.t[0] = t_start;
+#endif
   const int32_t nw = (u.sg.bits + 31) >> 5;
   if (job.lds) {  // uniform over the workgroup
     LdsReader rd;
@@ -498,6 +585,9 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   // 4. DC values: per component, the differences before this subsequence in its segment
   for (int c = 0; c < 3; c++) {
     const int ex = block_exclusive_scan(u.active ? dcsum[c] : 0, sh.scan, nullptr);
+#if MXD_HUFF_STATS
+    if (c == 0) st.t[2] = stat_clock();
+#endif
     __syncthreads();
     sh.done[t] = ex;
     __syncthreads();
@@ -505,16 +595,12 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     __syncthreads();
   }
 #if MXD_HUFF_STATS
+  int stat_sync = 0, stat_write = 0;
   {
-    int sync_syms = 0, write_syms = 0;
-    const int a = block_exclusive_scan(st.sync_syms, sh.scan, &sync_syms);
-    const int b = block_exclusive_scan(st.write_syms, sh.scan, &write_syms);
+    const int a = block_exclusive_scan(st.sync_syms, sh.scan, &stat_sync);
+    const int b = block_exclusive_scan(st.write_syms, sh.scan, &stat_write);
     (void)a;
     (void)b;
-    if (blockIdx.x < kStatJobs && t < 4) {  // lanes 0..3 of wave 0 (vector stores)
-      const int v[4] = {st.rounds, nsub, sync_syms, write_syms};
-      g_huff_stats[blockIdx.x * 4 + t] = v[t];
-    }
   }
 #endif
   if (u.active && dc0 >= 0) {
@@ -527,6 +613,18 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
       d[0] = (int16_t)pred[c];
     }
   }
+#if MXD_HUFF_STATS
+  __syncthreads();
+  st.t[3] = stat_clock();
+  // wave 0's lanes 0..7 (vector stores); thread 0's clocks
+  const uint64_t t0 = __shfl(st.t[0], 0, 64), t1 = __shfl(st.t[1], 0, 64), t2 = __shfl(st.t[2], 0, 64),
+                 t3 = __shfl(st.t[3], 0, 64), tk = __shfl(t_kernel, 0, 64);
+  if (blockIdx.x < kStatJobs && t < kStatInts) {
+    const int v[kStatInts] = {st.rounds,   nsub, stat_sync, stat_write, (int)(t1 - t0), (int)(t2 - t1),
+                              (int)(t3 - t2), (int)(t0 - tk)};
+    g_huff_stats[blockIdx.x * kStatInts + t] = v[t];
+  }
+#endif
 }
 
 }  // namespace
@@ -559,7 +657,8 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
 // launch's first n jobs.
 extern "C" int mxd_debug_huff_stats(int* host, int n) {
   if (n > mxd::kStatJobs) n = mxd::kStatJobs;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mxd::g_huff_stats), sizeof(int) * 4 * n, 0, hipMemcpyDeviceToHost) ==
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mxd::g_huff_stats), sizeof(int) * mxd::kStatInts * n, 0,
+                             hipMemcpyDeviceToHost) ==
                  hipSuccess
              ? 0
              : -1;

@@ -1,4 +1,4 @@
-"""Synchronisation statistics of the device entropy decode (diagnostic; needs
+"""Synchronisation statistics and phase durations of the device entropy decode (diagnostic; needs
 the -DMXD_HUFF_STATS=1 variant library in place of libmxd_amd.so,
 tools/variants.sh build hstats "-DMXD_HUFF_STATS=1" jpeghuff): per job the
 rounds until no subsequence's start state changed, the subsequences, and the
@@ -36,11 +36,17 @@ def main():
                                     dst=dst.ptr + i * 224 * 224 * 3, dst_stride=224 * 3))
             arr, n = capi.make_jpeg_images(entries)
             capi.jpeg_resize_crop_to_device(arr, n, capi.MXD_U8, 0)
-            st = np.zeros((len(datas), 4), np.int32)
+            st = np.zeros((len(datas), 8), np.int32)
             assert L.mxd_debug_huff_stats(st.ctypes.data_as(ctypes.c_void_p), len(datas)) == 0
             print(json.dumps(dict(dataset=name, min_bits=bits, rounds_mean=round(float(st[:, 0].mean()), 2),
                                   rounds_max=int(st[:, 0].max()), subsequences_mean=round(float(st[:, 1].mean()), 1),
-                                  sync_symbols_per_write_symbol=round(float(st[:, 2].sum() / st[:, 3].sum()), 3))),
+                                  sync_symbols_per_write_symbol=round(float(st[:, 2].sum() / st[:, 3].sum()), 3),
+                                  # phase durations, us (mean / max over jobs): staging, sync rounds, write, DC
+                                  us_stage=[round(float(st[:, 7].mean()) / 100, 1), round(float(st[:, 7].max()) / 100, 1)],
+                                  us_sync=[round(float(st[:, 4].mean()) / 100, 1), round(float(st[:, 4].max()) / 100, 1)],
+                                  us_write=[round(float(st[:, 5].mean()) / 100, 1), round(float(st[:, 5].max()) / 100, 1)],
+                                  us_dc=[round(float(st[:, 6].mean()) / 100, 1), round(float(st[:, 6].max()) / 100, 1)],
+                                  syms_per_sub_round=round(float(st[:, 2].sum() / max(1, (st[:, 1] * st[:, 0]).sum())), 1))),
                   flush=True)
             dst.free()
     capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, 0)
