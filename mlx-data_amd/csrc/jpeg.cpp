@@ -147,6 +147,36 @@ void build_huff(Huff& h, const uint8_t* bits /* [17], bits[0] unused */, const u
   h.present = true;
 }
 
+// build_huff through a small per-thread cache keyed by the DHT's counts and
+// values: files from one encoder carry the same tables, and deriving them is
+// about half of a markers-only parse (mxd_jpeg_coefs_parse).
+void cached_huff(Huff& h, const uint8_t* bits, const uint8_t* vals, int nvals) {
+  struct Entry {
+    uint8_t bits[17];
+    uint8_t vals[256];
+    int nvals = -1;
+    Huff h;
+  };
+  constexpr int kEntries = 8;
+  thread_local std::unique_ptr<Entry[]> cache;
+  thread_local int next = 0;
+  if (!cache) cache.reset(new Entry[kEntries]);
+  for (int i = 0; i < kEntries; i++) {
+    const Entry& e = cache[i];
+    if (e.nvals == nvals && std::memcmp(e.bits + 1, bits + 1, 16) == 0 && std::memcmp(e.vals, vals, nvals) == 0) {
+      h = e.h;
+      return;
+    }
+  }
+  build_huff(h, bits, vals, nvals);  // throws on a bogus table: nothing cached
+  Entry& e = cache[next];
+  next = (next + 1) % kEntries;
+  std::memcpy(e.bits, bits, 17);
+  std::memcpy(e.vals, vals, nvals);
+  e.nvals = nvals;
+  e.h = h;
+}
+
 inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v + ((-1) << s) + 1 : v; }
 
 // Entropy-coded segment reader: stops at a marker; bits needed past it are
@@ -743,7 +773,7 @@ struct Decoder {
       len -= count;
       const int cls = tc >> 4, idx = tc & 15;
       if (idx > 3) fail("Bogus DHT index");
-      build_huff(cls ? ac[idx] : dc[idx], bits, vals, count);
+      cached_huff(cls ? ac[idx] : dc[idx], bits, vals, count);
     }
     if (len != 0) fail("Bogus marker length");
   }
