@@ -31,9 +31,12 @@ namespace {
 #ifndef MXD_HUFF_STATS
 #define MXD_HUFF_STATS 0
 #endif
-// Tuning builds (-DMXD_HUFF_UNIFIED=1): one decode path for DC and AC symbols.
+// One decode path for DC and AC symbols (default; tuning builds
+// -DMXD_HUFF_UNIFIED=0 keep separate DC / fast-AC / general paths, whose
+// divergence cost 28 % more kernel time: 1.48 vs 1.15 ms per C4 batch of
+// 128, profiles/r04/r04h_*).
 #ifndef MXD_HUFF_UNIFIED
-#define MXD_HUFF_UNIFIED 0
+#define MXD_HUFF_UNIFIED 1
 #endif
 
 #if MXD_HUFF_STATS
@@ -60,6 +63,12 @@ struct LdsReader {
   int32_t nw;
   uint64_t buf;
   int32_t cnt, wi;
+
+  // base: the job's words in LDS; w0 / nw: the segment's first word and words
+  __device__ __forceinline__ void init(const void* base, int32_t w0, int32_t nwords) {
+    w = static_cast<const uint32_t*>(base) + w0;
+    nw = nwords;
+  }
 
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
@@ -99,6 +108,14 @@ struct GlobalReader {
   int32_t cnt, wi;      // wi: next word, relative to the segment
   int32_t ca;           // chunk held in A; B, C: the next two
   uint4 A, B, C;
+
+  // base: the job's words in device memory
+  __device__ __forceinline__ void init(const void* base, int32_t w0_, int32_t nwords) {
+    chunks = static_cast<const uint4*>(base);
+    w0 = w0_;
+    nw = nwords;
+    last_chunk = (w0_ + nwords - 1) >> 2;
+  }
 
   __device__ __forceinline__ uint4 fetch(int32_t ch) const {
     return ch <= last_chunk ? chunks[ch] : uint4{0u, 0u, 0u, 0u};
@@ -209,6 +226,8 @@ struct Shared {
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
   int32_t done[kHuffThreads];      // blocks a subsequence completes (sync pass)
+  int16_t sub_seg[kHuffThreads];   // segment of each subsequence
+  int16_t list[kHuffThreads];      // this round's subsequences to decode (compacted)
   int32_t scan[kHuffThreads / 64];
   int32_t flag[2];
 };
@@ -252,7 +271,7 @@ struct Dec {
   // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
   // value) receive the block's values.
 #if MXD_HUFF_UNIFIED
-  // One path for DC and AC symbols (tuning builds, -DMXD_HUFF_UNIFIED=1): the
+  // One path for DC and AC symbols: the
   // block's DC or AC table is selected, one lookup gives the symbol (codes
   // past the lookahead without a loop), the value bits follow; the lanes of a
   // wave, whichever symbol kind each decodes, run the same instructions.
@@ -371,6 +390,28 @@ struct Sub {
   int32_t start, end;
 };
 
+// Subsequence `id` of the job (its segment from sh.sub_seg).
+__device__ __forceinline__ Sub sub_of(const Shared& sh, const SegLds* seg, int sub_bits, int id, int nsub) {
+  Sub v;
+  const int si = sh.sub_seg[id];
+  v.sg = seg[si];
+  v.j = id - sh.seg_sub0[si];
+  const int nseg_sub = max(1, (v.sg.bits + sub_bits - 1) / sub_bits);
+  v.active = id < nsub;
+  v.first = v.j == 0;
+  v.last = v.j == nseg_sub - 1;
+  v.start = v.j * sub_bits;
+  v.end = v.last ? 0x7fffffff : v.start + sub_bits;
+  return v;
+}
+
+// Tuning builds (-DMXD_HUFF_COMPACT=0): every thread decodes its own
+// subsequence in every round it must, instead of the round's subsequences
+// being packed onto the first threads.
+#ifndef MXD_HUFF_COMPACT
+#define MXD_HUFF_COMPACT 1
+#endif
+
 #if MXD_HUFF_STATS
 struct Stats {
   int sync_syms = 0, write_syms = 0, rounds = 0;
@@ -385,13 +426,15 @@ struct Stats {};
 // Leaves the subsequence's per-component DC-difference sums in dcsum and the
 // blocks whose DC it decoded in [dc0, dc1).
 template <class R>
-__device__ __forceinline__ void decode_passes(R rd, Shared& sh, const HuffImgDev& im, const HuffDev* tab, const Sub& u,
+__device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, const HuffImgDev& im, const HuffDev* tab,
+                                              const SegLds* seg, int sub_bits, int nsub, const Sub& u,
                                               int16_t* coef, int (&dcsum)[3], int64_t& dc0, int64_t& dc1,
                                               Stats& st) {
   const int t = threadIdx.x;
   Dec dec{&im, tab, 0, 0};
   const auto nop_dc = [](int) {};
   const auto nop_ac = [](int, int) {};
+  R rd;
 
   // 1. synchronisation rounds (the last subsequence of a segment hands its
   // state to nobody: it decodes only in the write pass)
@@ -400,25 +443,40 @@ __device__ __forceinline__ void decode_passes(R rd, Shared& sh, const HuffImgDev
 #if MXD_HUFF_STATS
     st.rounds = round + 1;
 #endif
-    if (need) {
-      rd.seek(sh.in_pos[t]);
-      dec.b = sh.in_b[t];
-      dec.k = sh.in_k[t];
+    // this round's subsequences: compacted onto the first threads, so a
+    // round in which few start states changed runs few waves
+#if MXD_HUFF_COMPACT
+    int nact = 0;
+    const int slot = block_exclusive_scan(need ? 1 : 0, sh.scan, &nact);
+    if (need) sh.list[slot] = (int16_t)t;
+    __syncthreads();
+    const bool work = t < nact;
+    const int id = work ? sh.list[t] : t;
+#else
+    const bool work = need;
+    const int id = t;
+#endif
+    if (work) {
+      const Sub v = sub_of(sh, seg, sub_bits, id, nsub);
+      rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5);
+      rd.seek(sh.in_pos[id]);
+      dec.b = sh.in_b[id];
+      dec.k = sh.in_k[id];
       int done = 0;
       for (;;) {
         const int32_t p = rd.pos();
-        if (p >= u.end || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
+        if (p >= v.end || (dec.b == 0 && dec.k == 0 && p > v.sg.bits)) break;
         done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
 #if MXD_HUFF_STATS
         st.sync_syms++;
 #endif
       }
-      sh.out_pos[t] = rd.pos();
-      sh.out_b[t] = (int8_t)dec.b;
-      sh.out_k[t] = (int8_t)dec.k;
-      sh.done[t] = done;
-      need = false;
+      sh.out_pos[id] = rd.pos();
+      sh.out_b[id] = (int8_t)dec.b;
+      sh.out_k[id] = (int8_t)dec.k;
+      sh.done[id] = done;
     }
+    need = false;
     __syncthreads();
     if (t == 0) sh.flag[(round + 1) & 1] = 0;
     if (u.active && !u.first) {
@@ -449,6 +507,7 @@ __device__ __forceinline__ void decode_passes(R rd, Shared& sh, const HuffImgDev
 
   // 3. write pass
   if (u.active) {
+    rd.init(wbase, u.sg.word, (u.sg.bits + 31) >> 5);
     rd.seek(sh.in_pos[t]);
     dec.b = sh.in_b[t];
     dec.k = sh.in_k[t];
@@ -559,7 +618,9 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     sh.in_b[t] = 0;
     sh.in_k[t] = 0;
     sh.done[t] = 0;
+    sh.sub_seg[t] = (int16_t)si;
   }
+  __syncthreads();  // sub_seg of every subsequence before any round reads it
 
   int dcsum[3] = {0, 0, 0};
   int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
@@ -567,20 +628,10 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
 #if MXD_HUFF_STATS
   st.t[0] = t_start;
 #endif
-  const int32_t nw = (u.sg.bits + 31) >> 5;
-  if (job.lds) {  // uniform over the workgroup
-    LdsReader rd;
-    rd.w = lds_words + u.sg.word;
-    rd.nw = nw;
-    decode_passes(rd, sh, im, tab, u, coef, dcsum, dc0, dc1, st);
-  } else {
-    GlobalReader rd;
-    rd.chunks = reinterpret_cast<const uint4*>(words + word0);
-    rd.w0 = u.sg.word;
-    rd.nw = nw;
-    rd.last_chunk = (u.sg.word + nw - 1) >> 2;
-    decode_passes(rd, sh, im, tab, u, coef, dcsum, dc0, dc1, st);
-  }
+  if (job.lds)  // uniform over the workgroup
+    decode_passes<LdsReader>(lds_words, sh, im, tab, seg, sub_bits, nsub, u, coef, dcsum, dc0, dc1, st);
+  else
+    decode_passes<GlobalReader>(words + word0, sh, im, tab, seg, sub_bits, nsub, u, coef, dcsum, dc0, dc1, st);
 
   // 4. DC values: per component, the differences before this subsequence in its segment
   for (int c = 0; c < 3; c++) {
