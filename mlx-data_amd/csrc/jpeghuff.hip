@@ -266,6 +266,20 @@ struct Dec {
   const HuffImgDev* im;
   const HuffDev* tab;
   int b, k;
+  // the DC (bits 3b..3b+2) and AC (32 + 3b..) table of each block of the MCU,
+  // in a register instead of two LDS reads per symbol
+  uint64_t tpack;
+  int bpm;
+
+  __device__ __forceinline__ void init(const HuffImgDev* im_, const HuffDev* tab_) {
+    im = im_;
+    tab = tab_;
+    b = k = 0;
+    bpm = im_->bpm;
+    tpack = 0;
+    for (int j = 0; j < bpm; j++)
+      tpack |= ((uint64_t)(im_->blk_dc[j] & 7) << (3 * j)) | ((uint64_t)(im_->blk_ac[j] & 7) << (32 + 3 * j));
+  }
 
   // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
   // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
@@ -279,7 +293,7 @@ struct Dec {
   __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
     if (r.cnt < 32) r.refill();
     const bool dc = k == 0;
-    const HuffDev& t = tab[dc ? im->blk_dc[b] : im->blk_ac[b]];
+    const HuffDev& t = tab[(tpack >> ((dc ? 0 : 32) + 3 * b)) & 7];
     const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
     int sym;
     if (e) {
@@ -307,7 +321,7 @@ struct Dec {
     }
     if (end) {
       k = 0;
-      b = b + 1 == im->bpm ? 0 : b + 1;
+      b = b + 1 == bpm ? 0 : b + 1;
     }
     return end;
   }
@@ -431,7 +445,8 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
                                               int16_t* coef, int (&dcsum)[3], int64_t& dc0, int64_t& dc1,
                                               Stats& st) {
   const int t = threadIdx.x;
-  Dec dec{&im, tab, 0, 0};
+  Dec dec;
+  dec.init(&im, tab);
   const auto nop_dc = [](int) {};
   const auto nop_ac = [](int, int) {};
   R rd;
