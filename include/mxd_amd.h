@@ -217,6 +217,8 @@ int mxd_memset_async(void* dst, int value, size_t bytes, void* stream);
 int mxd_stream_create(int32_t device, void** stream);
 int mxd_stream_destroy(void* stream);
 int mxd_stream_synchronize(void* stream);
+/* Waits for all work on every stream of `device` (hipDeviceSynchronize). */
+int mxd_device_synchronize(int32_t device);
 int mxd_event_create(void** event);
 int mxd_event_destroy(void* event);
 int mxd_event_record(void* event, void* stream);

@@ -377,6 +377,13 @@ int mxd_stream_synchronize(void* stream) {
   return MXD_OK;
 }
 
+int mxd_device_synchronize(int32_t device) {
+  if (int rc = check_device(device)) return rc;
+  DeviceGuard g(device);
+  MXD_HIP(hipDeviceSynchronize());
+  return MXD_OK;
+}
+
 int mxd_event_create(void** event) {
   if (!event) return fail(MXD_ERR_INVALID, "mxd: null event");
   hipEvent_t e = nullptr;

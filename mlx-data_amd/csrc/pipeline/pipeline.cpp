@@ -1011,6 +1011,86 @@ ImagePlan deferred_plan(const std::shared_ptr<Array>& a) {
   return p;
 }
 
+// Device batch tensors (batch(..., device=d)), recycled by size like
+// BatchPool: a device allocation and its release (hipMalloc / hipFree, which
+// waits for the whole device) per batch serialised the prefetch workers of a
+// device pipeline.  A released block may still be read by work its consumer
+// (e.g. torch through DLPack) enqueued on a stream of its own, so it is only
+// reused after a device synchronisation that followed its release: blocks
+// released since the last one wait in `pending`; a request that finds no
+// idle block of its size synchronises the device once and makes every
+// pending block idle.  At most kMaxCached bytes wait per device.
+class DevicePool {
+ public:
+  std::shared_ptr<void> get(int device, int64_t n) {
+    const size_t cap = ((size_t)std::max<int64_t>(n, 1) + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+    void* p = take(device, cap, false);
+    if (!p && has_pending(device, cap)) {
+      std::vector<std::pair<size_t, void*>> now;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        now.swap(devs_[device].pending);
+      }
+      check(mxd_device_synchronize(device));  // everything released before this point is idle
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto& b : now) devs_[device].idle[b.first].push_back(b.second);
+      }
+      p = take(device, cap, true);
+    }
+    if (!p) check(mxd_malloc_device(&p, cap, device));
+    return std::shared_ptr<void>(p, [this, device, cap](void* q) { put(device, q, cap); });
+  }
+
+ private:
+  static constexpr size_t kMaxCached = (size_t)2 << 30;
+  struct Dev {
+    std::map<size_t, std::vector<void*>> idle;
+    std::vector<std::pair<size_t, void*>> pending;
+    size_t cached = 0;
+  };
+  void* take(int device, size_t cap, bool) {
+    std::lock_guard<std::mutex> lk(mu_);
+    Dev& d = devs_[device];
+    auto it = d.idle.find(cap);
+    if (it == d.idle.end() || it->second.empty()) return nullptr;
+    void* p = it->second.back();
+    it->second.pop_back();
+    d.cached -= cap;
+    return p;
+  }
+  bool has_pending(int device, size_t cap) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& b : devs_[device].pending)
+      if (b.first == cap) return true;
+    return false;
+  }
+  void put(int device, void* p, size_t cap) {
+    std::vector<void*> drop;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      Dev& d = devs_[device];
+      d.pending.emplace_back(cap, p);
+      d.cached += cap;
+      // over the cap: idle blocks of other sizes go first
+      for (auto it = d.idle.begin(); d.cached > kMaxCached && it != d.idle.end(); ++it)
+        while (d.cached > kMaxCached && !it->second.empty()) {
+          drop.push_back(it->second.back());
+          it->second.pop_back();
+          d.cached -= it->first;
+        }
+    }
+    for (void* q : drop) (void)mxd_free_device(q, device);
+  }
+  std::mutex mu_;
+  std::map<int, Dev> devs_;
+};
+
+DevicePool& device_pool() {
+  static DevicePool* p = new DevicePool();  // leaked on purpose: outlives static teardown
+  return *p;
+}
+
 // batch_arrays into device memory.  The fused case -- every array a pending
 // image filling the batch's pixel slots, nothing to pad -- has the kernel
 // write the batch in place; otherwise the host batch is built and uploaded.
@@ -1019,9 +1099,8 @@ std::shared_ptr<Array> device_batch(const std::vector<std::shared_ptr<Array>>& a
                                     int64_t item, bool ragged, double pad_value, int dim, bool has_dim, int device) {
   const auto type = arrs.front()->type();
   const int64_t isz = itemsize(type), bytes = shape_size(bshape) * isz;
-  void* ptr = nullptr;
-  check(mxd_malloc_device(&ptr, std::max<int64_t>(bytes, 1), device));
-  std::shared_ptr<void> mem(ptr, [device](void* p) { (void)mxd_free_device(p, device); });
+  std::shared_ptr<void> mem = device_pool().get(device, bytes);
+  void* ptr = mem.get();
   auto res = std::make_shared<Array>(type, bshape, mem, device);
   bool fused = !has_dim && !ragged && arrs.front()->ndim() == 3;
   for (const auto& a : arrs) fused = fused && deferred(*a) && a->shape(2) == bshape[3];

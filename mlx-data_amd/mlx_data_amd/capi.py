@@ -24,7 +24,7 @@ EXPORTS = (
     "mxd_describe_band_plan", "mxd_copy_bandwidth",
     "mxd_set_device", "mxd_malloc_device", "mxd_free_device", "mxd_malloc_pinned", "mxd_free_pinned",
     "mxd_memcpy_h2d_async", "mxd_memcpy_d2h_async", "mxd_memcpy2d_h2d_async", "mxd_memset_async",
-    "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize",
+    "mxd_stream_create", "mxd_stream_destroy", "mxd_stream_synchronize", "mxd_device_synchronize",
     "mxd_event_create", "mxd_event_destroy", "mxd_event_record", "mxd_event_synchronize", "mxd_event_elapsed_ms",
     "mxd_resize_crop_host", "mxd_resize_crop_to_device", "mxd_memcpy_h2d", "mxd_memcpy_d2h",
     "mxd_release_host_buffers",

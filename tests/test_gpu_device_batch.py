@@ -138,3 +138,31 @@ def test_torch_consumes_device_batch_via_dlpack():
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res == dict(ok=True, same=True, sum_ok=True), res
+
+
+def test_device_batch_blocks_recycled_safely():
+    """Device batch tensors come from a per-device pool (pipeline.cpp
+    DevicePool): a released block is reused only after a device
+    synchronisation that followed its release.  A torch consumer enqueues a
+    slow read of each batch on its own stream and drops the tensor at once;
+    the next batches (same size: reuse) must not disturb what it reads, and
+    every batch must equal the host batch."""
+    torch = pytest.importorskip("torch")
+    b = chain(dx.buffer_from_vector(samples(8, seed=5)))
+    host = b.batch(8)[0]["image"]
+    want = torch.from_numpy(host.astype(np.float32)).sum().item()
+    side = torch.cuda.Stream()
+    sums = []
+    for _ in range(12):
+        dev = b.batch(8, device=0)[0]["image"]
+        t = torch.from_dlpack(dev)
+        with torch.cuda.stream(side):
+            acc = torch.zeros((), device=t.device)
+            for _ in range(20):  # the side stream reads the block 20 times
+                acc = acc + t.float().sum()
+            sums.append(acc / 20)
+        del t, dev  # the block returns to the pool while the side stream may still read it
+    torch.cuda.synchronize()
+    assert all(abs(s.item() - want) < 1e-3 * abs(want) for s in sums)
+    again = b.batch(8, device=0)[0]["image"]
+    assert np.array_equal(again.numpy(), host)
