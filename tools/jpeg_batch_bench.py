@@ -55,7 +55,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--datasets", default="c4,c1")
     ap.add_argument("--huff-bits", default="0", help="device entropy: subsequence lengths to time (0: default)")
-    ap.add_argument("--huff-global", action="store_true", help="device entropy: also time words read from device memory")
+    ap.add_argument("--huff-global", action="store_true", help="device entropy: also time every length with words read from device memory")
+    ap.add_argument("--no-host", action="store_true", help="skip the host entropy decode runs")
     args = ap.parse_args()
     from mlx_data_amd import capi
 
@@ -64,8 +65,11 @@ def main():
     for name in args.datasets.split(","):
         datas = files(name, args.batch)
         line = dict(dataset=name, batch=args.batch, mean_file_bytes=round(float(np.mean([len(d) for d in datas])), 1))
-        runs = [(True, int(b), 0) for b in args.huff_bits.split(",")] + ([(True, 0, 1)] if args.huff_global else [])
-        runs.append((False, 0, 0))
+        runs = [(True, int(b), 0) for b in args.huff_bits.split(",")]
+        if args.huff_global:
+            runs += [(True, int(b), 1) for b in args.huff_bits.split(",")]
+        if not args.no_host:
+            runs.append((False, 0, 0))
         for dev, bits, glob in runs:
             capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
             capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, glob)
