@@ -17,8 +17,12 @@ if [ "$1" = build ]; then
   for o in resample wave band band_plan pixmap capi plan batch hostpath taps jpeg jpegdev jpeghuff; do
     if [[ " $SRCS " == *" $o "* ]]; then
       src=csrc/$o.hip; [ -f $src ] || src=csrc/$o.cpp
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
-        $FLAGS -c $src -o build/var_$NAME/$o.o || exit 1
+      if [ $o = jpeg ] || [ $o = band_plan ]; then  # host-only C++ (the Makefile's g++ rule)
+        g++ -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc $FLAGS -c $src -o build/var_$NAME/$o.o || exit 1
+      else
+        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
+          $FLAGS -c $src -o build/var_$NAME/$o.o || exit 1
+      fi
       OBJS="$OBJS build/var_$NAME/$o.o"
     else
       OBJS="$OBJS build/$o.o"
