@@ -1538,12 +1538,52 @@ EntropyScan entropy_scan(const Coefs* c) {
 void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   const Huff& h = cls ? c->d.ac[table_id] : c->d.dc[table_id];
   HuffDev& o = *static_cast<HuffDev*>(huff_dev);
-  std::memcpy(o.look, h.look, sizeof o.look);
+  static_assert(kHuffFacLook == kLook, "the combined AC table is the host decoder's");
+  // per-thread cache of built tables (a batch's files mostly share theirs),
+  // keyed by the derived code: maxcode, valoffset and the symbol values
+  struct Entry {
+    int32_t maxcode[18], valoffset[18];
+    uint8_t vals[256];
+    int nvals = -1;
+    HuffDev d;
+  };
+  constexpr int kEntries = 8;
+  thread_local std::unique_ptr<Entry[]> cache;
+  thread_local int next = 0;
+  if (!cache) cache.reset(new Entry[kEntries]);
+  for (int k = 0; k < kEntries; k++) {
+    const Entry& e = cache[k];
+    if (e.nvals == h.nvals && std::memcmp(e.maxcode, h.maxcode, sizeof e.maxcode) == 0 &&
+        std::memcmp(e.valoffset, h.valoffset, sizeof e.valoffset) == 0 &&
+        std::memcmp(e.vals, h.vals, (size_t)h.nvals) == 0) {
+      o = e.d;
+      return;
+    }
+  }
+  // symbol table over kHuffLook bits: the host table's entry for codes of up
+  // to kLook bits, else the shortest longer length l whose l-bit prefix of
+  // the index is <= maxcode[l] (canonical codes)
+  static_assert(kHuffLook >= kLook, "the device table extends the host one");
+  for (int i = 0; i < (1 << kHuffLook); i++) {
+    uint16_t e = h.look[i >> (kHuffLook - kLook)];
+    for (int l = kLook + 1; l <= kHuffLook && !e; l++) {
+      const int32_t code = i >> (kHuffLook - l);
+      if (code <= h.maxcode[l]) e = (uint16_t)((l << 8) | h.vals[(code + h.valoffset[l]) & 0xff]);
+    }
+    o.look[i] = e;
+  }
   std::memcpy(o.maxcode, h.maxcode, sizeof o.maxcode);
   std::memcpy(o.valoffset, h.valoffset, sizeof o.valoffset);
   std::memcpy(o.vals, h.vals, sizeof o.vals);
   for (int i = 0; i < (1 << kLook); i++)
     o.fac[i] = (uint32_t)(uint16_t)h.fac[i].val | ((uint32_t)h.fac[i].run << 16) | ((uint32_t)h.fac[i].len << 24);
+  Entry& e = cache[next];
+  next = (next + 1) % kEntries;
+  std::memcpy(e.maxcode, h.maxcode, sizeof e.maxcode);
+  std::memcpy(e.valoffset, h.valoffset, sizeof e.valoffset);
+  std::memcpy(e.vals, h.vals, (size_t)h.nvals);
+  e.nvals = h.nvals;
+  e.d = o;
 }
 
 // Mirrors Bits::fill's byte rules on a segment that ends at its marker's 0xFF.
