@@ -38,6 +38,11 @@ namespace {
 #ifndef MXD_HUFF_UNIFIED
 #define MXD_HUFF_UNIFIED 1
 #endif
+// Tuning builds (-DMXD_HUFF_PREFETCH=1): the LDS reader loads each word one
+// refill ahead.
+#ifndef MXD_HUFF_PREFETCH
+#define MXD_HUFF_PREFETCH 0
+#endif
 
 #if MXD_HUFF_STATS
 constexpr int kStatJobs = 1 << 16;
@@ -63,6 +68,9 @@ struct LdsReader {
   int32_t nw;
   uint64_t buf;
   int32_t cnt, wi;
+#if MXD_HUFF_PREFETCH
+  uint32_t nxt;  // w[wi] (clamped into the segment), loaded one refill ahead
+#endif
 
   // base: the job's words in LDS; w0 / nw: the segment's first word and words
   __device__ __forceinline__ void init(const void* base, int32_t w0, int32_t nwords) {
@@ -70,6 +78,28 @@ struct LdsReader {
     nw = nwords;
   }
 
+#if MXD_HUFF_PREFETCH
+  __device__ __forceinline__ uint32_t word(int32_t i) const { return w[i < nw ? i : max(nw - 1, 0)]; }
+  __device__ __forceinline__ void refill() {
+    while (cnt <= 32) {
+      const uint32_t x = wi < nw ? __builtin_bswap32(nxt) : 0u;
+      buf |= (uint64_t)x << (32 - cnt);
+      cnt += 32;
+      wi++;
+      nxt = word(wi);  // for the next refill: its latency overlaps this step's decode
+    }
+  }
+  __device__ __forceinline__ void seek(int32_t bit) {
+    wi = bit >> 5;
+    nxt = word(wi);
+    buf = 0;
+    cnt = 0;
+    refill();
+    const int s = bit & 31;
+    buf <<= s;
+    cnt -= s;
+  }
+#else
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
       const uint32_t x = wi < nw ? __builtin_bswap32(w[wi]) : 0u;
@@ -87,6 +117,7 @@ struct LdsReader {
     buf <<= s;
     cnt -= s;
   }
+#endif
   __device__ __forceinline__ int32_t pos() const { return wi * 32 - cnt; }
   __device__ __forceinline__ uint32_t take(int n) {  // n <= 16 bits (n = 0: 0)
     const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
@@ -336,7 +367,7 @@ struct Dec {
       return false;
     }
     const HuffDev& t = tab[im->blk_ac[b]];
-    const uint32_t f = t.fac[(uint32_t)(r.buf >> (64 - kHuffLook))];
+    const uint32_t f = t.fac[(uint32_t)(r.buf >> (64 - kHuffFacLook))];
     bool end;
     if (f >> 24) {
       r.buf <<= f >> 24;
@@ -539,7 +570,7 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
             dc1 = g + 1;
           },
           [&](int kk, int v) {
-            if (v) blk[sh.nat[kk]] = (int16_t)v;
+            blk[sh.nat[kk]] = (int16_t)v;  // nonzero: a coded AC coefficient (size > 0)
           });
       if (fin) {
         g++;
