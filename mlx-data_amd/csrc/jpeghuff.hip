@@ -38,10 +38,11 @@ namespace {
 #ifndef MXD_HUFF_UNIFIED
 #define MXD_HUFF_UNIFIED 1
 #endif
-// Tuning builds (-DMXD_HUFF_PREFETCH=1): the LDS reader loads each word one
-// refill ahead.
+// The LDS reader loads each word one refill ahead (default; tuning builds
+// -DMXD_HUFF_PREFETCH=0 load it when needed, on the symbol loop's dependency
+// chain: kernel 0.961 vs 1.094 ms per batch-bench call, profiles/r04/r04x_*).
 #ifndef MXD_HUFF_PREFETCH
-#define MXD_HUFF_PREFETCH 0
+#define MXD_HUFF_PREFETCH 1
 #endif
 
 #if MXD_HUFF_STATS
