@@ -436,6 +436,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       p.bh = cp.bh;
       p.qtab = (int32_t)c.qtabs.size();
       p.coded = cp.coded ? 1 : 0;
+      p.zigzag = pend_rel[i - first] >= 0 ? 1 : 0;  // decoded by jpeg_huff: zig-zag order
       c.qtabs.insert(c.qtabs.end(), cp.q, cp.q + 64);
       c.planes.push_back(p);
       m.plane[k] = c.samples;

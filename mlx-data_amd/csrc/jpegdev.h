@@ -20,6 +20,8 @@ struct JpegPlaneDev {
   int32_t bw, bh;       // blocks per row / column
   int32_t qtab;         // first entry of its quantisation table (uint16 elements)
   int32_t coded;        // 0: no scan carried it, its samples are 0
+  int32_t zigzag;       // 1: each block's coefficients in zig-zag order (the device entropy decode's), 0: natural
+  int32_t pad;
 };
 
 // Upsampling of one component to the output grid (jdsample.c), as jpeg.cpp

@@ -28,6 +28,12 @@ constexpr i64 F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 73
 
 __device__ __forceinline__ i64 descale(i64 x, int n) { return (x + ((i64)1 << (n - 1))) >> n; }
 
+// Zig-zag index -> natural index (jutils.c jpeg_natural_order), for blocks the
+// device entropy decode stores in zig-zag order.
+constexpr int kZigzagNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+                                41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                                30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
 __device__ __forceinline__ uint32_t range_limit(i64 x) {
   const i64 v = x + 128;
   return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v);
@@ -92,6 +98,8 @@ __global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coe
   {
     const int4* cp = reinterpret_cast<const int4*>(coef + p.coef + b * 64);
     const uint4* qp = reinterpret_cast<const uint4*>(qt + p.qtab);
+    int32_t c16[64];  // the block as stored
+    uint32_t q16[64];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int4 c = cp[k];
@@ -100,9 +108,19 @@ __global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coe
       const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        d[8 * k + 2 * j] = (int32_t)(int16_t)(cw[j] & 0xffff) * (int32_t)(qw[j] & 0xffff);
-        d[8 * k + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)cw[j] >> 16) * (int32_t)(qw[j] >> 16);
+        c16[8 * k + 2 * j] = (int32_t)(int16_t)(cw[j] & 0xffff);
+        c16[8 * k + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)cw[j] >> 16);
+        q16[8 * k + 2 * j] = qw[j] & 0xffff;
+        q16[8 * k + 2 * j + 1] = qw[j] >> 16;
       }
+    }
+    if (p.zigzag) {
+      // coefficient z of the block sits at natural position kZigzagNat[z] (compile-time indices)
+#pragma unroll
+      for (int z = 0; z < 64; z++) d[kZigzagNat[z]] = c16[z] * (int32_t)q16[kZigzagNat[z]];
+    } else {
+#pragma unroll
+      for (int n = 0; n < 64; n++) d[n] = c16[n] * (int32_t)q16[n];
     }
   }
   // pass 1: columns -> int workspace (descaled by CONST_BITS - PASS1_BITS)

@@ -52,13 +52,6 @@ __device__ int g_huff_stats[kStatJobs * kStatInts];
 __device__ __forceinline__ uint64_t stat_clock() { return __builtin_amdgcn_s_memrealtime(); }
 #endif
 
-// Zig-zag -> natural order, 16 extra entries absorbing a corrupt run past 63
-// (jpeg.cpp kNatural, jutils.c jpeg_natural_order); copied into LDS.
-__constant__ uint8_t kNatural[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
-                                 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
-                                 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
-                                 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
-
 // Bit readers over one segment's unstuffed bytes (32-bit words, big-endian
 // byte order); words past the segment read as zeros (libjpeg's zeros past
 // the data).  After refill() at least 33 bits are buffered.
@@ -253,7 +246,6 @@ struct SegLds {
 // they fit, the job's words follow in dynamic LDS: jpeg_huff_lds_bytes).
 struct Shared {
   HuffImgDev img;
-  uint8_t nat[80];
   int32_t seg_sub0[kHuffThreads];  // first subsequence of each segment of the job
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
@@ -571,7 +563,9 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
             dc1 = g + 1;
           },
           [&](int kk, int v) {
-            blk[sh.nat[kk]] = (int16_t)v;  // nonzero: a coded AC coefficient (size > 0)
+            // zig-zag order (jpeg_idct reorders); a corrupt run past 63 lands on 63, as
+            // jpeg_natural_order's extra entries put it
+            blk[min(kk, 63)] = (int16_t)v;
           });
       if (fin) {
         g++;
@@ -597,7 +591,6 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   const int t = threadIdx.x;
   const HuffJobDev job = jobs[blockIdx.x];
   if (t == 0) sh.img = imgs[segs[job.seg0].img];
-  if (t < 80) sh.nat[t] = kNatural[t];
   __syncthreads();
   const HuffImgDev& im = sh.img;
   HuffDev* tab = reinterpret_cast<HuffDev*>(dyn);
