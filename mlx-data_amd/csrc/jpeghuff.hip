@@ -38,6 +38,13 @@ namespace {
 #ifndef MXD_HUFF_UNIFIED
 #define MXD_HUFF_UNIFIED 1
 #endif
+// The symbol step without per-kind branches (default; tuning builds
+// -DMXD_HUFF_LEAN=0 keep the if / else chain of the unified step): code and
+// value bits consumed by one shift, the next coefficient index and block
+// selected arithmetically, one word refilled per step.
+#ifndef MXD_HUFF_LEAN
+#define MXD_HUFF_LEAN 1
+#endif
 // The LDS reader loads each word one refill ahead (default; tuning builds
 // -DMXD_HUFF_PREFETCH=0 load it when needed, on the symbol loop's dependency
 // chain: kernel 0.961 vs 1.094 ms per batch-bench call, profiles/r04/r04x_*).
@@ -74,6 +81,14 @@ struct LdsReader {
 
 #if MXD_HUFF_PREFETCH
   __device__ __forceinline__ uint32_t word(int32_t i) const { return w[i < nw ? i : max(nw - 1, 0)]; }
+  // one word (the caller knows cnt <= 32)
+  __device__ __forceinline__ void refill1() {
+    const uint32_t x = wi < nw ? __builtin_bswap32(nxt) : 0u;
+    buf |= (uint64_t)x << (32 - cnt);
+    cnt += 32;
+    wi++;
+    nxt = word(wi);
+  }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
       const uint32_t x = wi < nw ? __builtin_bswap32(nxt) : 0u;
@@ -94,6 +109,12 @@ struct LdsReader {
     cnt -= s;
   }
 #else
+  __device__ __forceinline__ void refill1() {
+    const uint32_t x = wi < nw ? __builtin_bswap32(w[wi]) : 0u;
+    buf |= (uint64_t)x << (32 - cnt);
+    cnt += 32;
+    wi++;
+  }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
       const uint32_t x = wi < nw ? __builtin_bswap32(w[wi]) : 0u;
@@ -144,6 +165,21 @@ struct GlobalReader {
 
   __device__ __forceinline__ uint4 fetch(int32_t ch) const {
     return ch <= last_chunk ? chunks[ch] : uint4{0u, 0u, 0u, 0u};
+  }
+  __device__ __forceinline__ void refill1() {
+    const int32_t a = w0 + wi;
+    if ((a >> 2) != ca) {
+      A = B;
+      B = C;
+      ca++;
+      C = fetch(ca + 2);
+    }
+    const int i = a & 3;
+    const uint32_t v = i == 0 ? A.x : i == 1 ? A.y : i == 2 ? A.z : A.w;
+    const uint32_t x = wi < nw ? __builtin_bswap32(v) : 0u;
+    buf |= (uint64_t)x << (32 - cnt);
+    cnt += 32;
+    wi++;
   }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
@@ -214,7 +250,7 @@ __device__ __forceinline__ int huff_symbol(const HuffDev& t, Reader& r) {
 // codes; jdhuff.c jpeg_huff_decode's search); none (corrupt data) consumes 16
 // bits and decodes as 0, as huff_symbol does.
 template <class Reader>
-__device__ __forceinline__ int huff_long(const HuffDev& t, Reader& r) {
+[[maybe_unused]] __device__ __forceinline__ int huff_long(const HuffDev& t, Reader& r) {
   const uint32_t p16 = (uint32_t)(r.buf >> 48);
   int len = 17;
 #pragma unroll
@@ -229,6 +265,23 @@ __device__ __forceinline__ int huff_long(const HuffDev& t, Reader& r) {
   r.buf <<= len;
   r.cnt -= len;
   return t.vals[(code + t.valoffset[len]) & 0xff];
+}
+
+// huff_long's search without consuming: the code's length (16 for corrupt
+// data, whose symbol is 0) and its symbol.
+[[maybe_unused]] __device__ __forceinline__ void huff_long_peek(const HuffDev& t, uint64_t buf, int& len, int& sym) {
+  const uint32_t p16 = (uint32_t)(buf >> 48);
+  int l = 17;
+#pragma unroll
+  for (int ll = 16; ll > kHuffLook; ll--)
+    if ((int32_t)(p16 >> (16 - ll)) <= t.maxcode[ll]) l = ll;
+  if (l > 16) {
+    len = 16;
+    sym = 0;
+  } else {
+    len = l;
+    sym = t.vals[((int32_t)(p16 >> (16 - l)) + t.valoffset[l]) & 0xff];
+  }
 }
 
 __device__ __forceinline__ int extend(uint32_t v, int s) {
@@ -308,7 +361,37 @@ struct Dec {
   // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
   // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
   // value) receive the block's values.
-#if MXD_HUFF_UNIFIED
+#if MXD_HUFF_UNIFIED && MXD_HUFF_LEAN
+  template <class Reader, class OnDc, class OnAc>
+  __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
+    if (r.cnt <= 32) r.refill1();  // >= 33 bits buffered: a step consumes <= 16 + 15
+    const bool dc = k == 0;
+    const HuffDev& t = tab[(tpack >> ((dc ? 0 : 32) + 3 * b)) & 7];
+    const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
+    int len, sym;
+    if (e) {
+      len = e >> 8;
+      sym = e & 0xff;
+    } else {
+      huff_long_peek(t, r.buf, len, sym);
+    }
+    const int sz = dc ? sym : sym & 15;
+    const int run = dc ? 0 : sym >> 4;
+    const uint32_t raw = sz ? (uint32_t)((r.buf << len) >> (64 - sz)) : 0u;
+    r.buf <<= len + sz;
+    r.cnt -= len + sz;
+    const int v = extend(raw, sz);
+    const int kpos = k + run;  // an AC coefficient's index (sz != 0)
+    // next index: after the DC 1; after a coefficient kpos + 1; ZRL k + 16; EOB 64
+    const int knew = dc ? 1 : sz ? kpos + 1 : run == 15 ? k + 16 : 64;
+    if (dc) on_dc(v);
+    else if (sz) on_ac(kpos, v);
+    const bool end = knew >= 64;
+    k = end ? 0 : knew;
+    b = end ? (b + 1 == bpm ? 0 : b + 1) : b;
+    return end;
+  }
+#elif MXD_HUFF_UNIFIED
   // One path for DC and AC symbols: the
   // block's DC or AC table is selected, one lookup gives the symbol (codes
   // past the lookahead without a loop), the value bits follow; the lanes of a
