@@ -45,6 +45,11 @@ namespace {
 #ifndef MXD_HUFF_LEAN
 #define MXD_HUFF_LEAN 1
 #endif
+// Branch-free refill in the lean step and the synchronisation loop's exit on
+// the subsequence end alone (default; tuning builds -DMXD_HUFF_LEAN2=0).
+#ifndef MXD_HUFF_LEAN2
+#define MXD_HUFF_LEAN2 1
+#endif
 // The LDS reader loads each word one refill ahead (default; tuning builds
 // -DMXD_HUFF_PREFETCH=0 load it when needed, on the symbol loop's dependency
 // chain: kernel 0.961 vs 1.094 ms per batch-bench call, profiles/r04/r04x_*).
@@ -89,6 +94,15 @@ struct LdsReader {
     wi++;
     nxt = word(wi);
   }
+  // refill1 when cnt <= 32, without a branch (the word load is issued either way)
+  __device__ __forceinline__ void refill_if() {
+    const bool need = cnt <= 32;
+    const uint32_t x = need && wi < nw ? __builtin_bswap32(nxt) : 0u;
+    buf |= (uint64_t)x << (need ? 32 - cnt : 0);
+    cnt += need ? 32 : 0;
+    wi += need ? 1 : 0;
+    nxt = word(wi);
+  }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
       const uint32_t x = wi < nw ? __builtin_bswap32(nxt) : 0u;
@@ -114,6 +128,9 @@ struct LdsReader {
     buf |= (uint64_t)x << (32 - cnt);
     cnt += 32;
     wi++;
+  }
+  __device__ __forceinline__ void refill_if() {
+    if (cnt <= 32) refill1();
   }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
@@ -180,6 +197,9 @@ struct GlobalReader {
     buf |= (uint64_t)x << (32 - cnt);
     cnt += 32;
     wi++;
+  }
+  __device__ __forceinline__ void refill_if() {
+    if (cnt <= 32) refill1();
   }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
@@ -364,7 +384,11 @@ struct Dec {
 #if MXD_HUFF_UNIFIED && MXD_HUFF_LEAN
   template <class Reader, class OnDc, class OnAc>
   __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
-    if (r.cnt <= 32) r.refill1();  // >= 33 bits buffered: a step consumes <= 16 + 15
+#if MXD_HUFF_LEAN2
+    r.refill_if();  // >= 33 bits buffered: a step consumes <= 16 + 15
+#else
+    if (r.cnt <= 32) r.refill1();
+#endif
     const bool dc = k == 0;
     const HuffDev& t = tab[(tpack >> ((dc ? 0 : 32) + 3 * b)) & 7];
     const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
@@ -587,7 +611,12 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
       int done = 0;
       for (;;) {
         const int32_t p = rd.pos();
+        // the segment's end can only stop the last subsequence, which the rounds never decode
+#if MXD_HUFF_LEAN2
+        if (p >= v.end) break;
+#else
         if (p >= v.end || (dec.b == 0 && dec.k == 0 && p > v.sg.bits)) break;
+#endif
         done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
 #if MXD_HUFF_STATS
         st.sync_syms++;
