@@ -323,6 +323,9 @@ struct Shared {
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
   int32_t done[kHuffThreads];      // blocks a subsequence completes (sync pass)
+  int64_t blk_off[kHuffMaxBlocks];  // block j of an MCU: offset of MCU (0, 0)'s block j in the coefficients,
+  int32_t blk_mxs[kHuffMaxBlocks];  // and its steps per MCU column / row (non-interleaved: per block)
+  int32_t blk_mys[kHuffMaxBlocks];
   int16_t sub_seg[kHuffThreads];   // segment of each subsequence
   int16_t list[kHuffThreads];      // this round's subsequences to decode (compacted)
   int32_t scan[kHuffThreads / 64];
@@ -366,6 +369,7 @@ struct Dec {
   // the DC (bits 3b..3b+2) and AC (32 + 3b..) table of each block of the MCU,
   // in a register instead of two LDS reads per symbol
   uint64_t tpack;
+  uint32_t cpack;  // component of each block of the MCU (bits 2b..2b+1)
   int bpm;
 
   __device__ __forceinline__ void init(const HuffImgDev* im_, const HuffDev* tab_) {
@@ -374,8 +378,11 @@ struct Dec {
     b = k = 0;
     bpm = im_->bpm;
     tpack = 0;
-    for (int j = 0; j < bpm; j++)
+    cpack = 0;
+    for (int j = 0; j < bpm; j++) {
       tpack |= ((uint64_t)(im_->blk_dc[j] & 7) << (3 * j)) | ((uint64_t)(im_->blk_ac[j] & 7) << (32 + 3 * j));
+      cpack |= (uint32_t)(im_->blk_comp[j] & 3) << (2 * j);
+    }
   }
 
   // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
@@ -662,7 +669,14 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
     rd.seek(sh.in_pos[t]);
     dec.b = sh.in_b[t];
     dec.k = sh.in_k[t];
-    int16_t* blk = coef + block_addr(im, min(g, seg_block1 - 1));
+    // block cursor: (MCU column, row, block of the MCU), advanced without divisions
+    const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
+    const uint32_t g0 = (uint32_t)min(g, seg_block1 - 1), m0 = g0 / bpm;
+    uint32_t cj = g0 - m0 * bpm, cmy = m0 / mcux, cmx = m0 - cmy * mcux;
+    auto addr = [&]() {
+      return coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
+    };
+    int16_t* blk = addr();
     for (;;) {
       const int32_t p = rd.pos();
       if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
@@ -670,7 +684,10 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
           rd,
           [&](int diff) {
             blk[0] = (int16_t)diff;
-            dcsum[im.blk_comp[dec.b]] += diff;
+            const int c = (dec.cpack >> (2 * dec.b)) & 3;
+            dcsum[0] += c == 0 ? diff : 0;
+            dcsum[1] += c == 1 ? diff : 0;
+            dcsum[2] += c == 2 ? diff : 0;
             if (dc0 < 0) dc0 = g;
             dc1 = g + 1;
           },
@@ -681,7 +698,14 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
           });
       if (fin) {
         g++;
-        if (g < seg_block1) blk = coef + block_addr(im, g);
+        cj++;
+        const bool wrap = cj == bpm;
+        cj = wrap ? 0 : cj;
+        cmx += wrap ? 1 : 0;
+        const bool row = cmx == mcux;
+        cmx = row ? 0 : cmx;
+        cmy += row ? 1 : 0;
+        blk = addr();  // past the segment's last block when g == seg_block1: never stored through
       }
 #if MXD_HUFF_STATS
       st.write_syms++;
@@ -705,6 +729,18 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   if (t == 0) sh.img = imgs[segs[job.seg0].img];
   __syncthreads();
   const HuffImgDev& im = sh.img;
+  if (t < im.bpm) {  // the block cursor's tables (read after stage 0's barrier)
+    if (!im.interleaved) {
+      sh.blk_off[0] = im.plane[0];
+      sh.blk_mxs[0] = 64;
+      sh.blk_mys[0] = im.bw[0] * 64;
+    } else {
+      const int c = im.blk_comp[t];
+      sh.blk_off[t] = im.plane[c] + ((int64_t)im.blk_dy[t] * im.bw[c] + im.blk_dx[t]) * 64;
+      sh.blk_mxs[t] = im.comp_h[c] * 64;
+      sh.blk_mys[t] = im.comp_v[c] * im.bw[c] * 64;
+    }
+  }
   HuffDev* tab = reinterpret_cast<HuffDev*>(dyn);
   SegLds* seg = reinterpret_cast<SegLds*>(reinterpret_cast<char*>(dyn) + lds_tables_bytes(im.ntables));
   const int64_t word0 = segs[job.seg0].word;  // the job's first word (16-byte aligned)
