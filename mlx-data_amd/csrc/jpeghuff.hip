@@ -366,10 +366,10 @@ struct Dec {
   const HuffImgDev* im;
   const HuffDev* tab;
   int b, k;
-  // the DC (bits 3b..3b+2) and AC (32 + 3b..) table of each block of the MCU,
-  // in a register instead of two LDS reads per symbol
-  uint64_t tpack;
-  uint32_t cpack;  // component of each block of the MCU (bits 2b..2b+1)
+  // per-block table indices and components in registers instead of LDS
+  // reads per symbol
+  uint32_t dpack, apack;  // the DC / AC table of each block of the MCU (bits 3b..3b+2)
+  uint32_t cpack;         // component of each block of the MCU (bits 2b..2b+1)
   int bpm;
 
   __device__ __forceinline__ void init(const HuffImgDev* im_, const HuffDev* tab_) {
@@ -377,10 +377,10 @@ struct Dec {
     tab = tab_;
     b = k = 0;
     bpm = im_->bpm;
-    tpack = 0;
-    cpack = 0;
+    dpack = apack = cpack = 0;
     for (int j = 0; j < bpm; j++) {
-      tpack |= ((uint64_t)(im_->blk_dc[j] & 7) << (3 * j)) | ((uint64_t)(im_->blk_ac[j] & 7) << (32 + 3 * j));
+      dpack |= (uint32_t)(im_->blk_dc[j] & 7) << (3 * j);
+      apack |= (uint32_t)(im_->blk_ac[j] & 7) << (3 * j);
       cpack |= (uint32_t)(im_->blk_comp[j] & 3) << (2 * j);
     }
   }
@@ -397,7 +397,7 @@ struct Dec {
     if (r.cnt <= 32) r.refill1();
 #endif
     const bool dc = k == 0;
-    const HuffDev& t = tab[(tpack >> ((dc ? 0 : 32) + 3 * b)) & 7];
+    const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
     const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
     int len, sym;
     if (e) {
@@ -431,7 +431,7 @@ struct Dec {
   __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
     if (r.cnt < 32) r.refill();
     const bool dc = k == 0;
-    const HuffDev& t = tab[(tpack >> ((dc ? 0 : 32) + 3 * b)) & 7];
+    const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
     const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
     int sym;
     if (e) {
