@@ -30,7 +30,14 @@
 
 namespace mxd {
 
-constexpr int kHuffLook = 9;      // lookahead bits of the fast tables
+// Lookahead bits of the device symbol table (tuning builds: -DMXD_HUFF_LOOK=9,
+// the host decoder's): at 11 a code longer than the lookahead -- the branch
+// every wave takes when any of its lanes meets one -- is rare.
+#ifndef MXD_HUFF_LOOK
+#define MXD_HUFF_LOOK 11
+#endif
+constexpr int kHuffLook = MXD_HUFF_LOOK;
+constexpr int kHuffFacLook = 9;  // lookahead of the combined AC table (the host decoder's)
 constexpr int kHuffMaxBlocks = 10;  // blocks per MCU (JPEG's limit)
 constexpr int kHuffThreads = 1024;  // subsequences per job (one workgroup)
 
@@ -43,7 +50,7 @@ struct HuffDev {
   uint8_t vals[256];
   // AC fast path: value (int16, bits 0..15), run (bits 16..23; 0xFF = end of
   // block, 15 = ZRL), bits to consume (24..31; 0 = take the general path)
-  uint32_t fac[1 << kHuffLook];
+  uint32_t fac[1 << kHuffFacLook];
 };
 static_assert(sizeof(HuffDev) % 16 == 0, "HuffDev keeps 16-byte alignment");
 
