@@ -563,6 +563,11 @@ __device__ __forceinline__ Sub sub_of(const Shared& sh, const SegLds* seg, int s
 #ifndef MXD_HUFF_COMPACT
 #define MXD_HUFF_COMPACT 1
 #endif
+// Tuning builds (-DMXD_HUFF_OVERLAP=<bits>): round 0 decodes that many bits
+// before each subsequence's start from the guessed state.
+#ifndef MXD_HUFF_OVERLAP
+#define MXD_HUFF_OVERLAP 0
+#endif
 
 #if MXD_HUFF_STATS
 struct Stats {
@@ -612,9 +617,24 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
     if (work) {
       const Sub v = sub_of(sh, seg, sub_bits, id, nsub);
       rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5);
-      rd.seek(sh.in_pos[id]);
-      dec.b = sh.in_b[id];
-      dec.k = sh.in_k[id];
+#if MXD_HUFF_OVERLAP > 0
+      // round 0: start the guess MXD_HUFF_OVERLAP bits early, so the decoder
+      // has had that long to fall into step when it reaches the subsequence
+      if (round == 0 && !v.first) {
+        rd.seek(max(0, v.start - MXD_HUFF_OVERLAP));
+        dec.b = 0;
+        dec.k = 0;
+        while (rd.pos() < v.start) dec.step(rd, nop_dc, nop_ac);
+        sh.in_pos[id] = rd.pos();
+        sh.in_b[id] = (int8_t)dec.b;
+        sh.in_k[id] = (int8_t)dec.k;
+      } else
+#endif
+      {
+        rd.seek(sh.in_pos[id]);
+        dec.b = sh.in_b[id];
+        dec.k = sh.in_k[id];
+      }
       int done = 0;
       for (;;) {
         const int32_t p = rd.pos();
