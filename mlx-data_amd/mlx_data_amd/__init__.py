@@ -7,14 +7,34 @@ include/mxd_amd.h (libmxd_amd.so, built in-tree).  ``capi`` binds that ABI;
 """
 import os
 
-# Hardware queues per process for the HIP runtime (read once, when HIP
-# initialises; a value the user set wins).  The pipeline's prefetch workers
-# each launch on a stream of their own, and with HIP's default of 4 queues
-# their small device calls serialise: JPEG pipeline into device batches at 16
-# workers, C4 106 k -> 138 k img/s and C1 122 k -> 152 k with 16 queues
-# (profiles/r04/hwq_*.jsonl).  No effect when another
-# library initialised HIP first.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
+def _raise_hw_queues():
+    """Hardware queues per process for the HIP runtime (read once, when HIP
+    initialises).  The pipeline's prefetch workers each launch on a stream of
+    their own; with HIP's default of 4 queues their small device calls
+    serialise: JPEG pipeline into device batches at 16 workers, C4 95-106 k ->
+    138-142 k img/s and C1 122 k -> 152 k with 16 queues
+    (profiles/r04/hwq_*.jsonl).
+
+    ``MXD_HW_QUEUES`` (default 16, at most 32; 0 leaves HIP's setting alone)
+    raises ``GPU_MAX_HW_QUEUES`` to at least that many -- also when the
+    environment exports HIP's default of 4 -- and never lowers it.  No effect
+    when another library initialised HIP first."""
+    try:
+        want = min(int(os.environ.get("MXD_HW_QUEUES", "16")), 32)
+    except ValueError:
+        raise ValueError("MXD_HW_QUEUES must be an integer") from None
+    if want <= 0:
+        return
+    try:
+        have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        have = 0
+    if have < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+
+
+_raise_hw_queues()
 
 from . import capi, image  # noqa: E402,F401
 
