@@ -156,7 +156,13 @@ def main():
     ap.add_argument("--cpu-images", type=int, default=512, help="files the CPU restatement runs over")
     ap.add_argument("--min-seconds", type=float, default=5.0, help="least duration of a timed surface run")
     ap.add_argument("--min-batches", type=int, default=16, help="least batches per worker of a timed surface run")
+    ap.add_argument("--tune", default="", help="tuning knobs for the GPU legs, e.g. HUFF_GLOBAL=1,HUFF_BITS=1024 "
+                    "(capi.set_tuning; MXD_TUNE_<name>)")
     args = ap.parse_args()
+    tune = {}
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        tune[k] = int(v)
     workers = [int(w) for w in args.workers.split(",")]
     variants = args.variants.split(",")
     # CPU legs first: their worker processes fork before any GPU call here
@@ -170,6 +176,10 @@ def main():
                     if v == "cpu":
                         n, dt = run_cpu(fl[:args.cpu_images], B, w, args.min_seconds)
                     else:
+                        if tune:
+                            from mlx_data_amd import capi
+                            for k, val in tune.items():
+                                capi.set_tuning(getattr(capi, "MXD_TUNE_" + k), val)
                         # warm-up with every worker busy twice over: tap tables, host-path
                         # contexts and the recycled batch buffers reach their steady state;
                         # its rate sizes the timed run: the file list repeated until the run
@@ -185,8 +195,11 @@ def main():
                                 break
                             repeat = max(repeat + 1, int(np.ceil(repeat * 1.25 * args.min_seconds / dt)))
                             n, dt = run_surface(fl, B, w, v, repeat)
-                    print(json.dumps(dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
-                                          images_per_s=round(n / dt, 1), batch=B)), flush=True)
+                    rec = dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
+                               images_per_s=round(n / dt, 1), batch=B)
+                    if tune and v != "cpu":
+                        rec["tune"] = tune
+                    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
