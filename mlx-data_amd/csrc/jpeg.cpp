@@ -1540,11 +1540,11 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   HuffDev& o = *static_cast<HuffDev*>(huff_dev);
   static_assert(kHuffFacLook == kLook, "the combined AC table is the host decoder's");
   // per-thread cache of built tables (a batch's files mostly share theirs),
-  // keyed by the derived code: maxcode, valoffset and the symbol values
+  // keyed by the class and the derived code: maxcode, valoffset and the symbol values
   struct Entry {
     int32_t maxcode[18], valoffset[18];
     uint8_t vals[256];
-    int nvals = -1;
+    int nvals = -1, cls = -1;
     HuffDev d;
   };
   constexpr int kEntries = 8;
@@ -1553,7 +1553,7 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   if (!cache) cache.reset(new Entry[kEntries]);
   for (int k = 0; k < kEntries; k++) {
     const Entry& e = cache[k];
-    if (e.nvals == h.nvals && std::memcmp(e.maxcode, h.maxcode, sizeof e.maxcode) == 0 &&
+    if (e.nvals == h.nvals && e.cls == cls && std::memcmp(e.maxcode, h.maxcode, sizeof e.maxcode) == 0 &&
         std::memcmp(e.valoffset, h.valoffset, sizeof e.valoffset) == 0 &&
         std::memcmp(e.vals, h.vals, (size_t)h.nvals) == 0) {
       o = e.d;
@@ -1571,6 +1571,7 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
       if (code <= h.maxcode[l]) e = (uint16_t)((l << 8) | h.vals[(code + h.valoffset[l]) & 0xff]);
     }
     o.look[i] = e;
+    o.step[i] = e ? huff_step_entry(cls, e >> 8, e & 0xff) : 0;
   }
   std::memcpy(o.maxcode, h.maxcode, sizeof o.maxcode);
   std::memcpy(o.valoffset, h.valoffset, sizeof o.valoffset);
@@ -1583,6 +1584,7 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   std::memcpy(e.valoffset, h.valoffset, sizeof e.valoffset);
   std::memcpy(e.vals, h.vals, (size_t)h.nvals);
   e.nvals = h.nvals;
+  e.cls = cls;
   e.d = o;
 }
 

@@ -51,7 +51,18 @@ struct HuffDev {
   // AC fast path: value (int16, bits 0..15), run (bits 16..23; 0xFF = end of
   // block, 15 = ZRL), bits to consume (24..31; 0 = take the general path)
   uint32_t fac[1 << kHuffFacLook];
+  // The symbol step over the same kHuffLook bits, in this table's class:
+  // bits 0..4 the bits a symbol consumes (code + value bits), 5..11 the
+  // coefficient-index advance (DC 1; a coefficient run + 1; ZRL 16; EOB 64),
+  // 12..15 the value bits; 0: code longer than kHuffLook.
+  uint16_t step[1 << kHuffLook];
 };
+// A step entry from a code's length and symbol (constexpr: host and device).
+constexpr uint16_t huff_step_entry(int cls, int len, int sym) {
+  return (uint16_t)(((len + (cls ? (sym & 15) : sym)) & 31) |
+                    ((cls ? ((sym & 15) != 0 || (sym >> 4) == 15 ? (sym >> 4) + 1 : 64) : 1) << 5) |
+                    ((cls ? (sym & 15) : sym) << 12));
+}
 static_assert(sizeof(HuffDev) % 16 == 0, "HuffDev keeps 16-byte alignment");
 
 // One image of a device entropy-decode launch.

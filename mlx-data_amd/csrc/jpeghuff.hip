@@ -56,12 +56,43 @@ namespace {
 #ifndef MXD_HUFF_PREFETCH
 #define MXD_HUFF_PREFETCH 1
 #endif
+// The lean step's next coefficient index by one select and every symbol's
+// store unconditional (tuning builds -DMXD_HUFF_LEAN3=1).
+#ifndef MXD_HUFF_LEAN3
+#define MXD_HUFF_LEAN3 0
+#endif
+// The class-specific step table (HuffDev::step; default): one lookup gives
+// the bits consumed, the index advance and the value bits, and implies
+// LEAN3's write-pass form (every symbol stores; tuning builds
+// -DMXD_HUFF_LEAN4=0 -DMXD_HUFF_LEAN3=0 restore the earlier step: kernel
+// 0.761 vs 0.692 (LEAN3) vs 0.634 ms (LEAN4) per batch-bench call,
+// profiles/r04/r04ag_*).
+#ifndef MXD_HUFF_LEAN4
+#define MXD_HUFF_LEAN4 1
+#endif
+// The synchronisation loop runs MXD_HUFF_UNROLL steps per check while the
+// subsequence's end is further than UNROLL - 1 steps (2, default, or 4; 1
+// checks every step: kernel 0.633 (1) vs 0.564 ms (2) per batch-bench call,
+// profiles/r04/r04ah_*); the write pass likewise runs MXD_HUFF_WUNROLL.
+// Byte-swapping the words once while they are staged into LDS instead of at
+// every refill measured nothing (0.632 ms) and is not kept.
+#ifndef MXD_HUFF_UNROLL
+#define MXD_HUFF_UNROLL 2
+#endif
+#ifndef MXD_HUFF_WUNROLL
+#define MXD_HUFF_WUNROLL 1
+#endif
+#if MXD_HUFF_LEAN4 && !MXD_HUFF_LEAN3
+#undef MXD_HUFF_LEAN3
+#define MXD_HUFF_LEAN3 1
+#endif
 
 #if MXD_HUFF_STATS
 constexpr int kStatJobs = 1 << 16;
-constexpr int kStatInts = 8;
+constexpr int kStatInts = 12;
 __device__ int g_huff_stats[kStatJobs * kStatInts];
 __device__ __forceinline__ uint64_t stat_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint64_t stat_cycles() { return __builtin_amdgcn_s_memtime(); }
 #endif
 
 // Bit readers over one segment's unstuffed bytes (32-bit words, big-endian
@@ -85,10 +116,11 @@ struct LdsReader {
   }
 
 #if MXD_HUFF_PREFETCH
+  static __device__ __forceinline__ uint32_t order(uint32_t x) { return __builtin_bswap32(x); }
   __device__ __forceinline__ uint32_t word(int32_t i) const { return w[i < nw ? i : max(nw - 1, 0)]; }
   // one word (the caller knows cnt <= 32)
   __device__ __forceinline__ void refill1() {
-    const uint32_t x = wi < nw ? __builtin_bswap32(nxt) : 0u;
+    const uint32_t x = wi < nw ? order(nxt) : 0u;
     buf |= (uint64_t)x << (32 - cnt);
     cnt += 32;
     wi++;
@@ -97,7 +129,7 @@ struct LdsReader {
   // refill1 when cnt <= 32, without a branch (the word load is issued either way)
   __device__ __forceinline__ void refill_if() {
     const bool need = cnt <= 32;
-    const uint32_t x = need && wi < nw ? __builtin_bswap32(nxt) : 0u;
+    const uint32_t x = need && wi < nw ? order(nxt) : 0u;
     buf |= (uint64_t)x << (need ? 32 - cnt : 0);
     cnt += need ? 32 : 0;
     wi += need ? 1 : 0;
@@ -105,7 +137,7 @@ struct LdsReader {
   }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
-      const uint32_t x = wi < nw ? __builtin_bswap32(nxt) : 0u;
+      const uint32_t x = wi < nw ? order(nxt) : 0u;
       buf |= (uint64_t)x << (32 - cnt);
       cnt += 32;
       wi++;
@@ -398,6 +430,29 @@ struct Dec {
 #endif
     const bool dc = k == 0;
     const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
+#if MXD_HUFF_LEAN4
+    // one lookup gives the bits to consume, the index advance and the value
+    // bits (HuffDev::step, built for the table's class)
+    int st = t.step[(uint32_t)(r.buf >> (64 - kHuffLook))];
+    if (!st) {
+      int len, sym;
+      huff_long_peek(t, r.buf, len, sym);
+      st = huff_step_entry(dc ? 0 : 1, len, sym);
+    }
+    const int shift = st & 31, adv = (st >> 5) & 127, sz = st >> 12;
+    // value bits: the sz bits after the code, in the buffer's top 32 bits (shift <= 31)
+    const uint32_t hi = (uint32_t)(r.buf >> 32);
+    const uint32_t raw = sz ? (hi >> (32 - shift)) & ((1u << sz) - 1u) : 0u;
+    r.buf <<= shift;
+    r.cnt -= shift;
+    const int v = extend(raw, sz);
+    // the index advance: DC 1, a coefficient run + 1 (stored at k + run), ZRL
+    // 16 (its zero at k + 15), EOB 64 (its zero at 63): every position stored
+    // is one of the block's not yet written
+    const int knew = k + adv;
+    on_ac(min(knew - 1, 63), v);
+    on_dc(dc, v);
+#else
     const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
     int len, sym;
     if (e) {
@@ -413,10 +468,21 @@ struct Dec {
     r.cnt -= len + sz;
     const int v = extend(raw, sz);
     const int kpos = k + run;  // an AC coefficient's index (sz != 0)
+#if MXD_HUFF_LEAN3
+    // next index: kpos + 1 after the DC (k = run = 0), a coefficient or a ZRL
+    // (run 15: k + 16); 64 after an EOB.  Every symbol stores: the DC at 0, a
+    // coefficient at kpos (a corrupt run past 63 lands on 63), and an EOB / ZRL
+    // its zero at an index of the block not yet written -- so no branch.
+    const int knew = (dc || sz != 0 || run == 15) ? kpos + 1 : 64;
+    on_ac(min(kpos, 63), v);
+    on_dc(dc, v);
+#else
     // next index: after the DC 1; after a coefficient kpos + 1; ZRL k + 16; EOB 64
     const int knew = dc ? 1 : sz ? kpos + 1 : run == 15 ? k + 16 : 64;
     if (dc) on_dc(v);
     else if (sz) on_ac(kpos, v);
+#endif
+#endif  // MXD_HUFF_LEAN4
     const bool end = knew >= 64;
     k = end ? 0 : knew;
     b = end ? (b + 1 == bpm ? 0 : b + 1) : b;
@@ -573,6 +639,8 @@ __device__ __forceinline__ Sub sub_of(const Shared& sh, const SegLds* seg, int s
 struct Stats {
   int sync_syms = 0, write_syms = 0, rounds = 0;
   uint64_t t[4] = {0, 0, 0, 0};  // thread 0: staged, synchronised, written, done
+  uint64_t c[2] = {0, 0};        // thread 0: shader clock at the write pass's start and end
+  uint64_t r[2] = {0, 0};        // and the real-time clock there
 };
 #else
 struct Stats {};
@@ -590,8 +658,8 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
   const int t = threadIdx.x;
   Dec dec;
   dec.init(&im, tab);
-  const auto nop_dc = [](int) {};
-  const auto nop_ac = [](int, int) {};
+  const auto nop_dc = [](auto...) {};
+  const auto nop_ac = [](auto...) {};
   R rd;
 
   // 1. synchronisation rounds (the last subsequence of a segment hands its
@@ -636,6 +704,17 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
         dec.k = sh.in_k[id];
       }
       int done = 0;
+#if MXD_HUFF_UNROLL > 1
+      // a step consumes <= 31 bits: while the end is further than UNROLL - 1
+      // steps can reach, the next UNROLL steps all start before it
+      while (rd.pos() + 31 * (MXD_HUFF_UNROLL - 1) < v.end) {
+#pragma unroll
+        for (int i = 0; i < MXD_HUFF_UNROLL; i++) done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
+#if MXD_HUFF_STATS
+        st.sync_syms += MXD_HUFF_UNROLL;
+#endif
+      }
+#endif
       for (;;) {
         const int32_t p = rd.pos();
         // the segment's end can only stop the last subsequence, which the rounds never decode
@@ -684,6 +763,11 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
   int64_t g = seg_block0 + (u.active ? before - sh.done[t - u.j] : 0);
 
   // 3. write pass
+#if MXD_HUFF_STATS
+  __syncthreads();
+  st.c[0] = stat_cycles();
+  st.r[0] = stat_clock();
+#endif
   if (u.active) {
     rd.init(wbase, u.sg.word, (u.sg.bits + 31) >> 5);
     rd.seek(sh.in_pos[t]);
@@ -697,9 +781,21 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
       return coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
     };
     int16_t* blk = addr();
-    for (;;) {
-      const int32_t p = rd.pos();
-      if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
+    auto wstep = [&]() {
+#if MXD_HUFF_LEAN3
+      const bool fin = dec.step(
+          rd,
+          [&](bool dc, int diff) {
+            const int c = (dec.cpack >> (2 * dec.b)) & 3;
+            dcsum[0] += dc && c == 0 ? diff : 0;
+            dcsum[1] += dc && c == 1 ? diff : 0;
+            dcsum[2] += dc && c == 2 ? diff : 0;
+            dc0 = dc && dc0 < 0 ? g : dc0;
+            dc1 = dc ? g + 1 : dc1;
+          },
+          // zig-zag order (jpeg_idct reorders)
+          [&](int kk, int v) { blk[kk] = (int16_t)v; });
+#else
       const bool fin = dec.step(
           rd,
           [&](int diff) {
@@ -716,6 +812,7 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
             // jpeg_natural_order's extra entries put it
             blk[min(kk, 63)] = (int16_t)v;
           });
+#endif
       if (fin) {
         g++;
         cj++;
@@ -730,6 +827,21 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
 #if MXD_HUFF_STATS
       st.write_syms++;
 #endif
+    };
+#if MXD_HUFF_WUNROLL > 1
+    // WUNROLL steps per check while none of them can reach the subsequence's
+    // end, the segment's last block or the bits past the data (a step
+    // consumes <= 31 bits and finishes <= 1 block)
+    const int32_t lim = min(u.end, u.sg.bits + 1);
+    while (rd.pos() + 31 * (MXD_HUFF_WUNROLL - 1) < lim && g + (MXD_HUFF_WUNROLL - 1) < seg_block1) {
+#pragma unroll
+      for (int i = 0; i < MXD_HUFF_WUNROLL; i++) wstep();
+    }
+#endif
+    for (;;) {
+      const int32_t p = rd.pos();
+      if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
+      wstep();
     }
   }
 }
@@ -841,6 +953,17 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   else
     decode_passes<GlobalReader>(words + word0, sh, im, tab, seg, sub_bits, nsub, u, coef, dcsum, dc0, dc1, st);
 
+#if MXD_HUFF_STATS
+  __syncthreads();
+  st.c[1] = stat_cycles();
+  st.r[1] = stat_clock();
+  if (t == 0) sh.flag[0] = 0;
+  __syncthreads();
+  atomicMax(&sh.flag[0], st.write_syms);  // an LDS atomic: the busiest thread's write-pass symbols
+  __syncthreads();
+  const int stat_wmax = sh.flag[0];
+  __syncthreads();
+#endif
   // 4. DC values: per component, the differences before this subsequence in its segment
   for (int c = 0; c < 3; c++) {
     const int ex = block_exclusive_scan(u.active ? dcsum[c] : 0, sh.scan, nullptr);
@@ -878,9 +1001,13 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   // wave 0's lanes 0..7 (vector stores); thread 0's clocks
   const uint64_t t0 = __shfl(st.t[0], 0, 64), t1 = __shfl(st.t[1], 0, 64), t2 = __shfl(st.t[2], 0, 64),
                  t3 = __shfl(st.t[3], 0, 64), tk = __shfl(t_kernel, 0, 64);
+  const uint64_t c0 = __shfl(st.c[0], 0, 64), c1 = __shfl(st.c[1], 0, 64);
+  const uint64_t r0 = __shfl(st.r[0], 0, 64), r1 = __shfl(st.r[1], 0, 64);
   if (blockIdx.x < kStatJobs && t < kStatInts) {
-    const int v[kStatInts] = {st.rounds,   nsub, stat_sync, stat_write, (int)(t1 - t0), (int)(t2 - t1),
-                              (int)(t3 - t2), (int)(t0 - tk)};
+    // write-pass shader cycles, the busiest thread's write symbols, and thread 0's
+    const int v[kStatInts] = {st.rounds,      nsub,           stat_sync,         stat_write,
+                              (int)(t1 - t0), (int)(t2 - t1), (int)(t3 - t2),    (int)(t0 - tk),
+                              (int)(c1 - c0), stat_wmax,      __shfl(st.write_syms, 0, 64), (int)(r1 - r0)};
     g_huff_stats[blockIdx.x * kStatInts + t] = v[t];
   }
 #endif

@@ -36,7 +36,7 @@ def main():
                                     dst=dst.ptr + i * 224 * 224 * 3, dst_stride=224 * 3))
             arr, n = capi.make_jpeg_images(entries)
             capi.jpeg_resize_crop_to_device(arr, n, capi.MXD_U8, 0)
-            st = np.zeros((len(datas), 8), np.int32)
+            st = np.zeros((len(datas), 12), np.int32)
             assert L.mxd_debug_huff_stats(st.ctypes.data_as(ctypes.c_void_p), len(datas)) == 0
             print(json.dumps(dict(dataset=name, min_bits=bits, rounds_mean=round(float(st[:, 0].mean()), 2),
                                   rounds_max=int(st[:, 0].max()), subsequences_mean=round(float(st[:, 1].mean()), 1),
@@ -46,7 +46,13 @@ def main():
                                   us_sync=[round(float(st[:, 4].mean()) / 100, 1), round(float(st[:, 4].max()) / 100, 1)],
                                   us_write=[round(float(st[:, 5].mean()) / 100, 1), round(float(st[:, 5].max()) / 100, 1)],
                                   us_dc=[round(float(st[:, 6].mean()) / 100, 1), round(float(st[:, 6].max()) / 100, 1)],
-                                  syms_per_sub_round=round(float(st[:, 2].sum() / max(1, (st[:, 1] * st[:, 0]).sum())), 1))),
+                                  syms_per_sub_round=round(float(st[:, 2].sum() / max(1, (st[:, 1] * st[:, 0]).sum())), 1),
+                                  # write pass: shader cycles per step of the busiest thread, and the
+                                  # shader clock (cycles / real-time ticks of 10 ns)
+                                  write_cycles_per_step=round(float((st[:, 8] / np.maximum(st[:, 9], 1)).mean()), 1),
+                                  write_max_syms=round(float(st[:, 9].mean()), 1),
+                                  write_t0_syms=round(float(st[:, 10].mean()), 1),
+                                  clock_ghz=round(float((st[:, 8] / np.maximum(st[:, 11], 1)).mean()) / 10, 3))),
                   flush=True)
             dst.free()
     capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, 0)
