@@ -386,7 +386,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       sd.mcus = (int32_t)std::min<int64_t>(h.rst_mcus, es.mcus - sd.mcu0);
       sd.sub_bits = sub_bits;
       c.raw.push_back({es.data + es.seg_begin[sgi], es.data + es.seg_end[sgi], c.words_bytes});
-      c.words_bytes += up(raw + 4, 16);  // zero padding past the data (a partial last word)
+      // zero padding past the data: a partial last word's tail and >= 1 zero word,
+      // which jpeghuff.hip's LDS reader reads for every word past the segment
+      c.words_bytes += up(raw + 4, 16);
       // jobs: consecutive segments of one image, <= kHuffThreads subsequences
       // (planned from the raw size; unstuffing only shortens a segment)
       const int32_t nsub = (int32_t)std::max<int64_t>(1, (8 * raw + sub_bits - 1) / sub_bits);

@@ -79,6 +79,11 @@ namespace {
 #ifndef MXD_HUFF_UNROLL
 #define MXD_HUFF_UNROLL 2
 #endif
+// The LDS reader takes words past its segment from the segment's zero
+// padding (default; tuning builds -DMXD_HUFF_ZPAD=0 select zero instead).
+#ifndef MXD_HUFF_ZPAD
+#define MXD_HUFF_ZPAD 1
+#endif
 #ifndef MXD_HUFF_WUNROLL
 #define MXD_HUFF_WUNROLL 1
 #endif
@@ -117,10 +122,19 @@ struct LdsReader {
 
 #if MXD_HUFF_PREFETCH
   static __device__ __forceinline__ uint32_t order(uint32_t x) { return __builtin_bswap32(x); }
+#if MXD_HUFF_ZPAD
+  // w[nw] is a zero word: every segment is staged with >= 4 zero bytes past
+  // its data, rounded up to 16 (hostpath.cpp), so words past the segment
+  // read as w[nw] without a separate zero select
+  __device__ __forceinline__ uint32_t word(int32_t i) const { return w[min(i, nw)]; }
+  __device__ __forceinline__ bool inside() const { return true; }
+#else
   __device__ __forceinline__ uint32_t word(int32_t i) const { return w[i < nw ? i : max(nw - 1, 0)]; }
+  __device__ __forceinline__ bool inside() const { return wi < nw; }
+#endif
   // one word (the caller knows cnt <= 32)
   __device__ __forceinline__ void refill1() {
-    const uint32_t x = wi < nw ? order(nxt) : 0u;
+    const uint32_t x = inside() ? order(nxt) : 0u;
     buf |= (uint64_t)x << (32 - cnt);
     cnt += 32;
     wi++;
@@ -129,7 +143,7 @@ struct LdsReader {
   // refill1 when cnt <= 32, without a branch (the word load is issued either way)
   __device__ __forceinline__ void refill_if() {
     const bool need = cnt <= 32;
-    const uint32_t x = need && wi < nw ? order(nxt) : 0u;
+    const uint32_t x = need && inside() ? order(nxt) : 0u;
     buf |= (uint64_t)x << (need ? 32 - cnt : 0);
     cnt += need ? 32 : 0;
     wi += need ? 1 : 0;
@@ -137,7 +151,7 @@ struct LdsReader {
   }
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
-      const uint32_t x = wi < nw ? order(nxt) : 0u;
+      const uint32_t x = inside() ? order(nxt) : 0u;
       buf |= (uint64_t)x << (32 - cnt);
       cnt += 32;
       wi++;
