@@ -94,7 +94,7 @@ namespace {
 
 #if MXD_HUFF_STATS
 constexpr int kStatJobs = 1 << 16;
-constexpr int kStatInts = 12;
+constexpr int kStatInts = 16;
 __device__ int g_huff_stats[kStatJobs * kStatInts];
 __device__ __forceinline__ uint64_t stat_clock() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ uint64_t stat_cycles() { return __builtin_amdgcn_s_memtime(); }
@@ -430,6 +430,8 @@ struct Dec {
       cpack |= (uint32_t)(im_->blk_comp[j] & 3) << (2 * j);
     }
   }
+  // component of the current block
+  __device__ __forceinline__ int comp() const { return (cpack >> (2 * b)) & 3; }
 
   // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
   // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
@@ -655,6 +657,7 @@ struct Stats {
   uint64_t t[4] = {0, 0, 0, 0};  // thread 0: staged, synchronised, written, done
   uint64_t c[2] = {0, 0};        // thread 0: shader clock at the write pass's start and end
   uint64_t r[2] = {0, 0};        // and the real-time clock there
+  int chg = 0, chg_pos = 0, chg_k = 0;  // start-state changes after round 0: all, same bit position, same (position, k)
 };
 #else
 struct Stats {};
@@ -754,6 +757,13 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
       const int32_t p = sh.out_pos[t - 1];
       const int8_t b = sh.out_b[t - 1], k = sh.out_k[t - 1];
       if (p != sh.in_pos[t] || b != sh.in_b[t] || k != sh.in_k[t]) {
+#if MXD_HUFF_STATS
+        if (round > 0) {
+          st.chg++;
+          st.chg_pos += p == sh.in_pos[t] ? 1 : 0;
+          st.chg_k += p == sh.in_pos[t] && k == sh.in_k[t] ? 1 : 0;
+        }
+#endif
         sh.in_pos[t] = p;
         sh.in_b[t] = b;
         sh.in_k[t] = k;
@@ -800,7 +810,7 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
       const bool fin = dec.step(
           rd,
           [&](bool dc, int diff) {
-            const int c = (dec.cpack >> (2 * dec.b)) & 3;
+            const int c = dec.comp();
             dcsum[0] += dc && c == 0 ? diff : 0;
             dcsum[1] += dc && c == 1 ? diff : 0;
             dcsum[2] += dc && c == 2 ? diff : 0;
@@ -991,12 +1001,18 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     __syncthreads();
   }
 #if MXD_HUFF_STATS
-  int stat_sync = 0, stat_write = 0;
+  int stat_sync = 0, stat_write = 0, stat_chg = 0, stat_chg_pos = 0, stat_chg_k = 0;
   {
     const int a = block_exclusive_scan(st.sync_syms, sh.scan, &stat_sync);
     const int b = block_exclusive_scan(st.write_syms, sh.scan, &stat_write);
+    const int c = block_exclusive_scan(st.chg, sh.scan, &stat_chg);
+    const int d = block_exclusive_scan(st.chg_pos, sh.scan, &stat_chg_pos);
+    const int e = block_exclusive_scan(st.chg_k, sh.scan, &stat_chg_k);
     (void)a;
     (void)b;
+    (void)c;
+    (void)d;
+    (void)e;
   }
 #endif
   if (u.active && dc0 >= 0) {
@@ -1021,7 +1037,8 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     // write-pass shader cycles, the busiest thread's write symbols, and thread 0's
     const int v[kStatInts] = {st.rounds,      nsub,           stat_sync,         stat_write,
                               (int)(t1 - t0), (int)(t2 - t1), (int)(t3 - t2),    (int)(t0 - tk),
-                              (int)(c1 - c0), stat_wmax,      __shfl(st.write_syms, 0, 64), (int)(r1 - r0)};
+                              (int)(c1 - c0), stat_wmax,      __shfl(st.write_syms, 0, 64), (int)(r1 - r0),
+                              stat_chg,       stat_chg_pos,   stat_chg_k,        0};
     g_huff_stats[blockIdx.x * kStatInts + t] = v[t];
   }
 #endif

@@ -36,7 +36,7 @@ def main():
                                     dst=dst.ptr + i * 224 * 224 * 3, dst_stride=224 * 3))
             arr, n = capi.make_jpeg_images(entries)
             capi.jpeg_resize_crop_to_device(arr, n, capi.MXD_U8, 0)
-            st = np.zeros((len(datas), 12), np.int32)
+            st = np.zeros((len(datas), 16), np.int32)
             assert L.mxd_debug_huff_stats(st.ctypes.data_as(ctypes.c_void_p), len(datas)) == 0
             print(json.dumps(dict(dataset=name, min_bits=bits, rounds_mean=round(float(st[:, 0].mean()), 2),
                                   rounds_max=int(st[:, 0].max()), subsequences_mean=round(float(st[:, 1].mean()), 1),
@@ -52,7 +52,12 @@ def main():
                                   write_cycles_per_step=round(float((st[:, 8] / np.maximum(st[:, 9], 1)).mean()), 1),
                                   write_max_syms=round(float(st[:, 9].mean()), 1),
                                   write_t0_syms=round(float(st[:, 10].mean()), 1),
-                                  clock_ghz=round(float((st[:, 8] / np.maximum(st[:, 11], 1)).mean()) / 10, 3))),
+                                  clock_ghz=round(float((st[:, 8] / np.maximum(st[:, 11], 1)).mean()) / 10, 3),
+                                  # start-state changes after round 0, and the shares that kept the
+                                  # bit position (phase only) and the position and coefficient index
+                                  changes=int(st[:, 12].sum()),
+                                  share_same_pos=round(float(st[:, 13].sum() / max(1, st[:, 12].sum())), 3),
+                                  share_same_pos_k=round(float(st[:, 14].sum() / max(1, st[:, 12].sum())), 3))),
                   flush=True)
             dst.free()
     capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, 0)
