@@ -170,7 +170,11 @@ int mxd_set_kernel_policy(int32_t policy);
  * subsequences must synchronise);
  * MXD_TUNE_HUFF_GLOBAL: 1 = the device entropy decode reads every job's
  * entropy-coded words from device memory (default: from LDS for the jobs
- * whose words fit it). */
+ * whose words fit it);
+ * MXD_TUNE_HOST_WAIT: how a host-path call waits for its chunks (read when
+ * a host-path context's events are first created): 0 / 1 = events created
+ * with hipEventBlockingSync, the waiting thread sleeps (default); 2 = HIP's
+ * default polling wait. */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -179,7 +183,8 @@ enum mxd_tune {
   MXD_TUNE_STREAMS = 4,
   MXD_TUNE_HUFF_BITS = 5,
   MXD_TUNE_HUFF_GLOBAL = 6,
-  MXD_TUNE_COUNT = 7
+  MXD_TUNE_HOST_WAIT = 7,
+  MXD_TUNE_COUNT = 8
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 

@@ -242,7 +242,14 @@ struct CtxLease {
 
 int init_slot(Slot& s) {
   if (!s.stream) MXD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-  if (!s.done) MXD_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  // the calling thread sleeps on the chunk's event instead of polling
+  // (MXD_TUNE_HOST_WAIT 2: polling): with 16 prefetch workers on 16 cores the
+  // polling waits took the cores the other workers' parsing and staging need
+  // (JPEG device batch at 16 workers, C4 137 k -> 156-161 k img/s, C1
+  // 176-192 k -> 205-208 k; profiles/r04/host_wait_ab.jsonl)
+  if (!s.done)
+    MXD_HIP(hipEventCreateWithFlags(
+        &s.done, hipEventDisableTiming | (g_tune[MXD_TUNE_HOST_WAIT].load() == 2 ? 0 : hipEventBlockingSync)));
   return MXD_OK;
 }
 

@@ -56,6 +56,7 @@ MXD_TUNE_DESC = 3
 MXD_TUNE_STREAMS = 4
 MXD_TUNE_HUFF_BITS = 5
 MXD_TUNE_HUFF_GLOBAL = 6
+MXD_TUNE_HOST_WAIT = 7
 
 
 class MxdImage(ctypes.Structure):
