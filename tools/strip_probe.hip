@@ -53,12 +53,21 @@ struct Geo {
   double bytes;             // algorithmic bytes per launch
 };
 
+// The product's blockIdx -> XCD-contiguous remap (csrc/devutil.h xcd_remap):
+// XCD k runs a contiguous range of units, in dispatch order.
+__device__ __forceinline__ int remap_xcd(int b, int n) {
+  const int q = n >> 3, r = n & 7;
+  const int xcd = b & 7, idx = b >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 template <int NH, int D, int PF>
 __global__ __launch_bounds__(kWaves * 64) void probe(const uint8_t* __restrict__ base, char* __restrict__ out,
-                                                     int nbands, int strips, Geo g) {
+                                                     int nbands, int strips, Geo g, int remap) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wave);
+  const int blk = remap ? remap_xcd(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int unit = __builtin_amdgcn_readfirstlane(blk * kWaves + wave);
   const int per_img = nbands * strips;
   if (unit >= g.imgs * per_img) return;
   const int img = unit / per_img;
@@ -171,22 +180,26 @@ double timeit(const char* name, double bytes, const std::function<void()>& f) {
   return us;
 }
 
+// rounds: band count multiplied so the units fill that many occupancy rounds
+// (shorter bands, more of them: the "sweep" form, where the dispatcher starts
+// each XCD's next units in address order as earlier ones finish).
 template <int NH, int D, int PF>
-void run(const uint8_t* const* srcs, char* const* outs, const Geo& g, int strips, int cus) {
+void run(const uint8_t* const* srcs, char* const* outs, const Geo& g, int strips, int cus, int rounds = 1,
+         int remap = 0) {
   auto k = probe<NH, D, PF>;
   const int lds = kWaves * kInst;
   int occ = 0;
   CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k), kWaves * 64, lds));
   // units fill one round of the resident waves (the product planner's rule)
   const int waves = occ * kWaves * cus;
-  const int nbands = waves / (g.imgs * strips) > 0 ? waves / (g.imgs * strips) : 1;
+  const int nbands = rounds * (waves / (g.imgs * strips) > 0 ? waves / (g.imgs * strips) : 1);
   const int units = g.imgs * strips * nbands;
   char name[160];
-  snprintf(name, sizeof name, "%-6s strips=%d NH=%d D=%d PF=%d (%2d waves/CU, bands %d)", g.name, strips, NH, D, PF,
-           occ * kWaves, nbands);
+  snprintf(name, sizeof name, "%-6s strips=%d NH=%d D=%d PF=%d R=%d X=%d (%2d waves/CU, bands %d)", g.name, strips, NH,
+           D, PF, rounds, remap, occ * kWaves, nbands);
   timeit(name, g.bytes, [&] {
     hipLaunchKernelGGL(k, dim3((units + kWaves - 1) / kWaves), dim3(kWaves * 64), lds, 0, srcs[g_iter & 1],
-                       outs[g_iter & 1], nbands, strips, g);
+                       outs[g_iter & 1], nbands, strips, g, remap);
   });
 }
 
@@ -212,22 +225,24 @@ int main() {
   const uint8_t* srcs[2] = {s0, s1};
   char* outs[2] = {o0, o1};
   printf("# %d CUs\n", cus);
+  // Round 5: the sweep and sibling forms against the
+  // one-round band layout, C2 and 480p.
   for (int rep = 0; rep < 2; rep++) {
-    run<1, 4, 0>(srcs, outs, p480, 2, cus);
-    run<1, 4, 2>(srcs, outs, p480, 2, cus);
-    run<1, 4, 1>(srcs, outs, p480, 2, cus);
-    run<2, 4, 0>(srcs, outs, p480, 1, cus);
-    run<2, 4, 0>(srcs, outs, p720, 2, cus);
-    run<2, 4, 2>(srcs, outs, p720, 2, cus);
-    run<1, 4, 0>(srcs, outs, p720, 3, cus);
-    run<3, 4, 0>(srcs, outs, p720, 1, cus);
     run<2, 4, 0>(srcs, outs, c2, 2, cus);
-    run<2, 4, 2>(srcs, outs, c2, 2, cus);
-    run<2, 4, 1>(srcs, outs, c2, 2, cus);
-    run<2, 4, 0>(srcs, outs, c2, 3, cus);
-    run<1, 4, 0>(srcs, outs, c2, 4, cus);
-    run<4, 4, 0>(srcs, outs, c2, 1, cus);
-    run<4, 2, 0>(srcs, outs, c2, 1, cus);
+    run<2, 4, 0>(srcs, outs, c2, 2, cus, 1, 1);
+    run<2, 4, 0>(srcs, outs, c2, 2, cus, 2, 1);
+    run<2, 4, 0>(srcs, outs, c2, 2, cus, 4, 1);
+    run<2, 4, 0>(srcs, outs, c2, 2, cus, 8, 1);
+    run<2, 4, 0>(srcs, outs, c2, 2, cus, 4, 0);
+    run<1, 4, 0>(srcs, outs, c2, 8, cus);        // sibling: a workgroup's 8 waves = the 8 strips of one band
+    run<1, 4, 0>(srcs, outs, c2, 8, cus, 1, 1);
+    run<1, 4, 0>(srcs, outs, c2, 8, cus, 4, 1);
+    run<1, 4, 0>(srcs, outs, c2, 4, cus, 1, 1);
+    run<1, 4, 0>(srcs, outs, p480, 2, cus);
+    run<1, 4, 0>(srcs, outs, p480, 2, cus, 1, 1);
+    run<1, 4, 0>(srcs, outs, p480, 2, cus, 4, 1);
+    run<1, 4, 0>(srcs, outs, p480, 2, cus, 8, 1);
+    run<1, 4, 0>(srcs, outs, p480, 4, cus, 1, 1);
   }
   return 0;
 }
