@@ -32,7 +32,11 @@
 extern "C" {
 #endif
 
-#define MXD_ABI_VERSION 4
+/* 5: the round-4 additions (numbered in round 5): mxd_jpeg_coefs_parse (device
+ * entropy decode pending), mxd_jpeg_coefs_entropy_pending,
+ * mxd_device_synchronize, and the tuning knobs MXD_TUNE_HUFF_BITS,
+ * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS. */
+#define MXD_ABI_VERSION 5
 
 enum mxd_status {
   MXD_OK = 0,
@@ -174,7 +178,10 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_HOST_WAIT: how a host-path call waits for its chunks (read when
  * a host-path context's events are first created): 0 / 1 = events created
  * with hipEventBlockingSync, the waiting thread sleeps (default); 2 = HIP's
- * default polling wait. */
+ * default polling wait;
+ * MXD_TUNE_HOST_STREAMS: streams per device the host-path calls launch on
+ * (read when a host-path context is first set up): 0 = every context slot
+ * owns one (default); n > 0 = the slots share n library streams. */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -184,7 +191,8 @@ enum mxd_tune {
   MXD_TUNE_HUFF_BITS = 5,
   MXD_TUNE_HUFF_GLOBAL = 6,
   MXD_TUNE_HOST_WAIT = 7,
-  MXD_TUNE_COUNT = 8
+  MXD_TUNE_HOST_STREAMS = 8,
+  MXD_TUNE_COUNT = 9
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 

@@ -240,8 +240,38 @@ struct CtxLease {
   ~CtxLease() { host_pool().release(device, ctx); }
 };
 
+// MXD_TUNE_HOST_STREAMS > 0: host-path slots share that many library
+// streams per device (round robin as slots are first set up) instead of
+// owning one each, so 16 prefetch workers do not spread their device calls
+// over 32 streams when HIP maps a process's streams onto fewer hardware
+// queues (GPU_MAX_HW_QUEUES, 4 by default).  Read when a slot is first set up.
+int shared_stream(hipStream_t* out, int32_t n) {
+  static std::mutex mu;
+  static std::map<int, std::pair<std::vector<hipStream_t>, int64_t>> pools;
+  int dev = 0;
+  MXD_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto& pl = pools[dev];
+  if ((int32_t)pl.first.size() < n) {
+    hipStream_t st = nullptr;
+    MXD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    pl.first.push_back(st);
+    *out = st;
+    return MXD_OK;
+  }
+  *out = pl.first[(size_t)(pl.second++ % (int64_t)pl.first.size())];
+  return MXD_OK;
+}
+
 int init_slot(Slot& s) {
-  if (!s.stream) MXD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  if (!s.stream) {
+    const int32_t shared = g_tune[MXD_TUNE_HOST_STREAMS].load();
+    if (shared > 0) {
+      if (int rc = shared_stream(&s.stream, shared)) return rc;
+    } else {
+      MXD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    }
+  }
   // the calling thread sleeps on the chunk's event instead of polling
   // (MXD_TUNE_HOST_WAIT 2: polling): with 16 prefetch workers on 16 cores the
   // polling waits took the cores the other workers' parsing and staging need

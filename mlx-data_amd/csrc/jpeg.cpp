@@ -939,6 +939,9 @@ struct Decoder {
         p += 1;
         continue;
       }
+      // the device decoder keeps a segment's bit count and word offsets in
+      // int32: segments past 2^28 bytes go to the host decoder
+      if (p - b >= ((size_t)1 << 28)) throw NotDevice{};
       seg_begin.push_back((int64_t)b);
       seg_end.push_back((int64_t)p);
       if (m >= 0xD0 && m <= 0xD7) {
@@ -1128,6 +1131,10 @@ struct Decoder {
         case 0xCF:
           unsupported_sof(m);
         case 0xC4:
+          // a table defined after the recorded scan (before EOI): the host
+          // decoded that scan at its SOS with the earlier tables, the device
+          // would read the later ones -- decode such files on the host
+          if (pending) throw NotDevice{};
           read_dht();
           break;
         case 0xCC:
@@ -1136,6 +1143,7 @@ struct Decoder {
           read_dqt();
           break;
         case 0xDD:
+          if (pending) throw NotDevice{};  // likewise a restart interval after the recorded scan
           if (u16() != 4) fail("Bogus marker length");
           restart_interval = u16();
           break;

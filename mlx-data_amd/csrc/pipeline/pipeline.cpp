@@ -1017,29 +1017,45 @@ ImagePlan deferred_plan(const std::shared_ptr<Array>& a) {
 // device pipeline.  A released block may still be read by work its consumer
 // (e.g. torch through DLPack) enqueued on a stream of its own, so it is only
 // reused after a device synchronisation that followed its release: blocks
-// released since the last one wait in `pending`; a request that finds no
+// released since the last one wait in `pending`.  A request that finds no
 // idle block of its size synchronises the device once and makes every
-// pending block idle.  At most kMaxCached bytes wait per device.
+// pending block idle when a pending block has its size, or when the pending
+// blocks hold more than half of kMaxCached (batches of changing shapes: their
+// blocks would otherwise wait forever); idle blocks past kMaxCached are then
+// freed, other sizes first.  So at most kMaxCached bytes (plus one block)
+// stay cached per device, idle and pending together.
 class DevicePool {
  public:
   std::shared_ptr<void> get(int device, int64_t n) {
     const size_t cap = ((size_t)std::max<int64_t>(n, 1) + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
-    void* p = take(device, cap, false);
-    if (!p && has_pending(device, cap)) {
+    void* p = take(device, cap);
+    if (!p && must_drain(device, cap)) {
       std::vector<std::pair<size_t, void*>> now;
       {
         std::lock_guard<std::mutex> lk(mu_);
-        now.swap(devs_[device].pending);
+        Dev& d = devs_[device];
+        now.swap(d.pending);
+        d.pending_bytes = 0;
       }
       check(mxd_device_synchronize(device));  // everything released before this point is idle
+      std::vector<void*> drop;
       {
         std::lock_guard<std::mutex> lk(mu_);
-        for (auto& b : now) devs_[device].idle[b.first].push_back(b.second);
+        Dev& d = devs_[device];
+        for (auto& b : now) d.idle[b.first].push_back(b.second);
+        evict(d, cap, &drop);
       }
-      p = take(device, cap, true);
+      for (void* q : drop) (void)mxd_free_device(q, device);
+      p = take(device, cap);
     }
     if (!p) check(mxd_malloc_device(&p, cap, device));
     return std::shared_ptr<void>(p, [this, device, cap](void* q) { put(device, q, cap); });
+  }
+
+  // Bytes the pool holds for `device` (idle + pending): tests bound it.
+  size_t cached(int device) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return devs_[device].cached;
   }
 
  private:
@@ -1047,9 +1063,9 @@ class DevicePool {
   struct Dev {
     std::map<size_t, std::vector<void*>> idle;
     std::vector<std::pair<size_t, void*>> pending;
-    size_t cached = 0;
+    size_t cached = 0, pending_bytes = 0;
   };
-  void* take(int device, size_t cap, bool) {
+  void* take(int device, size_t cap) {
     std::lock_guard<std::mutex> lk(mu_);
     Dev& d = devs_[device];
     auto it = d.idle.find(cap);
@@ -1059,11 +1075,26 @@ class DevicePool {
     d.cached -= cap;
     return p;
   }
-  bool has_pending(int device, size_t cap) {
+  bool must_drain(int device, size_t cap) {
     std::lock_guard<std::mutex> lk(mu_);
-    for (auto& b : devs_[device].pending)
+    const Dev& d = devs_[device];
+    if (d.pending.empty()) return false;
+    if (d.pending_bytes > kMaxCached / 2) return true;
+    for (auto& b : d.pending)
       if (b.first == cap) return true;
     return false;
+  }
+  // Frees idle blocks (other sizes than `keep` first) while over the cap.
+  static void evict(Dev& d, size_t keep, std::vector<void*>* drop) {
+    for (int pass = 0; pass < 2 && d.cached > kMaxCached; pass++)
+      for (auto it = d.idle.begin(); d.cached > kMaxCached && it != d.idle.end(); ++it) {
+        if ((pass == 0) == (it->first == keep)) continue;
+        while (d.cached > kMaxCached && !it->second.empty()) {
+          drop->push_back(it->second.back());
+          it->second.pop_back();
+          d.cached -= it->first;
+        }
+      }
   }
   void put(int device, void* p, size_t cap) {
     std::vector<void*> drop;
@@ -1071,14 +1102,9 @@ class DevicePool {
       std::lock_guard<std::mutex> lk(mu_);
       Dev& d = devs_[device];
       d.pending.emplace_back(cap, p);
+      d.pending_bytes += cap;
       d.cached += cap;
-      // over the cap: idle blocks of other sizes go first
-      for (auto it = d.idle.begin(); d.cached > kMaxCached && it != d.idle.end(); ++it)
-        while (d.cached > kMaxCached && !it->second.empty()) {
-          drop.push_back(it->second.back());
-          it->second.pop_back();
-          d.cached -= it->first;
-        }
+      evict(d, cap, &drop);  // over the cap: idle blocks of other sizes go first
     }
     for (void* q : drop) (void)mxd_free_device(q, device);
   }
@@ -1091,6 +1117,11 @@ DevicePool& device_pool() {
   return *p;
 }
 
+}  // namespace
+
+size_t device_pool_bytes(int device) { return device_pool().cached(device); }
+
+namespace {
 // batch_arrays into device memory.  The fused case -- every array a pending
 // image filling the batch's pixel slots, nothing to pad -- has the kernel
 // write the batch in place; otherwise the host batch is built and uploaded.

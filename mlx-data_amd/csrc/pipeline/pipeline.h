@@ -131,6 +131,8 @@ void set_device_decode(bool on);
 void set_device_entropy(bool on);
 bool device_entropy();
 bool device_decode();
+// Bytes the device batch pool holds for `device` (idle and pending blocks).
+size_t device_pool_bytes(int device);
 
 // ---------------------------------------------------------------- state
 struct State {

@@ -511,6 +511,7 @@ PYBIND11_MODULE(_pipeline, m) {
   m.def("set_device_entropy", &set_device_entropy, py::arg("on"));
   m.def("device_entropy", &device_entropy);
   m.def("device_decode", &device_decode);
+  m.def("_device_pool_bytes", &device_pool_bytes, py::arg("device"));
 
   // The decoder holds a Python callable: drop it before the interpreter goes.
   py::module_::import("atexit").attr("register")(py::cpp_function([] { set_image_decoder(nullptr); }));

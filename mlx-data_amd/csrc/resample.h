@@ -87,23 +87,11 @@ constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; 
 // DMAX 5 (1080p / 4K -> 512, C5) takes 4 slots: its RGB u8 kernel then fits
 // 124 VGPRs (4 waves per SIMD instead of 3 at 5 slots), C5 0.3244 -> 0.3204 ms
 // per launch (profiles/r03/ring_variants.jsonl, variant ring4).
-// Tuning builds only (-DMXD_NARROW_RING=1): narrow RGB scatter lanes (4
-// pixels = 12 bytes per lane: 480p, 720p and ImageNet shapes -> 256) at DMAX
-// 2 / 3 take rings of 4 / 3 slots (3 / 2 rows ahead), so their kernels fit 64
-// VGPRs and run 8 waves per SIMD instead of 6 (the 480p row pattern alone
-// runs 110 us at 16 waves per CU and 84 us at 32, profiles/r04/inflight_a.txt
-// and strip_probe.txt).  Measured against the common ring on one box
-// (profiles/r04/ring_pack_b.jsonl): 480p 0.0935 vs 0.0903 ms per launch, C4
-// 0.0236 vs 0.0227, 720p / mixed C3 within 0.3 % -- the shallower ring costs
-// more than the occupancy gains, so the product keeps the common ring.
-#ifndef MXD_NARROW_RING
-#define MXD_NARROW_RING 0
-#endif
-constexpr bool scatter_narrow_ring(int dmax, int lane_bytes) {
-  return MXD_NARROW_RING != 0 && MXD_RING_FIXED == 0 && lane_bytes == 12 && (dmax == 2 || dmax == 3);
-}
+// (Narrow-lane rings of 4 / 3 slots at DMAX 2 / 3, 8 waves per SIMD, were
+// measured in round 4 and lost: 480p 0.0935 vs 0.0903 ms per launch, C4
+// 0.0236 vs 0.0227, profiles/r04/ring_pack_b.jsonl.)
 constexpr int scatter_ring_slots(int dmax, int lane_bytes = 0) {
-  if (scatter_narrow_ring(dmax, lane_bytes)) return dmax == 2 ? 4 : 3;
+  (void)lane_bytes;
   if (MXD_RING_FIXED > 0 && dmax >= 2) return MXD_RING_FIXED;
   if (dmax == 5 && MXD_RING == 6) return 4;
   if (MXD_RING % dmax == 0) return MXD_RING;

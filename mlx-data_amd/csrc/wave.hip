@@ -313,38 +313,9 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Packed u8 stores (tuning builds only, -DMXD_U8_PACK=1; the product stores
-// one byte per channel): the 3-byte RGB pixels of 64 consecutive lanes are
-// 192 contiguous bytes; lane m gathers bytes 4m .. 4m+3 of them from lanes
-// 4m/3 and 4m/3+1 (ds_bpermute, no LDS allocation) and stores one dword -- 48
-// dword stores per 64 pixels instead of 3 x 64 byte stores.  Measured against
-// byte stores on one box (profiles/r04/ring_pack_b.jsonl, one process per
-// build, 5 reps): C3's 480p 0.0898 vs 0.0903 ms per launch, 720p 0.1674 vs
-// 0.1653, mixed C3 0.4555 vs 0.4513, C5 0.3249 vs 0.3203 -- store
-// instructions are not what bounds the u8 kernels.
-#ifndef MXD_U8_PACK
-#define MXD_U8_PACK 0
-#endif
-
-// Lane `src`'s value of v (ds_bpermute_b32: byte address = 4 src).
-__device__ __forceinline__ uint32_t lane_value(uint32_t v, int src) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
-}
-
-// Stores the RGB bytes of pixels [0, n) (n <= 64) of a run that starts at the
-// 4-byte aligned `row`; lane l holds pixel l's bytes in px (b0 | b1 << 8 | b2 << 16).
-__device__ __forceinline__ void store_rgb_packed(__attribute__((address_space(1))) uint8_t* row, uint32_t px, int n,
-                                                 int lane) {
-  const int nbytes = 3 * n;
-  const int a = (4 * lane) / 3, o = (4 * lane) % 3;
-  const uint32_t lo = lane_value(px, a), hi = lane_value(px, min(a + 1, 63));
-  const uint32_t w = (lo >> (8 * o)) | (hi << (8 * (3 - o)));
-  if (4 * lane + 4 <= nbytes) {
-    *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(row + 4 * lane) = w;
-  } else if (4 * lane < nbytes) {  // the run's last, partial dword
-    for (int b = 0; b < nbytes - 4 * lane; b++) row[4 * lane + b] = (uint8_t)(w >> (8 * b));
-  }
-}
+// u8 outputs are stored one byte per channel: dword stores of 4 packed bytes
+// gathered across lanes measured no better (round 4, profiles/r04/ring_pack_b.jsonl:
+// 480p 0.0898 vs 0.0903 ms per launch, C5 0.3249 vs 0.3203).
 
 // Horizontal pass of one strip: lane l owns output pixels l + 64 q (q < Q).
 template <class L, bool F32, int T, int Q>
@@ -373,8 +344,6 @@ struct HStrip {
   // H taps of an output row from the LDS planes, stbir encode, store into
   // drow (the output row, pixel ox0 first).
   __device__ __forceinline__ void run(const float* planes, char* drow, int lane) const {
-    // u8 RGB with a 4-byte aligned strip row (wave-uniform): packed stores
-    const bool pack = !F32 && C == 3 && MXD_U8_PACK != 0 && (reinterpret_cast<uintptr_t>(drow) & 3) == 0;
 #pragma unroll
     for (int q = 0; q < Q; q++) {
       const int px = lane + kLanes * q;
@@ -389,14 +358,6 @@ struct HStrip {
       }
       if (q > 0 && kLanes * q >= npx) break;  // uniform: no lane has pixels left
       if ((MXD_ABLATE & 2) && s[0] != -1.0f) continue;
-      if constexpr (!F32 && C == 3) {
-        if (pack) {
-          // 64 q is a multiple of 4 pixels, so 192 q bytes keep the alignment
-          const uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
-          store_rgb_packed(GLOBAL_PTR(uint8_t, drow) + 3 * kLanes * q, v, min(kLanes, npx - kLanes * q), lane);
-          continue;
-        }
-      }
       if (px < npx) {
         if constexpr (F32) {
           auto* d = GLOBAL_PTR(float, drow) + px * C;
@@ -488,13 +449,11 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
 // parse inside __launch_bounds__)
 constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; }
 
-// Minimum waves per SIMD the register allocation must allow: 8 for the
-// narrow-ring scatter kernels (resample.h scatter_narrow_ring: <= 64 VGPRs),
-// else by lane width.
+// Minimum waves per SIMD the register allocation must allow, by lane width.
 constexpr int min_waves(int c, int p, int kind, int dmax) {
-  return kind == 2 && scatter_narrow_ring(dmax, lane_bytes(c, p)) ? 8
-         : lane_bytes(c, p) > 16                                   ? MXD_MIN_WAVES_WIDE
-                                                                    : MXD_MIN_WAVES;
+  (void)kind;
+  (void)dmax;
+  return lane_bytes(c, p) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES;
 }
 
 // One unit (image, band, strip) by the calling wave; planes = its LDS rows.

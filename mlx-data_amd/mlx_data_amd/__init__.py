@@ -16,22 +16,34 @@ def _raise_hw_queues():
     138-142 k img/s and C1 122 k -> 152 k with 16 queues
     (profiles/r04/hwq_*.jsonl).
 
-    ``MXD_HW_QUEUES`` (default 16, at most 32; 0 leaves HIP's setting alone)
-    raises ``GPU_MAX_HW_QUEUES`` to at least that many -- also when the
-    environment exports HIP's default of 4 -- and never lowers it.  No effect
-    when another library initialised HIP first."""
+    A ``GPU_MAX_HW_QUEUES`` the environment already sets is the user's (or
+    the machine's) choice and is left alone.  When it is unset, the package
+    sets it to ``MXD_HW_QUEUES`` (default 16, at most 32; 0: leave HIP's
+    default).  An explicit ``MXD_HW_QUEUES`` is the opt-in for raising an
+    exported value; the change is then logged to stderr.  No effect when
+    another library initialised HIP first."""
+    explicit = "MXD_HW_QUEUES" in os.environ
     try:
         want = min(int(os.environ.get("MXD_HW_QUEUES", "16")), 32)
     except ValueError:
         raise ValueError("MXD_HW_QUEUES must be an integer") from None
     if want <= 0:
         return
-    try:
-        have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-    except ValueError:
-        have = 0
-    if have < want:
+    have = os.environ.get("GPU_MAX_HW_QUEUES")
+    if have is None:
         os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+        return
+    if not explicit:
+        return  # the exported setting wins
+    try:
+        cur = int(have)
+    except ValueError:
+        cur = 0
+    if cur < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+        import sys
+
+        print("mlx_data_amd: GPU_MAX_HW_QUEUES %s -> %d (MXD_HW_QUEUES)" % (have, want), file=sys.stderr)
 
 
 _raise_hw_queues()

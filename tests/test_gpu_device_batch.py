@@ -183,3 +183,23 @@ def test_device_batch_blocks_recycled_safely():
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res == dict(sums_ok=True, again=True), res
+
+
+def test_device_pool_stays_bounded_over_changing_shapes():
+    """Batches whose byte size changes every time: each released
+    block waits for a device synchronisation before reuse; the pool drains its
+    pending blocks once they pass half its cap, so idle + pending stays within
+    the 2 GiB cap (plus the block in use) however many shapes go by."""
+    from mlx_data_amd import _pipeline
+
+    cap = 2 << 30
+    peak = 0
+    for mb in range(1, 81):  # 1..80 MiB per batch: 3.2 GiB of distinct sizes in all
+        a = np.full(((mb << 20) // 3072, 1024, 3), mb % 251, np.uint8)
+        d = dx.buffer_from_vector([dict(image=a)]).batch(1, device=0)[0]["image"]
+        if mb % 20 == 0:
+            assert np.array_equal(d.numpy()[0, -1], a[-1])
+        del d
+        peak = max(peak, _pipeline._device_pool_bytes(0))
+        assert _pipeline._device_pool_bytes(0) <= cap + (mb << 20), (mb, _pipeline._device_pool_bytes(0))
+    assert peak > cap // 2  # the drain was exercised

@@ -1,6 +1,8 @@
-"""CPU: the package raises HIP's hardware-queue count before HIP initialises
-(mlx_data_amd/__init__.py; DESIGN.md section 7: the prefetch workers' device
-calls serialise over HIP's default 4 queues)."""
+"""CPU: the package sets HIP's hardware-queue count before HIP initialises
+when the environment leaves it unset, and honours an exported value unless
+MXD_HW_QUEUES explicitly asks for more (mlx_data_amd/__init__.py; DESIGN.md
+section 7: the prefetch workers' device calls serialise over HIP's default 4
+queues; ADVICE r4: an exported setting is the user's)."""
 import os
 import subprocess
 import sys
@@ -22,9 +24,10 @@ def queues_after_import(**env):
 
 @pytest.mark.parametrize("env, want", [
     ({}, "16"),                                                  # unset -> package default
-    ({"GPU_MAX_HW_QUEUES": "4"}, "16"),                          # HIP's default exported -> raised
-    ({"GPU_MAX_HW_QUEUES": "24"}, "24"),                         # never lowered
-    ({"MXD_HW_QUEUES": "8", "GPU_MAX_HW_QUEUES": "4"}, "8"),
+    ({"GPU_MAX_HW_QUEUES": "4"}, "4"),                           # exported -> the user's setting wins
+    ({"GPU_MAX_HW_QUEUES": "24"}, "24"),
+    ({"MXD_HW_QUEUES": "8", "GPU_MAX_HW_QUEUES": "4"}, "8"),    # explicit opt-in raises (and logs)
+    ({"MXD_HW_QUEUES": "8", "GPU_MAX_HW_QUEUES": "24"}, "24"),  # never lowered
     ({"MXD_HW_QUEUES": "64"}, "32"),                             # clamped to 32
     ({"MXD_HW_QUEUES": "0", "GPU_MAX_HW_QUEUES": "4"}, "4"),     # 0 leaves HIP's setting alone
     ({"MXD_HW_QUEUES": "0"}, "unset"),

@@ -1,7 +1,11 @@
 """The host scheduler under ThreadSanitizer (VERDICT r1 weak
 11): tests/native/sched_stress.cpp -- Prefetch / OrderedPrefetch / ThreadPool
 over shared streams and buffers, set_state churn against drawing workers,
-shared arrays batched from many threads -- compiled with -fsanitize=thread
+shared arrays batched from many threads, and a Prefetch /
+OrderedPrefetch whose last reference is released by one of its own pool's
+tasks with others still queued, at one and four workers (the pre-fix code
+deadlocks or aborts with EDEADLK there; the stress binary fails fast on it) --
+compiled with -fsanitize=thread
 together with the pipeline sources and run on the CPU.  Any race report fails
 the test (halt_on_error)."""
 import os
