@@ -43,6 +43,15 @@ Extra fields:
                 bounded sample at 1, 8 and all of this rank's cores (rank 0,
                 N = 1, c2 only), with Pillow BILINEAR and torch-CPU bilinear
                 antialias on all cores as independent CPU points.
+  e2e_jpeg      the end-to-end JPEG pipeline (configs[3]'s chain on one GPU's
+                slice): 128 ImageNet-shape JPEG files (seed
+                2, Pillow q=90) through the operator surface -- load_image ->
+                image_resize_smallest_side(256) -> image_center_crop(224) ->
+                image_to_float -> batch(128, device=0) -> prefetch(16, 16) --
+                repeated for >= 3 s; beside it the same with the Huffman
+                decode on the host, and the reference-algorithm CPU
+                restatement (Pillow's libjpeg-turbo decode -> the oracle's C
+                stbir -> crop -> /255) on the same files and this rank's cores.
   e2e           the product's host-resident path (mxd_resize_crop_host: host
                 images in, host batch out; the kernel reads each image's
                 source footprint and writes results over PCIe, from / to
@@ -63,6 +72,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mlx-data_amd"))
 
 import numpy as np  # noqa: E402
+
+# The JPEG pipeline's prefetch workers each launch on a stream of their own;
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (the
+# boxes export 4).  The benchmark opts in to 16 (the package honours an
+# exported value unless MXD_HW_QUEUES asks for more; DESIGN.md section 7:
+# C4 114-116 k img/s with 4 queues, 146-150 k with 16).  The C2 line does not
+# depend on it (profiles/r04/hwq_bench.jsonl).
+os.environ.setdefault("MXD_HW_QUEUES", "16")
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 C = 3
@@ -451,6 +468,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (default: the workload's)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-e2e-jpeg", action="store_true")
     ap.add_argument("--no-copy", action="store_true")
     # kernel policy (include/mxd_amd.h mxd_policy; tuning measurements only)
     ap.add_argument("--policy", type=int, default=0, help=argparse.SUPPRESS)
@@ -609,6 +627,10 @@ def main():
     if ranks.rank == 0 and ranks.world == 1 and not args.no_cpu and args.workload == "c2":
         cpu = cpu_baseline()
 
+    jpeg = None
+    if ranks.rank == 0 and ranks.world == 1 and not args.no_e2e_jpeg and args.workload == "c2":
+        jpeg = e2e_jpeg(dev, no_cpu=args.no_cpu)
+
     for src, dst, _, _ in sets:
         src.free()
         dst.free()
@@ -616,6 +638,7 @@ def main():
         line = bench_line(args.workload, ranks.world, B, args.steps, args.warmup, wall, roofline, cpu, e2e,
                           manifest(capi, dev))
         line["config"]["streams"] = len(streams)
+        line["e2e_jpeg"] = jpeg
         print(json.dumps(line), flush=True)
     ranks.close()
 
@@ -739,6 +762,74 @@ def e2e_host(capi, args, sizes, geoms, f32, host, offs, pitches, dev):
                     "page-locked staging and copied out; chunks overlapped over two slots; synchronous per call. "
                     "pinned_value: host images and batch in page-locked memory, read and written in place by the "
                     "kernel (zero copy)"}
+
+
+def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False):
+    """configs[3]'s chain on one GPU's slice (see the module docstring).
+    Returns images/s of the device batch (Huffman decode on the GPU), the same
+    with the Huffman decode on the host, and the CPU restatement."""
+    try:
+        from PIL import Image  # noqa: F401  (the synthetic files and the CPU leg)
+    except ImportError:
+        return None
+    import tempfile
+
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_pipeline as bp
+    from mlx_data_amd import capi
+    from mlx_data_amd import data as dx
+
+    cores = host_cores()
+    workers = min(workers, cores)
+    with tempfile.TemporaryDirectory() as root:
+        files = bp.make_files(root, "c4", batch)  # seed 2: ImageNet shapes 500x375 / 375x500 / 500x333
+        mb = sum(os.path.getsize(f) for f in files) / 1e6
+
+        def leg(variant):
+            bp.run_surface(files, batch, workers, variant, 2 * workers)  # warm: contexts, pools, tables
+            repeat = 4 * workers
+            for _ in range(4):
+                n, dt = bp.run_surface(files, batch, workers, variant, repeat)
+                if dt >= min_s:
+                    break
+                repeat = int(np.ceil(repeat * 1.2 * min_s / max(dt, 1e-3)))
+            return round(n / dt, 1), n, round(dt, 3)
+
+        value, n, dt = leg("device")
+        hostent, n2, dt2 = leg("device_hostent")
+        cpu = None
+        if not no_cpu:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle as O
+
+            lib = O.lib()
+            u8p = ctypes.POINTER(ctypes.c_uint8)
+            per = 8
+
+            def cpu_batch(b):
+                crops = np.empty((per, 224, 224, C), np.uint8)
+                for i in range(per):
+                    f = files[(b * per + i) % len(files)]
+                    img = np.ascontiguousarray(np.asarray(Image.open(f).convert("RGB")))
+                    h, w = img.shape[:2]
+                    assert lib.orc_resize_smallest_side_center_crop(img.ctypes.data_as(u8p), w, h, C, 256, 224, 224,
+                                                                    crops[i].ctypes.data_as(u8p)) == 0
+                return crops.astype("float32") / 255
+
+            nb = max(cores, int(np.ceil(2 * len(files) / per)))
+            t = _pool_rate(cores, nb, cpu_batch)
+            cpu = {"value": round(nb * per / t, 1), "unit": "images/s", "cores": cores, "kind": "port",
+                   "sample": f"{nb * per} decodes of the same files on {cores} threads: Pillow (libjpeg-turbo) decode "
+                             f"-> oracle C stbir resize 256 -> crop 224 -> astype(float32)/255"}
+    return {"value": value, "unit": "images/s", "images": n, "seconds": dt, "workers": workers, "cores": cores,
+            "batch": batch, "files": len(files), "file_mb": round(mb, 2),
+            "host_entropy_value": hostent, "host_entropy_seconds": dt2, "cpu_restatement": cpu,
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "devices": dx.devices(),
+            "device_entropy": dx.device_entropy(), "abi": capi.lib().mxd_abi_version(),
+            "chain": "files -> load_image -> image_resize_smallest_side(256) -> image_center_crop(224, 224) -> "
+                     "image_to_float -> batch(128, device=0) -> prefetch(workers, workers); Huffman + IDCT + "
+                     "upsampling + colour + resize + crop + normalize on the GPU, markers parsed on the host; "
+                     "host_entropy_value: the Huffman decode on the host (set_device_entropy(False))"}
 
 
 if __name__ == "__main__":

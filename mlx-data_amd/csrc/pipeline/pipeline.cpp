@@ -204,7 +204,10 @@ mxd_jpeg_image jpeg_desc(const ImagePlan& p, const JpegSource& j, void* dst, int
 // One device's share of the jobs: plans over entropy-decoded JPEGs in one
 // decode + resize call (the GPU finishes the decode), the rest in one resize
 // call.  Returns the C ABI status (message in mxd_last_error()).
+std::atomic<int64_t> g_run_calls{0}, g_run_jpeg{0};  // diagnostics (run_on_stats)
+
 int run_on(const Job* jobs, size_t n, int32_t dtype, int device, bool dst_device) {
+  g_run_calls.fetch_add(1);
   std::vector<mxd_image> plain;
   std::vector<mxd_jpeg_image> jp;
   std::vector<std::shared_ptr<const JpegSource>> keep;  // alive for the call
@@ -217,6 +220,7 @@ int run_on(const Job* jobs, size_t n, int32_t dtype, int device, bool dst_device
       plain.push_back(plan_desc(j.plan, j.dst, j.stride));
     }
   }
+  g_run_jpeg.fetch_add((int64_t)jp.size());
   if (!jp.empty()) {
     const int rc = dst_device ? mxd_jpeg_resize_crop_to_device(jp.data(), (int32_t)jp.size(), dtype, device)
                               : mxd_jpeg_resize_crop_host(jp.data(), (int32_t)jp.size(), dtype, device);
@@ -1120,6 +1124,15 @@ DevicePool& device_pool() {
 }  // namespace
 
 size_t device_pool_bytes(int device) { return device_pool().cached(device); }
+
+std::pair<int64_t, int64_t> run_on_stats(bool reset) {
+  const std::pair<int64_t, int64_t> r{g_run_calls.load(), g_run_jpeg.load()};
+  if (reset) {
+    g_run_calls = 0;
+    g_run_jpeg = 0;
+  }
+  return r;
+}
 
 namespace {
 // batch_arrays into device memory.  The fused case -- every array a pending

@@ -133,6 +133,9 @@ bool device_entropy();
 bool device_decode();
 // Bytes the device batch pool holds for `device` (idle and pending blocks).
 size_t device_pool_bytes(int device);
+// Per-device batch calls made (fused launches, one per device slice) and the
+// JPEG images they carried since the last reset (diagnostics, tests).
+std::pair<int64_t, int64_t> run_on_stats(bool reset);
 
 // ---------------------------------------------------------------- state
 struct State {

@@ -88,3 +88,59 @@ def test_c4_slice_device_decode_equals_host_decode_and_oracle(c4_files):
         m, f = compare(q[i], O.crop(O.resize(img, tw, th), cx, cy, 224, 224))
         worst, frac = max(worst, m), max(frac, f)
     assert worst <= 1 and frac < 0.002, (worst, frac)
+
+
+@pytest.fixture(scope="module")
+def c4_files_1024(tmp_path_factory):
+    """configs[3]'s whole batch: 1024 ImageNet-shape files (seed 2 shapes),
+    Pillow q=90, baseline: every file takes the device entropy decode."""
+    from PIL import Image
+
+    d = tmp_path_factory.mktemp("c4_1024")
+    rng = np.random.default_rng(2)
+    sizes = [C4_SIZES[i] for i in rng.integers(0, len(C4_SIZES), 1024)]
+    files = []
+    base = synth(500, 500, 3, 7)
+    for i, (w, h) in enumerate(sizes):
+        y, x = (i * 37) % (500 - h + 1), (i * 53) % (500 - w + 1)
+        p = d / f"{i:04d}.jpg"
+        Image.fromarray(np.ascontiguousarray(np.roll(base, i, axis=1)[y:y + h, x:x + w])).save(p, quality=90)
+        files.append(str(p))
+    return files
+
+
+def test_c4_batch_split_over_eight_devices(c4_files_1024):
+    """C4's multi-GPU form rehearsed on one card --
+    set_devices([0] * 8) with the 1024-file batch, device entropy decode on:
+    eight slices of 128 (op/Shard.cpp:11-20's contiguous split), each one
+    fused JPEG call (Huffman + IDCT + colour + resize on the GPU), and the
+    batch byte-identical to set_devices([0])."""
+    from mlx_data_amd import _pipeline
+    from mlx_data_amd import data as dx
+
+    assert dx.device_entropy() and dx.device_decode()
+    assert _pipeline._split_batch(1024, 8) == [(k, 128 * k, 128 * (k + 1)) for k in range(8)]
+    before = dx.devices()
+
+    def run(devs):
+        dx.set_devices(devs)
+        d = (dx.buffer_from_vector([dict(image=f.encode(), idx=np.int64(i)) for i, f in enumerate(c4_files_1024)])
+             .load_image("image").image_resize_smallest_side("image", 256).image_center_crop("image", 224, 224)
+             .image_to_float("image"))
+        _pipeline._run_on_stats(True)
+        b = d.batch(1024)[0]
+        calls, jpegs = _pipeline._run_on_stats(True)
+        assert b["idx"].tolist() == list(range(1024))
+        return b["image"], calls, jpegs
+
+    try:
+        one, calls1, j1 = run([0])
+        eight, calls8, j8 = run([0] * 8)
+    finally:
+        dx.set_devices(before)
+    assert (calls1, j1) == (1, 1024)
+    assert (calls8, j8) == (8, 1024)
+    assert eight.shape == (1024, 224, 224, 3)
+    assert np.array_equal(one.view(np.uint32), eight.view(np.uint32))
+    q = np.rint(eight * 255).astype(np.uint8)
+    assert np.array_equal(eight.view(np.uint32), LUT[q].view(np.uint32))

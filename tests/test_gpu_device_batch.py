@@ -196,7 +196,8 @@ def test_device_pool_stays_bounded_over_changing_shapes():
     peak = 0
     for mb in range(1, 81):  # 1..80 MiB per batch: 3.2 GiB of distinct sizes in all
         a = np.full(((mb << 20) // 3072, 1024, 3), mb % 251, np.uint8)
-        d = dx.buffer_from_vector([dict(image=a)]).batch(1, device=0)[0]["image"]
+        d = dx.buffer_from_vector([dict(image=a)]).batch(1, device=0, device_keys=["image"])[0]["image"]
+        assert isinstance(d, dx.DeviceArray)
         if mb % 20 == 0:
             assert np.array_equal(d.numpy()[0, -1], a[-1])
         del d

@@ -193,6 +193,30 @@ def test_device_entropy_parse_routes_and_host_finish():
             assert np.array_equal(c.finish(), GOLD[f"{k}_rgb"]), k
 
 
+def test_device_entropy_tables_after_the_scan_go_to_the_host():
+    """a DHT or DRI between the recorded scan and EOI must not
+    reach the device decode (the host decodes the scan at its SOS with the
+    tables and interval in force there).  Such files are entropy-decoded on
+    the host and give Pillow's bytes."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(5)
+    b = io.BytesIO()
+    Image.fromarray(_smooth(rng, 48, 64, 3)).save(b, "JPEG", quality=80)
+    data = b.getvalue()
+    assert capi.JpegCoefs(data, device_entropy=True).entropy_pending
+    i = data.index(b"\xff\xc4")
+    n = int.from_bytes(data[i + 2:i + 4], "big")
+    dht = data[i:i + 2 + n]
+    # a DC table 0 of other codes: the device would decode with it
+    other = b"\xff\xc4\x00\x1f\x00" + bytes([0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0]) + bytes(range(11, -1, -1))
+    dri = b"\xff\xdd\x00\x04\x00\x02"
+    for tail in (dht, other, dri, other + dri):
+        mod = data[:-2] + tail + data[-2:]
+        c = capi.JpegCoefs(mod, device_entropy=True)
+        assert not c.entropy_pending, tail[:2]
+        assert np.array_equal(c.finish(), np.asarray(Image.open(io.BytesIO(mod)).convert("RGB")))
+
+
 def test_device_entropy_parse_errors_match_host():
     """The markers-only parse reports the host decode's errors (a DC table
     with a category above 15 is libjpeg's "Bogus Huffman table definition")."""
