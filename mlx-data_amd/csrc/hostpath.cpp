@@ -32,6 +32,7 @@ struct Slot {
   size_t dev_out_cap = 0;
   uint8_t* dev_mid = nullptr;  // JPEG chunks: IDCT samples + decoded RGB images
   size_t dev_mid_cap = 0;
+  int32_t* huff_err = nullptr;  // page-locked: the entropy decode's error word, copied back with the chunk
 };
 
 struct HostCtx {
@@ -66,6 +67,8 @@ void free_slot_buffers(Slot& s) {
   if (s.dev_in) (void)hipFree(s.dev_in);
   if (s.dev_out) (void)hipFree(s.dev_out);
   if (s.dev_mid) (void)hipFree(s.dev_mid);
+  if (s.huff_err) (void)hipHostFree(s.huff_err);
+  s.huff_err = nullptr;
   s.pin_in = s.pin_out = s.dev_in = s.dev_out = s.dev_mid = nullptr;
   s.pin_in_cap = s.pin_out_cap = s.dev_in_cap = s.dev_out_cap = s.dev_mid_cap = 0;
 }
@@ -349,6 +352,7 @@ struct JpegChunk {
   std::vector<int32_t> seg_count;    // and their number
   int64_t words_off = 0, words_bytes = 0, htabs_off = 0, himgs_off = 0, hsegs_off = 0, hjobs_off = 0;
   int64_t coef_off = 0, dev_end = 0;
+  int64_t pub_off = 0;  // the jobs' publication records + launch control, zeroed with the coefficients
   int32_t huff_threads = 0;
   int64_t huff_lds = 0;  // the largest job's dynamic LDS (its words included when they fit)
 };
@@ -399,60 +403,79 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       c.htabs.emplace_back();
       mxd::jpeg::device_table(coefs_of(jimg[i].coefs), es.table_class[t], es.table_id[t], &c.htabs.back());
     }
-    // subsequence length: every segment in <= kHuffThreads subsequences, at
-    // least kHuffMinBits bits (MXD_TUNE_HUFF_BITS overrides the minimum)
-    int64_t max_bits = 0;
-    for (int sgi = 0; sgi < es.nseg; sgi++) max_bits = std::max(max_bits, 8 * (es.seg_end[sgi] - es.seg_begin[sgi]));
+    // subsequence length: kHuffMinBits (MXD_TUNE_HUFF_BITS overrides it;
+    // a multiple of 32); segments of any length split over several jobs
     const int32_t knob = g_tune[MXD_TUNE_HUFF_BITS].load();
-    const int64_t min_bits = knob > 0 ? knob : kHuffMinBits;
-    const int32_t sub_bits =
-        (int32_t)up(std::max<int64_t>(min_bits, (max_bits + mxd::kHuffThreads - 1) / mxd::kHuffThreads), 32);
+    const int32_t sub_bits = (int32_t)up(knob > 0 ? knob : kHuffMinBits, 32);
+    h.sub_bits = sub_bits;
     c.seg_first[i - first] = (int32_t)c.hsegs.size();
     c.seg_count[i - first] = es.nseg;
     const int32_t img_index = (int32_t)c.himgs.size();
-    const size_t first_job = c.hjobs.size();
-    c.hjobs.push_back(mxd::HuffJobDev{(int32_t)c.hsegs.size(), 0, 0, 0, 0, {0, 0, 0}});  // the image's first job
-    int32_t job_sub = 0;
+    const int32_t seg_base = (int32_t)c.hsegs.size();
+    std::vector<int64_t> sub_first;  // per segment: its first subsequence (image-wide numbering)
+    int64_t nsub_img = 0;
     for (int sgi = 0; sgi < es.nseg; sgi++) {
       const int64_t raw = es.seg_end[sgi] - es.seg_begin[sgi];
       mxd::HuffSegDev sd{};
       sd.word = c.words_bytes / 4;
-      sd.bits = 0;  // set once unstuffed
+      sd.bits = (int32_t)(8 * es.seg_bytes[sgi]);
       sd.img = img_index;
       sd.mcu0 = (int64_t)sgi * h.rst_mcus;
       sd.mcus = (int32_t)std::min<int64_t>(h.rst_mcus, es.mcus - sd.mcu0);
-      sd.sub_bits = sub_bits;
+      sd.nsub = (int32_t)std::max<int64_t>(1, (sd.bits + sub_bits - 1) / sub_bits);
       c.raw.push_back({es.data + es.seg_begin[sgi], es.data + es.seg_end[sgi], c.words_bytes});
       // zero padding past the data: a partial last word's tail and >= 1 zero word,
       // which jpeghuff.hip's LDS reader reads for every word past the segment
       c.words_bytes += up(raw + 4, 16);
-      // jobs: consecutive segments of one image, <= kHuffThreads subsequences
-      // (planned from the raw size; unstuffing only shortens a segment)
-      const int32_t nsub = (int32_t)std::max<int64_t>(1, (8 * raw + sub_bits - 1) / sub_bits);
-      const int64_t seg16 = up(raw + 4, 16) / 16;  // its staged words, 16-byte units
-      if (c.hjobs.back().nseg > 0 &&
-          (job_sub + nsub > mxd::kHuffThreads ||
-           mxd::jpeg_huff_lds_bytes(es.ntables, c.hjobs.back().nseg + 1, 4 * (c.hjobs.back().words16 + seg16)) >
-               mxd::jpeg_huff_lds_budget())) {
-        c.hjobs.push_back(mxd::HuffJobDev{(int32_t)c.hsegs.size(), 0, 0, 0, 0, {0, 0, 0}});
-        job_sub = 0;
-      }
-      c.hjobs.back().nseg++;
-      c.hjobs.back().nsub += nsub;
-      c.hjobs.back().words16 += (int32_t)seg16;
-      job_sub += nsub;
-      c.huff_threads = std::max(c.huff_threads, c.hjobs.back().nsub);
+      sub_first.push_back(nsub_img);
+      nsub_img += sd.nsub;
       c.hsegs.push_back(sd);
+    }
+    sub_first.push_back(nsub_img);
+    // jobs: runs of at most kHuffThreads - kHuffWarm own subsequences, evenly
+    // sized; a cut inside a segment gives the next job a warm-up of up to
+    // kHuffWarm subsequences before its own (jpeghuff.h); cuts within a few
+    // subsequences of a segment start move there (restart markers: no warm-up)
+    const int64_t cap = mxd::kHuffThreads - mxd::kHuffWarm;
+    const int64_t njob = (nsub_img + cap - 1) / cap;
+    std::vector<int64_t> cuts{0};
+    for (int64_t q = 1; q < njob; q++) {
+      int64_t cut = q * nsub_img / njob;
+      const int64_t sgi = std::upper_bound(sub_first.begin(), sub_first.end(), cut) - sub_first.begin() - 1;
+      if (cut - sub_first[sgi] <= 32 && sub_first[sgi] > cuts.back()) cut = sub_first[sgi];
+      cuts.push_back(cut);
+    }
+    cuts.push_back(nsub_img);
+    for (size_t q = 0; q + 1 < cuts.size(); q++) {
+      const int64_t a0 = cuts[q], b0 = cuts[q + 1];
+      const int64_t sa = std::upper_bound(sub_first.begin(), sub_first.end(), a0) - sub_first.begin() - 1;
+      const int64_t ja = a0 - sub_first[sa];  // the first own subsequence's index in its segment
+      const int64_t warm = std::min<int64_t>(mxd::kHuffWarm, ja);
+      const int64_t sl = std::upper_bound(sub_first.begin(), sub_first.end(), b0 - 1) - sub_first.begin() - 1;
+      const int64_t jl = b0 - 1 - sub_first[sl];  // the last subsequence's index in its segment
+      const mxd::HuffSegDev& s0 = c.hsegs[seg_base + sa];
+      const mxd::HuffSegDev& s1 = c.hsegs[seg_base + sl];
+      mxd::HuffJobDev jb{};
+      jb.seg0 = (int32_t)(seg_base + sa);
+      jb.nseg = (int32_t)(sl - sa + 1);
+      jb.sub0 = (int32_t)(ja - warm);
+      jb.nsub = (int32_t)(b0 - a0 + warm);
+      jb.warm = (int32_t)warm;
+      jb.pred = ja > 0 ? 1 : 0;
+      jb.word0 = s0.word + (((int64_t)jb.sub0 * sub_bits / 32) & ~(int64_t)3);
+      // words staged: to the last segment's staged end when the job reaches
+      // it, else 4 words past its last subsequence (a step reads <= 2 past)
+      const int64_t seg_end = s1.word + up(es.seg_end[sl] - es.seg_begin[sl] + 4, 16) / 4;
+      const int64_t end = jl == s1.nsub - 1 ? seg_end : std::min(seg_end, s1.word + (jl + 1) * sub_bits / 32 + 4);
+      jb.words16 = (int32_t)((end - jb.word0 + 3) / 4);
+      const int64_t with = mxd::jpeg_huff_lds_bytes(es.ntables, jb.nseg, 4 * (int64_t)jb.words16);
+      jb.lds = with <= mxd::jpeg_huff_lds_budget() && g_tune[MXD_TUNE_HUFF_GLOBAL].load() == 0 ? 1 : 0;
+      c.huff_lds = std::max(c.huff_lds, jb.lds ? with : mxd::jpeg_huff_lds_bytes(es.ntables, jb.nseg, 0));
+      c.huff_threads = std::max(c.huff_threads, jb.nsub);
+      c.hjobs.push_back(jb);
     }
     c.himgs.push_back(h);
     coef_rel += up(info.coef_count * 2, 256);
-    // per job: its words from LDS when they fit (MXD_TUNE_HUFF_GLOBAL: never);
-    // the launch's dynamic LDS is the largest job's
-    for (size_t q = first_job; q < c.hjobs.size(); q++) {
-      const int64_t with = mxd::jpeg_huff_lds_bytes(es.ntables, c.hjobs[q].nseg, 4 * (int64_t)c.hjobs[q].words16);
-      c.hjobs[q].lds = with <= mxd::jpeg_huff_lds_budget() && g_tune[MXD_TUNE_HUFF_GLOBAL].load() == 0 ? 1 : 0;
-      c.huff_lds = std::max(c.huff_lds, c.hjobs[q].lds ? with : mxd::jpeg_huff_lds_bytes(es.ntables, c.hjobs[q].nseg, 0));
-    }
   }
   for (int32_t i = first; i < end; i++) {
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
@@ -511,7 +534,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
   c.imgs_off = up(c.planes_off + (int64_t)(c.planes.size() * sizeof(mxd::JpegPlaneDev)), 256);
   c.q_off = up(c.imgs_off + (int64_t)(c.imgs.size() * sizeof(mxd::JpegImgDev)), 256);
   c.end = c.q_off + (int64_t)(c.qtabs.size() * sizeof(uint16_t));
-  c.coef_off = up(c.end, 256);
+  c.pub_off = up(c.end, 256);
+  c.coef_off = up(c.pub_off + (int64_t)(c.hjobs.size() * sizeof(mxd::HuffPubDev)) + (int64_t)sizeof(mxd::HuffCtlDev),
+                  256);
   c.dev_end = c.coef_off + coef_rel;
   for (mxd::HuffImgDev& h : c.himgs) h.coef += c.coef_off / 2;
   for (size_t k = 0, pi = 0; k < (size_t)(end - first); k++) {
@@ -599,7 +624,12 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (!dst_device && im.dst_stride < s.out_row)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
   }
-  // Chunks of about kChunk staged bytes (at least one image each).
+  // Chunks of about kChunk staged bytes (at least one image each).  A JPEG
+  // whose entropy decode runs on the device stages only its compressed
+  // segments, and counts an eighth of its coefficient bytes (device memory):
+  // ~300 ImageNet-size files a chunk, so a 128-file batch is one entropy
+  // launch over the whole GPU rather than three of ~40 files on ~80 CUs
+  // (round 5).
   constexpr int64_t kChunk = 24 << 20;
   // (and at most 65535 images: the JPEG colour kernel puts one image per grid row)
   constexpr int32_t kChunkImages = 65535;
@@ -607,8 +637,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   for (int32_t i = 0; i < n;) {
     int32_t j = i;
     int64_t bytes = 0;
-    while (j < n && j - i < kChunkImages && (j == i || bytes + st[j].in_size <= kChunk)) {
-      bytes += st[j].in_size;
+    auto size = [&](int32_t q) { return st[q].pending ? st[q].in_size / 8 : st[q].in_size; };
+    while (j < n && j - i < kChunkImages && (j == i || bytes + size(j) <= kChunk)) {
+      bytes += size(j);
       j++;
     }
     chunks.push_back({i, j});
@@ -633,6 +664,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     Slot& sl = ctx.slot[k & 1];
     MXD_HIP(hipEventSynchronize(sl.done));
     pending[k & 1] = -1;
+    if (sl.huff_err && *sl.huff_err) {
+      *sl.huff_err = 0;
+      return fail(MXD_ERR_DEVICE, "jpeg entropy decode: a job never received its predecessor's state");
+    }
     if (dst_device) return MXD_OK;  // the kernel wrote the destinations
     int64_t bytes = 0;
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++) bytes += st[i].out_row * images[i].crop_h;
@@ -776,16 +811,24 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (in_staged > 0 && !pin_in_dev)
       MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
     if (jpeg) {
-      if (!jc.hjobs.empty() &&
-          mxd::launch_jpeg_huff(reinterpret_cast<const uint32_t*>(sl.dev_in + jc.words_off),
-                                reinterpret_cast<const mxd::HuffDev*>(sl.dev_in + jc.htabs_off),
-                                reinterpret_cast<const mxd::HuffImgDev*>(sl.dev_in + jc.himgs_off),
-                                reinterpret_cast<const mxd::HuffSegDev*>(sl.dev_in + jc.hsegs_off),
-                                reinterpret_cast<const mxd::HuffJobDev*>(sl.dev_in + jc.hjobs_off),
-                                (int32_t)jc.hjobs.size(), jc.huff_threads,
-                                jc.huff_lds,
-                                reinterpret_cast<int16_t*>(sl.dev_in), sl.stream))
-        return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
+      if (!jc.hjobs.empty()) {
+        // the jobs' publication records and the ticket start zero (the
+        // decode zeroes every block it starts, and the blocks insufficient
+        // data leaves undecoded)
+        MXD_HIP(hipMemsetAsync(sl.dev_in + jc.pub_off, 0, (size_t)(jc.coef_off - jc.pub_off), sl.stream));
+        auto* pub = reinterpret_cast<mxd::HuffPubDev*>(sl.dev_in + jc.pub_off);
+        auto* ctl = reinterpret_cast<mxd::HuffCtlDev*>(pub + jc.hjobs.size());
+        if (mxd::launch_jpeg_huff(reinterpret_cast<const uint32_t*>(sl.dev_in + jc.words_off),
+                                  reinterpret_cast<const mxd::HuffDev*>(sl.dev_in + jc.htabs_off),
+                                  reinterpret_cast<const mxd::HuffImgDev*>(sl.dev_in + jc.himgs_off),
+                                  reinterpret_cast<const mxd::HuffSegDev*>(sl.dev_in + jc.hsegs_off),
+                                  reinterpret_cast<const mxd::HuffJobDev*>(sl.dev_in + jc.hjobs_off),
+                                  (int32_t)jc.hjobs.size(), jc.huff_threads, jc.huff_lds, pub, ctl,
+                                  reinterpret_cast<int16_t*>(sl.dev_in), sl.stream))
+          return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
+        if (!sl.huff_err) MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.huff_err), 64, hipHostMallocDefault));
+        MXD_HIP(hipMemcpyAsync(sl.huff_err, &ctl->error, sizeof(int32_t), hipMemcpyDeviceToHost, sl.stream));
+      }
       mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
                             reinterpret_cast<const mxd::JpegPlaneDev*>(sl.dev_in + jc.planes_off),

@@ -701,6 +701,7 @@ struct Decoder {
   bool pending = false;
   int scans = 0;
   std::vector<int64_t> seg_begin, seg_end;
+  std::vector<int64_t> seg_bytes;  // unstuffed bytes of each segment (what unstuff() writes)
   int scan_ns = 0;
   int scan_comp[4] = {0, 0, 0, 0};  // frame index of each scan component (SOS order)
   int64_t scan_mcus = 0;
@@ -926,6 +927,7 @@ struct Decoder {
     const int64_t nseg = restart_interval ? (scan_mcus + restart_interval - 1) / restart_interval : 1;
     size_t p = pos, b = pos;
     int next_rst = 0;
+    int64_t dropped = 0;  // bytes unstuff() drops: the 0x00 of 0xFF 0x00, fill 0xFF bytes
     for (;;) {
       const uint8_t* f = static_cast<const uint8_t*>(std::memchr(data + p, 0xFF, size - p));
       if (!f || (size_t)(f - data) + 1 >= size) throw NotDevice{};  // no marker after the data: truncated
@@ -933,10 +935,12 @@ struct Decoder {
       const uint8_t m = data[p + 1];
       if (m == 0x00) {
         p += 2;
+        dropped++;
         continue;
       }
       if (m == 0xFF) {
         p += 1;
+        dropped++;
         continue;
       }
       // the device decoder keeps a segment's bit count and word offsets in
@@ -944,6 +948,8 @@ struct Decoder {
       if (p - b >= ((size_t)1 << 28)) throw NotDevice{};
       seg_begin.push_back((int64_t)b);
       seg_end.push_back((int64_t)p);
+      seg_bytes.push_back((int64_t)(p - b) - dropped);
+      dropped = 0;
       if (m >= 0xD0 && m <= 0xD7) {
         if (!restart_interval || m != 0xD0 + next_rst || (int64_t)seg_begin.size() >= nseg) throw NotDevice{};
         next_rst = (next_rst + 1) & 7;
@@ -1513,6 +1519,7 @@ EntropyScan entropy_scan(const Coefs* c) {
   e.nseg = (int)d.seg_begin.size();
   e.seg_begin = d.seg_begin.data();
   e.seg_end = d.seg_end.data();
+  e.seg_bytes = d.seg_bytes.data();
   e.data = d.data;
   e.mcus = d.scan_mcus;
   e.restart_interval = d.restart_interval;
@@ -1546,7 +1553,6 @@ EntropyScan entropy_scan(const Coefs* c) {
 void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   const Huff& h = cls ? c->d.ac[table_id] : c->d.dc[table_id];
   HuffDev& o = *static_cast<HuffDev*>(huff_dev);
-  static_assert(kHuffFacLook == kLook, "the combined AC table is the host decoder's");
   // per-thread cache of built tables (a batch's files mostly share theirs),
   // keyed by the class and the derived code: maxcode, valoffset and the symbol values
   struct Entry {
@@ -1568,24 +1574,50 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
       return;
     }
   }
-  // symbol table over kHuffLook bits: the host table's entry for codes of up
-  // to kLook bits, else the shortest longer length l whose l-bit prefix of
-  // the index is <= maxcode[l] (canonical codes)
-  static_assert(kHuffLook >= kLook, "the device table extends the host one");
-  for (int i = 0; i < (1 << kHuffLook); i++) {
-    uint16_t e = h.look[i >> (kHuffLook - kLook)];
-    for (int l = kLook + 1; l <= kHuffLook && !e; l++) {
-      const int32_t code = i >> (kHuffLook - l);
-      if (code <= h.maxcode[l]) e = (uint16_t)((l << 8) | h.vals[(code + h.valoffset[l]) & 0xff]);
+  std::memset(&o, 0, sizeof o);
+  // The code starting a 16-bit pattern: its length and symbol, jdhuff.c
+  // jpeg_huff_decode's search (the shortest l whose l-bit prefix is <=
+  // maxcode[l]; canonical codes); none (corrupt data): 16 bits, symbol 0.
+  auto code_at = [&](uint32_t p16, int* len, int* sym) {
+    for (int l = 1; l <= 16; l++) {
+      const int32_t code = (int32_t)(p16 >> (16 - l));
+      if (code <= h.maxcode[l]) {
+        *len = l;
+        *sym = h.vals[(code + h.valoffset[l]) & 0xff];
+        return;
+      }
     }
-    o.look[i] = e;
-    o.step[i] = e ? huff_step_entry(cls, e >> 8, e & 0xff) : 0;
+    *len = 16;
+    *sym = 0;
+  };
+  // step table over kHuffLook bits (0: a longer code or none)
+  int first_long = 1 << kHuffLook;  // the first kHuffLook-bit prefix without a code that fits it
+  for (int i = 0; i < (1 << kHuffLook); i++) {
+    int len, sym;
+    code_at((uint32_t)i << (16 - kHuffLook), &len, &sym);
+    const bool fits = len <= kHuffLook && (int32_t)(i >> (kHuffLook - len)) <= h.maxcode[len];
+    o.step[i] = fits ? huff_step_entry(cls, len, sym) : 0;
+    if (!fits && first_long == (1 << kHuffLook)) first_long = i;
+  }
+  // longer codes (canonical: every prefix from first_long up to the top has
+  // none that fits) over 16 bits, when they take <= kHuffLong patterns
+  const int32_t base = first_long << (16 - kHuffLook);
+  o.long_base = 65536;
+  if (65536 - base <= kHuffLong) {
+    bool ok = true;
+    for (int i = first_long; i < (1 << kHuffLook); i++) ok = ok && o.step[i] == 0;
+    if (ok) {
+      o.long_base = base;
+      for (int32_t v = base; v < 65536; v++) {
+        int len, sym;
+        code_at((uint32_t)v, &len, &sym);
+        o.step_long[v - base] = huff_step_entry(cls, len, sym);
+      }
+    }
   }
   std::memcpy(o.maxcode, h.maxcode, sizeof o.maxcode);
   std::memcpy(o.valoffset, h.valoffset, sizeof o.valoffset);
   std::memcpy(o.vals, h.vals, sizeof o.vals);
-  for (int i = 0; i < (1 << kLook); i++)
-    o.fac[i] = (uint32_t)(uint16_t)h.fac[i].val | ((uint32_t)h.fac[i].run << 16) | ((uint32_t)h.fac[i].len << 24);
   Entry& e = cache[next];
   next = (next + 1) % kEntries;
   std::memcpy(e.maxcode, h.maxcode, sizeof e.maxcode);

@@ -68,6 +68,7 @@ struct EntropyScan {
   int nseg;                      // entropy-coded segments (restart intervals)
   const int64_t* seg_begin;      // raw bytes of segment s: [seg_begin[s], seg_end[s]) of `data`
   const int64_t* seg_end;
+  const int64_t* seg_bytes;      // its unstuffed bytes (what unstuff writes)
   const uint8_t* data;           // the file
   int64_t mcus;                  // MCUs of the scan
   int restart_interval;          // MCUs per segment (0: one segment)

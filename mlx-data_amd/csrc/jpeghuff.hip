@@ -1,221 +1,85 @@
 // jpeghuff.hip -- device-side Huffman (entropy) decode of sequential JPEG
 // scans: the half of load_image's decode (ImageJPEG.cpp:99-146, libjpeg's
 // jdhuff.c) that round 3 still ran on the host (VERDICT r3 missing 1).  The
-// algorithm and data layout are described in jpeghuff.h; the arithmetic is
-// jpeg.cpp's host block decoder (Bits::block_seq), symbol by symbol, so the
-// coefficients are the host decoder's bit for bit (tests/test_gpu_jpeg_entropy.py).
+// algorithm, the jobs and the data layout are described in jpeghuff.h; the
+// arithmetic is jpeg.cpp's host block decoder (Bits::block_seq), symbol by
+// symbol, so the coefficients are the host decoder's bit for bit
+// (tests/test_gpu_jpeg_entropy.py).
 //
-// One workgroup per job (segments of one image, <= kHuffThreads
-// subsequences), one thread per subsequence:
-//   0. the image's Huffman tables into LDS; its coefficient blocks zeroed;
+// One workgroup per job, one thread per subsequence:
+//   0. the job's ticket (its index, in the order workgroups start); the
+//      image's Huffman tables, the job's segment records and words into LDS;
 //   1. synchronisation rounds: every subsequence whose start state changed
 //      decodes to its end; each hands its exit state to the next one of its
 //      segment; repeat until no state changes;
-//   2. block counts prefix-summed per segment -> each subsequence's first block;
-//   3. write pass: decode again, storing AC coefficients and DC differences;
-//   4. DC: per-component sums of the differences prefix-summed per segment,
+//   2. a job that continues a segment waits for the previous job's exit
+//      state; if its own first subsequence started elsewhere, the rounds run
+//      again from the true state;
+//   3. block counts prefix-summed per segment -> each subsequence's first
+//      block; the job's exit state and block index published;
+//   4. write pass: decode again, storing AC coefficients and DC differences;
+//   5. DC: per-component sums of the differences prefix-summed per segment
+//      (the continued segment's from the previous job's published sums),
 //      then each subsequence turns its blocks' differences into values.
+// (Round 4's kernel, one workgroup per image, and its tuning variants are
+// measured in profiles/r04/ and described in DESIGN.md section 8.)
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 
 #include "jpeghuff.h"
 
 namespace mxd {
 namespace {
 
-
-// Diagnostic builds only (-DMXD_HUFF_STATS=1; never in the product library):
-// per job, the synchronisation rounds and the symbols decoded in them and in
-// the write pass, and the durations of the phases (s_memrealtime ticks, 10 ns:
-// staging, synchronisation, write pass, DC), read back with
-// mxd_debug_huff_stats (kStatInts per job).
-#ifndef MXD_HUFF_STATS
-#define MXD_HUFF_STATS 0
-#endif
-// One decode path for DC and AC symbols (default; tuning builds
-// -DMXD_HUFF_UNIFIED=0 keep separate DC / fast-AC / general paths, whose
-// divergence cost 28 % more kernel time: 1.48 vs 1.15 ms per C4 batch of
-// 128, profiles/r04/r04h_*).
-#ifndef MXD_HUFF_UNIFIED
-#define MXD_HUFF_UNIFIED 1
-#endif
-// The symbol step without per-kind branches (default; tuning builds
-// -DMXD_HUFF_LEAN=0 keep the if / else chain of the unified step): code and
-// value bits consumed by one shift, the next coefficient index and block
-// selected arithmetically, one word refilled per step.
-#ifndef MXD_HUFF_LEAN
-#define MXD_HUFF_LEAN 1
-#endif
-// Branch-free refill in the lean step and the synchronisation loop's exit on
-// the subsequence end alone (default; tuning builds -DMXD_HUFF_LEAN2=0).
-#ifndef MXD_HUFF_LEAN2
-#define MXD_HUFF_LEAN2 1
-#endif
-// The LDS reader loads each word one refill ahead (default; tuning builds
-// -DMXD_HUFF_PREFETCH=0 load it when needed, on the symbol loop's dependency
-// chain: kernel 0.961 vs 1.094 ms per batch-bench call, profiles/r04/r04x_*).
-#ifndef MXD_HUFF_PREFETCH
-#define MXD_HUFF_PREFETCH 1
-#endif
-// The lean step's next coefficient index by one select and every symbol's
-// store unconditional (tuning builds -DMXD_HUFF_LEAN3=1).
-#ifndef MXD_HUFF_LEAN3
-#define MXD_HUFF_LEAN3 0
-#endif
-// The class-specific step table (HuffDev::step; default): one lookup gives
-// the bits consumed, the index advance and the value bits, and implies
-// LEAN3's write-pass form (every symbol stores; tuning builds
-// -DMXD_HUFF_LEAN4=0 -DMXD_HUFF_LEAN3=0 restore the earlier step: kernel
-// 0.761 vs 0.692 (LEAN3) vs 0.634 ms (LEAN4) per batch-bench call,
-// profiles/r04/r04ag_*).
-#ifndef MXD_HUFF_LEAN4
-#define MXD_HUFF_LEAN4 1
-#endif
-// The synchronisation loop runs MXD_HUFF_UNROLL steps per check while the
-// subsequence's end is further than UNROLL - 1 steps (2, default, or 4; 1
-// checks every step: kernel 0.633 (1) vs 0.564 ms (2) per batch-bench call,
-// profiles/r04/r04ah_*); the write pass likewise runs MXD_HUFF_WUNROLL.
-// Byte-swapping the words once while they are staged into LDS instead of at
-// every refill measured nothing (0.632 ms) and is not kept.
-#ifndef MXD_HUFF_UNROLL
-#define MXD_HUFF_UNROLL 2
-#endif
-#ifndef MXD_HUFF_WUNROLL
-#define MXD_HUFF_WUNROLL 1
-#endif
-// The LDS reader takes words past its segment from the segment's zero
-// padding (default; tuning builds -DMXD_HUFF_ZPAD=0 select zero instead:
-// 0.568 vs 0.535 ms, profiles/r04/r04aj_*).
-#ifndef MXD_HUFF_ZPAD
-#define MXD_HUFF_ZPAD 1
-#endif
-#if !(MXD_HUFF_UNIFIED && MXD_HUFF_LEAN)
-// the earlier steps keep the earlier write-pass form
-#undef MXD_HUFF_LEAN3
-#define MXD_HUFF_LEAN3 0
-#undef MXD_HUFF_LEAN4
-#define MXD_HUFF_LEAN4 0
-#elif MXD_HUFF_LEAN4
-#undef MXD_HUFF_LEAN3
-#define MXD_HUFF_LEAN3 1
-#endif
-
-#if MXD_HUFF_STATS
-constexpr int kStatJobs = 1 << 16;
-constexpr int kStatInts = 16;
-__device__ int g_huff_stats[kStatJobs * kStatInts];
-__device__ __forceinline__ uint64_t stat_clock() { return __builtin_amdgcn_s_memrealtime(); }
-__device__ __forceinline__ uint64_t stat_cycles() { return __builtin_amdgcn_s_memtime(); }
-#endif
-
 // Bit readers over one segment's unstuffed bytes (32-bit words, big-endian
 // byte order); words past the segment read as zeros (libjpeg's zeros past
-// the data).  After refill() at least 33 bits are buffered.
+// the data).  After a refill at least 33 bits are buffered.
 //
-// LdsReader: the job's words staged in LDS.
+// LdsReader: the job's words staged in LDS.  Every segment is staged with
+// >= 4 zero bytes past its data, rounded up to 16 (hostpath.cpp), so a word
+// past the segment reads as w[nw] (zero) without a separate select; words
+// are loaded one refill ahead (off the symbol loop's dependency chain).
 struct LdsReader {
   const uint32_t* w;
   int32_t nw;
   uint64_t buf;
   int32_t cnt, wi;
-#if MXD_HUFF_PREFETCH
-  uint32_t nxt;  // w[wi] (clamped into the segment), loaded one refill ahead
-#endif
+  uint32_t nxt;
 
-  // base: the job's words in LDS; w0 / nw: the segment's first word and words
-  __device__ __forceinline__ void init(const void* base, int32_t w0, int32_t nwords) {
+  // base: the job's words in LDS; w0 / nw: the segment's first word (relative
+  // to base, negative for a segment the job starts inside) and its words,
+  // `lim`: the last word staged for it
+  __device__ __forceinline__ void init(const void* base, int32_t w0, int32_t nwords, int32_t lim) {
     w = static_cast<const uint32_t*>(base) + w0;
-    nw = nwords;
+    nw = min(nwords, lim);
   }
-
-#if MXD_HUFF_PREFETCH
-  static __device__ __forceinline__ uint32_t order(uint32_t x) { return __builtin_bswap32(x); }
-#if MXD_HUFF_ZPAD
-  // w[nw] is a zero word: every segment is staged with >= 4 zero bytes past
-  // its data, rounded up to 16 (hostpath.cpp), so words past the segment
-  // read as w[nw] without a separate zero select
   __device__ __forceinline__ uint32_t word(int32_t i) const { return w[min(i, nw)]; }
-  __device__ __forceinline__ bool inside() const { return true; }
-#else
-  __device__ __forceinline__ uint32_t word(int32_t i) const { return w[i < nw ? i : max(nw - 1, 0)]; }
-  __device__ __forceinline__ bool inside() const { return wi < nw; }
-#endif
-  // one word (the caller knows cnt <= 32)
-  __device__ __forceinline__ void refill1() {
-    const uint32_t x = inside() ? order(nxt) : 0u;
-    buf |= (uint64_t)x << (32 - cnt);
-    cnt += 32;
-    wi++;
-    nxt = word(wi);
-  }
-  // refill1 when cnt <= 32, without a branch (the word load is issued either way)
+  // one word when cnt <= 32, without a branch (the next word's load is issued either way)
   __device__ __forceinline__ void refill_if() {
     const bool need = cnt <= 32;
-    const uint32_t x = need && inside() ? order(nxt) : 0u;
+    const uint32_t x = need ? __builtin_bswap32(nxt) : 0u;
     buf |= (uint64_t)x << (need ? 32 - cnt : 0);
     cnt += need ? 32 : 0;
     wi += need ? 1 : 0;
     nxt = word(wi);
   }
-  __device__ __forceinline__ void refill() {
-    while (cnt <= 32) {
-      const uint32_t x = inside() ? order(nxt) : 0u;
-      buf |= (uint64_t)x << (32 - cnt);
-      cnt += 32;
-      wi++;
-      nxt = word(wi);  // for the next refill: its latency overlaps this step's decode
-    }
-  }
   __device__ __forceinline__ void seek(int32_t bit) {
     wi = bit >> 5;
+    buf = (uint64_t)__builtin_bswap32(word(wi)) << 32 | __builtin_bswap32(word(wi + 1));
+    wi += 2;
     nxt = word(wi);
-    buf = 0;
-    cnt = 0;
-    refill();
     const int s = bit & 31;
     buf <<= s;
-    cnt -= s;
+    cnt = 64 - s;
   }
-#else
-  __device__ __forceinline__ void refill1() {
-    const uint32_t x = wi < nw ? __builtin_bswap32(w[wi]) : 0u;
-    buf |= (uint64_t)x << (32 - cnt);
-    cnt += 32;
-    wi++;
-  }
-  __device__ __forceinline__ void refill_if() {
-    if (cnt <= 32) refill1();
-  }
-  __device__ __forceinline__ void refill() {
-    while (cnt <= 32) {
-      const uint32_t x = wi < nw ? __builtin_bswap32(w[wi]) : 0u;
-      buf |= (uint64_t)x << (32 - cnt);
-      cnt += 32;
-      wi++;
-    }
-  }
-  __device__ __forceinline__ void seek(int32_t bit) {
-    wi = bit >> 5;
-    buf = 0;
-    cnt = 0;
-    refill();
-    const int s = bit & 31;
-    buf <<= s;
-    cnt -= s;
-  }
-#endif
   __device__ __forceinline__ int32_t pos() const { return wi * 32 - cnt; }
-  __device__ __forceinline__ uint32_t take(int n) {  // n <= 16 bits (n = 0: 0)
-    const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
-    buf <<= n;
-    cnt -= n;
-    return v;
-  }
 };
 
-// GlobalReader: the job's words in device memory (jobs whose words do not
-// fit LDS), read in 16-byte chunks two chunks ahead of the one being
-// consumed, so a chunk's load latency hides behind ~256 bits of decoding
-// instead of stalling every word.  Chunks past the segment are not loaded.
+// GlobalReader: the job's words in device memory (MXD_TUNE_HUFF_GLOBAL), read
+// in 16-byte chunks two chunks ahead of the one being consumed, so a chunk's
+// load latency hides behind ~256 bits of decoding.  Chunks past the segment
+// are not loaded.
 struct GlobalReader {
   const uint4* chunks;  // the job's words (16-byte aligned)
   int32_t w0, nw;       // the segment's first word (relative to the job's) and its words
@@ -225,20 +89,18 @@ struct GlobalReader {
   int32_t ca;           // chunk held in A; B, C: the next two
   uint4 A, B, C;
 
-  // base: the job's words in device memory
-  __device__ __forceinline__ void init(const void* base, int32_t w0_, int32_t nwords) {
+  __device__ __forceinline__ void init(const void* base, int32_t w0_, int32_t nwords, int32_t) {
     chunks = static_cast<const uint4*>(base);
     w0 = w0_;
     nw = nwords;
     last_chunk = (w0_ + nwords - 1) >> 2;
   }
-
   __device__ __forceinline__ uint4 fetch(int32_t ch) const {
     return ch <= last_chunk ? chunks[ch] : uint4{0u, 0u, 0u, 0u};
   }
-  __device__ __forceinline__ void refill1() {
+  __device__ __forceinline__ uint32_t next_word() {
     const int32_t a = w0 + wi;
-    if ((a >> 2) != ca) {
+    if ((a >> 2) != ca) {  // words are consumed in order: the next chunk
       A = B;
       B = C;
       ca++;
@@ -247,28 +109,13 @@ struct GlobalReader {
     const int i = a & 3;
     const uint32_t v = i == 0 ? A.x : i == 1 ? A.y : i == 2 ? A.z : A.w;
     const uint32_t x = wi < nw ? __builtin_bswap32(v) : 0u;
-    buf |= (uint64_t)x << (32 - cnt);
-    cnt += 32;
     wi++;
+    return x;
   }
   __device__ __forceinline__ void refill_if() {
-    if (cnt <= 32) refill1();
-  }
-  __device__ __forceinline__ void refill() {
-    while (cnt <= 32) {
-      const int32_t a = w0 + wi;
-      if ((a >> 2) != ca) {  // words are consumed in order: the next chunk
-        A = B;
-        B = C;
-        ca++;
-        C = fetch(ca + 2);
-      }
-      const int i = a & 3;
-      const uint32_t v = i == 0 ? A.x : i == 1 ? A.y : i == 2 ? A.z : A.w;
-      const uint32_t x = wi < nw ? __builtin_bswap32(v) : 0u;
-      buf |= (uint64_t)x << (32 - cnt);
+    if (cnt <= 32) {
+      buf |= (uint64_t)next_word() << (32 - cnt);
       cnt += 32;
-      wi++;
     }
   }
   __device__ __forceinline__ void seek(int32_t bit) {
@@ -279,82 +126,30 @@ struct GlobalReader {
     C = fetch(ca + 2);
     buf = 0;
     cnt = 0;
-    refill();
+    while (cnt <= 32) {
+      buf |= (uint64_t)next_word() << (32 - cnt);
+      cnt += 32;
+    }
     const int s = bit & 31;
     buf <<= s;
     cnt -= s;
   }
   __device__ __forceinline__ int32_t pos() const { return wi * 32 - cnt; }
-  __device__ __forceinline__ uint32_t take(int n) {
-    const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
-    buf <<= n;
-    cnt -= n;
-    return v;
-  }
 };
 
-// jdhuff.c jpeg_huff_decode on a buffer of >= 16 bits: a code longer than 16
-// bits (corrupt data) consumes 16 bits and decodes as 0.
-template <class Reader>
-__device__ __forceinline__ int huff_symbol(const HuffDev& t, Reader& r) {
-  const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
-  if (e) {
-    r.buf <<= e >> 8;
-    r.cnt -= e >> 8;
-    return e & 0xff;
-  }
-  int l = kHuffLook + 1;
-  int32_t code = (int32_t)(r.buf >> (64 - l));
-  while (code > t.maxcode[l]) {
-    if (++l > 16) {
-      r.buf <<= 16;
-      r.cnt -= 16;
-      return 0;
-    }
-    code = (int32_t)(r.buf >> (64 - l));
-  }
-  r.buf <<= l;
-  r.cnt -= l;
-  return t.vals[(code + t.valoffset[l]) & 0xff];
-}
-
-// A code longer than kHuffLook bits without a loop: its length is the
-// shortest l in kHuffLook+1..16 whose l-bit prefix is <= maxcode[l] (canonical
-// codes; jdhuff.c jpeg_huff_decode's search); none (corrupt data) consumes 16
-// bits and decodes as 0, as huff_symbol does.
-template <class Reader>
-[[maybe_unused]] __device__ __forceinline__ int huff_long(const HuffDev& t, Reader& r) {
-  const uint32_t p16 = (uint32_t)(r.buf >> 48);
-  int len = 17;
-#pragma unroll
-  for (int l = 16; l > kHuffLook; l--)
-    if ((int32_t)(p16 >> (16 - l)) <= t.maxcode[l]) len = l;
-  if (len > 16) {
-    r.buf <<= 16;
-    r.cnt -= 16;
-    return 0;
-  }
-  const int32_t code = (int32_t)(p16 >> (16 - len));
-  r.buf <<= len;
-  r.cnt -= len;
-  return t.vals[(code + t.valoffset[len]) & 0xff];
-}
-
-// huff_long's search without consuming: the code's length (16 for corrupt
-// data, whose symbol is 0) and its symbol.
-[[maybe_unused]] __device__ __forceinline__ void huff_long_peek(const HuffDev& t, uint64_t buf, int& len, int& sym) {
+// The step of a code longer than the tables cover (tables whose long codes
+// need more than kHuffLong patterns, or a corrupt pattern): jdhuff.c
+// jpeg_huff_decode's search -- the shortest l in kHuffLook+1..16 whose l-bit
+// prefix is <= maxcode[l]; none (corrupt data) consumes 16 bits and decodes
+// as symbol 0.
+__device__ __noinline__ int huff_search_step(const HuffDev& t, uint64_t buf, int cls) {
   const uint32_t p16 = (uint32_t)(buf >> 48);
   int l = 17;
 #pragma unroll
   for (int ll = 16; ll > kHuffLook; ll--)
     if ((int32_t)(p16 >> (16 - ll)) <= t.maxcode[ll]) l = ll;
-  if (l > 16) {
-    len = 16;
-    sym = 0;
-  } else {
-    len = l;
-    sym = t.vals[((int32_t)(p16 >> (16 - l)) + t.valoffset[l]) & 0xff];
-  }
+  if (l > 16) return huff_step_entry(cls, 16, 0);
+  return huff_step_entry(cls, l, t.vals[((int32_t)(p16 >> (16 - l)) + t.valoffset[l]) & 0xff]);
 }
 
 __device__ __forceinline__ int extend(uint32_t v, int s) {
@@ -366,13 +161,18 @@ struct SegLds {
   int32_t word;  // first word, relative to the job's first word
   int32_t bits;
   int32_t mcu0, mcus;
+  int32_t lim;   // last word staged for it (relative to the segment's first word)
+  int32_t nsub;  // its subsequences
+  int32_t pad[2];
 };
 
 // Per-job shared state (static part; the tables, segment records and, when
 // they fit, the job's words follow in dynamic LDS: jpeg_huff_lds_bytes).
 struct Shared {
   HuffImgDev img;
-  int32_t seg_sub0[kHuffThreads];  // first subsequence of each segment of the job
+  HuffJobDev job;
+  int32_t ticket;
+  int32_t seg_sub0[kHuffThreads];  // first subsequence (job-local) of each segment of the job
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
   int32_t done[kHuffThreads];      // blocks a subsequence completes (sync pass)
@@ -383,6 +183,8 @@ struct Shared {
   int16_t list[kHuffThreads];      // this round's subsequences to decode (compacted)
   int32_t scan[kHuffThreads / 64];
   int32_t flag[2];
+  int64_t pred_blocks;             // the previous job's published block index
+  int32_t pred_dc[3];
 };
 
 // Block-wide exclusive prefix sum of v (every thread of the workgroup calls it).
@@ -416,187 +218,58 @@ __device__ int block_exclusive_scan(int v, int* totals, int* total_out) {
 // Decoder state machine over one segment: block b of the MCU, next
 // coefficient k (0 = the DC difference), symbols from Reader r.
 struct Dec {
-  const HuffImgDev* im;
   const HuffDev* tab;
   int b, k;
-  // per-block table indices and components in registers instead of LDS
-  // reads per symbol
+  // per-block table indices and components in registers
   uint32_t dpack, apack;  // the DC / AC table of each block of the MCU (bits 3b..3b+2)
   uint32_t cpack;         // component of each block of the MCU (bits 2b..2b+1)
   int bpm;
 
-  __device__ __forceinline__ void init(const HuffImgDev* im_, const HuffDev* tab_) {
-    im = im_;
+  __device__ __forceinline__ void init(const HuffImgDev& im, const HuffDev* tab_) {
     tab = tab_;
     b = k = 0;
-    bpm = im_->bpm;
+    bpm = im.bpm;
     dpack = apack = cpack = 0;
     for (int j = 0; j < bpm; j++) {
-      dpack |= (uint32_t)(im_->blk_dc[j] & 7) << (3 * j);
-      apack |= (uint32_t)(im_->blk_ac[j] & 7) << (3 * j);
-      cpack |= (uint32_t)(im_->blk_comp[j] & 3) << (2 * j);
+      dpack |= (uint32_t)(im.blk_dc[j] & 7) << (3 * j);
+      apack |= (uint32_t)(im.blk_ac[j] & 7) << (3 * j);
+      cpack |= (uint32_t)(im.blk_comp[j] & 3) << (2 * j);
     }
   }
-  // component of the current block
   __device__ __forceinline__ int comp() const { return (cpack >> (2 * b)) & 3; }
 
-  // Decodes one symbol.  Returns true at the end of a block (b, k advanced to
-  // the next block's start).  For the write pass, on_dc(diff) / on_ac(pos,
-  // value) receive the block's values.
-#if MXD_HUFF_UNIFIED && MXD_HUFF_LEAN
-  template <class Reader, class OnDc, class OnAc>
-  __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
-#if MXD_HUFF_LEAN2
+  // Decodes one symbol; returns true at the end of a block (b, k advanced to
+  // the next block's start).  on_sym(dc, position, value) receives every
+  // symbol's store: the DC difference at 0, a coefficient at its index, an
+  // EOB's / ZRL's zero at an index of the block not yet written (so no
+  // branch; a corrupt run past 63 lands on 63, as jpeg_natural_order's extra
+  // entries put it).  One lookup gives the bits a symbol consumes, the index
+  // advance and the value bits; codes longer than kHuffLook bits come from
+  // the second table, read beside the first (no branch), and only tables too
+  // large for it search.
+  template <class Reader, class OnSym>
+  __device__ __forceinline__ bool step(Reader& r, OnSym&& on_sym) {
     r.refill_if();  // >= 33 bits buffered: a step consumes <= 16 + 15
-#else
-    if (r.cnt <= 32) r.refill1();
-#endif
     const bool dc = k == 0;
     const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
-#if MXD_HUFF_LEAN4
-    // one lookup gives the bits to consume, the index advance and the value
-    // bits (HuffDev::step, built for the table's class)
-    int st = t.step[(uint32_t)(r.buf >> (64 - kHuffLook))];
-    if (!st) {
-      int len, sym;
-      huff_long_peek(t, r.buf, len, sym);
-      st = huff_step_entry(dc ? 0 : 1, len, sym);
-    }
+    const uint32_t top16 = (uint32_t)(r.buf >> 48);
+    const int st1 = t.step[top16 >> (16 - kHuffLook)];
+    const int st2 = t.step_long[min(max((int)top16 - t.long_base, 0), kHuffLong - 1)];
+    int st = st1 ? st1 : st2;
+    if (!st) st = huff_search_step(t, r.buf, dc ? 0 : 1);
     const int shift = st & 31, adv = (st >> 5) & 127, sz = st >> 12;
     // value bits: the sz bits after the code, in the buffer's top 32 bits (shift <= 31)
     const uint32_t hi = (uint32_t)(r.buf >> 32);
     const uint32_t raw = sz ? (hi >> (32 - shift)) & ((1u << sz) - 1u) : 0u;
     r.buf <<= shift;
     r.cnt -= shift;
-    const int v = extend(raw, sz);
-    // the index advance: DC 1, a coefficient run + 1 (stored at k + run), ZRL
-    // 16 (its zero at k + 15), EOB 64 (its zero at 63): every position stored
-    // is one of the block's not yet written
     const int knew = k + adv;
-    on_ac(min(knew - 1, 63), v);
-    on_dc(dc, v);
-#else
-    const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
-    int len, sym;
-    if (e) {
-      len = e >> 8;
-      sym = e & 0xff;
-    } else {
-      huff_long_peek(t, r.buf, len, sym);
-    }
-    const int sz = dc ? sym : sym & 15;
-    const int run = dc ? 0 : sym >> 4;
-    const uint32_t raw = sz ? (uint32_t)((r.buf << len) >> (64 - sz)) : 0u;
-    r.buf <<= len + sz;
-    r.cnt -= len + sz;
-    const int v = extend(raw, sz);
-    const int kpos = k + run;  // an AC coefficient's index (sz != 0)
-#if MXD_HUFF_LEAN3
-    // next index: kpos + 1 after the DC (k = run = 0), a coefficient or a ZRL
-    // (run 15: k + 16); 64 after an EOB.  Every symbol stores: the DC at 0, a
-    // coefficient at kpos (a corrupt run past 63 lands on 63), and an EOB / ZRL
-    // its zero at an index of the block not yet written -- so no branch.
-    const int knew = (dc || sz != 0 || run == 15) ? kpos + 1 : 64;
-    on_ac(min(kpos, 63), v);
-    on_dc(dc, v);
-#else
-    // next index: after the DC 1; after a coefficient kpos + 1; ZRL k + 16; EOB 64
-    const int knew = dc ? 1 : sz ? kpos + 1 : run == 15 ? k + 16 : 64;
-    if (dc) on_dc(v);
-    else if (sz) on_ac(kpos, v);
-#endif
-#endif  // MXD_HUFF_LEAN4
+    on_sym(dc, min(knew - 1, 63), raw, sz);
     const bool end = knew >= 64;
     k = end ? 0 : knew;
     b = end ? (b + 1 == bpm ? 0 : b + 1) : b;
     return end;
   }
-#elif MXD_HUFF_UNIFIED
-  // One path for DC and AC symbols: the
-  // block's DC or AC table is selected, one lookup gives the symbol (codes
-  // past the lookahead without a loop), the value bits follow; the lanes of a
-  // wave, whichever symbol kind each decodes, run the same instructions.
-  template <class Reader, class OnDc, class OnAc>
-  __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
-    if (r.cnt < 32) r.refill();
-    const bool dc = k == 0;
-    const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
-    const int e = t.look[(uint32_t)(r.buf >> (64 - kHuffLook))];
-    int sym;
-    if (e) {
-      r.buf <<= e >> 8;
-      r.cnt -= e >> 8;
-      sym = e & 0xff;
-    } else {
-      sym = huff_long(t, r);
-    }
-    const int run = dc ? 0 : sym >> 4, sz = dc ? sym : sym & 15;
-    const int v = extend(r.take(sz), sz);
-    bool end = false;
-    if (dc) {
-      on_dc(v);
-      k = 1;
-    } else if (sz) {
-      k += run;
-      on_ac(k, v);
-      end = ++k >= 64;
-    } else if (run == 15) {
-      k += 16;
-      end = k >= 64;
-    } else {
-      end = true;
-    }
-    if (end) {
-      k = 0;
-      b = b + 1 == bpm ? 0 : b + 1;
-    }
-    return end;
-  }
-#else
-  template <class Reader, class OnDc, class OnAc>
-  __device__ __forceinline__ bool step(Reader& r, OnDc&& on_dc, OnAc&& on_ac) {
-    if (r.cnt < 32) r.refill();
-    if (k == 0) {
-      const int s = huff_symbol(tab[im->blk_dc[b]], r);
-      on_dc(extend(r.take(s), s));
-      k = 1;
-      return false;
-    }
-    const HuffDev& t = tab[im->blk_ac[b]];
-    const uint32_t f = t.fac[(uint32_t)(r.buf >> (64 - kHuffFacLook))];
-    bool end;
-    if (f >> 24) {
-      r.buf <<= f >> 24;
-      r.cnt -= f >> 24;
-      const int run = (f >> 16) & 0xff;
-      if (run == 0xff) {
-        end = true;
-      } else {
-        k += run;
-        on_ac(k, (int)(int16_t)(f & 0xffff));
-        end = ++k >= 64;
-      }
-    } else {
-      const int rs = huff_symbol(t, r);
-      const int run = rs >> 4, sz = rs & 15;
-      if (sz) {
-        k += run;
-        on_ac(k, extend(r.take(sz), sz));
-        end = ++k >= 64;
-      } else if (run == 15) {
-        k += 16;
-        end = k >= 64;
-      } else {
-        end = true;
-      }
-    }
-    if (end) {
-      k = 0;
-      b = b + 1 == im->bpm ? 0 : b + 1;
-    }
-    return end;
-  }
-#endif
 };
 
 // Coefficient offset of block g (decode order) of the image: blocks number
@@ -622,185 +295,204 @@ __host__ __device__ constexpr int64_t lds_words_at(int ntables, int nseg) {
   return (lds_tables_bytes(ntables) + (int64_t)nseg * sizeof(SegLds) + 15) / 16 * 16;
 }
 
-// One thread's subsequence: its segment (in LDS form), its index in the
-// segment and its bit range.
+// One thread's subsequence: its segment (LDS form), its index in the segment
+// and its bit range.
 struct Sub {
   SegLds sg;
   int j;
-  bool active, first, last;
+  bool active, own, first, seg_last, job_last;
   int32_t start, end;
 };
 
-// Subsequence `id` of the job (its segment from sh.sub_seg).
-__device__ __forceinline__ Sub sub_of(const Shared& sh, const SegLds* seg, int sub_bits, int id, int nsub) {
+__device__ __forceinline__ Sub sub_of(const Shared& sh, const SegLds* seg, int id, int nsub) {
   Sub v;
   const int si = sh.sub_seg[id];
   v.sg = seg[si];
-  v.j = id - sh.seg_sub0[si];
-  const int nseg_sub = max(1, (v.sg.bits + sub_bits - 1) / sub_bits);
+  v.j = id - sh.seg_sub0[si] + (si == 0 ? sh.job.sub0 : 0);
   v.active = id < nsub;
+  v.own = id >= sh.job.warm;
   v.first = v.j == 0;
-  v.last = v.j == nseg_sub - 1;
-  v.start = v.j * sub_bits;
-  v.end = v.last ? 0x7fffffff : v.start + sub_bits;
+  v.seg_last = v.j == v.sg.nsub - 1;
+  v.job_last = id == nsub - 1;
+  v.start = v.j * sh.img.sub_bits;
+  v.end = v.seg_last ? 0x7fffffff : v.start + sh.img.sub_bits;
   return v;
 }
 
-// Each round's subsequences packed onto the first threads (default; tuning
-// builds -DMXD_HUFF_COMPACT=0 let every thread decode its own: 0.824 vs
-// 0.750 ms per batch-bench call with the lean step, profiles/r04/r04ad_*).
-#ifndef MXD_HUFF_COMPACT
-#define MXD_HUFF_COMPACT 1
-#endif
-// Tuning builds (-DMXD_HUFF_OVERLAP=<bits>): round 0 decodes that many bits
-// before each subsequence's start from the guessed state.
-#ifndef MXD_HUFF_OVERLAP
-#define MXD_HUFF_OVERLAP 0
-#endif
-
-#if MXD_HUFF_STATS
-struct Stats {
-  int sync_syms = 0, write_syms = 0, rounds = 0;
-  uint64_t t[4] = {0, 0, 0, 0};  // thread 0: staged, synchronised, written, done
-  uint64_t c[2] = {0, 0};        // thread 0: shader clock at the write pass's start and end
-  uint64_t r[2] = {0, 0};        // and the real-time clock there
-  int chg = 0, chg_pos = 0, chg_k = 0;  // start-state changes after round 0: all, same bit position, same (position, k)
-};
-#else
-struct Stats {};
-#endif
-
-// Passes 1-3 over the job with bit reader `rd` (LdsReader or GlobalReader):
-// synchronisation rounds, each subsequence's first block, the write pass.
-// Leaves the subsequence's per-component DC-difference sums in dcsum and the
-// blocks whose DC it decoded in [dc0, dc1).
+// Synchronisation rounds over the job's subsequences (bit reader R), from
+// the start states in sh.in_*; `need`: this thread's subsequence starts
+// changed (the last subsequence of a segment hands its state to nobody: it
+// decodes only in the write pass).  `fixed`: a job-local subsequence whose
+// start is known (the previous job's exit), which its predecessor in the job
+// (the warm-up) no longer hands a state to.
 template <class R>
-__device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, const HuffImgDev& im, const HuffDev* tab,
-                                              const SegLds* seg, int sub_bits, int nsub, const Sub& u,
-                                              int16_t* coef, int (&dcsum)[3], int64_t& dc0, int64_t& dc1,
-                                              Stats& st) {
+__device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, const SegLds* seg, int nsub,
+                            const Sub& u, bool need, int fixed = -1) {
   const int t = threadIdx.x;
   Dec dec;
-  dec.init(&im, tab);
-  const auto nop_dc = [](auto...) {};
-  const auto nop_ac = [](auto...) {};
+  dec.init(sh.img, tab);
   R rd;
-
-  // 1. synchronisation rounds (the last subsequence of a segment hands its
-  // state to nobody: it decodes only in the write pass)
-  bool need = u.active && !u.last;
-  for (int round = 0;; round++) {
-#if MXD_HUFF_STATS
-    st.rounds = round + 1;
-#endif
-    // this round's subsequences: compacted onto the first threads, so a
+  for (;;) {
+    // this round's subsequences, compacted onto the first threads, so a
     // round in which few start states changed runs few waves
-#if MXD_HUFF_COMPACT
     int nact = 0;
     const int slot = block_exclusive_scan(need ? 1 : 0, sh.scan, &nact);
+    if (nact == 0) break;  // uniform
     if (need) sh.list[slot] = (int16_t)t;
     __syncthreads();
-    const bool work = t < nact;
-    const int id = work ? sh.list[t] : t;
-#else
-    const bool work = need;
-    const int id = t;
-#endif
-    if (work) {
-      const Sub v = sub_of(sh, seg, sub_bits, id, nsub);
-      rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5);
-#if MXD_HUFF_OVERLAP > 0
-      // round 0: start the guess MXD_HUFF_OVERLAP bits early, so the decoder
-      // has had that long to fall into step when it reaches the subsequence
-      if (round == 0 && !v.first) {
-        rd.seek(max(0, v.start - MXD_HUFF_OVERLAP));
-        dec.b = 0;
-        dec.k = 0;
-        while (rd.pos() < v.start) dec.step(rd, nop_dc, nop_ac);
-        sh.in_pos[id] = rd.pos();
-        sh.in_b[id] = (int8_t)dec.b;
-        sh.in_k[id] = (int8_t)dec.k;
-      } else
-#endif
-      {
-        rd.seek(sh.in_pos[id]);
-        dec.b = sh.in_b[id];
-        dec.k = sh.in_k[id];
-      }
+    if (t < nact) {
+      const int id = sh.list[t];
+      const Sub v = sub_of(sh, seg, id, nsub);
+      rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5, v.sg.lim);
+      rd.seek(sh.in_pos[id]);
+      dec.b = sh.in_b[id];
+      dec.k = sh.in_k[id];
       int done = 0;
-#if MXD_HUFF_UNROLL > 1
-      // a step consumes <= 31 bits: while the end is further than UNROLL - 1
-      // steps can reach, the next UNROLL steps all start before it
-      while (rd.pos() + 31 * (MXD_HUFF_UNROLL - 1) < v.end) {
-#pragma unroll
-        for (int i = 0; i < MXD_HUFF_UNROLL; i++) done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
-#if MXD_HUFF_STATS
-        st.sync_syms += MXD_HUFF_UNROLL;
-#endif
+      const auto nop = [](bool, int, uint32_t, int) {};
+      // a step consumes <= 31 bits: while the end is further than one step,
+      // two steps both start before it
+      while (rd.pos() + 31 < v.end) {
+        done += dec.step(rd, nop) ? 1 : 0;
+        done += dec.step(rd, nop) ? 1 : 0;
       }
-#endif
-      for (;;) {
-        const int32_t p = rd.pos();
-        // the segment's end can only stop the last subsequence, which the rounds never decode
-#if MXD_HUFF_LEAN2
-        if (p >= v.end) break;
-#else
-        if (p >= v.end || (dec.b == 0 && dec.k == 0 && p > v.sg.bits)) break;
-#endif
-        done += dec.step(rd, nop_dc, nop_ac) ? 1 : 0;
-#if MXD_HUFF_STATS
-        st.sync_syms++;
-#endif
-      }
+      while (rd.pos() < v.end) done += dec.step(rd, nop) ? 1 : 0;
       sh.out_pos[id] = rd.pos();
       sh.out_b[id] = (int8_t)dec.b;
       sh.out_k[id] = (int8_t)dec.k;
       sh.done[id] = done;
     }
-    need = false;
     __syncthreads();
-    if (t == 0) sh.flag[(round + 1) & 1] = 0;
-    if (u.active && !u.first) {
+    // hand the new exits on (to the next subsequence of the same segment): a
+    // predecessor that did not decode this round left the exit it handed on
+    // before, which its successor's start already equals
+    need = false;
+    if (u.active && !u.first && t > 0 && t != fixed) {
       const int32_t p = sh.out_pos[t - 1];
       const int8_t b = sh.out_b[t - 1], k = sh.out_k[t - 1];
       if (p != sh.in_pos[t] || b != sh.in_b[t] || k != sh.in_k[t]) {
-#if MXD_HUFF_STATS
-        if (round > 0) {
-          st.chg++;
-          st.chg_pos += p == sh.in_pos[t] ? 1 : 0;
-          st.chg_k += p == sh.in_pos[t] && k == sh.in_k[t] ? 1 : 0;
-        }
-#endif
         sh.in_pos[t] = p;
         sh.in_b[t] = b;
         sh.in_k[t] = k;
-        need = !u.last;
-        sh.flag[round & 1] = 1;
+        need = !u.seg_last;
       }
     }
-    __syncthreads();
-    if (!sh.flag[round & 1]) break;
   }
-#if MXD_HUFF_STATS
-  st.t[1] = stat_clock();
-#endif
+}
 
-  // 2. first block of each subsequence: the blocks completed before it in its segment
-  const int before = block_exclusive_scan(u.active && !u.last ? sh.done[t] : 0, sh.scan, nullptr);
-  __syncthreads();
-  sh.done[t] = before;  // reuse: exclusive prefix (over the whole job)
-  __syncthreads();
-  const int64_t seg_block0 = (int64_t)u.sg.mcu0 * im.bpm, seg_block1 = ((int64_t)u.sg.mcu0 + u.sg.mcus) * im.bpm;
-  int64_t g = seg_block0 + (u.active ? before - sh.done[t - u.j] : 0);
+// Publication words (jpeghuff.h HuffPubDev): device-scope relaxed atomics,
+// each its own ready flag -- polled with no cache maintenance per poll
+// (an acquire on every poll invalidated the XCD's L2 each time).
+__device__ __forceinline__ void publish(HuffPubDev* p, int i, uint64_t v) {
+  __hip_atomic_store(&p->w[i], v | kHuffValid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-  // 3. write pass
-#if MXD_HUFF_STATS
+constexpr int kSpinLimit = 1 << 22;  // s_sleep(8) each: ~1 s, then the job reports an error
+
+// Waits (one thread) for word i of the previous job's publication; returns it
+// without the valid bit, or 0 (and the launch's error word set) when it
+// never comes.
+__device__ uint64_t wait_pub(const HuffPubDev* p, int i, HuffCtlDev* ctl) {
+  for (int n = 0; n < kSpinLimit; n++) {
+    const uint64_t v = __hip_atomic_load(&p->w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v & kHuffValid) return v & ~kHuffValid;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __hip_atomic_store(&ctl->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return 0;
+}
+
+template <class R>
+__device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, const SegLds* seg, int nsub,
+                           int16_t* coef, HuffPubDev* pub, HuffCtlDev* ctl) {
+  const int t = threadIdx.x;
+  const HuffImgDev& im = sh.img;
+  const HuffJobDev& job = sh.job;
+  const bool act = t < nsub;
+  Sub u = sub_of(sh, seg, min(t, nsub - 1), nsub);
+  u.active = act;  // threads past the job's subsequences take part in the scans only
+
+  // 1. rounds from the guessed starts (segment starts are exact)
+  sync_rounds<R>(wbase, sh, tab, seg, nsub, u, act && !u.seg_last);
+
+  // 2. the previous job's exit: the true start of the first own subsequence
+  if (job.pred) {
+    if (t == 0) {
+      const HuffPubDev* p = pub + sh.ticket - 1;
+      const uint64_t st = wait_pub(p, 0, ctl);
+      sh.pred_blocks = (int64_t)wait_pub(p, 1, ctl);
+      const int32_t pos = (int32_t)(uint32_t)st;
+      const int b = (int)((st >> 32) & 255), k = (int)((st >> 40) & 255);
+      const int w = job.warm;
+      const bool changed = pos != sh.in_pos[w] || b != sh.in_b[w] || k != sh.in_k[w];
+      sh.in_pos[w] = pos;
+      sh.in_b[w] = (int8_t)b;
+      sh.in_k[w] = (int8_t)k;
+      sh.flag[0] = changed ? 1 : 0;
+    }
+    __syncthreads();
+    const bool again = sh.flag[0] != 0;
+    __syncthreads();
+    if (again)  // uniform
+      sync_rounds<R>(wbase, sh, tab, seg, nsub, u, t == job.warm && !u.seg_last, job.warm);
+  }
+
+  // 3. first block of each own subsequence: the blocks its segment's earlier
+  // own subsequences complete, from the segment's start (or, for the segment
+  // the job continues, from the previous job's block index)
+  const bool counts = act && u.own && !u.seg_last;
+  const int my_done = counts ? sh.done[t] : 0;
+  const int before = block_exclusive_scan(my_done, sh.scan, nullptr);
   __syncthreads();
-  st.c[0] = stat_cycles();
-  st.r[0] = stat_clock();
-#endif
-  if (u.active) {
-    rd.init(wbase, u.sg.word, (u.sg.bits + 31) >> 5);
+  sh.done[t] = before;  // reuse: exclusive prefix over the job
+  __syncthreads();
+  // the segment's first own subsequence (job-local)
+  const int seg_first = max(sh.seg_sub0[sh.sub_seg[min(t, nsub - 1)]], (int)job.warm);
+  const bool continued = job.pred && sh.sub_seg[min(t, nsub - 1)] == 0;
+  const int64_t seg_block0 = continued ? sh.pred_blocks : (int64_t)u.sg.mcu0 * im.bpm;
+  const int64_t seg_block1 = ((int64_t)u.sg.mcu0 + u.sg.mcus) * im.bpm;
+  int64_t g = seg_block0 + (act ? before - sh.done[seg_first] : 0);
+  if (act && u.job_last && !u.seg_last) {  // publish the exit for the next job
+    HuffPubDev* p = pub + sh.ticket;
+    publish(p, 1, (uint64_t)(g + my_done));
+    publish(p, 0, (uint64_t)(uint32_t)sh.out_pos[t] | ((uint64_t)(uint8_t)sh.out_b[t] << 32) |
+                      ((uint64_t)(uint8_t)sh.out_k[t] << 40));
+  }
+
+  // 4. write pass (own subsequences)
+  Dec dec;
+  dec.init(im, tab);
+  int dcsum[3] = {0, 0, 0};
+  int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
+  if (act && u.own) {
+    // Zero the coefficient positions this subsequence decodes (the pass
+    // below stores only the symbols' positions): the rest of the block it
+    // starts inside, its whole blocks, and the start of the block it ends
+    // inside -- each position of a block zeroed and then written by the one
+    // thread that decodes it, so neighbours (in this job or the next) never
+    // race.  The segment's last subsequence zeroes to the segment's end, which
+    // leaves the blocks of data that ran out early zero (libjpeg's
+    // insufficient-data rule).
+    {
+      auto zero = [&](int64_t b, int k0, int k1) {
+        int16_t* d = coef + block_addr(im, b);
+        if (k0 == 0 && k1 == 64) {
+          uint4* z = reinterpret_cast<uint4*>(d);
+#pragma unroll
+          for (int q = 0; q < 8; q++) z[q] = uint4{0u, 0u, 0u, 0u};
+        } else {
+          for (int q = k0; q < k1; q++) d[q] = 0;
+        }
+      };
+      const int ke = sh.in_k[t];
+      const int64_t gx = g + my_done;                     // the block it ends inside (non-last)
+      const int kx = u.seg_last ? 0 : sh.out_k[t];
+      if (ke != 0 && g < seg_block1) zero(g, ke, !u.seg_last && gx == g ? kx : 64);
+      const int64_t full_end = u.seg_last ? seg_block1 : min(seg_block1, gx);
+      for (int64_t b = g + (ke != 0 ? 1 : 0); b < full_end; b++) zero(b, 0, 64);
+      if (kx != 0 && gx < seg_block1 && !(ke != 0 && gx == g)) zero(gx, 0, kx);
+    }
+    R rd;
+    rd.init(wbase, u.sg.word, (u.sg.bits + 31) >> 5, u.sg.lim);
     rd.seek(sh.in_pos[t]);
     dec.b = sh.in_b[t];
     dec.k = sh.in_k[t];
@@ -812,38 +504,19 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
       return coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
     };
     int16_t* blk = addr();
-    auto wstep = [&]() {
-#if MXD_HUFF_LEAN3
-      const bool fin = dec.step(
-          rd,
-          [&](bool dc, int diff) {
-            const int c = dec.comp();
-            dcsum[0] += dc && c == 0 ? diff : 0;
-            dcsum[1] += dc && c == 1 ? diff : 0;
-            dcsum[2] += dc && c == 2 ? diff : 0;
-            dc0 = dc && dc0 < 0 ? g : dc0;
-            dc1 = dc ? g + 1 : dc1;
-          },
-          // zig-zag order (jpeg_idct reorders)
-          [&](int kk, int v) { blk[kk] = (int16_t)v; });
-#else
-      const bool fin = dec.step(
-          rd,
-          [&](int diff) {
-            blk[0] = (int16_t)diff;
-            const int c = (dec.cpack >> (2 * dec.b)) & 3;
-            dcsum[0] += c == 0 ? diff : 0;
-            dcsum[1] += c == 1 ? diff : 0;
-            dcsum[2] += c == 2 ? diff : 0;
-            if (dc0 < 0) dc0 = g;
-            dc1 = g + 1;
-          },
-          [&](int kk, int v) {
-            // zig-zag order (jpeg_idct reorders); a corrupt run past 63 lands on 63, as
-            // jpeg_natural_order's extra entries put it
-            blk[min(kk, 63)] = (int16_t)v;
-          });
-#endif
+    for (;;) {
+      const int32_t p = rd.pos();
+      if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
+      const bool fin = dec.step(rd, [&](bool dc, int kk, uint32_t raw, int sz) {
+        const int v = extend(raw, sz);
+        const int c = dec.comp();
+        dcsum[0] += dc && c == 0 ? v : 0;
+        dcsum[1] += dc && c == 1 ? v : 0;
+        dcsum[2] += dc && c == 2 ? v : 0;
+        dc0 = dc && dc0 < 0 ? g : dc0;
+        dc1 = dc ? g + 1 : dc1;
+        blk[kk] = (int16_t)v;  // zig-zag order (jpeg_idct reorders)
+      });
       if (fin) {
         g++;
         cj++;
@@ -855,24 +528,41 @@ __device__ __forceinline__ void decode_passes(const void* wbase, Shared& sh, con
         cmy += row ? 1 : 0;
         blk = addr();  // past the segment's last block when g == seg_block1: never stored through
       }
-#if MXD_HUFF_STATS
-      st.write_syms++;
-#endif
-    };
-#if MXD_HUFF_WUNROLL > 1
-    // WUNROLL steps per check while none of them can reach the subsequence's
-    // end, the segment's last block or the bits past the data (a step
-    // consumes <= 31 bits and finishes <= 1 block)
-    const int32_t lim = min(u.end, u.sg.bits + 1);
-    while (rd.pos() + 31 * (MXD_HUFF_WUNROLL - 1) < lim && g + (MXD_HUFF_WUNROLL - 1) < seg_block1) {
-#pragma unroll
-      for (int i = 0; i < MXD_HUFF_WUNROLL; i++) wstep();
     }
-#endif
-    for (;;) {
-      const int32_t p = rd.pos();
-      if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
-      wstep();
+  }
+
+  // 5. DC values: per component, the differences before this subsequence in
+  // its segment (the continued segment starts from the previous job's sums)
+  if (job.pred && t == 0) {
+    const HuffPubDev* p = pub + sh.ticket - 1;
+    for (int c = 0; c < 3; c++) sh.pred_dc[c] = (int32_t)(uint32_t)wait_pub(p, 2 + c, ctl);
+  }
+  int last_sum[3];
+  for (int c = 0; c < 3; c++) {
+    int total = 0;
+    const int ex = block_exclusive_scan(act && u.own ? dcsum[c] : 0, sh.scan, &total);
+    __syncthreads();
+    sh.done[t] = ex;
+    __syncthreads();
+    const int base = continued ? sh.pred_dc[c] : 0;
+    const int at_first = sh.done[seg_first];
+    const int mine = dcsum[c];
+    dcsum[c] = act && u.own ? base + ex - at_first : 0;  // this subsequence's predictor start
+    last_sum[c] = dcsum[c] + mine;                       // through this subsequence
+    __syncthreads();
+  }
+  if (act && u.job_last && !u.seg_last) {
+    HuffPubDev* p = pub + sh.ticket;
+    for (int c = 0; c < 3; c++) publish(p, 2 + c, (uint64_t)(uint32_t)last_sum[c]);
+  }
+  if (act && u.own && dc0 >= 0) {
+    int pred[3] = {dcsum[0], dcsum[1], dcsum[2]};
+    for (int64_t b = dc0; b < dc1; b++) {
+      const int bj = (int)(b % im.bpm);
+      const int c = im.blk_comp[bj];
+      int16_t* d = coef + block_addr(im, b);
+      pred[c] += d[0];
+      d[0] = (int16_t)pred[c];
     }
   }
 }
@@ -881,18 +571,22 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
                                                           const HuffDev* __restrict__ tables,
                                                           const HuffImgDev* __restrict__ imgs,
                                                           const HuffSegDev* __restrict__ segs,
-                                                          const HuffJobDev* __restrict__ jobs, int16_t* coef) {
+                                                          const HuffJobDev* __restrict__ jobs, HuffPubDev* pub,
+                                                          HuffCtlDev* ctl, int16_t* coef) {
   __shared__ Shared sh;
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-#if MXD_HUFF_STATS
-  const uint64_t t_kernel = stat_clock();
-#endif
   const int t = threadIdx.x;
-  const HuffJobDev job = jobs[blockIdx.x];
-  if (t == 0) sh.img = imgs[segs[job.seg0].img];
+  // 0. the job: tickets in the order workgroups start (a job only ever waits
+  // for a smaller ticket, i.e. for a workgroup that has started)
+  if (t == 0) {
+    sh.ticket = __hip_atomic_fetch_add(&ctl->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh.job = jobs[sh.ticket];
+    sh.img = imgs[segs[sh.job.seg0].img];
+  }
   __syncthreads();
+  const HuffJobDev& job = sh.job;
   const HuffImgDev& im = sh.img;
-  if (t < im.bpm) {  // the block cursor's tables (read after stage 0's barrier)
+  if (t < im.bpm) {  // the block cursor's tables
     if (!im.interleaved) {
       sh.blk_off[0] = im.plane[0];
       sh.blk_mxs[0] = 64;
@@ -906,11 +600,6 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   }
   HuffDev* tab = reinterpret_cast<HuffDev*>(dyn);
   SegLds* seg = reinterpret_cast<SegLds*>(reinterpret_cast<char*>(dyn) + lds_tables_bytes(im.ntables));
-  const int64_t word0 = segs[job.seg0].word;  // the job's first word (16-byte aligned)
-  const int sub_bits = segs[job.seg0].sub_bits;
-
-  // 0. tables, segment records and (job.lds) words into LDS; zero the job's
-  // coefficient blocks
   {
     const uint4* src = reinterpret_cast<const uint4*>(tables + im.tables);
     const int n16 = im.ntables * (int)(sizeof(HuffDev) / 16);
@@ -918,34 +607,32 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   }
   uint32_t* lds_words = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dyn) + lds_words_at(im.ntables, job.nseg));
   if (job.lds) {
-    const uint4* src = reinterpret_cast<const uint4*>(words + word0);
+    const uint4* src = reinterpret_cast<const uint4*>(words + job.word0);
     uint4* dst = reinterpret_cast<uint4*>(lds_words);
     for (int i = t; i < job.words16; i += blockDim.x) dst[i] = src[i];
   }
+  // segment records: words relative to the job's first word; subsequences
+  // of the job per segment (the first from sub0, the job's count overall)
   int nsub_mine = 0;
   if (t < job.nseg) {
     const HuffSegDev g = segs[job.seg0 + t];
-    seg[t] = SegLds{(int32_t)(g.word - word0), g.bits, (int32_t)g.mcu0, g.mcus};
-    nsub_mine = max(1, (g.bits + sub_bits - 1) / sub_bits);
+    const int32_t rel = (int32_t)(g.word - job.word0);
+    SegLds s;
+    s.word = rel;
+    s.bits = g.bits;
+    s.mcu0 = (int32_t)g.mcu0;
+    s.mcus = g.mcus;
+    s.nsub = g.nsub;
+    s.lim = job.words16 * 4 - 1 - rel;  // the last word staged for it
+    seg[t] = s;
+    nsub_mine = g.nsub - (t == 0 ? job.sub0 : 0);
   }
-  int nsub = 0;
-  const int sub0 = block_exclusive_scan(nsub_mine, sh.scan, &nsub);
+  int total = 0;
+  const int sub0 = block_exclusive_scan(nsub_mine, sh.scan, &total);
   if (t < job.nseg) sh.seg_sub0[t] = sub0;
-  {
-    const HuffSegDev& s0 = segs[job.seg0];
-    const HuffSegDev& s1 = segs[job.seg0 + job.nseg - 1];
-    const int64_t b0 = s0.mcu0 * im.bpm, b1 = (s1.mcu0 + (int64_t)s1.mcus) * im.bpm;
-    for (int64_t g = b0 + (t >> 3); g < b1; g += blockDim.x >> 3)
-      reinterpret_cast<uint4*>(coef + block_addr(im, g))[t & 7] = uint4{0, 0, 0, 0};
-  }
-  if (t == 0) sh.flag[0] = sh.flag[1] = 0;
   __syncthreads();
-#if MXD_HUFF_STATS
-  const uint64_t t_start = stat_clock();
-#endif
-
-  // this thread's subsequence: its segment (binary search of seg_sub0) and bit range
-  int si = 0;
+  const int nsub = job.nsub;
+  // this thread's subsequence: its segment (binary search of seg_sub0) and start state
   if (t < nsub) {
     int lo = 0, hi = job.nseg - 1;
     while (lo < hi) {
@@ -953,102 +640,18 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
       if (sh.seg_sub0[mid] <= t) lo = mid;
       else hi = mid - 1;
     }
-    si = lo;
-  }
-  Sub u;
-  u.sg = seg[si];
-  u.j = t - sh.seg_sub0[si];  // index inside the segment
-  const int nseg_sub = max(1, (u.sg.bits + sub_bits - 1) / sub_bits);
-  u.active = t < nsub;
-  u.first = u.j == 0;
-  u.last = u.j == nseg_sub - 1;
-  u.start = u.j * sub_bits;
-  u.end = u.last ? 0x7fffffff : u.start + sub_bits;
-  if (u.active) {
-    sh.in_pos[t] = u.start;
+    sh.sub_seg[t] = (int16_t)lo;
+    const int j = t - sh.seg_sub0[lo] + (lo == 0 ? job.sub0 : 0);
+    sh.in_pos[t] = j * im.sub_bits;
     sh.in_b[t] = 0;
     sh.in_k[t] = 0;
     sh.done[t] = 0;
-    sh.sub_seg[t] = (int16_t)si;
   }
-  __syncthreads();  // sub_seg of every subsequence before any round reads it
-
-  int dcsum[3] = {0, 0, 0};
-  int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
-  Stats st;
-#if MXD_HUFF_STATS
-  st.t[0] = t_start;
-#endif
+  __syncthreads();
   if (job.lds)  // uniform over the workgroup
-    decode_passes<LdsReader>(lds_words, sh, im, tab, seg, sub_bits, nsub, u, coef, dcsum, dc0, dc1, st);
+    decode_job<LdsReader>(lds_words, sh, tab, seg, nsub, coef, pub, ctl);
   else
-    decode_passes<GlobalReader>(words + word0, sh, im, tab, seg, sub_bits, nsub, u, coef, dcsum, dc0, dc1, st);
-
-#if MXD_HUFF_STATS
-  __syncthreads();
-  st.c[1] = stat_cycles();
-  st.r[1] = stat_clock();
-  if (t == 0) sh.flag[0] = 0;
-  __syncthreads();
-  atomicMax(&sh.flag[0], st.write_syms);  // an LDS atomic: the busiest thread's write-pass symbols
-  __syncthreads();
-  const int stat_wmax = sh.flag[0];
-  __syncthreads();
-#endif
-  // 4. DC values: per component, the differences before this subsequence in its segment
-  for (int c = 0; c < 3; c++) {
-    const int ex = block_exclusive_scan(u.active ? dcsum[c] : 0, sh.scan, nullptr);
-#if MXD_HUFF_STATS
-    if (c == 0) st.t[2] = stat_clock();
-#endif
-    __syncthreads();
-    sh.done[t] = ex;
-    __syncthreads();
-    dcsum[c] = u.active ? ex - sh.done[t - u.j] : 0;  // this subsequence's predictor start
-    __syncthreads();
-  }
-#if MXD_HUFF_STATS
-  int stat_sync = 0, stat_write = 0, stat_chg = 0, stat_chg_pos = 0, stat_chg_k = 0;
-  {
-    const int a = block_exclusive_scan(st.sync_syms, sh.scan, &stat_sync);
-    const int b = block_exclusive_scan(st.write_syms, sh.scan, &stat_write);
-    const int c = block_exclusive_scan(st.chg, sh.scan, &stat_chg);
-    const int d = block_exclusive_scan(st.chg_pos, sh.scan, &stat_chg_pos);
-    const int e = block_exclusive_scan(st.chg_k, sh.scan, &stat_chg_k);
-    (void)a;
-    (void)b;
-    (void)c;
-    (void)d;
-    (void)e;
-  }
-#endif
-  if (u.active && dc0 >= 0) {
-    int pred[3] = {dcsum[0], dcsum[1], dcsum[2]};
-    for (int64_t b = dc0; b < dc1; b++) {
-      const int bj = (int)(b % im.bpm);
-      const int c = im.blk_comp[bj];
-      int16_t* d = coef + block_addr(im, b);
-      pred[c] += d[0];
-      d[0] = (int16_t)pred[c];
-    }
-  }
-#if MXD_HUFF_STATS
-  __syncthreads();
-  st.t[3] = stat_clock();
-  // wave 0's lanes 0..7 (vector stores); thread 0's clocks
-  const uint64_t t0 = __shfl(st.t[0], 0, 64), t1 = __shfl(st.t[1], 0, 64), t2 = __shfl(st.t[2], 0, 64),
-                 t3 = __shfl(st.t[3], 0, 64), tk = __shfl(t_kernel, 0, 64);
-  const uint64_t c0 = __shfl(st.c[0], 0, 64), c1 = __shfl(st.c[1], 0, 64);
-  const uint64_t r0 = __shfl(st.r[0], 0, 64), r1 = __shfl(st.r[1], 0, 64);
-  if (blockIdx.x < kStatJobs && t < kStatInts) {
-    // write-pass shader cycles, the busiest thread's write symbols, and thread 0's
-    const int v[kStatInts] = {st.rounds,      nsub,           stat_sync,         stat_write,
-                              (int)(t1 - t0), (int)(t2 - t1), (int)(t3 - t2),    (int)(t0 - tk),
-                              (int)(c1 - c0), stat_wmax,      __shfl(st.write_syms, 0, 64), (int)(r1 - r0),
-                              stat_chg,       stat_chg_pos,   stat_chg_k,        0};
-    g_huff_stats[blockIdx.x * kStatInts + t] = v[t];
-  }
-#endif
+    decode_job<GlobalReader>(words + job.word0, sh, tab, seg, nsub, coef, pub, ctl);
 }
 
 }  // namespace
@@ -1060,31 +663,28 @@ int64_t jpeg_huff_lds_bytes(int ntables, int nseg, int64_t words) {
 }
 
 int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImgDev* imgs, const HuffSegDev* segs,
-                     const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, int16_t* coef,
-                     void* stream) {
+                     const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, HuffPubDev* pub,
+                     HuffCtlDev* ctl, int16_t* coef, void* stream) {
   if (njobs <= 0) return 0;
   threads = (threads + 63) / 64 * 64;
   threads = threads < 64 ? 64 : threads > kHuffThreads ? kHuffThreads : threads;
+  if (lds_bytes > jpeg_huff_lds_budget()) return -1;
   auto k = jpeg_huff;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds_bytes) != hipSuccess)
-    return -1;
+  // the kernel's dynamic-LDS limit, raised once per device to the budget
+  // (setting it per launch from concurrent threads raced with
+  // other threads' launches)
+  static std::once_flag once[64];
+  static int set_rc[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+  std::call_once(once[dev], [&] {
+    set_rc[dev] = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)jpeg_huff_lds_budget()) == hipSuccess ? 0 : -1;
+  });
+  if (set_rc[dev]) return -1;
   hipLaunchKernelGGL(k, dim3(njobs), dim3(threads), (size_t)lds_bytes, reinterpret_cast<hipStream_t>(stream), words,
-                     tables, imgs, segs, jobs, coef);
+                     tables, imgs, segs, jobs, pub, ctl, coef);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace mxd
-
-#if MXD_HUFF_STATS
-// (rounds, subsequences, sync-pass symbols, write-pass symbols) of the last
-// launch's first n jobs.
-extern "C" int mxd_debug_huff_stats(int* host, int n) {
-  if (n > mxd::kStatJobs) n = mxd::kStatJobs;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mxd::g_huff_stats), sizeof(int) * mxd::kStatInts * n, 0,
-                             hipMemcpyDeviceToHost) ==
-                 hipSuccess
-             ? 0
-             : -1;
-}
-#endif

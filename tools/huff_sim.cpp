@@ -18,6 +18,7 @@
 // Build: g++ -O2 -std=c++17 -Imlx-data_amd/csrc -Iinclude tools/huff_sim.cpp mlx-data_amd/csrc/jpeg.cpp -o tools/huff_sim
 // Run:   tools/huff_sim [--sub BITS] [--threads N] [--dmax D] [--spec 0|1] FILE...
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -159,7 +160,8 @@ struct Opts {
   int spec_from = 1;  // first round that may speculate
   int krange = 1;
   int phase = 0;      // 1: the anchor / phase-map design; 2: design B (overlap, variants, breaks)
-  int overlap = 512;  // design B: round 0 starts this many bits before each piece     // accept a variant for entry indices its first block's EOB makes equivalent
+  int overlap = 512;
+  int jobs = 0;       // emulate the round-5 kernel's jobs  // design B: round 0 starts this many bits before each piece     // accept a variant for entry indices its first block's EOB makes equivalent
 };
 
 struct Stats {
@@ -488,6 +490,206 @@ bool design_b(const Img& im, const Opts& o, std::vector<Sub>& subs, std::vector<
   return true;
 }
 
+// Round-5 kernel emulation (--jobs 1): hostpath.cpp's job planning and
+// jpeghuff.hip decode_job, job after job (the look-back sees the previous
+// job's publication), each job's rounds as the workgroup runs them.  Checks
+// the kernel's logic on the CPU; returns false on a mismatch.
+int kZigzagNat2(int z) {
+  static const int nat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+                              41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                              30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+  return nat[z];
+}
+
+struct JobStats {
+  int64_t jobs = 0, fixes = 0, max_rounds = 0;
+} g_js;
+
+bool emulate_jobs(const Img& im, const Opts& o, const std::vector<int16_t>& host, const jpeg::CoefInfo& hinfo) {
+  const int sb = o.sub_bits;
+  const int nseg = (int)im.segs.size();
+  std::vector<int64_t> nsub(nseg), sub_first;
+  int64_t N = 0;
+  for (int g = 0; g < nseg; g++) {
+    nsub[g] = std::max<int64_t>(1, (im.segs[g].bits + sb - 1) / sb);
+    sub_first.push_back(N);
+    N += nsub[g];
+  }
+  sub_first.push_back(N);
+  const int64_t cap = kHuffThreads - kHuffWarm;
+  const int64_t njob = (N + cap - 1) / cap;
+  std::vector<int64_t> cuts{0};
+  for (int64_t q = 1; q < njob; q++) {
+    int64_t cut = q * N / njob;
+    const int64_t sgi = std::upper_bound(sub_first.begin(), sub_first.end(), cut) - sub_first.begin() - 1;
+    if (cut - sub_first[sgi] <= 32 && sub_first[sgi] > cuts.back()) cut = sub_first[sgi];
+    cuts.push_back(cut);
+  }
+  cuts.push_back(N);
+  std::vector<int16_t> coef(host.size(), 0);
+  struct Pub {
+    State st;
+    int64_t blocks;
+    int dc[3];
+  } pub{};
+  for (size_t q = 0; q + 1 < cuts.size(); q++) {
+    g_js.jobs++;
+    const int64_t a0 = cuts[q], b0 = cuts[q + 1];
+    const int64_t sa = std::upper_bound(sub_first.begin(), sub_first.end(), a0) - sub_first.begin() - 1;
+    const int64_t ja = a0 - sub_first[sa];
+    const int warm = (int)std::min<int64_t>(kHuffWarm, ja);
+    const bool pred = ja > 0;
+    const int n = (int)(b0 - a0 + warm);
+    // job-local subsequences
+    struct L {
+      int seg;
+      int64_t j;
+      bool first, seg_last, own, job_last;
+      int64_t start, end;
+    };
+    std::vector<L> sub(n);
+    for (int t = 0; t < n; t++) {
+      const int64_t gidx = a0 - warm + t;
+      const int sg = (int)(std::upper_bound(sub_first.begin(), sub_first.end(), gidx) - sub_first.begin() - 1);
+      L& l = sub[t];
+      l.seg = sg;
+      l.j = gidx - sub_first[sg];
+      l.first = l.j == 0;
+      l.seg_last = l.j == nsub[sg] - 1;
+      l.own = t >= warm;
+      l.job_last = t == n - 1;
+      l.start = l.j * sb;
+      l.end = l.seg_last ? INT64_MAX : l.start + sb;
+    }
+    std::vector<State> in(n), out(n);
+    std::vector<int64_t> done(n, 0);
+    for (int t = 0; t < n; t++) in[t] = State{sub[t].start, 0, 0};
+    auto rounds = [&](std::vector<char> need, int fixed) {
+      int r = 0;
+      for (;; r++) {
+        bool any = false;
+        for (int t = 0; t < n; t++)
+          if (need[t]) {
+            any = true;
+            int64_t stp = 0, bl = 0;
+            Sub u{sub[t].seg, sub[t].start, sub[t].end, sub[t].first, sub[t].seg_last};
+            out[t] = run(im, u, in[t], &stp, &bl);
+            done[t] = bl;
+          }
+        if (!any) break;
+        std::vector<char> nn(n, 0);
+        for (int t = 1; t < n; t++) {
+          if (sub[t].first || t == fixed) continue;
+          if (out[t - 1] != in[t]) {
+            in[t] = out[t - 1];
+            nn[t] = !sub[t].seg_last;
+          }
+        }
+        need = nn;
+      }
+      g_js.max_rounds = std::max<int64_t>(g_js.max_rounds, r);
+    };
+    std::vector<char> need(n);
+    for (int t = 0; t < n; t++) need[t] = !sub[t].seg_last;
+    rounds(need, -1);
+    if (pred) {
+      if (pub.st != in[warm]) {
+        g_js.fixes++;
+        in[warm] = pub.st;
+        std::vector<char> nd(n, 0);
+        nd[warm] = !sub[warm].seg_last;
+        rounds(nd, warm);
+      }
+    }
+    // blocks and write pass, DC
+    std::vector<int64_t> g(n, 0);
+    std::vector<std::array<int, 3>> dcs(n, {0, 0, 0});
+    int64_t acc = 0;
+    int cur_seg = -1;
+    for (int t = warm; t < n; t++) {
+      if (sub[t].seg != cur_seg) {
+        cur_seg = sub[t].seg;
+        acc = (pred && sub[t].seg == sub[warm].seg) ? pub.blocks : im.segs[cur_seg].mcu0 * im.bpm;
+      }
+      g[t] = acc;
+      if (!sub[t].seg_last) acc += done[t];
+      if (t == n - 1 && !sub[t].seg_last) {
+        // publication: exit, block index (dc below)
+      }
+    }
+    Pub np{};
+    if (!sub[n - 1].seg_last) {
+      np.st = out[n - 1];
+      np.blocks = g[n - 1] + done[n - 1];
+    }
+    // write pass
+    std::vector<std::array<int64_t, 2>> dcr(n, {-1, -1});
+    for (int t = warm; t < n; t++) {
+      const Seg& sg = im.segs[sub[t].seg];
+      State st = in[t];
+      int64_t gg = g[t];
+      const int64_t g1 = (sg.mcu0 + sg.mcus) * im.bpm;
+      while (!(st.pos >= sub[t].end || gg >= g1 || (st.b == 0 && st.k == 0 && st.pos > sg.bits))) {
+        const int bj = (int)(gg % im.bpm);
+        const int ci = im.es.blk_comp[bj];
+        const jpeg::CoefPlane& cp = hinfo.comp[ci];
+        int64_t m = gg / im.bpm, bx, by;
+        if (im.es.interleaved) {
+          by = (m / im.es.mcux) * cp.v + im.es.blk_dy[bj];
+          bx = (m % im.es.mcux) * cp.h + im.es.blk_dx[bj];
+        } else {
+          by = gg / im.es.mcux;
+          bx = gg % im.es.mcux;
+        }
+        int16_t* blk = coef.data() + cp.off + (by * cp.bw + bx) * 64;
+        const bool dc = st.k == 0;
+        int kk, v;
+        const bool fin = step(im, sg, st, &kk, &v);
+        if (dc) {
+          dcs[t][ci] += v;
+          if (dcr[t][0] < 0) dcr[t][0] = gg;
+          dcr[t][1] = gg + 1;
+          blk[0] = (int16_t)v;
+        } else {
+          blk[kZigzagNat2(kk)] = (int16_t)v;
+        }
+        if (fin) gg++;
+      }
+    }
+    // DC prefix per segment, fix-up
+    std::array<int, 3> base{0, 0, 0};
+    cur_seg = -1;
+    for (int t = warm; t < n; t++) {
+      if (sub[t].seg != cur_seg) {
+        cur_seg = sub[t].seg;
+        for (int c = 0; c < 3; c++) base[c] = (pred && sub[t].seg == sub[warm].seg) ? pub.dc[c] : 0;
+      }
+      std::array<int, 3> pr = base;
+      if (dcr[t][0] >= 0)
+        for (int64_t b = dcr[t][0]; b < dcr[t][1]; b++) {
+          const int bj = (int)(b % im.bpm);
+          const int ci = im.es.blk_comp[bj];
+          const jpeg::CoefPlane& cp = hinfo.comp[ci];
+          int64_t m = b / im.bpm, bx, by;
+          if (im.es.interleaved) {
+            by = (m / im.es.mcux) * cp.v + im.es.blk_dy[bj];
+            bx = (m % im.es.mcux) * cp.h + im.es.blk_dx[bj];
+          } else {
+            by = b / im.es.mcux;
+            bx = b % im.es.mcux;
+          }
+          int16_t* d = coef.data() + cp.off + (by * cp.bw + bx) * 64;
+          pr[ci] += d[0];
+          d[0] = (int16_t)pr[ci];
+        }
+      for (int c = 0; c < 3; c++) base[c] += dcs[t][c];
+    }
+    for (int c = 0; c < 3; c++) np.dc[c] = base[c];
+    pub = np;
+  }
+  return coef == host;
+}
+
 bool load(const char* path, Img& im, std::vector<int16_t>& host_coef, std::vector<int64_t>& plane_off,
           jpeg::CoefInfo& hinfo) {
   std::ifstream f(path, std::ios::binary);
@@ -594,6 +796,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--krange")) o.krange = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--phase")) o.phase = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--overlap")) o.overlap = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--jobs")) o.jobs = std::atoi(argv[++i]);
     else files.push_back(argv[i]);
   }
   int nf = 0, bad = 0, maxr = 0;
@@ -609,6 +812,15 @@ int main(int argc, char** argv) {
     std::vector<State> in;
     std::vector<int64_t> done;
     Stats st;
+    if (o.jobs) {
+      const bool ok = emulate_jobs(im, o, host, hinfo);
+      if (!ok) {
+        std::printf("%s: JOBS MISMATCH\n", p);
+        bad++;
+      }
+      nf++;
+      continue;
+    }
     PhaseStats ps;
     const bool ok_sync = o.phase == 2   ? design_b(im, o, subs, in, done, st)
                          : o.phase == 1 ? phase_sync(im, o, subs, in, done, st, ps)
@@ -642,6 +854,11 @@ int main(int argc, char** argv) {
     }
   }
   if (!nf) return 1;
+  if (o.jobs) {
+    std::printf("jobs emulation: files %d bad %d, jobs %lld, predecessor fixes %lld, most rounds %lld\n", nf, bad,
+                (long long)g_js.jobs, (long long)g_js.fixes, (long long)g_js.max_rounds);
+    return bad ? 2 : 0;
+  }
   if (o.phase == 2)
     std::printf("design B: pieces/file %.0f, breaks/file %.2f, most breaks in a file %lld, round 0 %.2f passes, "
                 "round 1 %.2f passes (longest variant decode %lld steps), break decodes %.3f passes\n",
