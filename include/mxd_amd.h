@@ -35,7 +35,8 @@ extern "C" {
 /* 5: the round-4 additions (numbered in round 5): mxd_jpeg_coefs_parse (device
  * entropy decode pending), mxd_jpeg_coefs_entropy_pending,
  * mxd_device_synchronize, and the tuning knobs MXD_TUNE_HUFF_BITS,
- * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS. */
+ * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS,
+ * MXD_TUNE_HUFF_JOB. */
 #define MXD_ABI_VERSION 5
 
 enum mxd_status {
@@ -181,7 +182,9 @@ int mxd_set_kernel_policy(int32_t policy);
  * default polling wait;
  * MXD_TUNE_HOST_STREAMS: streams per device the host-path calls launch on
  * (read when a host-path context is first set up): 0 = every context slot
- * owns one (default); n > 0 = the slots share n library streams. */
+ * owns one (default); n > 0 = the slots share n library streams;
+ * MXD_TUNE_HUFF_JOB: most own subsequences per device entropy-decode job
+ * (workgroup); 0 = kHuffThreads - kHuffWarm (1000). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -192,7 +195,8 @@ enum mxd_tune {
   MXD_TUNE_HUFF_GLOBAL = 6,
   MXD_TUNE_HOST_WAIT = 7,
   MXD_TUNE_HOST_STREAMS = 8,
-  MXD_TUNE_COUNT = 9
+  MXD_TUNE_HUFF_JOB = 9,
+  MXD_TUNE_COUNT = 10
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 

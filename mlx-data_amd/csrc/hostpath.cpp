@@ -334,7 +334,7 @@ struct JpegChunk {
   std::vector<uint16_t> qtabs;
   int64_t planes_off = 0, imgs_off = 0, q_off = 0, end = 0;  // in the staged input
   int64_t samples = 0, rgb_off = 0, mid_bytes = 0;             // in dev_mid
-  int64_t nblocks = 0, max_quad_rows = 0;
+  int64_t nblocks = 0, max_quad_rows = 0;  // max_quad_rows: the colour kernel's threads per image (8 pixels each)
   // Device entropy decode of the chunk's pending images (jpeghuff.h): their
   // unstuffed segments (words_off..), tables, image / segment / job records in
   // the staged input; their coefficients in dev_in past the staged bytes
@@ -436,7 +436,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     // sized; a cut inside a segment gives the next job a warm-up of up to
     // kHuffWarm subsequences before its own (jpeghuff.h); cuts within a few
     // subsequences of a segment start move there (restart markers: no warm-up)
-    const int64_t cap = mxd::kHuffThreads - mxd::kHuffWarm;
+    const int32_t job_knob = g_tune[MXD_TUNE_HUFF_JOB].load();
+    const int64_t cap = job_knob > 0 ? std::min<int64_t>(job_knob, mxd::kHuffThreads - mxd::kHuffWarm)
+                                     : mxd::kHuffThreads - mxd::kHuffWarm;
     const int64_t njob = (nsub_img + cap - 1) / cap;
     std::vector<int64_t> cuts{0};
     for (int64_t q = 1; q < njob; q++) {
@@ -520,7 +522,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     }
     m.out = c.mid_bytes;  // relative to rgb_off, fixed below
     c.mid_bytes += up((int64_t)m.pitch * m.height, 256);
-    c.max_quad_rows = std::max<int64_t>(c.max_quad_rows, (int64_t)m.height * m.quads);
+    c.max_quad_rows = std::max<int64_t>(c.max_quad_rows, (int64_t)m.height * ((info.width + 7) / 8));
     c.imgs.push_back(m);
   }
   c.rgb_off = c.samples;

@@ -1600,7 +1600,8 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
     if (!fits && first_long == (1 << kHuffLook)) first_long = i;
   }
   // longer codes (canonical: every prefix from first_long up to the top has
-  // none that fits) over 16 bits, when they take <= kHuffLong patterns
+  // none that fits) over the top kHuffLong 16-bit patterns, indexed from
+  // 65536 - kHuffLong (the kernel's constant base), when they lie there
   const int32_t base = first_long << (16 - kHuffLook);
   o.long_base = 65536;
   if (65536 - base <= kHuffLong) {
@@ -1611,7 +1612,7 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
       for (int32_t v = base; v < 65536; v++) {
         int len, sym;
         code_at((uint32_t)v, &len, &sym);
-        o.step_long[v - base] = huff_step_entry(cls, len, sym);
+        o.step_long[v - (65536 - kHuffLong)] = huff_step_entry(cls, len, sym);
       }
     }
   }

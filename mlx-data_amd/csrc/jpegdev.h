@@ -45,16 +45,16 @@ struct JpegImgDev {
   int32_t ncomp;     // 1 (grey, replicated) or 3
   int32_t rgb;       // 1: the components are R, G, B (no YCbCr conversion)
   int32_t width, height;
-  int32_t pitch;     // bytes per RGB row (a multiple of 64, >= 3 * round_up(width, 4))
-  int32_t quads;     // threads per row: ceil(width / 4)
+  int32_t pitch;     // bytes per RGB row (a multiple of 64, >= 3 * round_up(width, 8))
+  int32_t quads;     // ceil(width / 4) (diagnostics; the colour kernel runs ceil(width / 8) threads per row)
 };
 
 // Dequantise + IDCT every block of `nplanes` planes (`nblocks` in total).
 void launch_jpeg_idct(const int16_t* coef, const uint16_t* qtabs, const JpegPlaneDev* planes, int32_t nplanes,
                       int64_t nblocks, uint8_t* samples, hipStream_t stream);
-// Upsample + colour-convert `n` images (max_quads_rows = max over images of
-// height * quads, the grid's x extent).
-void launch_jpeg_color(const uint8_t* samples, const JpegImgDev* imgs, int32_t n, int64_t max_quad_rows,
+// Upsample + colour-convert `n` images (max_oct_rows = max over images of
+// height * ceil(width / 8), the grid's x extent).
+void launch_jpeg_color(const uint8_t* samples, const JpegImgDev* imgs, int32_t n, int64_t max_oct_rows,
                        uint8_t* rgb, hipStream_t stream);
 
 }  // namespace mxd

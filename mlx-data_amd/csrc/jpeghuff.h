@@ -56,11 +56,12 @@ constexpr int kHuffWarm = 24;       // warm-up subsequences of a job that starts
 // pattern -- bits 0..4 the bits a symbol consumes (code + value bits), 5..11
 // the coefficient-index advance (DC 1; a coefficient run + 1; ZRL 16; EOB
 // 64), 12..15 the value bits -- over kHuffLook bits (0: a longer code), and
-// for the longer codes over 16 bits from `long_base` on (canonical codes:
-// every code longer than kHuffLook bits lies in the top range of 16-bit
-// patterns; patterns no code starts map to "16 bits, symbol 0", the host
-// decoder's corrupt-code rule).  A table whose long codes need more than
-// kHuffLong patterns keeps long_base = 65536 and is searched (maxcode /
+// for the longer codes over the top kHuffLong 16-bit patterns, indexed from
+// 65536 - kHuffLong (canonical codes: every code longer than kHuffLook bits
+// lies in the top range of 16-bit patterns, from `long_base` on; patterns no
+// code starts map to "16 bits, symbol 0", the host decoder's corrupt-code
+// rule).  A table whose long codes reach below the top kHuffLong patterns
+// keeps long_base = 65536, an empty second table, and is searched (maxcode /
 // valoffset / vals).
 struct HuffDev {
   uint16_t step[1 << kHuffLook];

@@ -254,7 +254,7 @@ struct Dec {
     const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
     const uint32_t top16 = (uint32_t)(r.buf >> 48);
     const int st1 = t.step[top16 >> (16 - kHuffLook)];
-    const int st2 = t.step_long[min(max((int)top16 - t.long_base, 0), kHuffLong - 1)];
+    const int st2 = t.step_long[max((int)top16 - (65536 - kHuffLong), 0)];  // no dependent load of a base
     int st = st1 ? st1 : st2;
     if (!st) st = huff_search_step(t, r.buf, dc ? 0 : 1);
     const int shift = st & 31, adv = (st >> 5) & 127, sz = st >> 12;

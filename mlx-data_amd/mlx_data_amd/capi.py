@@ -58,6 +58,7 @@ MXD_TUNE_HUFF_BITS = 5
 MXD_TUNE_HUFF_GLOBAL = 6
 MXD_TUNE_HOST_WAIT = 7
 MXD_TUNE_HOST_STREAMS = 8
+MXD_TUNE_HUFF_JOB = 9
 
 
 class MxdImage(ctypes.Structure):

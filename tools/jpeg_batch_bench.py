@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--huff-bits", default="0", help="device entropy: subsequence lengths to time (0: default)")
     ap.add_argument("--huff-global", action="store_true", help="device entropy: also time every length with words read from device memory")
     ap.add_argument("--no-host", action="store_true", help="skip the host entropy decode runs")
+    ap.add_argument("--huff-job", default="0", help="device entropy: own subsequences per job to time (0: default)")
     args = ap.parse_args()
     from mlx_data_amd import capi
 
@@ -70,16 +71,17 @@ def main():
         batch = int(nb) if nb else args.batch
         datas = files(name, batch)
         line = dict(dataset=name, batch=batch, mean_file_bytes=round(float(np.mean([len(d) for d in datas])), 1))
-        runs = [(True, int(b), 0) for b in args.huff_bits.split(",")]
+        runs = [(True, int(b), 0, int(j)) for b in args.huff_bits.split(",") for j in args.huff_job.split(",")]
         if args.huff_global:
-            runs += [(True, int(b), 1) for b in args.huff_bits.split(",")]
+            runs += [(True, int(b), 1, 0) for b in args.huff_bits.split(",")]
         if not args.no_host:
-            runs.append((False, 0, 0))
-        for dev, bits, glob in runs:
+            runs.append((False, 0, 0, 0))
+        for dev, bits, glob, job in runs:
             capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
             capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, glob)
-            tag = ("device_entropy" + (f"_bits{bits}" if bits else "") + ("_global" if glob else "")) if dev \
-                else "host_entropy"
+            capi.set_tuning(capi.MXD_TUNE_HUFF_JOB, job)
+            tag = ("device_entropy" + (f"_bits{bits}" if bits else "") + ("_global" if glob else "") +
+                   (f"_job{job}" if job else "")) if dev else "host_entropy"
             line[f"{tag}_host_us_per_image"] = round(per_image(lambda d: capi.JpegCoefs(d, dev).close(), datas), 1)
             coefs = [capi.JpegCoefs(d, dev) for d in datas]
             assert all(c.entropy_pending == dev for c in coefs)
@@ -106,6 +108,7 @@ def main():
                 c.close()
         capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, 0)
         capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, 0)
+        capi.set_tuning(capi.MXD_TUNE_HUFF_JOB, 0)
         print(json.dumps(line), flush=True)
 
 
