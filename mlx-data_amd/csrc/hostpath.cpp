@@ -355,6 +355,7 @@ struct JpegChunk {
   int64_t pub_off = 0;  // the jobs' publication records + launch control, zeroed with the coefficients
   int32_t huff_threads = 0;
   int64_t huff_lds = 0;  // the largest job's dynamic LDS (its words included when they fit)
+  bool huff_search = false;  // some table needs the searching kernel (HuffDev::search)
 };
 
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
@@ -402,6 +403,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     for (int t = 0; t < es.ntables; t++) {
       c.htabs.emplace_back();
       mxd::jpeg::device_table(coefs_of(jimg[i].coefs), es.table_class[t], es.table_id[t], &c.htabs.back());
+      c.huff_search = c.huff_search || c.htabs.back().search != 0;
     }
     // subsequence length: kHuffMinBits (MXD_TUNE_HUFF_BITS overrides it;
     // a multiple of 32); segments of any length split over several jobs
@@ -826,7 +828,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                   reinterpret_cast<const mxd::HuffSegDev*>(sl.dev_in + jc.hsegs_off),
                                   reinterpret_cast<const mxd::HuffJobDev*>(sl.dev_in + jc.hjobs_off),
                                   (int32_t)jc.hjobs.size(), jc.huff_threads, jc.huff_lds, pub, ctl,
-                                  reinterpret_cast<int16_t*>(sl.dev_in), sl.stream))
+                                  reinterpret_cast<int16_t*>(sl.dev_in), jc.huff_search, sl.stream))
           return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
         if (!sl.huff_err) MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.huff_err), 64, hipHostMallocDefault));
         MXD_HIP(hipMemcpyAsync(sl.huff_err, &ctl->error, sizeof(int32_t), hipMemcpyDeviceToHost, sl.stream));

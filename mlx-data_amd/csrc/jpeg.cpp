@@ -1604,10 +1604,12 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   // 65536 - kHuffLong (the kernel's constant base), when they lie there
   const int32_t base = first_long << (16 - kHuffLook);
   o.long_base = 65536;
+  o.search = 1;
   if (65536 - base <= kHuffLong) {
     bool ok = true;
     for (int i = first_long; i < (1 << kHuffLook); i++) ok = ok && o.step[i] == 0;
     if (ok) {
+      o.search = 0;
       o.long_base = base;
       for (int32_t v = base; v < 65536; v++) {
         int len, sym;

@@ -67,7 +67,7 @@ struct HuffDev {
   uint16_t step[1 << kHuffLook];
   uint16_t step_long[kHuffLong];
   int32_t long_base;
-  int32_t pad0;
+  int32_t search;  // 1: the two lookups do not cover every pattern (the launch takes the searching kernel)
   int32_t maxcode[18];
   int32_t valoffset[18];
   uint8_t vals[256];
@@ -158,9 +158,10 @@ int64_t jpeg_huff_lds_budget();
 // subsequences; lds_bytes: the largest job's dynamic LDS, its words included
 // when it reads them from LDS); coefficient offsets in HuffImgDev are int16
 // elements of `coef`, segment words index `words`; pub (njobs records) and ctl
-// must be zero.  Returns 0, or -1 if the launch failed.
+// must be zero; search: some table has HuffDev::search set.  Returns 0, or -1
+// if the launch failed.
 int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImgDev* imgs, const HuffSegDev* segs,
                      const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, HuffPubDev* pub,
-                     HuffCtlDev* ctl, int16_t* coef, void* stream);
+                     HuffCtlDev* ctl, int16_t* coef, bool search, void* stream);
 
 }  // namespace mxd

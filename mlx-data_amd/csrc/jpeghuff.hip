@@ -217,6 +217,7 @@ __device__ int block_exclusive_scan(int v, int* totals, int* total_out) {
 
 // Decoder state machine over one segment: block b of the MCU, next
 // coefficient k (0 = the DC difference), symbols from Reader r.
+template <bool SEARCH>
 struct Dec {
   const HuffDev* tab;
   int b, k;
@@ -256,7 +257,9 @@ struct Dec {
     const int st1 = t.step[top16 >> (16 - kHuffLook)];
     const int st2 = t.step_long[max((int)top16 - (65536 - kHuffLong), 0)];  // no dependent load of a base
     int st = st1 ? st1 : st2;
-    if (!st) st = huff_search_step(t, r.buf, dc ? 0 : 1);
+    if constexpr (SEARCH) {  // launches with a table the two lookups do not cover
+      if (!st) st = huff_search_step(t, r.buf, dc ? 0 : 1);
+    }
     const int shift = st & 31, adv = (st >> 5) & 127, sz = st >> 12;
     // value bits: the sz bits after the code, in the buffer's top 32 bits (shift <= 31)
     const uint32_t hi = (uint32_t)(r.buf >> 32);
@@ -325,11 +328,11 @@ __device__ __forceinline__ Sub sub_of(const Shared& sh, const SegLds* seg, int i
 // decodes only in the write pass).  `fixed`: a job-local subsequence whose
 // start is known (the previous job's exit), which its predecessor in the job
 // (the warm-up) no longer hands a state to.
-template <class R>
+template <class R, bool SEARCH>
 __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, const SegLds* seg, int nsub,
                             const Sub& u, bool need, int fixed = -1) {
   const int t = threadIdx.x;
-  Dec dec;
+  Dec<SEARCH> dec;
   dec.init(sh.img, tab);
   R rd;
   for (;;) {
@@ -401,7 +404,7 @@ __device__ uint64_t wait_pub(const HuffPubDev* p, int i, HuffCtlDev* ctl) {
   return 0;
 }
 
-template <class R>
+template <class R, bool SEARCH>
 __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, const SegLds* seg, int nsub,
                            int16_t* coef, HuffPubDev* pub, HuffCtlDev* ctl) {
   const int t = threadIdx.x;
@@ -412,7 +415,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
   u.active = act;  // threads past the job's subsequences take part in the scans only
 
   // 1. rounds from the guessed starts (segment starts are exact)
-  sync_rounds<R>(wbase, sh, tab, seg, nsub, u, act && !u.seg_last);
+  sync_rounds<R, SEARCH>(wbase, sh, tab, seg, nsub, u, act && !u.seg_last);
 
   // 2. the previous job's exit: the true start of the first own subsequence
   if (job.pred) {
@@ -433,7 +436,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     const bool again = sh.flag[0] != 0;
     __syncthreads();
     if (again)  // uniform
-      sync_rounds<R>(wbase, sh, tab, seg, nsub, u, t == job.warm && !u.seg_last, job.warm);
+      sync_rounds<R, SEARCH>(wbase, sh, tab, seg, nsub, u, t == job.warm && !u.seg_last, job.warm);
   }
 
   // 3. first block of each own subsequence: the blocks its segment's earlier
@@ -459,7 +462,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
   }
 
   // 4. write pass (own subsequences)
-  Dec dec;
+  Dec<SEARCH> dec;
   dec.init(im, tab);
   int dcsum[3] = {0, 0, 0};
   int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
@@ -567,6 +570,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
   }
 }
 
+template <bool SEARCH>
 __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __restrict__ words,
                                                           const HuffDev* __restrict__ tables,
                                                           const HuffImgDev* __restrict__ imgs,
@@ -649,9 +653,9 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   }
   __syncthreads();
   if (job.lds)  // uniform over the workgroup
-    decode_job<LdsReader>(lds_words, sh, tab, seg, nsub, coef, pub, ctl);
+    decode_job<LdsReader, SEARCH>(lds_words, sh, tab, seg, nsub, coef, pub, ctl);
   else
-    decode_job<GlobalReader>(words + job.word0, sh, tab, seg, nsub, coef, pub, ctl);
+    decode_job<GlobalReader, SEARCH>(words + job.word0, sh, tab, seg, nsub, coef, pub, ctl);
 }
 
 }  // namespace
@@ -664,13 +668,13 @@ int64_t jpeg_huff_lds_bytes(int ntables, int nseg, int64_t words) {
 
 int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImgDev* imgs, const HuffSegDev* segs,
                      const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, HuffPubDev* pub,
-                     HuffCtlDev* ctl, int16_t* coef, void* stream) {
+                     HuffCtlDev* ctl, int16_t* coef, bool search, void* stream) {
   if (njobs <= 0) return 0;
   threads = (threads + 63) / 64 * 64;
   threads = threads < 64 ? 64 : threads > kHuffThreads ? kHuffThreads : threads;
   if (lds_bytes > jpeg_huff_lds_budget()) return -1;
-  auto k = jpeg_huff;
-  // the kernel's dynamic-LDS limit, raised once per device to the budget
+  auto k = search ? jpeg_huff<true> : jpeg_huff<false>;
+  // the kernels' dynamic-LDS limit, raised once per device to the budget
   // (setting it per launch from concurrent threads raced with
   // other threads' launches)
   static std::once_flag once[64];
@@ -678,8 +682,13 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
   std::call_once(once[dev], [&] {
-    set_rc[dev] = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)jpeg_huff_lds_budget()) == hipSuccess ? 0 : -1;
+    const int lim = (int)jpeg_huff_lds_budget();
+    set_rc[dev] = hipFuncSetAttribute(reinterpret_cast<const void*>(jpeg_huff<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess &&
+                          hipFuncSetAttribute(reinterpret_cast<const void*>(jpeg_huff<false>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess
+                      ? 0
+                      : -1;
   });
   if (set_rc[dev]) return -1;
   hipLaunchKernelGGL(k, dim3(njobs), dim3(threads), (size_t)lds_bytes, reinterpret_cast<hipStream_t>(stream), words,

@@ -245,3 +245,27 @@ def test_large_image_many_jobs(word_source):
     b = _encode(_smooth(rng, 1800, 2400), quality=97, subsampling=0)
     coefs = _check_identity([a, b])
     assert all(c.entropy_pending for c in coefs)
+
+
+@pytest.mark.parametrize("bits", [0, 32])
+def test_deep_tables_take_the_searching_decoder(bits, word_source):
+    """Tables whose codes longer than 11 bits reach below the top 1/64 of the
+    code space (tests/jpeg_enc.py; no Pillow file has one) need the searching
+    decoder (HuffDev::search): a batch mixing such files -- grey, 4:4:4,
+    restart intervals, a noise image long enough for several jobs -- with
+    Pillow files, equal to the host decoder and to Pillow."""
+    import jpeg_enc as J
+
+    assert J.first_long_prefix(J.DEEP_DC[0]) < 2016 and J.first_long_prefix(J.DEEP_AC[0]) < 2016
+    rng = np.random.default_rng(31)
+    datas = [J.encode(rng.integers(0, 256, (37, 53), dtype=np.uint8)),
+             J.encode(_smooth(rng, 120, 97), restart_mcus=3),
+             J.encode(_smooth(rng, 200, 330)[:, :, 0], q=1),
+             J.encode(rng.integers(0, 256, (384, 512, 3), dtype=np.uint8), q=1),
+             _encode(_smooth(rng, 150, 170), quality=85)]
+    prev = capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
+    try:
+        coefs = _check_identity(datas)
+    finally:
+        capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, prev)
+    assert all(c.entropy_pending for c in coefs)

@@ -230,3 +230,22 @@ def test_device_entropy_parse_errors_match_host():
     for dev in (False, True):
         with pytest.raises(capi.MxdError, match="Bogus Huffman table definition"):
             capi.JpegCoefs(bytes(data), device_entropy=dev)
+
+
+def test_deep_huffman_tables_host_decode_matches_pillow():
+    """Huffman tables with many codes longer than 11 bits low in the code
+    space (tests/jpeg_enc.py): the host decoder's slow path equals Pillow's
+    libjpeg-turbo, and the device-entropy parse still takes such files (the
+    GPU decoder searches their tables; tests/test_gpu_jpeg_entropy.py)."""
+    import jpeg_enc as J
+    from PIL import Image
+
+    rng = np.random.default_rng(32)
+    for a, rs in [(rng.integers(0, 256, (45, 61), dtype=np.uint8), 0),
+                  (rng.integers(0, 256, (70, 90, 3), dtype=np.uint8), 5)]:
+        d = J.encode(a, restart_mcus=rs, q=1)
+        want = np.asarray(Image.open(io.BytesIO(d)).convert("RGB"))
+        assert np.array_equal(capi.jpeg_decode(d), want)
+        c = capi.JpegCoefs(d, device_entropy=True)
+        assert c.entropy_pending
+        assert np.array_equal(c.finish(), want)

@@ -161,7 +161,8 @@ struct Opts {
   int krange = 1;
   int phase = 0;      // 1: the anchor / phase-map design; 2: design B (overlap, variants, breaks)
   int overlap = 512;
-  int jobs = 0;       // emulate the round-5 kernel's jobs  // design B: round 0 starts this many bits before each piece     // accept a variant for entry indices its first block's EOB makes equivalent
+  int jobs = 0;       // emulate the round-5 kernel's jobs
+  int r0_overlap = 0; // rounds: round 0 starts each subsequence this many bits early  // design B: round 0 starts this many bits before each piece     // accept a variant for entry indices its first block's EOB makes equivalent
 };
 
 struct Stats {
@@ -189,6 +190,20 @@ bool sync(const Img& im, const Opts& o, std::vector<Sub>& subs, std::vector<Stat
   for (int i = 0; i < n; i++) in[i].pos = subs[i].start;
   std::vector<char> need(n, 0);
   for (int i = 0; i < n; i++) need[i] = !subs[i].last;
+  // round-0 overlap (--r0-overlap W): a subsequence's start state is the
+  // state a decoder from a guess W bits earlier reaches at its start
+  int64_t r0_extra = 0;
+  if (o.r0_overlap > 0)
+    for (int i = 0; i < n; i++) {
+      if (subs[i].first) continue;
+      Sub w = subs[i];
+      w.end = subs[i].start;
+      int64_t stp = 0, bl = 0;
+      in[i] = run(im, w, State{std::max<int64_t>(0, subs[i].start - o.r0_overlap), 0, 0}, &stp, &bl);
+      st.work_steps += stp;
+      r0_extra = std::max(r0_extra, stp);
+    }
+  st.crit_steps += r0_extra;
   for (int round = 0;; round++) {
     std::vector<int> heads;
     for (int i = 0; i < n; i++)
@@ -797,6 +812,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--phase")) o.phase = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--overlap")) o.overlap = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--jobs")) o.jobs = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--r0-overlap")) o.r0_overlap = std::atoi(argv[++i]);
     else files.push_back(argv[i]);
   }
   int nf = 0, bad = 0, maxr = 0;
