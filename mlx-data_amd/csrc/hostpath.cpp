@@ -832,6 +832,23 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
           return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
         if (!sl.huff_err) MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.huff_err), 64, hipHostMallocDefault));
         MXD_HIP(hipMemcpyAsync(sl.huff_err, &ctl->error, sizeof(int32_t), hipMemcpyDeviceToHost, sl.stream));
+#ifdef MXD_HUFF_STAMPS
+        // diagnostic build: the jobs' phase stamps (jpeghuff.hip) appended to $MXD_HUFF_STAMPS_FILE
+        if (const char* path = getenv("MXD_HUFF_STAMPS_FILE")) {
+          std::vector<mxd::HuffPubDev> rec(jc.hjobs.size());
+          MXD_HIP(hipStreamSynchronize(sl.stream));
+          MXD_HIP(hipMemcpy(rec.data(), pub, rec.size() * sizeof(mxd::HuffPubDev), hipMemcpyDeviceToHost));
+          static std::mutex mu;
+          std::lock_guard<std::mutex> lk(mu);
+          if (FILE* f = fopen(path, "ab")) {
+            const int64_t n = (int64_t)rec.size();
+            fwrite(&n, 8, 1, f);
+            for (const auto& r : rec) fwrite(&r.w[5], 8, 3, f);
+            for (const auto& j : jc.hjobs) fwrite(&j, sizeof(j), 1, f);
+            fclose(f);
+          }
+        }
+#endif
       }
       mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),

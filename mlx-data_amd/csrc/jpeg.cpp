@@ -1599,6 +1599,19 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
     o.step[i] = fits ? huff_step_entry(cls, len, sym) : 0;
     if (!fits && first_long == (1 << kHuffLook)) first_long = i;
   }
+  // AC pairs: a symbol other than EOB and the whole next one inside the
+  // kHuffLook bits (the next one's entry is that of the remaining bits
+  // shifted up: its code and value bits lie in them)
+  if (cls) {
+    uint16_t one[1 << kHuffLook];
+    for (int i = 0; i < (1 << kHuffLook); i++) one[i] = (uint16_t)o.step[i];
+    for (int i = 0; i < (1 << kHuffLook); i++) {
+      const int s1 = one[i] & 31, a1 = (one[i] >> 5) & 127;
+      if (!one[i] || a1 == 64 || s1 >= kHuffLook) continue;
+      const uint16_t e2 = one[(i << s1) & ((1 << kHuffLook) - 1)];
+      if (e2 && (e2 & 31) <= kHuffLook - s1) o.step[i] |= (uint32_t)e2 << 16;
+    }
+  }
   // longer codes (canonical: every prefix from first_long up to the top has
   // none that fits) over the top kHuffLong 16-bit patterns, indexed from
   // 65536 - kHuffLong (the kernel's constant base), when they lie there

@@ -62,9 +62,12 @@ constexpr int kHuffWarm = 24;       // warm-up subsequences of a job that starts
 // code starts map to "16 bits, symbol 0", the host decoder's corrupt-code
 // rule).  A table whose long codes reach below the top kHuffLong patterns
 // keeps long_base = 65536, an empty second table, and is searched (maxcode /
-// valoffset / vals).
+// valoffset / vals).  In an AC table's kHuffLook-bit entries, bits 16..31
+// hold a second symbol's step (0: none) when the pattern holds two whole
+// symbols, value bits included, the first of which is not an EOB: the
+// decoder takes both in one lookup (jpeghuff.hip Dec::step).
 struct HuffDev {
-  uint16_t step[1 << kHuffLook];
+  uint32_t step[1 << kHuffLook];
   uint16_t step_long[kHuffLong];
   int32_t long_base;
   int32_t search;  // 1: the two lookups do not cover every pattern (the launch takes the searching kernel)

@@ -185,7 +185,18 @@ struct Shared {
   int32_t flag[2];
   int64_t pred_blocks;             // the previous job's published block index
   int32_t pred_dc[3];
+#ifdef MXD_HUFF_STAMPS
+  uint64_t stamp[8];  // diagnostic build: s_memtime at the phase boundaries
+  int32_t rounds[2], nact[3];
+#endif
 };
+
+#ifdef MXD_HUFF_STAMPS
+#define HUFF_STAMP(i) \
+  if (threadIdx.x == 0) sh.stamp[i] = __builtin_amdgcn_s_memtime()
+#else
+#define HUFF_STAMP(i)
+#endif
 
 // Block-wide exclusive prefix sum of v (every thread of the workgroup calls it).
 __device__ int block_exclusive_scan(int v, int* totals, int* total_out) {
@@ -239,35 +250,48 @@ struct Dec {
   }
   __device__ __forceinline__ int comp() const { return (cpack >> (2 * b)) & 3; }
 
-  // Decodes one symbol; returns true at the end of a block (b, k advanced to
-  // the next block's start).  on_sym(dc, position, value) receives every
+  // Decodes one step -- one symbol, or two (jpeghuff.h HuffDev: an AC
+  // table's entry pairs a symbol with the next one when both, value bits
+  // included, lie inside the kHuffLook-bit lookup); returns true at the end
+  // of a block (b, k advanced to the next block's start).  The second symbol
+  // is taken only when the first does not end its block and ends before
+  // `rem` (the bits left to the decode's end, decremented by what the step
+  // consumes) runs out, so a decode stops at the same symbol boundary as one
+  // symbol at a time would.  on_sym(dc, position, value, size) receives every
   // symbol's store: the DC difference at 0, a coefficient at its index, an
   // EOB's / ZRL's zero at an index of the block not yet written (so no
   // branch; a corrupt run past 63 lands on 63, as jpeg_natural_order's extra
-  // entries put it).  One lookup gives the bits a symbol consumes, the index
-  // advance and the value bits; codes longer than kHuffLook bits come from
-  // the second table, read beside the first (no branch), and only tables too
-  // large for it search.
+  // entries put it); a step of one symbol repeats its store as the second
+  // (dc false: the DC sums count it once).  Codes longer than kHuffLook bits
+  // come from the second table, read beside the first (no branch), and only
+  // tables too large for it search.
   template <class Reader, class OnSym>
-  __device__ __forceinline__ bool step(Reader& r, OnSym&& on_sym) {
+  __device__ __forceinline__ bool step(Reader& r, int32_t& rem, OnSym&& on_sym) {
     r.refill_if();  // >= 33 bits buffered: a step consumes <= 16 + 15
     const bool dc = k == 0;
     const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
     const uint32_t top16 = (uint32_t)(r.buf >> 48);
-    const int st1 = t.step[top16 >> (16 - kHuffLook)];
-    const int st2 = t.step_long[max((int)top16 - (65536 - kHuffLong), 0)];  // no dependent load of a base
-    int st = st1 ? st1 : st2;
+    const uint32_t st1 = t.step[top16 >> (16 - kHuffLook)];
+    const uint32_t st2 = t.step_long[max((int)top16 - (65536 - kHuffLong), 0)];  // no dependent load of a base
+    uint32_t st = st1 ? st1 : st2;
     if constexpr (SEARCH) {  // launches with a table the two lookups do not cover
       if (!st) st = huff_search_step(t, r.buf, dc ? 0 : 1);
     }
-    const int shift = st & 31, adv = (st >> 5) & 127, sz = st >> 12;
-    // value bits: the sz bits after the code, in the buffer's top 32 bits (shift <= 31)
+    const int s1 = st & 31, a1 = (st >> 5) & 127, z1 = (st >> 12) & 15;
+    const int s2 = (st >> 16) & 31, a2 = (st >> 21) & 127, z2 = st >> 28;
+    const int k1 = k + a1;
+    const bool two = s2 != 0 && k1 < 64 && s1 < rem;
+    // value bits: the sz bits after each code, in the buffer's top 32 bits (s1 <= 31; a pair within 11)
     const uint32_t hi = (uint32_t)(r.buf >> 32);
-    const uint32_t raw = sz ? (hi >> (32 - shift)) & ((1u << sz) - 1u) : 0u;
+    const uint32_t raw1 = z1 ? (hi >> (32 - s1)) & ((1u << z1) - 1u) : 0u;
+    on_sym(dc, min(k1 - 1, 63), raw1, z1);
+    const int knew = two ? k1 + a2 : k1;
+    const uint32_t raw2 = z2 ? ((hi << s1) >> (32 - s2)) & ((1u << z2) - 1u) : 0u;
+    on_sym(false, min(knew - 1, 63), two ? raw2 : raw1, two ? z2 : z1);
+    const int shift = two ? s1 + s2 : s1;
     r.buf <<= shift;
     r.cnt -= shift;
-    const int knew = k + adv;
-    on_sym(dc, min(knew - 1, 63), raw, sz);
+    rem -= shift;
     const bool end = knew >= 64;
     k = end ? 0 : knew;
     b = end ? (b + 1 == bpm ? 0 : b + 1) : b;
@@ -335,11 +359,20 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
   Dec<SEARCH> dec;
   dec.init(sh.img, tab);
   R rd;
+#ifdef MXD_HUFF_STAMPS
+  int round = 0;
+#endif
   for (;;) {
     // this round's subsequences, compacted onto the first threads, so a
     // round in which few start states changed runs few waves
     int nact = 0;
     const int slot = block_exclusive_scan(need ? 1 : 0, sh.scan, &nact);
+#ifdef MXD_HUFF_STAMPS
+    if (t == 0) {
+      if (fixed < 0 && round > 0 && round < 4) sh.nact[round - 1] = nact;
+      sh.rounds[fixed < 0 ? 0 : 1] = ++round;
+    }
+#endif
     if (nact == 0) break;  // uniform
     if (need) sh.list[slot] = (int16_t)t;
     __syncthreads();
@@ -352,14 +385,15 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
       dec.k = sh.in_k[id];
       int done = 0;
       const auto nop = [](bool, int, uint32_t, int) {};
+      int32_t rem = v.end - sh.in_pos[id];
       // a step consumes <= 31 bits: while the end is further than one step,
       // two steps both start before it
-      while (rd.pos() + 31 < v.end) {
-        done += dec.step(rd, nop) ? 1 : 0;
-        done += dec.step(rd, nop) ? 1 : 0;
+      while (rem > 31) {
+        done += dec.step(rd, rem, nop) ? 1 : 0;
+        done += dec.step(rd, rem, nop) ? 1 : 0;
       }
-      while (rd.pos() < v.end) done += dec.step(rd, nop) ? 1 : 0;
-      sh.out_pos[id] = rd.pos();
+      while (rem > 0) done += dec.step(rd, rem, nop) ? 1 : 0;
+      sh.out_pos[id] = v.end - rem;
       sh.out_b[id] = (int8_t)dec.b;
       sh.out_k[id] = (int8_t)dec.k;
       sh.done[id] = done;
@@ -416,6 +450,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
 
   // 1. rounds from the guessed starts (segment starts are exact)
   sync_rounds<R, SEARCH>(wbase, sh, tab, seg, nsub, u, act && !u.seg_last);
+  HUFF_STAMP(2);
 
   // 2. the previous job's exit: the true start of the first own subsequence
   if (job.pred) {
@@ -439,6 +474,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
       sync_rounds<R, SEARCH>(wbase, sh, tab, seg, nsub, u, t == job.warm && !u.seg_last, job.warm);
   }
 
+  HUFF_STAMP(3);
   // 3. first block of each own subsequence: the blocks its segment's earlier
   // own subsequences complete, from the segment's start (or, for the segment
   // the job continues, from the previous job's block index)
@@ -507,10 +543,10 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
       return coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
     };
     int16_t* blk = addr();
+    int32_t rem = u.end - sh.in_pos[t];
     for (;;) {
-      const int32_t p = rd.pos();
-      if (p >= u.end || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && p > u.sg.bits)) break;
-      const bool fin = dec.step(rd, [&](bool dc, int kk, uint32_t raw, int sz) {
+      if (rem <= 0 || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && u.end - rem > u.sg.bits)) break;
+      const bool fin = dec.step(rd, rem, [&](bool dc, int kk, uint32_t raw, int sz) {
         const int v = extend(raw, sz);
         const int c = dec.comp();
         dcsum[0] += dc && c == 0 ? v : 0;
@@ -541,6 +577,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     for (int c = 0; c < 3; c++) sh.pred_dc[c] = (int32_t)(uint32_t)wait_pub(p, 2 + c, ctl);
   }
   int last_sum[3];
+  HUFF_STAMP(4);  // (thread 0's write pass; the scans below wait for the others)
   for (int c = 0; c < 3; c++) {
     int total = 0;
     const int ex = block_exclusive_scan(act && u.own ? dcsum[c] : 0, sh.scan, &total);
@@ -568,6 +605,22 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
       d[0] = (int16_t)pred[c];
     }
   }
+#ifdef MXD_HUFF_STAMPS
+  __syncthreads();
+  if (t == 0) {
+    // diagnostic build only: publication words 5..7, which nothing reads
+    const uint64_t* st = sh.stamp;
+    auto d = [&](int a, int b) { return std::min<uint64_t>((st[b] - st[a]) >> 4, (1u << 21) - 1); };
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    HuffPubDev* p = pub + sh.ticket;
+    p->w[5] = d(0, 1) | d(1, 2) << 21 | d(2, 3) << 42;
+    p->w[6] = d(3, 4) | std::min<uint64_t>((now - st[4]) >> 4, (1u << 21) - 1) << 21 |
+              (uint64_t)(sh.rounds[0] & 63) << 42 | (uint64_t)(sh.rounds[1] & 63) << 48;
+    p->w[7] = (uint64_t)(sh.nact[0] & 2047) | (uint64_t)(sh.nact[1] & 2047) << 11 |
+              (uint64_t)(sh.nact[2] & 2047) << 22 | (uint64_t)(st[7] & 0x3ffffffull) << 33 |
+              (uint64_t)(sh.ticket & 15) << 59;
+  }
+#endif
 }
 
 template <bool SEARCH>
@@ -580,6 +633,14 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   __shared__ Shared sh;
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   const int t = threadIdx.x;
+#ifdef MXD_HUFF_STAMPS
+  if (t == 0) {
+    sh.stamp[0] = __builtin_amdgcn_s_memtime();
+    sh.stamp[7] = __builtin_amdgcn_s_memrealtime();
+    sh.rounds[0] = sh.rounds[1] = 0;
+    sh.nact[0] = sh.nact[1] = sh.nact[2] = 0;
+  }
+#endif
   // 0. the job: tickets in the order workgroups start (a job only ever waits
   // for a smaller ticket, i.e. for a workgroup that has started)
   if (t == 0) {
@@ -652,6 +713,7 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     sh.done[t] = 0;
   }
   __syncthreads();
+  HUFF_STAMP(1);
   if (job.lds)  // uniform over the workgroup
     decode_job<LdsReader, SEARCH>(lds_words, sh, tab, seg, nsub, coef, pub, ctl);
   else

@@ -86,7 +86,7 @@ bool step(const Img& im, const Seg& s, State& st, int* kk = nullptr, int* v = nu
   const bool dc = st.k == 0;
   const HuffDev& t = im.tab[dc ? im.es.blk_dc[st.b] : im.es.blk_ac[st.b]];
   const uint64_t buf = peek64(s, st.pos);
-  int e = t.step[(uint32_t)(buf >> (64 - kHuffLook))];
+  int e = t.step[(uint32_t)(buf >> (64 - kHuffLook))] & 0xffff;  // one symbol a step (the kernel pairs some)
   {
     // code length histogram (diagnostics): the code's length is the step's consumed bits minus the value bits
     int len, sym;
@@ -149,6 +149,7 @@ State run(const Img& im, const Sub& u, State in, int64_t* steps, int64_t* blocks
 
 int64_t g_chg[3] = {0, 0, 0};
 int64_t g_len[18] = {0};
+int64_t g_pair[4][3] = {{0}};
 int64_t g_walk[4] = {0, 0, 0, 0};  // walk steps into a variant follower: all, same pos, same k class, accepted  // changes after round 0: all, same position, same position and index
 
 struct PhaseStats;
@@ -781,8 +782,29 @@ bool write_check(const Img& im, const std::vector<Sub>& subs, const std::vector<
       int16_t* blk = coef.data() + cp.off + (by * cp.bw + bx) * 64;
       const bool dc = stt.k == 0;
       int kk, v;
+      const int64_t p0 = stt.pos;
       const bool fin = step(im, s, stt, &kk, &v);
       st.write_steps++;
+      {
+        // pairing model (--pairs): greedy pairs of consecutive symbols of one block whose bits fit L
+        extern int64_t g_pair[4][3];
+        static int prev_len = -1, prev_dc = 0;
+        const int len = (int)(stt.pos - p0);
+        for (int L = 0; L < 4; L++) (void)L;
+        if (prev_len >= 0) {
+          // the previous symbol waits for a partner: this one (same block: the previous did not end it)
+          for (int L = 0; L < 4; L++) {
+            const int win = 10 + L;
+            if (prev_len + len <= win) g_pair[L][prev_dc ? 1 : 0]++;
+          }
+          prev_len = -1;
+        } else if (!fin) {
+          prev_len = len;
+          prev_dc = dc;
+        }
+        if (fin) prev_len = -1;
+        g_pair[0][2]++;
+      }
       if (dc) {
         pred[ci] += v;
         blk[0] = (int16_t)pred[ci];
@@ -902,6 +924,9 @@ int main(int argc, char** argv) {
   if (g_walk[0])
     std::printf("walk: %lld steps, same pos %.1f %%, same k class %.1f %%, accepted %.1f %%\n", (long long)g_walk[0],
                 100.0 * g_walk[1] / g_walk[0], 100.0 * g_walk[2] / g_walk[0], 100.0 * g_walk[3] / g_walk[0]);
+  for (int L = 0; L < 4; L++)
+    std::printf("pairs in %d bits: AC-AC %.1f %%, DC-AC %.1f %% of symbols paired\n", 10 + L,
+                200.0 * g_pair[L][0] / g_pair[0][2], 200.0 * g_pair[L][1] / g_pair[0][2]);
   std::printf("heads per round:");
   for (int r = 0; r < 20 && heads_sum[r] > 0; r++) std::printf(" %.0f/%.0f", heads_sum[r] / nf, items_sum[r] / nf);
   std::printf("\n");

@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--huff-global", action="store_true", help="device entropy: also time every length with words read from device memory")
     ap.add_argument("--no-host", action="store_true", help="skip the host entropy decode runs")
     ap.add_argument("--huff-job", default="0", help="device entropy: own subsequences per job to time (0: default)")
+    ap.add_argument("--seconds", type=float, default=2.0, help="timed loop length per run")
     args = ap.parse_args()
     from mlx_data_amd import capi
 
@@ -97,7 +98,7 @@ def main():
             for _ in range(3):
                 capi.jpeg_resize_crop_to_device(arr, n, capi.MXD_F32_DIV255, 0)
             k, t0 = 0, time.perf_counter()
-            while time.perf_counter() - t0 < 2.0:
+            while time.perf_counter() - t0 < args.seconds:
                 capi.jpeg_resize_crop_to_device(arr, n, capi.MXD_F32_DIV255, 0)
                 k += 1
             ms = (time.perf_counter() - t0) / k * 1e3
