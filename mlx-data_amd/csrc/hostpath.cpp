@@ -841,9 +841,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
           static std::mutex mu;
           std::lock_guard<std::mutex> lk(mu);
           if (FILE* f = fopen(path, "ab")) {
-            const int64_t n = (int64_t)rec.size();
+            const int64_t n = (int64_t)rec.size(), words = mxd::kHuffPubWords - 8;
             fwrite(&n, 8, 1, f);
-            for (const auto& r : rec) fwrite(&r.w[5], 8, 3, f);
+            fwrite(&words, 8, 1, f);
+            for (const auto& r : rec) fwrite(&r.w[8], 8, mxd::kHuffPubWords - 8, f);
             for (const auto& j : jc.hjobs) fwrite(&j, sizeof(j), 1, f);
             fclose(f);
           }

@@ -135,11 +135,16 @@ static_assert(sizeof(HuffJobDev) == 40, "HuffJobDev layout");
 // subsequence's exit state (bit position in bits 0..31, block of the MCU in
 // 32..39, coefficient index in 40..47), [1] the block index there, [2..4]
 // the DC-difference sums of that segment up to there, per component.
+#ifdef MXD_HUFF_STAMPS
+constexpr int kHuffPubWords = 32;  // diagnostic build: words 8.. hold the job's phase stamps (jpeghuff.hip)
+#else
+constexpr int kHuffPubWords = 8;
+#endif
 struct HuffPubDev {
-  uint64_t w[8];
+  uint64_t w[kHuffPubWords];
 };
 constexpr uint64_t kHuffValid = (uint64_t)1 << 63;
-static_assert(sizeof(HuffPubDev) == 64, "HuffPubDev layout");
+static_assert(sizeof(HuffPubDev) == 8 * kHuffPubWords, "HuffPubDev layout");
 
 // Launch control (device memory, zeroed before the launch): the job ticket
 // counter and an error word (1: a job gave up waiting for its predecessor).

@@ -182,12 +182,19 @@ struct Shared {
   int16_t sub_seg[kHuffThreads];   // segment of each subsequence
   int16_t list[kHuffThreads];      // this round's subsequences to decode (compacted)
   int32_t scan[kHuffThreads / 64];
+  int3 scan3[kHuffThreads / 64];
   int32_t flag[2];
   int64_t pred_blocks;             // the previous job's published block index
   int32_t pred_dc[3];
 #ifdef MXD_HUFF_STAMPS
-  uint64_t stamp[8];  // diagnostic build: s_memtime at the phase boundaries
-  int32_t rounds[2], nact[3];
+  // diagnostic build: s_memtime at the phase boundaries ([0] start, [1]
+  // loaded, [2] rounds done, [3] predecessor handled, [4] thread 0's write
+  // pass done), at the end of each of the first kRoundStamps rounds, and the
+  // lanes of each of them
+  uint64_t stamp[8];
+  uint64_t round_end[16];
+  int32_t nact[16];
+  int32_t rounds[2];
 #endif
 };
 
@@ -226,6 +233,42 @@ __device__ int block_exclusive_scan(int v, int* totals, int* total_out) {
   return before + x - v;
 }
 
+// The same over three ints at once (one set of barriers).
+__device__ void block_exclusive_scan3(const int* v, int* out, int3* totals) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  int x0 = v[0], x1 = v[1], x2 = v[2];
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y0 = __shfl_up(x0, d, 64), y1 = __shfl_up(x1, d, 64), y2 = __shfl_up(x2, d, 64);
+    if (lane >= d) {
+      x0 += y0;
+      x1 += y1;
+      x2 += y2;
+    }
+  }
+  if (lane == 63) totals[wave] = make_int3(x0, x1, x2);
+  __syncthreads();
+  if (wave == 0) {
+    int3 t = lane < nw ? totals[lane] : make_int3(0, 0, 0);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y0 = __shfl_up(t.x, d, 64), y1 = __shfl_up(t.y, d, 64), y2 = __shfl_up(t.z, d, 64);
+      if (lane >= d) {
+        t.x += y0;
+        t.y += y1;
+        t.z += y2;
+      }
+    }
+    if (lane < nw) totals[lane] = t;
+  }
+  __syncthreads();
+  const int3 before = wave > 0 ? totals[wave - 1] : make_int3(0, 0, 0);
+  __syncthreads();
+  out[0] = before.x + x0 - v[0];
+  out[1] = before.y + x1 - v[1];
+  out[2] = before.z + x2 - v[2];
+}
+
 // Decoder state machine over one segment: block b of the MCU, next
 // coefficient k (0 = the DC difference), symbols from Reader r.
 template <bool SEARCH>
@@ -261,8 +304,7 @@ struct Dec {
   // symbol's store: the DC difference at 0, a coefficient at its index, an
   // EOB's / ZRL's zero at an index of the block not yet written (so no
   // branch; a corrupt run past 63 lands on 63, as jpeg_natural_order's extra
-  // entries put it); a step of one symbol repeats its store as the second
-  // (dc false: the DC sums count it once).  Codes longer than kHuffLook bits
+  // entries put it).  Codes longer than kHuffLook bits
   // come from the second table, read beside the first (no branch), and only
   // tables too large for it search.
   template <class Reader, class OnSym>
@@ -286,8 +328,10 @@ struct Dec {
     const uint32_t raw1 = z1 ? (hi >> (32 - s1)) & ((1u << z1) - 1u) : 0u;
     on_sym(dc, min(k1 - 1, 63), raw1, z1);
     const int knew = two ? k1 + a2 : k1;
-    const uint32_t raw2 = z2 ? ((hi << s1) >> (32 - s2)) & ((1u << z2) - 1u) : 0u;
-    on_sym(false, min(knew - 1, 63), two ? raw2 : raw1, two ? z2 : z1);
+    if (two) {
+      const uint32_t raw2 = z2 ? ((hi << s1) >> (32 - s2)) & ((1u << z2) - 1u) : 0u;
+      on_sym(false, min(knew - 1, 63), raw2, z2);
+    }
     const int shift = two ? s1 + s2 : s1;
     r.buf <<= shift;
     r.cnt -= shift;
@@ -369,7 +413,10 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
     const int slot = block_exclusive_scan(need ? 1 : 0, sh.scan, &nact);
 #ifdef MXD_HUFF_STAMPS
     if (t == 0) {
-      if (fixed < 0 && round > 0 && round < 4) sh.nact[round - 1] = nact;
+      if (fixed < 0 && round < 16) {
+        sh.nact[round] = nact;
+        sh.round_end[round] = __builtin_amdgcn_s_memtime();  // the previous round's end
+      }
       sh.rounds[fixed < 0 ? 0 : 1] = ++round;
     }
 #endif
@@ -490,6 +537,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
   const int64_t seg_block0 = continued ? sh.pred_blocks : (int64_t)u.sg.mcu0 * im.bpm;
   const int64_t seg_block1 = ((int64_t)u.sg.mcu0 + u.sg.mcus) * im.bpm;
   int64_t g = seg_block0 + (act ? before - sh.done[seg_first] : 0);
+  const int64_t g_first = g;
   if (act && u.job_last && !u.seg_last) {  // publish the exit for the next job
     HuffPubDev* p = pub + sh.ticket;
     publish(p, 1, (uint64_t)(g + my_done));
@@ -502,6 +550,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
   dec.init(im, tab);
   int dcsum[3] = {0, 0, 0};
   int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
+  uint32_t cur0[3] = {0, 0, 0};  // the block cursor (block of the MCU, MCU column, row) at the first block
   if (act && u.own) {
     // Zero the coefficient positions this subsequence decodes (the pass
     // below stores only the symbols' positions): the rest of the block it
@@ -513,6 +562,9 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     // insufficient-data rule).
     {
       auto zero = [&](int64_t b, int k0, int k1) {
+#ifdef MXD_HUFF_NOSTORE_ZERO  // diagnostic build (wrong results): no zeroing stores
+        return;
+#endif
         int16_t* d = coef + block_addr(im, b);
         if (k0 == 0 && k1 == 64) {
           uint4* z = reinterpret_cast<uint4*>(d);
@@ -539,6 +591,9 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
     const uint32_t g0 = (uint32_t)min(g, seg_block1 - 1), m0 = g0 / bpm;
     uint32_t cj = g0 - m0 * bpm, cmy = m0 / mcux, cmx = m0 - cmy * mcux;
+    cur0[0] = cj;
+    cur0[1] = cmx;
+    cur0[2] = cmy;
     auto addr = [&]() {
       return coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
     };
@@ -554,7 +609,13 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
         dcsum[2] += dc && c == 2 ? v : 0;
         dc0 = dc && dc0 < 0 ? g : dc0;
         dc1 = dc ? g + 1 : dc1;
-        blk[kk] = (int16_t)v;  // zig-zag order (jpeg_idct reorders)
+        // zig-zag order (jpeg_idct reorders); zeros (EOB, ZRL, a zero DC
+        // difference) land on positions zeroed above
+#ifndef MXD_HUFF_NOSTORE_COEF  // diagnostic build (wrong results): no coefficient stores
+        if (v != 0) blk[kk] = (int16_t)v;
+#else
+        if (v == 12345) blk[kk] = 0;
+#endif
       });
       if (fin) {
         g++;
@@ -576,49 +637,82 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     const HuffPubDev* p = pub + sh.ticket - 1;
     for (int c = 0; c < 3; c++) sh.pred_dc[c] = (int32_t)(uint32_t)wait_pub(p, 2 + c, ctl);
   }
-  int last_sum[3];
   HUFF_STAMP(4);  // (thread 0's write pass; the scans below wait for the others)
+  // one scan for the three components
+  int ex[3];
+  {
+    const int z[3] = {0, 0, 0};
+    block_exclusive_scan3(act && u.own ? dcsum : z, ex, sh.scan3);
+  }
+  __syncthreads();
+  // (the start / exit arrays are free now: they hold the three prefixes)
+  sh.done[t] = ex[0];
+  sh.in_pos[t] = ex[1];
+  sh.out_pos[t] = ex[2];
+  __syncthreads();
+  const int first3[3] = {sh.done[seg_first], sh.in_pos[seg_first], sh.out_pos[seg_first]};
+  int last_sum[3];
   for (int c = 0; c < 3; c++) {
-    int total = 0;
-    const int ex = block_exclusive_scan(act && u.own ? dcsum[c] : 0, sh.scan, &total);
-    __syncthreads();
-    sh.done[t] = ex;
-    __syncthreads();
     const int base = continued ? sh.pred_dc[c] : 0;
-    const int at_first = sh.done[seg_first];
-    const int mine = dcsum[c];
-    dcsum[c] = act && u.own ? base + ex - at_first : 0;  // this subsequence's predictor start
-    last_sum[c] = dcsum[c] + mine;                       // through this subsequence
-    __syncthreads();
+    const int m = dcsum[c];
+    dcsum[c] = act && u.own ? base + ex[c] - first3[c] : 0;  // this subsequence's predictor start
+    last_sum[c] = dcsum[c] + m;                              // through this subsequence
   }
   if (act && u.job_last && !u.seg_last) {
     HuffPubDev* p = pub + sh.ticket;
     for (int c = 0; c < 3; c++) publish(p, 2 + c, (uint64_t)(uint32_t)last_sum[c]);
   }
   if (act && u.own && dc0 >= 0) {
-    int pred[3] = {dcsum[0], dcsum[1], dcsum[2]};
-    for (int64_t b = dc0; b < dc1; b++) {
-      const int bj = (int)(b % im.bpm);
-      const int c = im.blk_comp[bj];
-      int16_t* d = coef + block_addr(im, b);
-      pred[c] += d[0];
-      d[0] = (int16_t)pred[c];
+    // the DC differences of blocks [dc0, dc1) into values, four blocks' loads
+    // issued together (the cursor of the write pass, from its first block)
+    uint32_t cj = cur0[0], cmx = cur0[1], cmy = cur0[2];
+    const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
+    auto next = [&]() {
+      cj++;
+      const bool wrap = cj == bpm;
+      cj = wrap ? 0 : cj;
+      cmx += wrap ? 1 : 0;
+      const bool row = cmx == mcux;
+      cmx = row ? 0 : cmx;
+      cmy += row ? 1 : 0;
+    };
+    if (dc0 > g_first) next();  // the first block's DC belonged to the previous subsequence
+    int p0 = dcsum[0], p1 = dcsum[1], p2 = dcsum[2];
+    const uint32_t cpack = dec.cpack;
+    for (int64_t q = dc0; q < dc1; q += 4) {
+      int16_t* a[4];
+      int cc[4];
+      int16_t v[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        a[r] = coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
+        cc[r] = (int)((cpack >> (2 * cj)) & 3);
+        next();
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[r] = q + r < dc1 ? a[r][0] : (int16_t)0;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        if (q + r < dc1) {
+          const int x = (cc[r] == 0 ? (p0 += v[r]) : cc[r] == 1 ? (p1 += v[r]) : (p2 += v[r]));
+          a[r][0] = (int16_t)x;
+        }
+      }
     }
   }
 #ifdef MXD_HUFF_STAMPS
   __syncthreads();
   if (t == 0) {
-    // diagnostic build only: publication words 5..7, which nothing reads
-    const uint64_t* st = sh.stamp;
-    auto d = [&](int a, int b) { return std::min<uint64_t>((st[b] - st[a]) >> 4, (1u << 21) - 1); };
-    const uint64_t now = __builtin_amdgcn_s_memtime();
+    // diagnostic build only: publication words 8.., which nothing reads
     HuffPubDev* p = pub + sh.ticket;
-    p->w[5] = d(0, 1) | d(1, 2) << 21 | d(2, 3) << 42;
-    p->w[6] = d(3, 4) | std::min<uint64_t>((now - st[4]) >> 4, (1u << 21) - 1) << 21 |
-              (uint64_t)(sh.rounds[0] & 63) << 42 | (uint64_t)(sh.rounds[1] & 63) << 48;
-    p->w[7] = (uint64_t)(sh.nact[0] & 2047) | (uint64_t)(sh.nact[1] & 2047) << 11 |
-              (uint64_t)(sh.nact[2] & 2047) << 22 | (uint64_t)(st[7] & 0x3ffffffull) << 33 |
-              (uint64_t)(sh.ticket & 15) << 59;
+    sh.stamp[5] = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < 6; i++) p->w[8 + i] = sh.stamp[i];
+    p->w[14] = sh.stamp[7];  // s_memrealtime at the start
+    p->w[15] = (uint64_t)sh.rounds[0] | (uint64_t)sh.rounds[1] << 8 | (uint64_t)sh.ticket << 16;
+    for (int i = 0; i < 16; i++) {
+      const bool have = i < sh.rounds[0];
+      p->w[16 + i] = have ? (sh.round_end[i] & 0xffffffffffull) | (uint64_t)sh.nact[i] << 40 : 0;
+    }
   }
 #endif
 }
@@ -638,7 +732,6 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     sh.stamp[0] = __builtin_amdgcn_s_memtime();
     sh.stamp[7] = __builtin_amdgcn_s_memrealtime();
     sh.rounds[0] = sh.rounds[1] = 0;
-    sh.nact[0] = sh.nact[1] = sh.nact[2] = 0;
   }
 #endif
   // 0. the job: tickets in the order workgroups start (a job only ever waits

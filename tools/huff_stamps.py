@@ -1,7 +1,9 @@
 """Summarises the entropy decode's phase stamps (diagnostic build
--DMXD_HUFF_STAMPS, tools/r05_stamps.sh): per launch size, the median and
-max over jobs of each phase's shader cycles, the synchronisation rounds and
-the lanes of rounds 2..4, and the spread of the jobs' start times.
+-DMXD_HUFF_STAMPS, tools/r05_stamps.sh): per launch size, over jobs, the
+median / p90 / max shader cycles of each phase (load, rounds, predecessor,
+thread 0's write pass, the rest), the median cycles and lanes of each
+synchronisation round, the rounds histogram and the spread of the jobs'
+start times.
   python tools/huff_stamps.py FILE [skip]"""
 import json
 import struct
@@ -17,14 +19,19 @@ def read(path):
         b = f.read()
     i = 0
     while i < len(b):
-        (n,) = struct.unpack_from("<q", b, i)
-        i += 8
-        w = np.frombuffer(b, np.uint64, 3 * n, i).reshape(n, 3)
-        i += 24 * n
+        n, nw = struct.unpack_from("<qq", b, i)
+        i += 16
+        w = np.frombuffer(b, np.uint64, nw * n, i).reshape(n, nw).astype(np.int64)
+        i += 8 * nw * n
         jobs = np.frombuffer(b, np.int32, 10 * n, i).reshape(n, 10)
         i += 40 * n
         out.append((w, jobs))
     return out
+
+
+def stat(a):
+    a = np.asarray(a)
+    return dict(med=int(np.median(a)), p90=int(np.percentile(a, 90)), max=int(a.max()))
 
 
 def main():
@@ -34,29 +41,31 @@ def main():
     for w, jobs in recs[skip:]:
         by[len(w)].append((w, jobs))
     for n, runs in sorted(by.items()):
-        ph = defaultdict(list)
-        spread, rnd, nact = [], [], []
-        for w, jobs in runs:
-            m = (1 << 21) - 1
-            w5, w6, w7 = w[:, 0], w[:, 1], w[:, 2]
-            cols = dict(load=w5 & m, rounds=(w5 >> 21) & m, pred=(w5 >> 42) & m, write=w6 & m, tail=(w6 >> 21) & m)
-            for k, v in cols.items():
-                ph[k].append(v.astype(np.int64) * 16)
-            ph["total"].append(sum(v.astype(np.int64) for v in cols.values()) * 16)
-            rnd.append(((w6 >> 42) & 63).astype(np.int64))
-            ph["rounds_fix"].append(((w6 >> 48) & 63).astype(np.int64))
-            nact.append(np.stack([(w7 >> s) & 2047 for s in (0, 11, 22)], 1).astype(np.int64))
-            rt = ((w7 >> 33) & 0x3ffffff).astype(np.int64)
-            spread.append(int(rt.max() - rt.min()) * 10)  # ns (100 MHz)
+        W = np.concatenate([w for w, _ in runs])
+        st = W[:, 0:6]
+        names = ["load", "rounds", "pred", "write0", "rest"]
         line = dict(jobs=n, launches=len(runs))
-        for k, v in ph.items():
-            a = np.concatenate(v)
-            line[k] = dict(med=int(np.median(a)), p90=int(np.percentile(a, 90)), max=int(a.max()))
-        r = np.concatenate(rnd)
-        line["rounds_hist"] = {int(k): int(c) for k, c in zip(*np.unique(r, return_counts=True))}
-        line["nact_med"] = [int(x) for x in np.median(np.concatenate(nact), 0)]
+        for i, k in enumerate(names):
+            line[k] = stat(st[:, i + 1] - st[:, i])
+        line["total"] = stat(st[:, 5] - st[:, 0])
+        rounds = W[:, 7] & 255
+        line["rounds_hist"] = {int(k): int(c) for k, c in zip(*np.unique(rounds, return_counts=True))}
+        R = W[:, 8:24]
+        t_end = R & ((1 << 40) - 1)
+        lanes = R >> 40
+        per = []
+        for r in range(1, 12):
+            ok = rounds > r
+            if ok.sum() < len(W) // 2:
+                break
+            prev = np.where(r == 1, st[:, 1], 0) if False else t_end[:, r - 1]
+            d = (t_end[:, r] - t_end[:, r - 1])[ok]
+            per.append(dict(round=r, lanes=int(np.median(lanes[ok, r - 1])), cycles=int(np.median(d))))
+        line["per_round"] = per
+        line["first_scan"] = int(np.median(t_end[:, 0] - st[:, 1]))
+        rt = W[:, 6]
+        line["start_spread_ns_med"] = int(np.median([(w[:, 6].max() - w[:, 6].min()) * 10 for w, _ in runs]))
         line["nsub_med"] = int(np.median(np.concatenate([j[:, 5] for _, j in runs])))
-        line["start_spread_ns_med"] = int(np.median(spread))
         print(json.dumps(line))
 
 
