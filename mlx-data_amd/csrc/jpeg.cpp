@@ -1591,26 +1591,24 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
     *sym = 0;
   };
   // step table over kHuffLook bits (0: a longer code or none)
+  uint16_t one[1 << kHuffLook];
   int first_long = 1 << kHuffLook;  // the first kHuffLook-bit prefix without a code that fits it
   for (int i = 0; i < (1 << kHuffLook); i++) {
     int len, sym;
     code_at((uint32_t)i << (16 - kHuffLook), &len, &sym);
     const bool fits = len <= kHuffLook && (int32_t)(i >> (kHuffLook - len)) <= h.maxcode[len];
-    o.step[i] = fits ? huff_step_entry(cls, len, sym) : 0;
+    one[i] = fits ? huff_step_entry(cls, len, sym) : 0;
     if (!fits && first_long == (1 << kHuffLook)) first_long = i;
   }
   // AC pairs: a symbol other than EOB and the whole next one inside the
   // kHuffLook bits (the next one's entry is that of the remaining bits
   // shifted up: its code and value bits lie in them)
-  if (cls) {
-    uint16_t one[1 << kHuffLook];
-    for (int i = 0; i < (1 << kHuffLook); i++) one[i] = (uint16_t)o.step[i];
-    for (int i = 0; i < (1 << kHuffLook); i++) {
-      const int s1 = one[i] & 31, a1 = (one[i] >> 5) & 127;
-      if (!one[i] || a1 == 64 || s1 >= kHuffLook) continue;
-      const uint16_t e2 = one[(i << s1) & ((1 << kHuffLook) - 1)];
-      if (e2 && (e2 & 31) <= kHuffLook - s1) o.step[i] |= (uint32_t)e2 << 16;
-    }
+  for (int i = 0; i < (1 << kHuffLook); i++) {
+    o.step[i] = huff_step_single(one[i]);
+    const int s1 = one[i] & 31, a1 = (one[i] >> 5) & 127;
+    if (!cls || !one[i] || a1 == 64 || s1 >= kHuffLook) continue;
+    const uint16_t e2 = one[(i << s1) & ((1 << kHuffLook) - 1)];
+    if (e2 && (e2 & 31) <= kHuffLook - s1) o.step[i] = huff_step_pair(one[i], e2);
   }
   // longer codes (canonical: every prefix from first_long up to the top has
   // none that fits) over the top kHuffLong 16-bit patterns, indexed from
@@ -1620,14 +1618,14 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   o.search = 1;
   if (65536 - base <= kHuffLong) {
     bool ok = true;
-    for (int i = first_long; i < (1 << kHuffLook); i++) ok = ok && o.step[i] == 0;
+    for (int i = first_long; i < (1 << kHuffLook); i++) ok = ok && one[i] == 0;
     if (ok) {
       o.search = 0;
       o.long_base = base;
       for (int32_t v = base; v < 65536; v++) {
         int len, sym;
         code_at((uint32_t)v, &len, &sym);
-        o.step_long[v - (65536 - kHuffLong)] = huff_step_entry(cls, len, sym);
+        o.step_long[v - (65536 - kHuffLong)] = huff_step_single(huff_step_entry(cls, len, sym));
       }
     }
   }

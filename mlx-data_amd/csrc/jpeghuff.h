@@ -57,18 +57,22 @@ constexpr int kHuffWarm = 24;       // warm-up subsequences of a job that starts
 // the coefficient-index advance (DC 1; a coefficient run + 1; ZRL 16; EOB
 // 64), 12..15 the value bits -- over kHuffLook bits (0: a longer code), and
 // for the longer codes over the top kHuffLong 16-bit patterns, indexed from
-// 65536 - kHuffLong (canonical codes: every code longer than kHuffLook bits
-// lies in the top range of 16-bit patterns, from `long_base` on; patterns no
-// code starts map to "16 bits, symbol 0", the host decoder's corrupt-code
-// rule).  A table whose long codes reach below the top kHuffLong patterns
-// keeps long_base = 65536, an empty second table, and is searched (maxcode /
-// valoffset / vals).  In an AC table's kHuffLook-bit entries, bits 16..31
-// hold a second symbol's step (0: none) when the pattern holds two whole
-// symbols, value bits included, the first of which is not an EOB: the
-// decoder takes both in one lookup (jpeghuff.hip Dec::step).
+// 65536 - kHuffLong (the kernel's constant base) (canonical codes: every
+// code longer than kHuffLook bits lies in the top range of 16-bit patterns,
+// from `long_base` on; patterns no code starts map to "16 bits, symbol 0",
+// the host decoder's corrupt-code rule).  A table whose long codes reach
+// below the top kHuffLong patterns keeps long_base = 65536, an empty second
+// table, and is searched (maxcode / valoffset / vals).  Bits 16..31 of an
+// entry are the step of a PAIR: in an AC table's kHuffLook-bit entries, when
+// the pattern holds two whole symbols, value bits included, the first of
+// which is not an EOB, bits 16..20 the bits both consume, 21..27 the index
+// advance of both, 28..31 the second's value bits; otherwise the single
+// symbol's own bits and advance again (value bits 0), so the decoder takes
+// "the pair" whenever the first symbol leaves its block open (jpeghuff.hip
+// Dec::step).
 struct HuffDev {
   uint32_t step[1 << kHuffLook];
-  uint16_t step_long[kHuffLong];
+  uint32_t step_long[kHuffLong];
   int32_t long_base;
   int32_t search;  // 1: the two lookups do not cover every pattern (the launch takes the searching kernel)
   int32_t maxcode[18];
@@ -81,6 +85,15 @@ constexpr uint16_t huff_step_entry(int cls, int len, int sym) {
   return (uint16_t)(((len + (cls ? (sym & 15) : sym)) & 31) |
                     ((cls ? ((sym & 15) != 0 || (sym >> 4) == 15 ? (sym >> 4) + 1 : 64) : 1) << 5) |
                     ((cls ? (sym & 15) : sym) << 12));
+}
+// The table entry of a single symbol (its bits and advance repeated as the pair's).
+constexpr uint32_t huff_step_single(uint16_t e) { return e ? (uint32_t)e | (uint32_t)(e & 0xfff) << 16 : 0u; }
+// The table entry of a pair (first: a single entry of a symbol other than EOB, second: the next one's).
+constexpr uint32_t huff_step_pair(uint16_t first, uint16_t second) {
+  return (uint32_t)first |
+         (uint32_t)(((first & 31) + (second & 31)) | (((first >> 5) & 127) + ((second >> 5) & 127)) << 5 |
+                    (second >> 12) << 12)
+             << 16;
 }
 static_assert(sizeof(HuffDev) % 16 == 0, "HuffDev keeps 16-byte alignment");
 

@@ -32,20 +32,22 @@
 namespace mxd {
 namespace {
 
-// Bit readers over one segment's unstuffed bytes (32-bit words, big-endian
-// byte order); words past the segment read as zeros (libjpeg's zeros past
-// the data).  After a refill at least 33 bits are buffered.
+// Bit readers over one segment's unstuffed bytes (32-bit words); words past
+// the segment read as zeros (libjpeg's zeros past the data).  A reader keeps
+// the bit position as word index + offset and gives the 32-bit window there
+// (win); advance(n) moves it on by n <= 31 bits.
 //
-// LdsReader: the job's words staged in LDS.  Every segment is staged with
+// LdsReader: the job's words staged in LDS, byte-swapped by the staging loop
+// (so a window is a funnel shift of two words).  Every segment is staged with
 // >= 4 zero bytes past its data, rounded up to 16 (hostpath.cpp), so a word
-// past the segment reads as w[nw] (zero) without a separate select; words
-// are loaded one refill ahead (off the symbol loop's dependency chain).
+// past the segment reads as w[nw] (zero) without a separate select.  It holds
+// the two words under the window and loads the one after them a step ahead
+// (off the symbol loop's dependency chain).
 struct LdsReader {
   const uint32_t* w;
-  int32_t nw;
-  uint64_t buf;
-  int32_t cnt, wi;
-  uint32_t nxt;
+  int32_t nw;     // the segment's last word index read (its zero word)
+  int32_t wq, o;  // the window starts at bit o of word wq
+  uint32_t A, B, C;
 
   // base: the job's words in LDS; w0 / nw: the segment's first word (relative
   // to base, negative for a segment the job starts inside) and its words,
@@ -55,31 +57,30 @@ struct LdsReader {
     nw = min(nwords, lim);
   }
   __device__ __forceinline__ uint32_t word(int32_t i) const { return w[min(i, nw)]; }
-  // one word when cnt <= 32, without a branch (the next word's load is issued either way)
-  __device__ __forceinline__ void refill_if() {
-    const bool need = cnt <= 32;
-    const uint32_t x = need ? __builtin_bswap32(nxt) : 0u;
-    buf |= (uint64_t)x << (need ? 32 - cnt : 0);
-    cnt += need ? 32 : 0;
-    wi += need ? 1 : 0;
-    nxt = word(wi);
-  }
   __device__ __forceinline__ void seek(int32_t bit) {
-    wi = bit >> 5;
-    buf = (uint64_t)__builtin_bswap32(word(wi)) << 32 | __builtin_bswap32(word(wi + 1));
-    wi += 2;
-    nxt = word(wi);
-    const int s = bit & 31;
-    buf <<= s;
-    cnt = 64 - s;
+    wq = bit >> 5;
+    o = bit & 31;
+    A = word(wq);
+    B = word(wq + 1);
+    C = word(wq + 2);
   }
-  __device__ __forceinline__ int32_t pos() const { return wi * 32 - cnt; }
+  __device__ __forceinline__ uint32_t win() const { return (uint32_t)((((uint64_t)A << 32) | B) << o >> 32); }
+  __device__ __forceinline__ void advance(int n) {
+    const int t = o + n;
+    const bool next = t >= 32;
+    o = t & 31;
+    A = next ? B : A;
+    B = next ? C : B;
+    wq += next ? 1 : 0;
+    C = word(wq + 2);
+  }
+  __device__ __forceinline__ int32_t pos() const { return wq * 32 + o; }
 };
 
-// GlobalReader: the job's words in device memory (MXD_TUNE_HUFF_GLOBAL), read
-// in 16-byte chunks two chunks ahead of the one being consumed, so a chunk's
-// load latency hides behind ~256 bits of decoding.  Chunks past the segment
-// are not loaded.
+// GlobalReader: the job's words in device memory (MXD_TUNE_HUFF_GLOBAL, or a
+// job too large for LDS), unswapped, read in 16-byte chunks two chunks ahead
+// of the one being consumed, so a chunk's load latency hides behind ~256 bits
+// of decoding.  Chunks past the segment are not loaded.
 struct GlobalReader {
   const uint4* chunks;  // the job's words (16-byte aligned)
   int32_t w0, nw;       // the segment's first word (relative to the job's) and its words
@@ -112,7 +113,7 @@ struct GlobalReader {
     wi++;
     return x;
   }
-  __device__ __forceinline__ void refill_if() {
+  __device__ __forceinline__ void refill() {
     if (cnt <= 32) {
       buf |= (uint64_t)next_word() << (32 - cnt);
       cnt += 32;
@@ -134,6 +135,12 @@ struct GlobalReader {
     buf <<= s;
     cnt -= s;
   }
+  __device__ __forceinline__ uint32_t win() const { return (uint32_t)(buf >> 32); }
+  __device__ __forceinline__ void advance(int n) {
+    buf <<= n;
+    cnt -= n;
+    refill();  // >= 33 bits buffered again: a step consumes <= 31
+  }
   __device__ __forceinline__ int32_t pos() const { return wi * 32 - cnt; }
 };
 
@@ -142,14 +149,14 @@ struct GlobalReader {
 // jpeg_huff_decode's search -- the shortest l in kHuffLook+1..16 whose l-bit
 // prefix is <= maxcode[l]; none (corrupt data) consumes 16 bits and decodes
 // as symbol 0.
-__device__ __noinline__ int huff_search_step(const HuffDev& t, uint64_t buf, int cls) {
-  const uint32_t p16 = (uint32_t)(buf >> 48);
+__device__ __noinline__ uint32_t huff_search_step(const HuffDev& t, uint32_t win, int cls) {
+  const uint32_t p16 = win >> 16;
   int l = 17;
 #pragma unroll
   for (int ll = 16; ll > kHuffLook; ll--)
     if ((int32_t)(p16 >> (16 - ll)) <= t.maxcode[ll]) l = ll;
-  if (l > 16) return huff_step_entry(cls, 16, 0);
-  return huff_step_entry(cls, l, t.vals[((int32_t)(p16 >> (16 - l)) + t.valoffset[l]) & 0xff]);
+  if (l > 16) return huff_step_single(huff_step_entry(cls, 16, 0));
+  return huff_step_single(huff_step_entry(cls, l, t.vals[((int32_t)(p16 >> (16 - l)) + t.valoffset[l]) & 0xff]));
 }
 
 __device__ __forceinline__ int extend(uint32_t v, int s) {
@@ -297,44 +304,39 @@ struct Dec {
   // table's entry pairs a symbol with the next one when both, value bits
   // included, lie inside the kHuffLook-bit lookup); returns true at the end
   // of a block (b, k advanced to the next block's start).  The second symbol
-  // is taken only when the first does not end its block and ends before
-  // `rem` (the bits left to the decode's end, decremented by what the step
-  // consumes) runs out, so a decode stops at the same symbol boundary as one
-  // symbol at a time would.  on_sym(dc, position, value, size) receives every
-  // symbol's store: the DC difference at 0, a coefficient at its index, an
-  // EOB's / ZRL's zero at an index of the block not yet written (so no
-  // branch; a corrupt run past 63 lands on 63, as jpeg_natural_order's extra
-  // entries put it).  Codes longer than kHuffLook bits
-  // come from the second table, read beside the first (no branch), and only
-  // tables too large for it search.
+  // is taken when the first does not end its block.  A step may end past a
+  // subsequence's end (a pair whose first symbol ends at or past it): the
+  // sync and write passes share this rule, so a subsequence's exit and the
+  // symbols it writes agree.  `rem` counts the bits consumed down.
+  // on_sym(dc, position, value, size) receives the first symbol's store --
+  // the DC difference at 0, a coefficient at its index, an EOB's / ZRL's zero
+  // at an index of the block not yet written (a corrupt run past 63 lands on
+  // 63, as jpeg_natural_order's extra entries put it) -- and, when the step
+  // takes two and the second has value bits, the second's.  Codes longer
+  // than kHuffLook bits come from the second table, read beside the first
+  // (no branch), and only tables too large for it search.
   template <class Reader, class OnSym>
   __device__ __forceinline__ bool step(Reader& r, int32_t& rem, OnSym&& on_sym) {
-    r.refill_if();  // >= 33 bits buffered: a step consumes <= 16 + 15
     const bool dc = k == 0;
     const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
-    const uint32_t top16 = (uint32_t)(r.buf >> 48);
-    const uint32_t st1 = t.step[top16 >> (16 - kHuffLook)];
-    const uint32_t st2 = t.step_long[max((int)top16 - (65536 - kHuffLong), 0)];  // no dependent load of a base
+    const uint32_t w = r.win();
+    const uint32_t st1 = t.step[w >> (32 - kHuffLook)];
+    const uint32_t st2 = t.step_long[max((int)(w >> 16) - (65536 - kHuffLong), 0)];  // no dependent load of a base
     uint32_t st = st1 ? st1 : st2;
     if constexpr (SEARCH) {  // launches with a table the two lookups do not cover
-      if (!st) st = huff_search_step(t, r.buf, dc ? 0 : 1);
+      if (!st) st = huff_search_step(t, w, dc ? 0 : 1);
     }
     const int s1 = st & 31, a1 = (st >> 5) & 127, z1 = (st >> 12) & 15;
-    const int s2 = (st >> 16) & 31, a2 = (st >> 21) & 127, z2 = st >> 28;
+    const int s12 = (st >> 16) & 31, a12 = (st >> 21) & 127, z2 = st >> 28;
     const int k1 = k + a1;
-    const bool two = s2 != 0 && k1 < 64 && s1 < rem;
-    // value bits: the sz bits after each code, in the buffer's top 32 bits (s1 <= 31; a pair within 11)
-    const uint32_t hi = (uint32_t)(r.buf >> 32);
-    const uint32_t raw1 = z1 ? (hi >> (32 - s1)) & ((1u << z1) - 1u) : 0u;
+    const bool two = k1 < 64;  // a single symbol's entry repeats it as the "pair"
+    // value bits: the z bits ending each symbol (s1 <= 31; a pair within 11 bits)
+    const uint32_t raw1 = z1 ? (w >> (32 - s1)) & ((1u << z1) - 1u) : 0u;
     on_sym(dc, min(k1 - 1, 63), raw1, z1);
-    const int knew = two ? k1 + a2 : k1;
-    if (two) {
-      const uint32_t raw2 = z2 ? ((hi << s1) >> (32 - s2)) & ((1u << z2) - 1u) : 0u;
-      on_sym(false, min(knew - 1, 63), raw2, z2);
-    }
-    const int shift = two ? s1 + s2 : s1;
-    r.buf <<= shift;
-    r.cnt -= shift;
+    const int knew = two ? k + a12 : k1;
+    if (two && z2) on_sym(false, min(knew - 1, 63), (w >> (32 - s12)) & ((1u << z2) - 1u), z2);
+    const int shift = two ? s12 : s1;
+    r.advance(shift);
     rem -= shift;
     const bool end = knew >= 64;
     k = end ? 0 : knew;
@@ -764,10 +766,13 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     for (int i = t; i < n16; i += blockDim.x) dyn[i] = src[i];
   }
   uint32_t* lds_words = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dyn) + lds_words_at(im.ntables, job.nseg));
-  if (job.lds) {
+  if (job.lds) {  // byte-swapped: LdsReader's windows are funnel shifts
     const uint4* src = reinterpret_cast<const uint4*>(words + job.word0);
     uint4* dst = reinterpret_cast<uint4*>(lds_words);
-    for (int i = t; i < job.words16; i += blockDim.x) dst[i] = src[i];
+    for (int i = t; i < job.words16; i += blockDim.x) {
+      const uint4 v = src[i];
+      dst[i] = uint4{__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z), __builtin_bswap32(v.w)};
+    }
   }
   // segment records: words relative to the job's first word; subsequences
   // of the job per segment (the first from sub0, the job's count overall)
