@@ -17,8 +17,9 @@
 //      again from the true state;
 //   3. block counts prefix-summed per segment -> each subsequence's first
 //      block; the job's exit state and block index published;
-//   4. write pass: decode again, storing AC coefficients and DC differences;
-//   5. DC: per-component sums of the differences prefix-summed per segment
+//   4. the job's blocks zeroed by the whole workgroup (whole lines);
+//   5. write pass: decode again, storing AC coefficients and DC differences;
+//   6. DC: per-component sums of the differences prefix-summed per segment
 //      (the continued segment's from the previous job's published sums),
 //      then each subsequence turns its blocks' differences into values.
 // (Round 4's kernel, one workgroup per image, and its tuning variants are
@@ -192,6 +193,8 @@ struct Shared {
   int3 scan3[kHuffThreads / 64];
   int32_t flag[2];
   int64_t pred_blocks;             // the previous job's published block index
+  int64_t zero_range[2];           // the job's first and last block (jpeghuff.hip step 4)
+  int32_t zero_k[2];               // the job's part of them starts at / ends before these positions
   int32_t pred_dc[3];
 #ifdef MXD_HUFF_STAMPS
   // diagnostic build: s_memtime at the phase boundaries ([0] start, [1]
@@ -547,43 +550,54 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
                       ((uint64_t)(uint8_t)sh.out_k[t] << 40));
   }
 
-  // 4. write pass (own subsequences)
+  // 4. Zero the job's blocks (the write pass stores only the symbols'
+  // positions): every block it decodes whole or in part -- [z0, z1) in decode
+  // order, contiguous over the job's segments; the segment's last
+  // subsequence's range runs to the segment's end, which leaves the blocks of
+  // data that ran out early zero (libjpeg's insufficient-data rule) -- by the
+  // whole workgroup in 16-byte pieces, consecutive threads on consecutive
+  // pieces, so a block's 128 bytes go out as one line.  Not the first block
+  // when the previous job decodes its start, nor the last when the next job
+  // decodes its end: the neighbouring job writes into those with no barrier
+  // in between, so their owners here zero them position by position.
+  const int ke = sh.in_k[t];
+  const int64_t gx = g + my_done;                   // the block it ends inside (non-last)
+  const int kx = u.seg_last ? 0 : sh.out_k[t];
+  // the job's first block (from position kf on: the previous job decodes its
+  // start) and its last (to position kl: the next job decodes the rest)
+  if (act && t == job.warm) {
+    sh.zero_range[0] = g;
+    sh.zero_k[0] = g < seg_block1 ? ke : 0;
+  }
+  if (act && u.job_last) {
+    sh.zero_range[1] = u.seg_last ? seg_block1 : gx;
+    sh.zero_k[1] = gx < seg_block1 ? kx : 0;
+  }
+  __syncthreads();
+  {
+    const int64_t first = sh.zero_range[0], last = sh.zero_range[1];
+    const int kf = sh.zero_k[0], kl = sh.zero_k[1];
+    const int64_t z0 = first + (kf != 0 ? 1 : 0), pieces = (last - z0) * 8;
+#ifndef MXD_HUFF_NOSTORE_ZERO  // (diagnostic build (wrong results): no zeroing stores)
+    for (int64_t c = t; c < pieces; c += blockDim.x)
+      reinterpret_cast<uint4*>(coef + block_addr(im, z0 + (c >> 3)))[c & 7] = uint4{0u, 0u, 0u, 0u};
+    auto zero = [&](int64_t b, int k0, int k1) {
+      int16_t* d = coef + block_addr(im, b);
+      for (int q = k0; q < k1; q++) d[q] = 0;
+    };
+    if (t == job.warm && kf != 0) zero(first, kf, last == first && kl != 0 ? kl : 64);
+    if (act && u.job_last && kl != 0 && !(last == first && kf != 0)) zero(last, 0, kl);
+#endif
+  }
+  __syncthreads();  // the zeros land before the coefficients
+
+  // 5. write pass (own subsequences)
   Dec<SEARCH> dec;
   dec.init(im, tab);
   int dcsum[3] = {0, 0, 0};
   int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
   uint32_t cur0[3] = {0, 0, 0};  // the block cursor (block of the MCU, MCU column, row) at the first block
   if (act && u.own) {
-    // Zero the coefficient positions this subsequence decodes (the pass
-    // below stores only the symbols' positions): the rest of the block it
-    // starts inside, its whole blocks, and the start of the block it ends
-    // inside -- each position of a block zeroed and then written by the one
-    // thread that decodes it, so neighbours (in this job or the next) never
-    // race.  The segment's last subsequence zeroes to the segment's end, which
-    // leaves the blocks of data that ran out early zero (libjpeg's
-    // insufficient-data rule).
-    {
-      auto zero = [&](int64_t b, int k0, int k1) {
-#ifdef MXD_HUFF_NOSTORE_ZERO  // diagnostic build (wrong results): no zeroing stores
-        return;
-#endif
-        int16_t* d = coef + block_addr(im, b);
-        if (k0 == 0 && k1 == 64) {
-          uint4* z = reinterpret_cast<uint4*>(d);
-#pragma unroll
-          for (int q = 0; q < 8; q++) z[q] = uint4{0u, 0u, 0u, 0u};
-        } else {
-          for (int q = k0; q < k1; q++) d[q] = 0;
-        }
-      };
-      const int ke = sh.in_k[t];
-      const int64_t gx = g + my_done;                     // the block it ends inside (non-last)
-      const int kx = u.seg_last ? 0 : sh.out_k[t];
-      if (ke != 0 && g < seg_block1) zero(g, ke, !u.seg_last && gx == g ? kx : 64);
-      const int64_t full_end = u.seg_last ? seg_block1 : min(seg_block1, gx);
-      for (int64_t b = g + (ke != 0 ? 1 : 0); b < full_end; b++) zero(b, 0, 64);
-      if (kx != 0 && gx < seg_block1 && !(ke != 0 && gx == g)) zero(gx, 0, kx);
-    }
     R rd;
     rd.init(wbase, u.sg.word, (u.sg.bits + 31) >> 5, u.sg.lim);
     rd.seek(sh.in_pos[t]);
@@ -633,11 +647,17 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     }
   }
 
-  // 5. DC values: per component, the differences before this subsequence in
+  // 6. DC values: per component, the differences before this subsequence in
   // its segment (the continued segment starts from the previous job's sums)
   if (job.pred && t == 0) {
     const HuffPubDev* p = pub + sh.ticket - 1;
+#ifdef MXD_HUFF_STAMPS
+    sh.stamp[6] = __builtin_amdgcn_s_memtime();
+#endif
     for (int c = 0; c < 3; c++) sh.pred_dc[c] = (int32_t)(uint32_t)wait_pub(p, 2 + c, ctl);
+#ifdef MXD_HUFF_STAMPS
+    sh.stamp[6] = __builtin_amdgcn_s_memtime() - sh.stamp[6];
+#endif
   }
   HUFF_STAMP(4);  // (thread 0's write pass; the scans below wait for the others)
   // one scan for the three components
@@ -710,7 +730,8 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     sh.stamp[5] = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < 6; i++) p->w[8 + i] = sh.stamp[i];
     p->w[14] = sh.stamp[7];  // s_memrealtime at the start
-    p->w[15] = (uint64_t)sh.rounds[0] | (uint64_t)sh.rounds[1] << 8 | (uint64_t)sh.ticket << 16;
+    p->w[15] = (uint64_t)sh.rounds[0] | (uint64_t)sh.rounds[1] << 8 | (uint64_t)sh.ticket << 16 |
+               (uint64_t)(job.pred ? sh.stamp[6] : 0) << 32;  // cycles waiting for the previous job's DC sums
     for (int i = 0; i < 16; i++) {
       const bool have = i < sh.rounds[0];
       p->w[16 + i] = have ? (sh.round_end[i] & 0xffffffffffull) | (uint64_t)sh.nact[i] << 40 : 0;
