@@ -411,6 +411,27 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
 #ifdef MXD_HUFF_STAMPS
   int round = 0;
 #endif
+  // decodes subsequence id from its start state to its end: exit state and blocks completed
+  auto decode_one = [&](int id, const Sub& v) {
+    rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5, v.sg.lim);
+    rd.seek(sh.in_pos[id]);
+    dec.b = sh.in_b[id];
+    dec.k = sh.in_k[id];
+    int done = 0;
+    const auto nop = [](bool, int, uint32_t, int) {};
+    int32_t rem = v.end - sh.in_pos[id];
+    // a step consumes <= 31 bits: while the end is further than one step,
+    // two steps both start before it
+    while (rem > 31) {
+      done += dec.step(rd, rem, nop) ? 1 : 0;
+      done += dec.step(rd, rem, nop) ? 1 : 0;
+    }
+    while (rem > 0) done += dec.step(rd, rem, nop) ? 1 : 0;
+    sh.out_pos[id] = v.end - rem;
+    sh.out_b[id] = (int8_t)dec.b;
+    sh.out_k[id] = (int8_t)dec.k;
+    sh.done[id] = done;
+  };
   for (;;) {
     // this round's subsequences, compacted onto the first threads, so a
     // round in which few start states changed runs few waves
@@ -428,27 +449,48 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
     if (nact == 0) break;  // uniform
     if (need) sh.list[slot] = (int16_t)t;
     __syncthreads();
+    if (nact <= 64) {
+      // The last rounds in one wave, with no workgroup barrier: a round's
+      // changed subsequences never outnumber the previous round's, so each
+      // lane follows its chain -- decodes its subsequence, hands the exit on
+      // and, when that changed the next one's start, decodes the next one.
+      // The lanes step together, so a round's decodes read their starts
+      // before its hand-offs write any (as the workgroup rounds do).
+      if (t < 64) {
+        int id = t < nact ? sh.list[t] : -1;
+        while (__ballot(id >= 0) != 0) {
+          if (id >= 0) {
+            const Sub v = sub_of(sh, seg, id, nsub);
+            decode_one(id, v);
+            int next = -1;
+            if (!v.seg_last && !v.job_last && id + 1 != fixed) {  // the job's next subsequence, of the same segment
+              const int32_t p = sh.out_pos[id];
+              const int8_t b = sh.out_b[id], k = sh.out_k[id];
+              if (p != sh.in_pos[id + 1] || b != sh.in_b[id + 1] || k != sh.in_k[id + 1]) {
+                sh.in_pos[id + 1] = p;
+                sh.in_b[id + 1] = b;
+                sh.in_k[id + 1] = k;
+                next = v.j + 1 == v.sg.nsub - 1 ? -1 : id + 1;  // a segment's last subsequence waits for the write pass
+              }
+            }
+            id = next;
+          }
+#ifdef MXD_HUFF_STAMPS
+          const int live = __popcll(__ballot(id >= 0));
+          if (t == 0 && fixed < 0 && round < 16) {
+            sh.nact[round] = live;
+            sh.round_end[round] = __builtin_amdgcn_s_memtime();
+          }
+          if (t == 0) sh.rounds[fixed < 0 ? 0 : 1] = ++round;
+#endif
+        }
+      }
+      __syncthreads();
+      break;
+    }
     if (t < nact) {
       const int id = sh.list[t];
-      const Sub v = sub_of(sh, seg, id, nsub);
-      rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5, v.sg.lim);
-      rd.seek(sh.in_pos[id]);
-      dec.b = sh.in_b[id];
-      dec.k = sh.in_k[id];
-      int done = 0;
-      const auto nop = [](bool, int, uint32_t, int) {};
-      int32_t rem = v.end - sh.in_pos[id];
-      // a step consumes <= 31 bits: while the end is further than one step,
-      // two steps both start before it
-      while (rem > 31) {
-        done += dec.step(rd, rem, nop) ? 1 : 0;
-        done += dec.step(rd, rem, nop) ? 1 : 0;
-      }
-      while (rem > 0) done += dec.step(rd, rem, nop) ? 1 : 0;
-      sh.out_pos[id] = v.end - rem;
-      sh.out_b[id] = (int8_t)dec.b;
-      sh.out_k[id] = (int8_t)dec.k;
-      sh.done[id] = done;
+      decode_one(id, sub_of(sh, seg, id, nsub));
     }
     __syncthreads();
     // hand the new exits on (to the next subsequence of the same segment): a
