@@ -620,7 +620,6 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     const int64_t first = sh.zero_range[0], last = sh.zero_range[1];
     const int kf = sh.zero_k[0], kl = sh.zero_k[1];
     const int64_t z0 = first + (kf != 0 ? 1 : 0), pieces = (last - z0) * 8;
-#ifndef MXD_HUFF_NOSTORE_ZERO  // (diagnostic build (wrong results): no zeroing stores)
     for (int64_t c = t; c < pieces; c += blockDim.x)
       reinterpret_cast<uint4*>(coef + block_addr(im, z0 + (c >> 3)))[c & 7] = uint4{0u, 0u, 0u, 0u};
     auto zero = [&](int64_t b, int k0, int k1) {
@@ -629,7 +628,6 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     };
     if (t == job.warm && kf != 0) zero(first, kf, last == first && kl != 0 ? kl : 64);
     if (act && u.job_last && kl != 0 && !(last == first && kf != 0)) zero(last, 0, kl);
-#endif
   }
   __syncthreads();  // the zeros land before the coefficients
 
@@ -669,11 +667,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
         dc1 = dc ? g + 1 : dc1;
         // zig-zag order (jpeg_idct reorders); zeros (EOB, ZRL, a zero DC
         // difference) land on positions zeroed above
-#ifndef MXD_HUFF_NOSTORE_COEF  // diagnostic build (wrong results): no coefficient stores
         if (v != 0) blk[kk] = (int16_t)v;
-#else
-        if (v == 12345) blk[kk] = 0;
-#endif
       });
       if (fin) {
         g++;
