@@ -184,7 +184,11 @@ int mxd_set_kernel_policy(int32_t policy);
  * (read when a host-path context is first set up): 0 = every context slot
  * owns one (default); n > 0 = the slots share n library streams;
  * MXD_TUNE_HUFF_JOB: most own subsequences per device entropy-decode job
- * (workgroup); 0 = kHuffThreads - kHuffWarm (1000). */
+ * (workgroup); 0 = kHuffThreads - kHuffWarm (1000);
+ * MXD_TUNE_JPEG_RGB: 1 = every device-finished JPEG goes through an RGB
+ * frame (jpeg_color) before the resize; 0 (default) = a 4:2:0 image whose
+ * resize runs on a scatter wave kernel is resized straight from its sample
+ * planes (no RGB frame). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -196,7 +200,8 @@ enum mxd_tune {
   MXD_TUNE_HOST_WAIT = 7,
   MXD_TUNE_HOST_STREAMS = 8,
   MXD_TUNE_HUFF_JOB = 9,
-  MXD_TUNE_COUNT = 10
+  MXD_TUNE_JPEG_RGB = 10,
+  MXD_TUNE_COUNT = 11
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 
@@ -355,6 +360,11 @@ int mxd_jpeg_resize_crop_host(const mxd_jpeg_image* images, int32_t n, int32_t o
 
 /* Device destinations on `device` (like mxd_resize_crop_to_device). */
 int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int32_t out_dtype, int32_t device);
+
+/* Diagnostics: *count = the images the two calls above resized straight from
+ * their sample planes (4:2:0 on a scatter wave kernel, MXD_TUNE_JPEG_RGB 0:
+ * no RGB frame) since the last reset; reset != 0 zeroes it after reading. */
+int mxd_jpeg_plane_sources(int64_t* count, int32_t reset);
 
 /* ---- pixel maps: rotate / affine and channel reduction --
  *

@@ -342,7 +342,11 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       } else {
         if (int rc = tables().get(device, im.src_w, im.resize_w, &p.xt)) return rc;
         if (int rc = tables().get(device, im.src_h, im.resize_h, &p.yt)) return rc;
-        if (!no_wave) {
+        if (st.ycc) {
+          // JPEG planes (the host path checked ycc_plan_ok): a wave kernel or nothing
+          plan_wave(im, st, f32, out_dtype, p);
+          if (!p.wave) return fail(MXD_ERR_UNSUPPORTED, "mxd: no wave kernel for a JPEG plane source");
+        } else if (!no_wave) {
           if (g_policy.load() & MXD_POLICY_PREFER_BAND) {
             plan_band(im, st, f32, p);
             if (!p.band) plan_wave(im, st, f32, out_dtype, p);
@@ -375,6 +379,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     d.crop_w = im.crop_w;
     d.crop_h = im.crop_h;
     d.flip = im.flip ? 1 : 0;
+    d.ycc = st.ycc;
   };
 
   // Descriptors of one upload: band-kernel images first, then wave-kernel
@@ -465,7 +470,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   // shift).
   auto key = [&](int32_t i) {
     const ImgPlan& p = plans[i];
-    return std::make_tuple(p.kind, p.bucket, p.s, p.dmax, p.q, p.shift, p.pp);
+    return std::make_tuple(p.kind, p.bucket, p.s, p.dmax, p.q, p.shift, p.pp, p.ycc);
   };
   std::vector<int32_t> order;
   for (int32_t i = 0; i < n; i++)
@@ -482,7 +487,8 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     const ImgPlan& p = plans[order[k]];
     if (groups.empty() || key(order[groups.back().first]) != key(order[k]))
       groups.push_back(
-          {k, 0, 0, 0, mxd::WaveCfg{channels, f32, p.bucket, 0, 0, p.kind, p.s, p.dmax, p.q, p.shift, p.pp}});
+          {k, 0, 0, 0, mxd::WaveCfg{channels, f32, p.bucket, 0, 0, p.kind, p.s, p.dmax, p.q, p.shift, p.pp, 0, 1,
+                                    p.ycc ? 1 : 0}});
     groups.back().count++;
   }
   for (Group& g : groups) {

@@ -494,6 +494,12 @@ int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int3
   return jpeg_path(images, n, out_dtype, device, true);
 }
 
+int mxd_jpeg_plane_sources(int64_t* count, int32_t reset) {
+  if (!count) return fail(MXD_ERR_INVALID, "mxd: null count");
+  *count = reset ? g_plane_sources.exchange(0) : g_plane_sources.load();
+  return MXD_OK;
+}
+
 int mxd_release_host_buffers(void) {
   host_trim();
   return MXD_OK;

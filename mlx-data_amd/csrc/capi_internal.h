@@ -159,6 +159,7 @@ struct ImgPlan {
   int32_t s = 0, dmax = 0, p = 0;  // scatter shape (ScatterShape)
   int32_t nstrips = 0, tx = 0, q = 0, shift = 0;
   int32_t pp = 0;  // source pixels per lane
+  bool ycc = false;  // reads JPEG sample planes (Stored::ycc)
 };
 
 // Shape of the scatter schedule for crop rows [off, off+len) of a vertical
@@ -196,16 +197,22 @@ int32_t wave_capacity_cached(const mxd::WaveCfg& cfg, int32_t device);
 // Where an image's source bytes live: the whole image at mxd_image::src, or
 // (host path) only its staged footprint: `rows` rows from source row y0 and
 // columns from source pixel x0 at base, `stride` bytes apart.
+// ycc: a JPEG image's sample planes instead (base = its Y plane; wave.hip
+// YccSrc): only a scatter wave kernel with RGB pixel lanes runs it.
 struct Stored {
   const uint8_t* base;
   int64_t stride;
   int32_t x0, y0, rows;
+  const mxd::YccDev* ycc = nullptr;
 };
 
 Stored whole(const mxd_image& im);
 bool wave_layout_ok(const mxd_image& im, const Stored& st, int32_t out_dtype);
 void plan_band(const mxd_image& im, const Stored& st, int32_t f32, ImgPlan& p);
 void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_dtype, ImgPlan& p);
+// Whether run_batch would resize image im from the JPEG planes st.ycc
+// describes (a scatter wave kernel with RGB pixel lanes takes it).
+bool ycc_plan_ok(const mxd_image& im, const Stored& st, int32_t out_dtype, int32_t device);
 
 // What a plan depends on: geometry, the stored region's layout and the
 // alignments of source and destination.
@@ -233,6 +240,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
 int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device,
               const mxd_jpeg_image* jpeg = nullptr);
 int jpeg_path(const mxd_jpeg_image* jimg, int32_t n, int32_t out_dtype, int32_t device, bool dst_device);
+extern std::atomic<int64_t> g_plane_sources;  // images resized from their JPEG sample planes (mxd_jpeg_plane_sources)
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c);
 // Frees the buffers of every idle host-path context (mxd_release_host_buffers).
 void host_trim();

@@ -332,7 +332,8 @@ struct JpegChunk {
   std::vector<mxd::JpegPlaneDev> planes;
   std::vector<mxd::JpegImgDev> imgs;
   std::vector<uint16_t> qtabs;
-  int64_t planes_off = 0, imgs_off = 0, q_off = 0, end = 0;  // in the staged input
+  std::vector<mxd::YccDev> ycc;  // per image: its planes as a resize source (used when JpegImgDev::skip)
+  int64_t planes_off = 0, imgs_off = 0, q_off = 0, ycc_off = 0, end = 0;  // in the staged input
   int64_t samples = 0, rgb_off = 0, mid_bytes = 0;             // in dev_mid
   int64_t nblocks = 0, max_quad_rows = 0;  // max_quad_rows: the colour kernel's threads per image (8 pixels each)
   // Device entropy decode of the chunk's pending images (jpeghuff.h): their
@@ -357,6 +358,8 @@ struct JpegChunk {
   int64_t huff_lds = 0;  // the largest job's dynamic LDS (its words included when they fit)
   bool huff_search = false;  // some table needs the searching kernel (HuffDev::search)
 };
+
+std::atomic<int64_t> g_plane_sources{0};
 
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
 
@@ -489,7 +492,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     m.width = info.width;
     m.height = info.height;
     m.pitch = (int32_t)rgb_pitch(info.width);
-    m.quads = (info.width + 3) / 4;
+    m.skip = 0;
     for (int k = 0; k < m.ncomp; k++) {
       const mxd::jpeg::CoefPlane& cp = info.comp[k];
       mxd::JpegPlaneDev p{};
@@ -537,7 +540,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
   c.planes_off = up(c.hjobs_off + (int64_t)(c.hjobs.size() * sizeof(mxd::HuffJobDev)), 256);
   c.imgs_off = up(c.planes_off + (int64_t)(c.planes.size() * sizeof(mxd::JpegPlaneDev)), 256);
   c.q_off = up(c.imgs_off + (int64_t)(c.imgs.size() * sizeof(mxd::JpegImgDev)), 256);
-  c.end = c.q_off + (int64_t)(c.qtabs.size() * sizeof(uint16_t));
+  c.ycc.assign(c.imgs.size(), mxd::YccDev{});
+  c.ycc_off = up(c.q_off + (int64_t)(c.qtabs.size() * sizeof(uint16_t)), 16);
+  c.end = c.ycc_off + (int64_t)(c.ycc.size() * sizeof(mxd::YccDev));
   c.pub_off = up(c.end, 256);
   c.coef_off = up(c.pub_off + (int64_t)(c.hjobs.size() * sizeof(mxd::HuffPubDev)) + (int64_t)sizeof(mxd::HuffCtlDev),
                   256);
@@ -773,7 +778,6 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       }
       std::memcpy(sl.pin_in + jc.planes_off, jc.planes.data(), jc.planes.size() * sizeof(mxd::JpegPlaneDev));
       for (auto& m : jc.imgs) m.out += jc.rgb_off;
-      std::memcpy(sl.pin_in + jc.imgs_off, jc.imgs.data(), jc.imgs.size() * sizeof(mxd::JpegImgDev));
       std::memcpy(sl.pin_in + jc.q_off, jc.qtabs.data(), jc.qtabs.size() * sizeof(uint16_t));
     }
     for (int32_t j = 0; j < cn; j++) {
@@ -781,7 +785,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const mxd_image& im = images[i];
       const Stage& s = st[i];
       if (jpeg) {
-        const mxd::JpegImgDev& m = jc.imgs[j];
+        mxd::JpegImgDev& m = jc.imgs[j];
         const uint8_t* win = sl.dev_mid + m.out + (int64_t)jpeg[i].win_y * m.pitch + (int64_t)jpeg[i].win_x * 3;
         where[j] = Stored{win, m.pitch, 0, 0, im.src_h};
         dev_imgs[j].src = win;
@@ -791,6 +795,30 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
           dev_imgs[j].dst_stride = s.out_row;
         } else if (s.dst_dev) {
           dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
+        }
+        // 4:2:0 YCbCr resized straight from its sample planes when a scatter
+        // wave kernel takes it: no RGB frame (jpeg_color skips the image)
+        const bool h2v2 = m.ncomp == 3 && !m.rgb && m.mode[0] == mxd::kUpFull && m.mode[1] == mxd::kUpH2V2 &&
+                          m.mode[2] == mxd::kUpH2V2 && m.stride[1] == m.stride[2] && m.dw[1] == m.dw[2] &&
+                          m.dh[1] == m.dh[2] && m.plane[0] < m.plane[1] && m.plane[1] < m.plane[2];
+        if (h2v2 && g_tune[MXD_TUNE_JPEG_RGB].load() != 1 && (jpeg[i].win_x & 3) == 0) {
+          mxd::YccDev& y = jc.ycc[j];
+          y.cb = m.plane[1] - m.plane[0];
+          y.cr = m.plane[2] - m.plane[0];
+          y.ystride = m.stride[0];
+          y.cstride = m.stride[1];
+          y.dw = m.dw[1];
+          y.dh = m.dh[1];
+          y.win_x = jpeg[i].win_x;
+          y.win_y = jpeg[i].win_y;
+          y.records = (int32_t)std::min<int64_t>(y.cr + (int64_t)y.cstride * y.dh, INT32_MAX);
+          const Stored planes{sl.dev_mid + m.plane[0], m.stride[0], 0, 0, im.src_h,
+                              reinterpret_cast<const mxd::YccDev*>(sl.dev_in + jc.ycc_off) + j};
+          if (y.cr + (int64_t)y.cstride * y.dh < INT32_MAX && ycc_plan_ok(dev_imgs[j], planes, out_dtype, device)) {
+            where[j] = planes;  // (dev_imgs[j] keeps the RGB frame's geometry, which run_batch validates)
+            m.skip = 1;
+            g_plane_sources.fetch_add(1, std::memory_order_relaxed);
+          }
         }
         continue;
       }
@@ -811,6 +839,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       } else if (s.dst_dev) {
         dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
       }
+    }
+    if (jpeg) {  // (after the fused-source decisions above)
+      std::memcpy(sl.pin_in + jc.imgs_off, jc.imgs.data(), jc.imgs.size() * sizeof(mxd::JpegImgDev));
+      std::memcpy(sl.pin_in + jc.ycc_off, jc.ycc.data(), jc.ycc.size() * sizeof(mxd::YccDev));
     }
     if (in_staged > 0 && !pin_in_dev)
       MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
@@ -855,8 +887,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
                             reinterpret_cast<const mxd::JpegPlaneDev*>(sl.dev_in + jc.planes_off),
                             (int32_t)jc.planes.size(), jc.nblocks, sl.dev_mid, sl.stream);
-      mxd::launch_jpeg_color(sl.dev_mid, reinterpret_cast<const mxd::JpegImgDev*>(sl.dev_in + jc.imgs_off), cn,
-                             jc.max_quad_rows, sl.dev_mid, sl.stream);
+      bool rgb_frames = false;  // some image still needs its RGB frame
+      for (const auto& m : jc.imgs) rgb_frames = rgb_frames || !m.skip;
+      if (rgb_frames)
+        mxd::launch_jpeg_color(sl.dev_mid, reinterpret_cast<const mxd::JpegImgDev*>(sl.dev_in + jc.imgs_off), cn,
+                               jc.max_quad_rows, sl.dev_mid, sl.stream);
       MXD_HIP(hipGetLastError());
     }
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {

@@ -46,7 +46,7 @@ struct JpegImgDev {
   int32_t rgb;       // 1: the components are R, G, B (no YCbCr conversion)
   int32_t width, height;
   int32_t pitch;     // bytes per RGB row (a multiple of 64, >= 3 * round_up(width, 8))
-  int32_t quads;     // ceil(width / 4) (diagnostics; the colour kernel runs ceil(width / 8) threads per row)
+  int32_t skip;      // 1: a wave kernel reads the planes itself (ImgDev::ycc): no RGB frame
 };
 
 // Dequantise + IDCT every block of `nplanes` planes (`nblocks` in total).

@@ -15,6 +15,7 @@
 //   107 us per 128-file C4 batch before, four pixels per thread through a
 //   per-pixel switch).
 #include "jpegdev.h"
+#include "jpegycc.h"
 
 namespace mxd {
 namespace {
@@ -178,10 +179,6 @@ __device__ __forceinline__ int sample_at(const uint8_t* __restrict__ pl, const J
   }
 }
 
-constexpr int kFixCrR = 91881, kFixCbB = 116130, kFixCrG = 46802, kFixCbG = 22554, kHalf16 = 1 << 15;
-
-__device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
-
 // Eight output pixels x0..x0+7 of row y (x0 a multiple of 8).  Common
 // layouts read their samples as aligned dwords and upsample with static byte
 // indices: 4:2:0 (h2v2 fancy), 4:2:2 (h2v1 fancy), 4:4:4 and grey; any other
@@ -199,17 +196,12 @@ __device__ __forceinline__ void load12(const uint8_t* row, int c, int row_bytes,
 }
 __device__ __forceinline__ int byte_at(const uint32_t (&d)[3], int e) { return (int)((d[e >> 2] >> (8 * (e & 3))) & 255u); }
 
-__device__ __forceinline__ void ycc_to_rgb(int y, int cb, int cr, uint32_t* px) {
-  cb -= 128;
-  cr -= 128;
-  px[0] = clamp255(y + ((kFixCrR * cr + kHalf16) >> 16));
-  px[1] = clamp255(y + ((-kFixCbG * cb + kHalf16 - kFixCrG * cr) >> 16));
-  px[2] = clamp255(y + ((kFixCbB * cb + kHalf16) >> 16));
-}
+__device__ __forceinline__ void ycc_to_rgb(int y, int cb, int cr, uint32_t* px) { jpeg_ycc_to_rgb(y, cb, cr, px); }
 
 __global__ __launch_bounds__(256) void jpeg_color(const uint8_t* __restrict__ samples,
                                                   const JpegImgDev* __restrict__ imgs, uint8_t* __restrict__ rgb) {
   const JpegImgDev& m = imgs[blockIdx.y];
+  if (m.skip) return;  // its resize reads the planes (ImgDev::ycc)
   const int octs = (m.width + 7) >> 3;
   const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
   if (t >= (i64)m.height * octs) return;

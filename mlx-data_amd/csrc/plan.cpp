@@ -385,7 +385,17 @@ bool scatter_kernel_for(int32_t c, int32_t f32, int32_t xw, const ScatterShape& 
 // shorter row pieces), then the narrower lane width.
 void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_dtype, ImgPlan& p) {
   p.wave = false;
-  if (!wave_layout_ok(im, st, out_dtype)) return;
+  p.ycc = false;
+  const bool ycc = st.ycc != nullptr;
+  if (ycc) {
+    // JPEG planes: the RGB-row layout rules do not apply, only the output's
+    const uintptr_t o = reinterpret_cast<uintptr_t>(im.dst) | (uintptr_t)im.dst_stride;
+    if (im.channels != 3 || ((reinterpret_cast<uintptr_t>(st.base) | (uintptr_t)st.stride) & 3) != 0 ||
+        (out_dtype == MXD_F32_DIV255 && (o & 3) != 0))
+      return;
+  } else if (!wave_layout_ok(im, st, out_dtype)) {
+    return;
+  }
   const int32_t c = im.channels;
   const int32_t shift = (reinterpret_cast<uintptr_t>(st.base) & 3) != 0 ? 1 : 0;
   // Scatter when the vertical axis downsamples into a shape with a kernel,
@@ -398,6 +408,7 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
   const int32_t widths[2] = {dp, c == 3 && !(policy & MXD_POLICY_NARROW) ? 8 : dp};
   for (int32_t pp : widths) {
     if (p.wave && pp == p.pp) continue;
+    if (ycc && pp != 4) continue;  // plane sources: four RGB pixels per lane
     int32_t ns = 0, tx = 0, q = 0;
     if (!wave_strips(*p.xt, im, pp, &ns, &tx, &q)) continue;
     if (p.wave && ns >= p.nstrips) continue;
@@ -420,15 +431,17 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
       cand.s = sh.s;
       cand.dmax = td;
       cand.p = sh.p;
-    } else if (gb > 0 && mxd::wave_has_kernel(mxd::WaveCfg{c, f32, gb, 0, 0, 0, 0, 0, q, shift, pp})) {
+    } else if (!ycc && gb > 0 && mxd::wave_has_kernel(mxd::WaveCfg{c, f32, gb, 0, 0, 0, 0, 0, q, shift, pp})) {
       cand.kind = 0;
       cand.bucket = gb;
     } else {
       continue;
     }
     cand.wave = true;
+    cand.ycc = ycc;
     p = cand;
   }
+  if (ycc) return;
   // RGB scatter: byte lanes (one 1-KiB contiguous load per wave and row)
   // instead of wide pixel lanes when they cut the crop into no more strips,
   // at <= 2 output pixels per lane (measured: 720p -> 224 with two strips 4 %
@@ -461,7 +474,16 @@ PlanKey plan_key(const mxd_image& im, const Stored& st) {
   return PlanKey{{im.src_w, im.src_h, im.channels, im.resize_w, im.resize_h, im.crop_x, im.crop_y, im.crop_w,
                   im.crop_h, im.flip ? 1 : 0, im.rgba_weighted, st.x0, st.rows, (int32_t)ss, (int32_t)(ss >> 32),
                   (int32_t)ds, (int32_t)(ds >> 32), (int32_t)(reinterpret_cast<uintptr_t>(st.base) & 15),
-                  (int32_t)(reinterpret_cast<uintptr_t>(im.dst) & 15), 0}};
+                  (int32_t)(reinterpret_cast<uintptr_t>(im.dst) & 15), st.ycc ? 1 : 0}};
+}
+
+bool ycc_plan_ok(const mxd_image& im, const Stored& st, int32_t out_dtype, int32_t device) {
+  if (!st.ycc || (g_policy.load() & MXD_POLICY_NO_WAVE)) return false;
+  ImgPlan p;
+  if (tables().get(device, im.src_w, im.resize_w, &p.xt) != MXD_OK) return false;
+  if (tables().get(device, im.src_h, im.resize_h, &p.yt) != MXD_OK) return false;
+  plan_wave(im, st, out_dtype == MXD_F32_DIV255 ? 1 : 0, out_dtype, p);
+  return p.wave && p.ycc;
 }
 
 

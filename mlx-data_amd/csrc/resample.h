@@ -32,8 +32,26 @@ struct ImgDev {
   int32_t nstrips, ty, tx, group;
   int32_t src_w, src_h;  // src_h: rows stored at src (the whole image, or a staged footprint)
   int32_t src_x0, src_y0;  // source pixel at src (0, 0 unless only a footprint is stored)
+  const struct YccDev* ycc;  // wave kernels: the source is JPEG sample planes, not RGB (null: RGB at src)
 };
-static_assert(sizeof(ImgDev) == 104, "ImgDev layout");
+static_assert(sizeof(ImgDev) == 112, "ImgDev layout");
+
+// A JPEG image's sample planes as a wave kernel's source (the fused decode
+// finish): 4:2:0 YCbCr as jpeg_idct writes them; the kernel
+// makes the RGB pixels of the rows it reads in registers, by jpeg_color's
+// rules (h2v2 fancy upsampling, jdcolor's fixed-point YCbCr -> RGB).
+// ImgDev::src is the Y plane's first byte; the source image is the window
+// from (win_x, win_y) (win_x a multiple of 4) of win_w x win_h =
+// ImgDev::src_w x src_h pixels.
+struct YccDev {
+  int64_t cb, cr;          // Cb / Cr plane: byte offset from the Y plane
+  int32_t ystride, cstride;
+  int32_t dw, dh;          // chroma plane samples per row / rows (jdsample's downsampled size)
+  int32_t win_x, win_y;
+  int32_t records;         // bytes from the Y plane to the Cr plane's end (the buffer's range)
+  int32_t pad;
+};
+static_assert(sizeof(YccDev) == 48, "YccDev layout");
 
 struct LaunchCfg {
   int32_t vec;        // bytes per thread per source row: 16 (16-byte aligned rows) or 1
@@ -63,6 +81,7 @@ struct WaveCfg {
   int32_t p;  // source pixels per lane (wave_default_p, or 8 for wide RGB windows; RGB 16 = byte lanes)
   int32_t per_img = 0;  // units of every image when all images of the launch have the same count, else 0
   int32_t prio = 1;     // progress-based wave priority (off for the concurrent launches of a mixed batch)
+  int32_t ycc = 0;      // sources are JPEG sample planes (ImgDev::ycc; scatter, p = 4, no shift)
 };
 
 // Scatter schedule geometry, shared by the kernel and the host builder:

@@ -50,6 +50,7 @@
 #include <utility>
 
 #include "devutil.h"
+#include "jpegycc.h"
 #include "resample.h"
 
 namespace mxd {
@@ -198,6 +199,13 @@ struct Raw {
   uint32_t d[ND];
 };
 
+// Raw bytes -> f32 planes: x[c][p] = byte C*p + c (p pixels of the lane).
+template <int C, int P>
+__device__ __forceinline__ void to_planes(const Raw<P * C / 4>& v, float (&x)[C][P]) {
+#pragma unroll
+  for (int i = 0; i < P * C; i++) x[i % C][i / C] = (float)((v.d[i >> 2] >> (8 * (i & 3))) & 0xffu);
+}
+
 // n consecutive dwords of a buffer row into w[0..n).
 template <int N>
 __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_t* w) {
@@ -225,9 +233,11 @@ __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_
 // outside the stored region read zeros, never other memory.
 template <class L, bool SHIFT>
 struct Src {
+  using RawT = Raw<L::ND>;
   Rsrc live, dead;
   int stride, voff, voff2, sh, y0;  // voff2: the second window half (L::SPLIT)
 
+  __device__ __forceinline__ void planes(const RawT& v, float (&x)[L::VC][L::VP]) const { to_planes<L::VC, L::VP>(v, x); }
   __device__ __forceinline__ Raw<L::ND> load(int r) const {
     constexpr int ND = L::ND;
     const bool ok = r >= 0 && !(MXD_ABLATE & 1);
@@ -266,12 +276,72 @@ struct Src {
   }
 };
 
-// Raw bytes -> f32 planes: x[c][p] = byte C*p + c (p pixels of the lane).
-template <int C, int P>
-__device__ __forceinline__ void to_planes(const Raw<P * C / 4>& v, float (&x)[C][P]) {
+// JPEG sample planes as the source of RGB pixel lanes (P = 4; resample.h
+// YccDev): a row load fetches the lane's four Y samples and, per chroma
+// component, the samples c - 1 .. c + 2 (c: the chroma column of its first
+// pixel) of the two chroma rows the row's fancy upsampling blends; planes()
+// makes the four RGB pixels from them with jpegdev.hip jpeg_color's
+// arithmetic (jpeg.cpp upsample_row h2v2, jdcolor.c), so the resampled bytes
+// are those of the RGB frame jpeg_color would have written.
+struct YccRaw {
+  uint32_t y;
+  uint32_t c[2][2][2];  // [Cb / Cr][near / far row][two dwords from the lane's chroma dword]
+};
+
+struct YccSrc {
+  using RawT = YccRaw;
+  Rsrc live, dead;
+  int ystride, cstride, cb, cr, dw, dh, wy;
+  int yoff;  // the lane's Y byte in window row 0 (kNoLoad: a lane past the window)
+  int coff;  // its chroma dword's byte offset in a chroma row (kNoLoad likewise)
+  int e;     // byte of sample c - 1 in the two chroma dwords (-1 at the left edge: c = 0)
+  int ci;    // c
+
+  __device__ __forceinline__ YccRaw load(int r) const {
+    const bool ok = r >= 0 && !(MXD_ABLATE & 1);
+    const Rsrc rs = ok ? live : dead;
+    const int ry = wy + (ok ? r : 0);  // image row
+    const int iy = ry >> 1;
+    const uint32_t c0 = (uint32_t)(min(iy, dh - 1) * cstride) + (uint32_t)coff;
+    const uint32_t c1 = (uint32_t)(min(max((ry & 1) ? iy + 1 : iy - 1, 0), dh - 1) * cstride) + (uint32_t)coff;
+    YccRaw v;
+    v.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((uint32_t)yoff + (uint32_t)((ok ? r : 0) * ystride)), 0, 0);
+    const uint32_t offs[2][2] = {{c0 + (uint32_t)cb, c1 + (uint32_t)cb}, {c0 + (uint32_t)cr, c1 + (uint32_t)cr}};
 #pragma unroll
-  for (int i = 0; i < P * C; i++) x[i % C][i / C] = (float)((v.d[i >> 2] >> (8 * (i & 3))) & 0xffu);
-}
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)offs[k][j], 0, 0);
+        v.c[k][j][0] = t.x;
+        v.c[k][j][1] = t.y;
+      }
+    return v;
+  }
+
+  __device__ __forceinline__ void planes(const YccRaw& v, float (&x)[3][4]) const {
+    int cs[2][4];  // chroma samples c - 1 .. c + 2: near * 3 + far
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t n = e < 0 ? v.c[k][0][0] << 8 : __builtin_amdgcn_alignbyte(v.c[k][0][1], v.c[k][0][0], e);
+      const uint32_t f = e < 0 ? v.c[k][1][0] << 8 : __builtin_amdgcn_alignbyte(v.c[k][1][1], v.c[k][1][0], e);
+#pragma unroll
+      for (int q = 0; q < 4; q++) cs[k][q] = (int)((n >> (8 * q)) & 255u) * 3 + (int)((f >> (8 * q)) & 255u);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = ci + (j >> 1), q = 1 + (j >> 1);
+      int ch[2];
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+        ch[k] = (j & 1) ? (i == dw - 1 ? (cs[k][q] * 4 + 7) >> 4 : (cs[k][q] * 3 + cs[k][q + 1] + 7) >> 4)
+                        : (i == 0 ? (cs[k][q] * 4 + 8) >> 4 : (cs[k][q] * 3 + cs[k][q - 1] + 8) >> 4);
+      uint32_t px[3];
+      jpeg_ycc_to_rgb((int)((v.y >> (8 * j)) & 255u), ch[0], ch[1], px);
+#pragma unroll
+      for (int c = 0; c < 3; c++) x[c][j] = (float)px[c];
+    }
+  }
+};
 
 // acc += w * x (pairs of pixels per v_pk_fma_f32).
 template <int C, int P>
@@ -384,8 +454,8 @@ struct HStrip {
 
 // Runs a band's scatter schedule (see the top of the file); on_row(acc, y) is
 // called with the V sums of every completed output row y.
-template <class L, int S, int DMAX, bool SHIFT, class OnRow, class Start>
-__device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const Src<L, SHIFT>& src, OnRow&& on_row,
+template <class L, int S, int DMAX, class SrcT, class OnRow, class Start>
+__device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const SrcT& src, OnRow&& on_row,
                                              Start&& start, bool prio, bool sync = false) {
   constexpr int C = L::VC;
   constexpr int R = scatter_ring_slots(DMAX, L::LB);
@@ -399,7 +469,7 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
   float acc[S][C][P];
 #pragma unroll
   for (int s = 0; s < S; s++) zero_planes<C, P>(acc[s]);
-  Raw<L::ND> ring[R];
+  typename SrcT::RawT ring[R];
   static_for<LA>([&](auto ic) {
     __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's counted waits assume it
     ring[decltype(ic)::value] = src.load(itab[decltype(ic)::value * E + 1]);
@@ -427,7 +497,7 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
             return;
           }
           float x[C][P];
-          to_planes<C, P>(ring[i % R], x);
+          src.planes(ring[i % R], x);
           static_for<S>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int wbits = ent[j * E + 2 + k];
@@ -457,7 +527,7 @@ constexpr int min_waves(int c, int p, int kind, int dmax) {
 }
 
 // One unit (image, band, strip) by the calling wave; planes = its LDS rows.
-template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
+template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC>
 __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int nimgs, int per_img, int unit,
                                          float* __restrict__ planes, int lane, bool prio) {
   using L = Lay<C, P>;
@@ -602,8 +672,34 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    scatter_band<L, S, DMAX, SHIFT>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio,
-                                    nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0);
+    const bool sync = nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
+    if constexpr (YCC) {
+      static_assert(C == 3 && P == 4 && !SHIFT, "JPEG plane sources: RGB pixel lanes, P = 4, aligned windows");
+      // the same window as the RGB source would have (hbase = wp0), read from the planes
+      const YccDev* yd = uniform_ptr<const YccDev*>(im.ycc);
+      YccSrc ys;
+      const int records = __builtin_amdgcn_readfirstlane(yd->records);
+      ys.live = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.src), (short)0, records, 0x00020000);
+      ys.dead = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr<void*>(im.src), (short)0, 0, 0x00020000);
+      ys.ystride = __builtin_amdgcn_readfirstlane(yd->ystride);
+      ys.cstride = __builtin_amdgcn_readfirstlane(yd->cstride);
+      ys.cb = __builtin_amdgcn_readfirstlane((int)yd->cb);
+      ys.cr = __builtin_amdgcn_readfirstlane((int)yd->cr);
+      ys.dw = __builtin_amdgcn_readfirstlane(yd->dw);
+      ys.dh = __builtin_amdgcn_readfirstlane(yd->dh);
+      ys.wy = __builtin_amdgcn_readfirstlane(yd->win_y);
+      const int wx = __builtin_amdgcn_readfirstlane(yd->win_x);
+      const int xl = wx + hbase + 4 * lane;  // the lane's first pixel (image column)
+      const bool on = 4 * lane < hi + 1 - hbase;
+      const int c = xl >> 1, d = c > 0 ? (c - 1) >> 2 : 0;
+      ys.yoff = on ? ys.wy * ys.ystride + xl : kNoLoad;
+      ys.coff = on ? 4 * d : kNoLoad;
+      ys.e = c - 1 - 4 * d;
+      ys.ci = c;
+      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), ys, finish_row, start, prio, sync);
+    } else {
+      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio, sync);
+    }
   }
 #if MXD_STAMPS
   if (lane == 0 && unit < kMaxStamped) {
@@ -613,7 +709,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
 #endif
 }
 
-template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT>
+template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC = false>
 __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void resample_wave(
     const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -628,7 +724,7 @@ __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void r
     for (int i = 0; i < L::PAD; i += kLanes)
       if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
   if (unit < nunits)
-    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT>(imgs, nimgs, per_img, unit, planes, lane,
+    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC>(imgs, nimgs, per_img, unit, planes, lane,
                                                     __builtin_amdgcn_readfirstlane(prio) != 0);
 }
 
@@ -678,11 +774,13 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   if (cfg.channels != 3) return nullptr;
 #define MXD_SCATTER(S_, D_, T_, Q_, P_)                                                           \
   if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == P_)              \
-    return cfg.shift ? resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, true>                  \
-                     : resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, false>;
+    return cfg.ycc ? (P_ == 4 && !cfg.shift ? resample_wave<3, 4, F32, T_, Q_, kScatter, S_, D_, false, true> \
+                                            : nullptr)                                            \
+           : cfg.shift ? resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, true>                \
+                       : resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, false>;
   // byte lanes (P = 16): any base alignment, no realignment variant
 #define MXD_SCATTER_B(S_, D_, T_, Q_)                                                             \
-  if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == 16)              \
+  if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == 16 && !cfg.ycc)  \
     return resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false>;
   MXD_SCATTER(2, 4, 8, 2, 8)    // 960 -> 256 (C2)
   MXD_SCATTER(2, 4, 8, 1, 4)
@@ -724,6 +822,7 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
 
 WaveKernel select_kernel(const WaveCfg& cfg) {
   if (cfg.kind == kScatter) return cfg.f32 ? select_scatter<true>(cfg) : select_scatter<false>(cfg);
+  if (cfg.ycc) return nullptr;  // JPEG plane sources: scatter kernels only
   switch (cfg.channels * 2 + (cfg.f32 ? 1 : 0)) {
     case 2: return select_q<1, false>(cfg);
     case 3: return select_q<1, true>(cfg);

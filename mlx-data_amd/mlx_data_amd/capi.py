@@ -32,7 +32,7 @@ EXPORTS = (
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
     "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
     "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
-    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device",
+    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources",
 )
 
 MXD_AFFINE = 0
@@ -59,6 +59,7 @@ MXD_TUNE_HUFF_GLOBAL = 6
 MXD_TUNE_HOST_WAIT = 7
 MXD_TUNE_HOST_STREAMS = 8
 MXD_TUNE_HUFF_JOB = 9
+MXD_TUNE_JPEG_RGB = 10
 
 
 class MxdImage(ctypes.Structure):
@@ -325,6 +326,14 @@ def make_jpeg_images(entries):
 
 def jpeg_resize_crop_host(images, n, out_dtype, device=0):
     check(lib().mxd_jpeg_resize_crop_host(images, n, out_dtype, device))
+
+
+def jpeg_plane_sources(reset=False):
+    """Images resized straight from their JPEG sample planes since the last
+    reset (mxd_jpeg_plane_sources)."""
+    c = ctypes.c_int64()
+    check(lib().mxd_jpeg_plane_sources(ctypes.byref(c), 1 if reset else 0))
+    return c.value
 
 
 def jpeg_resize_crop_to_device(images, n, out_dtype, device=0):

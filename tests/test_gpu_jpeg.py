@@ -136,6 +136,55 @@ def test_resize_crop_windows_equal_host_pixels(f32, device_dst):
         assert np.array_equal(g, w_)
 
 
+def _smallest_side(w, h, size):
+    return capi.resize_smallest_side_dims(w, h, size)
+
+
+@pytest.mark.parametrize("f32,device_dst", [(False, False), (True, False), (True, True)])
+def test_plane_sources_equal_rgb_frames(f32, device_dst):
+    """4:2:0 images whose resize runs on a scatter wave
+    kernel are resized straight from their sample planes (wave.hip YccSrc:
+    fancy upsampling + YCbCr -> RGB in registers, no RGB frame).  Every
+    output equals mxd_resize_crop_host on the host-decoded pixels and the
+    same call through the RGB frame (MXD_TUNE_JPEG_RGB = 1) byte for byte:
+    odd and tiny sizes, restart intervals, windows (x a multiple of 4, any
+    y), mirrored crops, downscales of every scatter shape and upscales."""
+    rng = np.random.default_rng(11)
+    datas, geoms = [], []
+    for i in range(28):
+        h, w = int(rng.integers(17, 900)), int(rng.integers(17, 900))
+        kw = dict(quality=int(rng.integers(30, 98)), subsampling=2)
+        if i % 5 == 4:
+            kw["restart_marker_blocks"] = 3
+        datas.append(_encode(_smooth(rng, h, w), **kw))
+        if i % 3 == 0:  # a window: x a multiple of 4, any y
+            ww, wh = int(rng.integers(16, w + 1)), int(rng.integers(16, h + 1))
+            wx = int(rng.integers(0, (w - ww) // 4 + 1)) * 4
+            wy = int(rng.integers(0, h - wh + 1))
+        else:
+            wx, wy, ww, wh = 0, 0, w, h
+        size = int(rng.choice([64, 128, 224, 256, 384]))
+        rw, rh = _smallest_side(ww, wh, size)
+        cw, ch = min(rw, int(rng.integers(1, 257))), min(rh, int(rng.integers(1, 257)))
+        cx, cy = capi.center_crop_origin(rw, rh, cw, ch)
+        geoms.append((wx, wy, ww, wh, rw, rh, cx, cy, cw, ch, i % 2))
+    coefs = [capi.JpegCoefs(d) for d in datas]
+    want = _host_ref([capi.jpeg_decode(d) for d in datas], geoms, f32)
+    capi.jpeg_plane_sources(reset=True)
+    got = _gpu(coefs, geoms, f32, device_dst)
+    fused = capi.jpeg_plane_sources(reset=True)
+    prev = capi.set_tuning(capi.MXD_TUNE_JPEG_RGB, 1)
+    try:
+        rgb = _gpu(coefs, geoms, f32, device_dst)
+    finally:
+        capi.set_tuning(capi.MXD_TUNE_JPEG_RGB, prev)
+    assert capi.jpeg_plane_sources(reset=True) == 0
+    assert fused >= 14, fused  # most of them take the plane source
+    for i, (g, r, w_) in enumerate(zip(got, rgb, want)):
+        assert np.array_equal(g, w_), (i, geoms[i])
+        assert np.array_equal(g, r), i
+
+
 def test_chunked_batch_of_large_images():
     """~150 MB of coefficients: several staging chunks over both slots."""
     rng = np.random.default_rng(3)
