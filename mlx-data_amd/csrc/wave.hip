@@ -234,6 +234,7 @@ __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_
 template <class L, bool SHIFT>
 struct Src {
   using RawT = Raw<L::ND>;
+  static constexpr int kLaneBytes = L::LB;  // (its scatter ring: resample.h scatter_ring_slots)
   Rsrc live, dead;
   int stride, voff, voff2, sh, y0;  // voff2: the second window half (L::SPLIT)
 
@@ -290,6 +291,7 @@ struct YccRaw {
 
 struct YccSrc {
   using RawT = YccRaw;
+  static constexpr int kLaneBytes = kYccLaneBytes;
   Rsrc live, dead;
   int ystride, cstride, cb, cr, dw, dh, wy;
   int yoff;  // the lane's Y byte in window row 0 (kNoLoad: a lane past the window)
@@ -326,15 +328,20 @@ struct YccSrc {
       const uint32_t f = e < 0 ? v.c[k][1][0] << 8 : __builtin_amdgcn_alignbyte(v.c[k][1][1], v.c[k][1][0], e);
 #pragma unroll
       for (int q = 0; q < 4; q++) cs[k][q] = (int)((n >> (8 * q)) & 255u) * 3 + (int)((f >> (8 * q)) & 255u);
+      // the row's edges: the first sample's left neighbour and the last
+      // one's right neighbour are the sample itself (jpeg.cpp's (4 s + 8) >> 4
+      // and (4 s + 7) >> 4); pixels past the row end are never read
+      cs[k][0] = ci == 0 ? cs[k][1] : cs[k][0];
+      cs[k][2] = ci == dw - 1 ? cs[k][1] : cs[k][2];
+      cs[k][3] = ci + 1 >= dw - 1 ? cs[k][2] : cs[k][3];
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const int i = ci + (j >> 1), q = 1 + (j >> 1);
+      const int q = 1 + (j >> 1);
       int ch[2];
 #pragma unroll
       for (int k = 0; k < 2; k++)
-        ch[k] = (j & 1) ? (i == dw - 1 ? (cs[k][q] * 4 + 7) >> 4 : (cs[k][q] * 3 + cs[k][q + 1] + 7) >> 4)
-                        : (i == 0 ? (cs[k][q] * 4 + 8) >> 4 : (cs[k][q] * 3 + cs[k][q - 1] + 8) >> 4);
+        ch[k] = (j & 1) ? (cs[k][q] * 3 + cs[k][q + 1] + 7) >> 4 : (cs[k][q] * 3 + cs[k][q - 1] + 8) >> 4;
       uint32_t px[3];
       jpeg_ycc_to_rgb((int)((v.y >> (8 * j)) & 255u), ch[0], ch[1], px);
 #pragma unroll
@@ -458,9 +465,9 @@ template <class L, int S, int DMAX, class SrcT, class OnRow, class Start>
 __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const SrcT& src, OnRow&& on_row,
                                              Start&& start, bool prio, bool sync = false) {
   constexpr int C = L::VC;
-  constexpr int R = scatter_ring_slots(DMAX, L::LB);
+  constexpr int R = scatter_ring_slots(DMAX, SrcT::kLaneBytes);
   constexpr int LA = R - 1;  // iterations loaded ahead
-  constexpr int BG = scatter_block_groups(S, DMAX, L::LB);
+  constexpr int BG = scatter_block_groups(S, DMAX, SrcT::kLaneBytes);
   constexpr int E = scatter_entry_words(S);
   constexpr int P = L::VP;
   const int ngroups = sched[0];

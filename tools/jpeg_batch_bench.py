@@ -62,11 +62,13 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the host entropy decode runs")
     ap.add_argument("--huff-job", default="0", help="device entropy: own subsequences per job to time (0: default)")
     ap.add_argument("--seconds", type=float, default=2.0, help="timed loop length per run")
+    ap.add_argument("--jpeg-rgb", type=int, default=0, help="MXD_TUNE_JPEG_RGB: 1 = always through an RGB frame")
     args = ap.parse_args()
     from mlx_data_amd import capi
 
     L = capi.lib()
     capi.check(L.mxd_set_device(0))
+    capi.set_tuning(capi.MXD_TUNE_JPEG_RGB, args.jpeg_rgb)
     for spec in args.datasets.split(","):
         name, _, nb = spec.partition(":")  # "l12:4": a dataset's own batch size
         batch = int(nb) if nb else args.batch
