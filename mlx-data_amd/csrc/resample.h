@@ -109,8 +109,13 @@ constexpr int scatter_gcd(int a, int b) { return b ? scatter_gcd(b, a % b) : a; 
 // (Narrow-lane rings of 4 / 3 slots at DMAX 2 / 3, 8 waves per SIMD, were
 // measured in round 4 and lost: 480p 0.0935 vs 0.0903 ms per launch, C4
 // 0.0236 vs 0.0227, profiles/r04/ring_pack_b.jsonl.)
+// JPEG plane sources (wave.hip YccSrc) hold 9 dwords per ring slot: their
+// ring is the smallest that keeps the unrolled block at S = 2 groups (3 slots
+// at DMAX 1, 4 at DMAX 2, DMAX up to 6, then 6 or 4).
+constexpr int kYccLaneBytes = 36;
 constexpr int scatter_ring_slots(int dmax, int lane_bytes = 0) {
-  (void)lane_bytes;
+  if (lane_bytes == kYccLaneBytes)
+    return dmax == 1 ? 3 : dmax == 2 ? 4 : dmax <= 6 ? dmax : (2 * dmax) % 6 == 0 ? 6 : 4;
   if (MXD_RING_FIXED > 0 && dmax >= 2) return MXD_RING_FIXED;
   if (dmax == 5 && MXD_RING == 6) return 4;
   if (MXD_RING % dmax == 0) return MXD_RING;

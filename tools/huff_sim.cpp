@@ -150,6 +150,7 @@ State run(const Img& im, const Sub& u, State in, int64_t* steps, int64_t* blocks
 int64_t g_chg[3] = {0, 0, 0};
 int64_t g_len[18] = {0};
 int64_t g_pair[4][3] = {{0}};
+int64_t g_multi[6][2] = {{0}};
 int64_t g_walk[4] = {0, 0, 0, 0};  // walk steps into a variant follower: all, same pos, same k class, accepted  // changes after round 0: all, same position, same position and index
 
 struct PhaseStats;
@@ -786,6 +787,27 @@ bool write_check(const Img& im, const std::vector<Sub>& subs, const std::vector<
       const bool fin = step(im, s, stt, &kk, &v);
       st.write_steps++;
       {
+        // multi-symbol model: greedy steps of up to M symbols of one block whose bits fit W
+        extern int64_t g_multi[6][2];
+        static int acc_bits[6] = {0}, acc_n[6] = {0};
+        static const int Wv[6] = {11, 12, 12, 13, 14, 16}, Mv[6] = {2, 2, 3, 3, 3, 4};
+        const int len = (int)(stt.pos - p0);
+        for (int m = 0; m < 6; m++) {
+          // does this symbol join the open step?
+          if (acc_n[m] > 0 && !dc && acc_bits[m] + len <= Wv[m] && acc_n[m] < Mv[m]) {
+            acc_bits[m] += len;
+            acc_n[m]++;
+          } else {
+            g_multi[m][0]++;  // a new step
+            acc_bits[m] = len <= Wv[m] ? len : 99;
+            acc_n[m] = 1;
+          }
+          if (fin || dc) acc_n[m] = dc && !fin ? acc_n[m] : 0;  // a block's end closes the step
+          if (dc) acc_n[m] = 0;  // DC tables hold single symbols
+          g_multi[m][1]++;
+        }
+      }
+      {
         // pairing model (--pairs): greedy pairs of consecutive symbols of one block whose bits fit L
         extern int64_t g_pair[4][3];
         static int prev_len = -1, prev_dc = 0;
@@ -927,6 +949,12 @@ int main(int argc, char** argv) {
   for (int L = 0; L < 4; L++)
     std::printf("pairs in %d bits: AC-AC %.1f %%, DC-AC %.1f %% of symbols paired\n", 10 + L,
                 200.0 * g_pair[L][0] / g_pair[0][2], 200.0 * g_pair[L][1] / g_pair[0][2]);
+  {
+    static const int Wv[6] = {11, 12, 12, 13, 14, 16}, Mv[6] = {2, 2, 3, 3, 3, 4};
+    for (int m = 0; m < 6; m++)
+      std::printf("steps per symbol, <= %d symbols in %d bits: %.3f\n", Mv[m], Wv[m],
+                  (double)g_multi[m][0] / g_multi[m][1]);
+  }
   std::printf("heads per round:");
   for (int r = 0; r < 20 && heads_sum[r] > 0; r++) std::printf(" %.0f/%.0f", heads_sum[r] / nf, items_sum[r] / nf);
   std::printf("\n");

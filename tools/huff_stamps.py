@@ -62,6 +62,13 @@ def main():
             d = (t_end[:, r] - t_end[:, r - 1])[ok]
             per.append(dict(round=r, lanes=int(np.median(lanes[ok, r - 1])), cycles=int(np.median(d))))
         line["per_round"] = per
+        pred = np.concatenate([j[:, 9] for _, j in runs]) != 0
+        dcw = W[:, 7] >> 32
+        for name, sel in (("pred_jobs", pred), ("first_jobs", ~pred)):
+            if sel.any():
+                line[name] = dict(n=int(sel.sum()), total=stat((st[:, 5] - st[:, 0])[sel]),
+                                  rounds=stat((st[:, 2] - st[:, 1])[sel]), after_rounds=stat((st[:, 5] - st[:, 3])[sel]),
+                                  dc_wait=stat(dcw[sel]))
         line["first_scan"] = int(np.median(t_end[:, 0] - st[:, 1]))
         rt = W[:, 6]
         line["start_spread_ns_med"] = int(np.median([(w[:, 6].max() - w[:, 6].min()) * 10 for w, _ in runs]))
