@@ -145,8 +145,8 @@ static_assert(sizeof(HuffJobDev) == 40, "HuffJobDev layout");
 // What a job publishes for the next one (device memory, zeroed before the
 // launch): 64-bit words, each written once with bit 63 set (so every word
 // is its own ready flag and no fence orders them): [0] its last own
-// subsequence's exit state (bit position in bits 0..31, block of the MCU in
-// 32..39, coefficient index in 40..47), [1] the block index there, [2..4]
+// subsequence's exit state (bit position in bits 0..31, 3 x the block of
+// the MCU in 32..39, coefficient index in 40..47), [1] the block index there, [2..4]
 // the DC-difference sums of that segment up to there, per component.
 #ifdef MXD_HUFF_STAMPS
 constexpr int kHuffPubWords = 32;  // diagnostic build: words 8.. hold the job's phase stamps (jpeghuff.hip)

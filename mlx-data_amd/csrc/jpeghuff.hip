@@ -44,7 +44,12 @@ namespace {
 // past the segment reads as w[nw] (zero) without a separate select.  It holds
 // the two words under the window and loads the one after them a step ahead
 // (off the symbol loop's dependency chain).
+template <bool CLAMP = true>
 struct LdsReader {
+  // The synchronisation rounds never decode a segment's last subsequence, so
+  // their reads stay within ~3 words of a subsequence end that lies inside
+  // the segment's staged words: they read without the clamp.
+  using Sync = LdsReader<false>;
   const uint32_t* w;
   int32_t nw;     // the segment's last word index read (its zero word)
   int32_t wq, o;  // the window starts at bit o of word wq
@@ -57,7 +62,10 @@ struct LdsReader {
     w = static_cast<const uint32_t*>(base) + w0;
     nw = min(nwords, lim);
   }
-  __device__ __forceinline__ uint32_t word(int32_t i) const { return w[min(i, nw)]; }
+  __device__ __forceinline__ uint32_t word(int32_t i) const {
+    if constexpr (CLAMP) return w[min(i, nw)];
+    return w[i];
+  }
   __device__ __forceinline__ void seek(int32_t bit) {
     wq = bit >> 5;
     o = bit & 31;
@@ -83,6 +91,7 @@ struct LdsReader {
 // of the one being consumed, so a chunk's load latency hides behind ~256 bits
 // of decoding.  Chunks past the segment are not loaded.
 struct GlobalReader {
+  using Sync = GlobalReader;
   const uint4* chunks;  // the job's words (16-byte aligned)
   int32_t w0, nw;       // the segment's first word (relative to the job's) and its words
   int32_t last_chunk;   // the segment's last chunk
@@ -160,8 +169,11 @@ __device__ __noinline__ uint32_t huff_search_step(const HuffDev& t, uint32_t win
   return huff_step_single(huff_step_entry(cls, l, t.vals[((int32_t)(p16 >> (16 - l)) + t.valoffset[l]) & 0xff]));
 }
 
-__device__ __forceinline__ int extend(uint32_t v, int s) {
-  return s == 0 ? 0 : (int)v < (1 << (s - 1)) ? (int)v + ((-1) << s) + 1 : (int)v;
+// jdhuff.c HUFF_EXTEND for s >= 1 value bits v: a leading 0 bit means
+// negative, v - (2^s - 1).
+__device__ __forceinline__ int extend_nz(uint32_t v, int s) {
+  const uint32_t mask = (1u << s) - 1u;
+  return v > (mask >> 1) ? (int)v : (int)v - (int)mask;
 }
 
 // One segment of the job in LDS.
@@ -184,7 +196,7 @@ struct Shared {
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
   int32_t done[kHuffThreads];      // blocks a subsequence completes (sync pass)
-  int64_t blk_off[kHuffMaxBlocks];  // block j of an MCU: offset of MCU (0, 0)'s block j in the coefficients,
+  int32_t blk_off[kHuffMaxBlocks];  // block j of an MCU: offset of MCU (0, 0)'s block j in the image's coefficients,
   int32_t blk_mxs[kHuffMaxBlocks];  // and its steps per MCU column / row (non-interleaved: per block)
   int32_t blk_mys[kHuffMaxBlocks];
   int16_t sub_seg[kHuffThreads];   // segment of each subsequence
@@ -214,6 +226,43 @@ struct Shared {
 #else
 #define HUFF_STAMP(i)
 #endif
+
+// The block of the MCU, MCU column and row of a block in decode order, and
+// its coefficient offset in the image (sh.blk_off / blk_mxs / blk_mys; 32-bit:
+// an image has < 2^31 coefficients), advanced without divisions.
+struct BlockCursor {
+  uint32_t j = 0, mx = 0, my = 0;
+  __device__ __forceinline__ void set(uint32_t g, uint32_t bpm, uint32_t mcux) {
+    const uint32_t m = g / bpm;
+    j = g - m * bpm;
+    my = m / mcux;
+    mx = m - my * mcux;
+  }
+  __device__ __forceinline__ int32_t off(const Shared& sh) const {
+    return sh.blk_off[j] + (int32_t)(my * (uint32_t)sh.blk_mys[j] + mx * (uint32_t)sh.blk_mxs[j]);
+  }
+  __device__ __forceinline__ void next(uint32_t bpm, uint32_t mcux) {
+    j++;
+    const bool wrap = j == bpm;
+    j = wrap ? 0 : j;
+    mx += wrap ? 1 : 0;
+    const bool row = mx == mcux;
+    mx = row ? 0 : mx;
+    my += row ? 1 : 0;
+  }
+  // forward by q MCUs and r < bpm blocks
+  __device__ __forceinline__ void advance(uint32_t q, uint32_t r, uint32_t bpm, uint32_t mcux) {
+    j += r;
+    const bool carry = j >= bpm;
+    j -= carry ? bpm : 0;
+    mx += q + (carry ? 1 : 0);
+    if (mx >= mcux) {
+      const uint32_t rows = mx / mcux;
+      my += rows;
+      mx -= rows * mcux;
+    }
+  }
+};
 
 // Block-wide exclusive prefix sum of v (every thread of the workgroup calls it).
 __device__ int block_exclusive_scan(int v, int* totals, int* total_out) {
@@ -279,29 +328,31 @@ __device__ void block_exclusive_scan3(const int* v, int* out, int3* totals) {
   out[2] = before.z + x2 - v[2];
 }
 
-// Decoder state machine over one segment: block b of the MCU, next
-// coefficient k (0 = the DC difference), symbols from Reader r.
+// Decoder state machine over one segment: block j of the MCU held as b =
+// 3 j (the bit offset of its fields in the packs below; the exit and start
+// states carry it so too), next coefficient k (0 = the DC difference),
+// symbols from Reader r.
 template <bool SEARCH>
 struct Dec {
   const HuffDev* tab;
   int b, k;
   // per-block table indices and components in registers
-  uint32_t dpack, apack;  // the DC / AC table of each block of the MCU (bits 3b..3b+2)
-  uint32_t cpack;         // component of each block of the MCU (bits 2b..2b+1)
-  int bpm;
+  uint32_t dpack, apack;  // the DC / AC table of each block of the MCU (bits 3j..3j+2)
+  uint32_t cpack;         // component of each block of the MCU (bits 3j..3j+1)
+  int bpm3;               // 3 x blocks per MCU
 
   __device__ __forceinline__ void init(const HuffImgDev& im, const HuffDev* tab_) {
     tab = tab_;
     b = k = 0;
-    bpm = im.bpm;
+    bpm3 = 3 * im.bpm;
     dpack = apack = cpack = 0;
-    for (int j = 0; j < bpm; j++) {
+    for (int j = 0; j < im.bpm; j++) {
       dpack |= (uint32_t)(im.blk_dc[j] & 7) << (3 * j);
       apack |= (uint32_t)(im.blk_ac[j] & 7) << (3 * j);
-      cpack |= (uint32_t)(im.blk_comp[j] & 3) << (2 * j);
+      cpack |= (uint32_t)(im.blk_comp[j] & 3) << (3 * j);
     }
   }
-  __device__ __forceinline__ int comp() const { return (cpack >> (2 * b)) & 3; }
+  __device__ __forceinline__ int comp() const { return (cpack >> b) & 3; }
 
   // Decodes one step -- one symbol, or two (jpeghuff.h HuffDev: an AC
   // table's entry pairs a symbol with the next one when both, value bits
@@ -321,10 +372,14 @@ struct Dec {
   template <class Reader, class OnSym>
   __device__ __forceinline__ bool step(Reader& r, int32_t& rem, OnSym&& on_sym) {
     const bool dc = k == 0;
-    const HuffDev& t = tab[((dc ? dpack : apack) >> (3 * b)) & 7];
+    const HuffDev& t = tab[((dc ? dpack : apack) >> b) & 7];
     const uint32_t w = r.win();
     const uint32_t st1 = t.step[w >> (32 - kHuffLook)];
-    const uint32_t st2 = t.step_long[max((int)(w >> 16) - (65536 - kHuffLong), 0)];  // no dependent load of a base
+    // the top kHuffLong 16-bit patterns, read beside the first lookup (no
+    // dependent load of a base); only used where st1 is 0, i.e. for patterns
+    // from 65536 - kHuffLong on, whose index the low bits are
+    static_assert((65536 - kHuffLong) % kHuffLong == 0, "long patterns start on a kHuffLong boundary");
+    const uint32_t st2 = t.step_long[(w >> 16) & (kHuffLong - 1)];
     uint32_t st = st1 ? st1 : st2;
     if constexpr (SEARCH) {  // launches with a table the two lookups do not cover
       if (!st) st = huff_search_step(t, w, dc ? 0 : 1);
@@ -343,7 +398,7 @@ struct Dec {
     rem -= shift;
     const bool end = knew >= 64;
     k = end ? 0 : knew;
-    b = end ? (b + 1 == bpm ? 0 : b + 1) : b;
+    b = end ? (b + 3 == bpm3 ? 0 : b + 3) : b;
     return end;
   }
 };
@@ -407,7 +462,7 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
   const int t = threadIdx.x;
   Dec<SEARCH> dec;
   dec.init(sh.img, tab);
-  R rd;
+  typename R::Sync rd;
 #ifdef MXD_HUFF_STAMPS
   int round = 0;
 #endif
@@ -603,8 +658,11 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
   // decodes its end: the neighbouring job writes into those with no barrier
   // in between, so their owners here zero them position by position.
   const int ke = sh.in_k[t];
+  const int32_t start_pos = sh.in_pos[t];
   const int64_t gx = g + my_done;                   // the block it ends inside (non-last)
   const int kx = u.seg_last ? 0 : sh.out_k[t];
+  const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
+  int16_t* const icoef = coef + im.coef;            // the image's coefficients
   // the job's first block (from position kf on: the previous job decodes its
   // start) and its last (to position kl: the next job decodes the rest)
   if (act && t == job.warm) {
@@ -620,8 +678,17 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     const int64_t first = sh.zero_range[0], last = sh.zero_range[1];
     const int kf = sh.zero_k[0], kl = sh.zero_k[1];
     const int64_t z0 = first + (kf != 0 ? 1 : 0), pieces = (last - z0) * 8;
-    for (int64_t c = t; c < pieces; c += blockDim.x)
-      reinterpret_cast<uint4*>(coef + block_addr(im, z0 + (c >> 3)))[c & 7] = uint4{0u, 0u, 0u, 0u};
+    if (t < pieces) {
+      // thread t's pieces: t, t + blockDim, ... -- blocks blockDim / 8 apart,
+      // reached by a cursor jump instead of a division per piece
+      const uint32_t jump = blockDim.x >> 3, jq = jump / bpm, jr = jump - jq * bpm;
+      BlockCursor zc;
+      zc.set((uint32_t)(z0 + (t >> 3)), bpm, mcux);
+      for (int64_t c = t; c < pieces; c += blockDim.x) {
+        reinterpret_cast<uint4*>(icoef + zc.off(sh))[t & 7] = uint4{0u, 0u, 0u, 0u};
+        zc.advance(jq, jr, bpm, mcux);
+      }
+    }
     auto zero = [&](int64_t b, int k0, int k1) {
       int16_t* d = coef + block_addr(im, b);
       for (int q = k0; q < k1; q++) d[q] = 0;
@@ -629,58 +696,47 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     if (t == job.warm && kf != 0) zero(first, kf, last == first && kl != 0 ? kl : 64);
     if (act && u.job_last && kl != 0 && !(last == first && kf != 0)) zero(last, 0, kl);
   }
+  // the start / exit / block-count arrays are free from here on: each thread
+  // keeps its DC-difference sums per component in its own slots of them
+  int* const dcslot[3] = {&sh.done[t], &sh.in_pos[t], &sh.out_pos[t]};
+  *dcslot[0] = *dcslot[1] = *dcslot[2] = 0;
   __syncthreads();  // the zeros land before the coefficients
 
   // 5. write pass (own subsequences)
   Dec<SEARCH> dec;
   dec.init(im, tab);
-  int dcsum[3] = {0, 0, 0};
-  int64_t dc0 = -1, dc1 = -1;  // blocks whose DC this subsequence decoded: [dc0, dc1)
-  uint32_t cur0[3] = {0, 0, 0};  // the block cursor (block of the MCU, MCU column, row) at the first block
+  int64_t dc0 = 0, dc1 = 0;  // blocks whose DC this subsequence decoded: [dc0, dc1)
+  BlockCursor cur0;          // the cursor at its first block
   if (act && u.own) {
     R rd;
     rd.init(wbase, u.sg.word, (u.sg.bits + 31) >> 5, u.sg.lim);
-    rd.seek(sh.in_pos[t]);
+    rd.seek(start_pos);
     dec.b = sh.in_b[t];
-    dec.k = sh.in_k[t];
-    // block cursor: (MCU column, row, block of the MCU), advanced without divisions
-    const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
-    const uint32_t g0 = (uint32_t)min(g, seg_block1 - 1), m0 = g0 / bpm;
-    uint32_t cj = g0 - m0 * bpm, cmy = m0 / mcux, cmx = m0 - cmy * mcux;
-    cur0[0] = cj;
-    cur0[1] = cmx;
-    cur0[2] = cmy;
-    auto addr = [&]() {
-      return coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
-    };
-    int16_t* blk = addr();
-    int32_t rem = u.end - sh.in_pos[t];
+    dec.k = ke;
+    BlockCursor cur;
+    cur.set((uint32_t)min(g, seg_block1 - 1), bpm, mcux);
+    cur0 = cur;
+    int16_t* blk = icoef + cur.off(sh);
+    int32_t rem = u.end - start_pos;
     for (;;) {
       if (rem <= 0 || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && u.end - rem > u.sg.bits)) break;
       const bool fin = dec.step(rd, rem, [&](bool dc, int kk, uint32_t raw, int sz) {
-        const int v = extend(raw, sz);
-        const int c = dec.comp();
-        dcsum[0] += dc && c == 0 ? v : 0;
-        dcsum[1] += dc && c == 1 ? v : 0;
-        dcsum[2] += dc && c == 2 ? v : 0;
-        dc0 = dc && dc0 < 0 ? g : dc0;
-        dc1 = dc ? g + 1 : dc1;
-        // zig-zag order (jpeg_idct reorders); zeros (EOB, ZRL, a zero DC
-        // difference) land on positions zeroed above
-        if (v != 0) blk[kk] = (int16_t)v;
+        // zig-zag order (jpeg_idct reorders); a symbol without value bits
+        // (EOB, ZRL, a zero DC difference) stores nothing: its position was zeroed
+        if (sz != 0) {
+          const int v = extend_nz(raw, sz);
+          blk[kk] = (int16_t)v;
+          if (dc) __hip_atomic_fetch_add(dcslot[dec.comp()], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       });
       if (fin) {
         g++;
-        cj++;
-        const bool wrap = cj == bpm;
-        cj = wrap ? 0 : cj;
-        cmx += wrap ? 1 : 0;
-        const bool row = cmx == mcux;
-        cmx = row ? 0 : cmx;
-        cmy += row ? 1 : 0;
-        blk = addr();  // past the segment's last block when g == seg_block1: never stored through
+        cur.next(bpm, mcux);
+        blk = icoef + cur.off(sh);  // past the segment's last block when g == seg_block1: never stored through
       }
     }
+    dc0 = g_first + (ke != 0 ? 1 : 0);
+    dc1 = g + (dec.k != 0 ? 1 : 0);
   }
 
   // 6. DC values: per component, the differences before this subsequence in
@@ -696,6 +752,8 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
 #endif
   }
   HUFF_STAMP(4);  // (thread 0's write pass; the scans below wait for the others)
+  __syncthreads();  // (every thread's LDS sums complete)
+  int dcsum[3] = {*dcslot[0], *dcslot[1], *dcslot[2]};
   // one scan for the three components
   int ex[3];
   {
@@ -703,7 +761,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     block_exclusive_scan3(act && u.own ? dcsum : z, ex, sh.scan3);
   }
   __syncthreads();
-  // (the start / exit arrays are free now: they hold the three prefixes)
+  // (the start / exit arrays hold the three prefixes now)
   sh.done[t] = ex[0];
   sh.in_pos[t] = ex[1];
   sh.out_pos[t] = ex[2];
@@ -720,21 +778,11 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     HuffPubDev* p = pub + sh.ticket;
     for (int c = 0; c < 3; c++) publish(p, 2 + c, (uint64_t)(uint32_t)last_sum[c]);
   }
-  if (act && u.own && dc0 >= 0) {
+  if (act && u.own && dc0 < dc1) {
     // the DC differences of blocks [dc0, dc1) into values, four blocks' loads
     // issued together (the cursor of the write pass, from its first block)
-    uint32_t cj = cur0[0], cmx = cur0[1], cmy = cur0[2];
-    const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
-    auto next = [&]() {
-      cj++;
-      const bool wrap = cj == bpm;
-      cj = wrap ? 0 : cj;
-      cmx += wrap ? 1 : 0;
-      const bool row = cmx == mcux;
-      cmx = row ? 0 : cmx;
-      cmy += row ? 1 : 0;
-    };
-    if (dc0 > g_first) next();  // the first block's DC belonged to the previous subsequence
+    BlockCursor c = cur0;
+    if (dc0 > g_first) c.next(bpm, mcux);  // the first block's DC belonged to the previous subsequence
     int p0 = dcsum[0], p1 = dcsum[1], p2 = dcsum[2];
     const uint32_t cpack = dec.cpack;
     for (int64_t q = dc0; q < dc1; q += 4) {
@@ -743,9 +791,9 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
       int16_t v[4];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        a[r] = coef + im.coef + sh.blk_off[cj] + (int64_t)cmy * sh.blk_mys[cj] + (int64_t)cmx * sh.blk_mxs[cj];
-        cc[r] = (int)((cpack >> (2 * cj)) & 3);
-        next();
+        a[r] = icoef + c.off(sh);
+        cc[r] = (int)((cpack >> (3 * c.j)) & 3);
+        c.next(bpm, mcux);
       }
 #pragma unroll
       for (int r = 0; r < 4; r++) v[r] = q + r < dc1 ? a[r][0] : (int16_t)0;
@@ -870,7 +918,7 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
   __syncthreads();
   HUFF_STAMP(1);
   if (job.lds)  // uniform over the workgroup
-    decode_job<LdsReader, SEARCH>(lds_words, sh, tab, seg, nsub, coef, pub, ctl);
+    decode_job<LdsReader<>, SEARCH>(lds_words, sh, tab, seg, nsub, coef, pub, ctl);
   else
     decode_job<GlobalReader, SEARCH>(words + job.word0, sh, tab, seg, nsub, coef, pub, ctl);
 }
