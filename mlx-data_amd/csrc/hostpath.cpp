@@ -523,7 +523,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
                   : h2 && v2 && cp.dw > 2 ? mxd::kUpH2V2
                                           : mxd::kUpRep;
       c.samples += up((int64_t)cp.bw * 8 * cp.bh * 8, 256);
-      c.nblocks += (int64_t)cp.bw * cp.bh;
+      c.nblocks += ((int64_t)cp.bw * cp.bh + 63) & ~(int64_t)63;  // jpeg_idct: a wave stays in one plane
     }
     m.out = c.mid_bytes;  // relative to rgb_off, fixed below
     c.mid_bytes += up((int64_t)m.pitch * m.height, 256);

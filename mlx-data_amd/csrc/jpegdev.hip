@@ -27,13 +27,10 @@ constexpr int kPass1Bits = 2;
 constexpr i64 F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633, F1501 = 12299,
               F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
 
-__device__ __forceinline__ i64 descale(i64 x, int n) { return (x + ((i64)1 << (n - 1))) >> n; }
 
-// Zig-zag index -> natural index (jutils.c jpeg_natural_order), for blocks the
-// device entropy decode stores in zig-zag order.
-constexpr int kZigzagNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
-                                41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
-                                30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+// Natural index -> zig-zag index (the inverse of jutils.c jpeg_natural_order),
+// for blocks the device entropy decode stores in zig-zag order.
+constexpr int kNatZigzag[64] = {0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
 __device__ __forceinline__ uint32_t range_limit(i64 x) {
   const i64 v = x + 128;
@@ -41,25 +38,42 @@ __device__ __forceinline__ uint32_t range_limit(i64 x) {
 }
 
 // One 1-D pass over 8 values (even part from 0/2/4/6, odd part from 1/3/5/7),
-// jidctint.c's arithmetic; outputs in natural order before descaling.
-__device__ __forceinline__ void idct8(i64 d0, i64 d1, i64 d2, i64 d3, i64 d4, i64 d5, i64 d6, i64 d7, i64* o) {
-  const i64 z1e = (d2 + d6) * F0541;
-  const i64 t2 = z1e + d6 * -F1847;
-  const i64 t3 = z1e + d2 * F0765;
-  const i64 t0 = (d0 + d4) * (1 << kConstBits);
-  const i64 t1 = (d0 - d4) * (1 << kConstBits);
-  const i64 t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
-  i64 a0 = d7, a1 = d5, a2 = d3, a3 = d1;
-  i64 z1 = a0 + a3, z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
-  const i64 z5 = (z3 + z4) * F1175;
-  a0 *= F0298;
-  a1 *= F2053;
-  a2 *= F3072;
-  a3 *= F1501;
-  z1 *= -F0899;
-  z2 *= -F2562;
-  z3 = z3 * -F1961 + z5;
-  z4 = z4 * -F0390 + z5;
+// jidctint.c's arithmetic; outputs in natural order before descaling.  T =
+// i64 is libjpeg-turbo's JLONG; T = int32_t gives the same values when every
+// input is below 2^14 in magnitude (the largest intermediate is then below
+// 2^30.7: products of an input sum < 2^16 and a 13-bit constant, sums of
+// three such), which is every block of a well-formed file (dequantised DCT
+// coefficients of 8-bit samples stay below 2^12).
+// x * k: int32 values here are below 2^17 and constants below 2^15, so the
+// 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate) is exact
+template <class T>
+__device__ __forceinline__ T mulk(T x, int k) {
+  return x * (T)k;
+}
+template <>
+__device__ __forceinline__ int32_t mulk<int32_t>(int32_t x, int k) {
+  return __mul24(x, k);
+}
+
+template <class T>
+__device__ __forceinline__ void idct8(T d0, T d1, T d2, T d3, T d4, T d5, T d6, T d7, T* o) {
+  const T z1e = mulk<T>(d2 + d6, F0541);
+  const T t2 = z1e + mulk<T>(d6, -F1847);
+  const T t3 = z1e + mulk<T>(d2, F0765);
+  const T t0 = (d0 + d4) * (T)(1 << kConstBits);
+  const T t1 = (d0 - d4) * (T)(1 << kConstBits);
+  const T t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+  T a0 = d7, a1 = d5, a2 = d3, a3 = d1;
+  T z1 = a0 + a3, z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
+  const T z5 = mulk<T>(z3 + z4, F1175);
+  a0 = mulk<T>(a0, F0298);
+  a1 = mulk<T>(a1, F2053);
+  a2 = mulk<T>(a2, F3072);
+  a3 = mulk<T>(a3, F1501);
+  z1 = mulk<T>(z1, -F0899);
+  z2 = mulk<T>(z2, -F2562);
+  z3 = mulk<T>(z3, -F1961) + z5;
+  z4 = mulk<T>(z4, -F0390) + z5;
   a0 += z1 + z3;
   a1 += z2 + z4;
   a2 += z2 + z3;
@@ -74,20 +88,67 @@ __device__ __forceinline__ void idct8(i64 d0, i64 d1, i64 d2, i64 d3, i64 d4, i6
   o[4] = t13 - a0;
 }
 
+template <class T>
+__device__ __forceinline__ T descale_t(T x, int n) {
+  return (x + ((T)1 << (n - 1))) >> n;
+}
+
+// The block with JLONG (64-bit) arithmetic, for blocks whose values leave
+// the int32 range (corrupt data): out of line, one column / row at a time,
+// so the common path's register allocation does not carry it.
+__device__ __noinline__ void idct_block_wide(const int32_t* __restrict__ din, uint8_t* out, int stride) {
+  int32_t ws[64];
+#pragma unroll 1
+  for (int c = 0; c < 8; c++) {
+    i64 o[8];
+    idct8<i64>(din[c], din[8 + c], din[16 + c], din[24 + c], din[32 + c], din[40 + c], din[48 + c], din[56 + c], o);
+#pragma unroll
+    for (int r = 0; r < 8; r++) ws[8 * r + c] = (int32_t)descale_t<i64>(o[r], kConstBits - kPass1Bits);
+  }
+#pragma unroll 1
+  for (int r = 0; r < 8; r++) {
+    const int32_t* w = ws + 8 * r;
+    i64 o[8];
+    idct8<i64>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    uint32_t lo4 = 0, hi4 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      lo4 |= range_limit(descale_t<i64>(o[c], kConstBits + kPass1Bits + 3)) << (8 * c);
+      hi4 |= range_limit(descale_t<i64>(o[c + 4], kConstBits + kPass1Bits + 3)) << (8 * c);
+    }
+    *reinterpret_cast<uint2*>(out + (i64)r * stride) = make_uint2(lo4, hi4);
+  }
+}
+
+// Whether every value of v is inside (-2^14, 2^14) (the int32 IDCT's range).
+__device__ __forceinline__ bool small14(const int32_t* v) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 64; i++) acc |= (uint32_t)(v[i] + 16384);
+  return acc < 32768u;
+}
+
 __global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coef, const uint16_t* __restrict__ qt,
                                                  const JpegPlaneDev* __restrict__ planes, int nplanes, i64 nblocks,
                                                  uint8_t* __restrict__ samples) {
   const i64 g = (i64)blockIdx.x * 256 + threadIdx.x;
-  if (g >= nblocks) return;
-  int lo = 0, hi = nplanes - 1;  // the last plane whose first block is <= g
+  // every plane's blocks start at a multiple of 64 in this numbering (the
+  // host pads them), so a wave lies in one plane: its record, quantisation
+  // table and flags are scalar (s_load), not per-lane vector loads
+  const i64 g0 = ((i64)__builtin_amdgcn_readfirstlane((int)(g >> 32)) << 32) |
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+  if (g0 >= nblocks) return;
+  int lo = 0, hi = nplanes - 1;  // the last plane whose first block is <= g0
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (planes[mid].first_block <= g) lo = mid;
+    if (planes[mid].first_block <= g0) lo = mid;
     else hi = mid - 1;
   }
+  lo = __builtin_amdgcn_readfirstlane(lo);
   const JpegPlaneDev p = planes[lo];
   const i64 b = g - p.first_block;
-  const int by = (int)(b / p.bw), bx = (int)(b - (i64)by * p.bw);
+  if (b >= (i64)p.bw * p.bh) return;  // the plane's padding
+  const int by = (int)((uint32_t)b / (uint32_t)p.bw), bx = (int)b - by * p.bw;  // (a plane holds < 2^31 blocks)
   const int stride = p.bw * 8;
   uint8_t* out = samples + p.out + (i64)by * 8 * stride + bx * 8;
   if (!p.coded) {
@@ -98,52 +159,62 @@ __global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coe
   int32_t d[64];
   {
     const int4* cp = reinterpret_cast<const int4*>(coef + p.coef + b * 64);
-    const uint4* qp = reinterpret_cast<const uint4*>(qt + p.qtab);
-    int32_t c16[64];  // the block as stored
-    uint32_t q16[64];
+    const uint16_t* q = qt + p.qtab;  // uniform: scalar loads
+    const bool zz = p.zigzag != 0;
+    int32_t cw[64];  // the block's 64 stored coefficients, in storage order
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int4 c = cp[k];
-      const uint4 q = qp[k];
-      const int32_t cw[4] = {c.x, c.y, c.z, c.w};
-      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+      const int32_t w4[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        c16[8 * k + 2 * j] = (int32_t)(int16_t)(cw[j] & 0xffff);
-        c16[8 * k + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)cw[j] >> 16);
-        q16[8 * k + 2 * j] = qw[j] & 0xffff;
-        q16[8 * k + 2 * j + 1] = qw[j] >> 16;
+        cw[8 * k + 2 * j] = (int32_t)(int16_t)(w4[j] & 0xffff);
+        cw[8 * k + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)w4[j] >> 16);
       }
     }
-    if (p.zigzag) {
-      // coefficient z of the block sits at natural position kZigzagNat[z] (compile-time indices)
+    // natural position n holds stored coefficient kNatZigzag[n] of a zig-zag
+    // block: both candidates are compile-time register indices, the choice a
+    // select (a runtime index would put the block in scratch memory)
 #pragma unroll
-      for (int z = 0; z < 64; z++) d[kZigzagNat[z]] = c16[z] * (int32_t)q16[kZigzagNat[z]];
-    } else {
-#pragma unroll
-      for (int n = 0; n < 64; n++) d[n] = c16[n] * (int32_t)q16[n];
-    }
+    for (int n = 0; n < 64; n++) d[n] = __mul24(zz ? cw[kNatZigzag[n]] : cw[n], (int32_t)q[n]);  // 16 x 16 bits: exact
   }
-  // pass 1: columns -> int workspace (descaled by CONST_BITS - PASS1_BITS)
+  // pass 1: columns -> int workspace (descaled by CONST_BITS - PASS1_BITS),
+  // in place (column c of d is read before it is written), in 32-bit
+  // arithmetic when every input allows it (small14; a block of corrupt data
+  // that does not takes the JLONG path, idct_block_wide); pass 2: rows ->
+  // samples, likewise
+  if (!small14(d)) {
+    int32_t dw[64];  // a memory copy for the out-of-line path only
+#pragma unroll
+    for (int i = 0; i < 64; i++) dw[i] = d[i];
+    idct_block_wide(dw, out, stride);
+    return;
+  }
   int32_t ws[64];
 #pragma unroll
   for (int c = 0; c < 8; c++) {
-    i64 o[8];
-    idct8(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c], o);
+    int32_t o[8];
+    idct8<int32_t>(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c], o);
 #pragma unroll
-    for (int r = 0; r < 8; r++) ws[8 * r + c] = (int32_t)descale(o[r], kConstBits - kPass1Bits);
+    for (int r = 0; r < 8; r++) ws[8 * r + c] = descale_t<int32_t>(o[r], kConstBits - kPass1Bits);
   }
-  // pass 2: rows -> samples
+  if (!small14(ws)) {
+    int32_t dw[64];  // (pass 1's values were exact: the wide path recomputes them)
+#pragma unroll
+    for (int i = 0; i < 64; i++) dw[i] = d[i];
+    idct_block_wide(dw, out, stride);
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int32_t* w = ws + 8 * r;
-    i64 o[8];
-    idct8(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    int32_t o[8];
+    idct8<int32_t>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
     uint32_t lo4 = 0, hi4 = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-      lo4 |= range_limit(descale(o[c], kConstBits + kPass1Bits + 3)) << (8 * c);
-      hi4 |= range_limit(descale(o[c + 4], kConstBits + kPass1Bits + 3)) << (8 * c);
+      lo4 |= range_limit(descale_t<int32_t>(o[c], kConstBits + kPass1Bits + 3)) << (8 * c);
+      hi4 |= range_limit(descale_t<int32_t>(o[c + 4], kConstBits + kPass1Bits + 3)) << (8 * c);
     }
     *reinterpret_cast<uint2*>(out + (i64)r * stride) = make_uint2(lo4, hi4);
   }

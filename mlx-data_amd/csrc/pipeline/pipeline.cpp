@@ -22,6 +22,13 @@
 
 #include "mxd_amd.h"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+
 namespace mxd {
 namespace pipe {
 
@@ -831,26 +838,59 @@ LoadImage::LoadImage(std::string ikey, std::string prefix, bool info, std::strin
       from_memory_(from_memory) {}
 
 namespace {
+// File reads with POSIX calls straight into a buffer sized from fstat: the
+// earlier stdio loop (64 KB chunks appended to a growing vector, after a
+// separate open for the signature) cost several times the read itself on an
+// 80 KB JPEG.
+struct Fd {
+  int fd;
+  explicit Fd(const std::string& path) : fd(::open(path.c_str(), O_RDONLY | O_CLOEXEC)) {}
+  ~Fd() {
+    if (fd >= 0) ::close(fd);
+  }
+  Fd(const Fd&) = delete;
+  Fd& operator=(const Fd&) = delete;
+};
+
+// Appends the file's bytes from the current offset to *out until EOF or until
+// *out holds `limit` bytes; false on a read error.  A regular file is read to
+// the size fstat gives; anything else until read() returns 0.
+bool read_to(int fd, size_t limit, std::vector<uint8_t>* out) {
+  struct stat st;
+  const bool regular = ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
+  size_t got = out->size();
+  const size_t want = regular ? std::min(limit, std::max(got, (size_t)st.st_size)) : limit;
+  if (regular) out->resize(want);
+  while (got < limit) {
+    if (got == out->size()) {
+      if (regular) break;  // fstat's size reached
+      out->resize(std::min(limit, got + std::max<size_t>(got, 1 << 16)));
+    }
+    const ssize_t r = ::read(fd, out->data() + got, out->size() - got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    if (r == 0) break;
+    got += (size_t)r;
+  }
+  out->resize(got);
+  return true;
+}
+
 // The whole file (the reference's check_signature fopen failure message).
 std::vector<uint8_t> read_file(const std::string& path) {
-  FILE* f = std::fopen(path.c_str(), "rb");
-  if (!f) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+  Fd f(path);
   std::vector<uint8_t> data;
-  uint8_t chunk[1 << 16];
-  size_t n;
-  while ((n = std::fread(chunk, 1, sizeof chunk, f)) > 0) data.insert(data.end(), chunk, chunk + n);
-  std::fclose(f);
+  if (f.fd < 0 || !read_to(f.fd, SIZE_MAX, &data)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
   return data;
 }
 
 // Up to `n` leading bytes of a file; false when it cannot be opened.
 bool read_prefix(const std::string& path, size_t n, std::vector<uint8_t>* out) {
-  FILE* f = std::fopen(path.c_str(), "rb");
-  if (!f) return false;
-  out->resize(n);
-  out->resize(std::fread(out->data(), 1, n, f));
-  std::fclose(f);
-  return true;
+  Fd f(path);
+  out->clear();
+  return f.fd >= 0 && read_to(f.fd, n, out);
 }
 
 // libjpeg's message without the C ABI's "load_jpeg: " prefix.
@@ -900,10 +940,11 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
   } else {
     // load_jpeg's signature check (ImageJPEG.cpp:74-86) first: only JPEGs are
     // read here, anything else goes to the stb_image hook by path.
-    std::vector<uint8_t> sig;
-    if (!read_prefix(path, 3, &sig)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
-    if (mxd_is_jpeg(sig.data(), sig.size())) {
-      file = read_file(path);
+    // One open: the signature, then (a JPEG) the rest of the file.
+    Fd f(path);
+    if (f.fd < 0 || !read_to(f.fd, 3, &file)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+    if (mxd_is_jpeg(file.data(), file.size())) {
+      if (!read_to(f.fd, SIZE_MAX, &file)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
       bytes = file.data();
       nbytes = file.size();
     }

@@ -84,12 +84,17 @@ def _dct_blocks(plane, q):
     return np.clip(z, -1023, 1023)
 
 
-def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0):
+def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0, coefs=None):
     """pixels: (H, W) or (H, W, 3) uint8 -> baseline JPEG bytes (4:4:4 when
-    three components, which are written as given: Y, Cb, Cr)."""
+    three components, which are written as given: Y, Cb, Cr).  q: the flat
+    quantiser (int) or a 64-entry table in natural order.  coefs: the
+    quantised blocks to write instead of the pixels' -- per component a
+    (rows, cols, 64) zig-zag array (DC within +-2047 of its neighbour, AC
+    within +-1023) -- pixels then only gives the frame size."""
     a = pixels if pixels.ndim == 3 else pixels[:, :, None]
     h, w, nc = a.shape
-    planes = [_dct_blocks(a[:, :, i], q) for i in range(nc)]
+    qt = np.full(64, q, np.int64) if np.isscalar(q) else np.asarray(q, np.int64)
+    planes = coefs if coefs is not None else [_dct_blocks(a[:, :, i], qt.reshape(8, 8)) for i in range(nc)]
     rows, cols = planes[0].shape[:2]
     dcc, acc = _codes(dc), _codes(ac)
     bits, pred = _Bits(), [0] * nc
@@ -133,7 +138,7 @@ def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0):
         return bytes([0xFF, marker]) + (len(body) + 2).to_bytes(2, "big") + body
 
     out = bytearray(b"\xff\xd8")
-    out += seg(0xDB, bytes([0]) + bytes([q] * 64))
+    out += seg(0xDB, bytes([0]) + bytes(qt[ZIGZAG].astype(np.uint8).tolist()))
     out += seg(0xC0, bytes([8]) + h.to_bytes(2, "big") + w.to_bytes(2, "big") + bytes([nc]) +
                b"".join(bytes([i + 1, 0x11, 0]) for i in range(nc)))
     out += seg(0xC4, bytes([0x00]) + bytes(dc[0]) + bytes(dc[1]) + bytes([0x10]) + bytes(ac[0]) + bytes(ac[1]))

@@ -269,3 +269,28 @@ def test_deep_tables_take_the_searching_decoder(bits, word_source):
     finally:
         capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, prev)
     assert all(c.entropy_pending for c in coefs)
+
+
+def test_out_of_range_coefficients_take_the_wide_idct():
+    """Dequantised blocks outside the 32-bit IDCT's range (|x| >= 2^14 in
+    either pass: no encoder of real pixels writes them, tests/jpeg_enc.py
+    writes them directly) take jpeg_idct's JLONG path (idct_block_wide) and
+    still equal the host decoder, which follows jidctint.c's JLONG
+    arithmetic.  Pillow is not compared: libjpeg-turbo's SIMD IDCT
+    dequantises in 16 bits, so on such data it leaves jidctint.c's results."""
+    import jpeg_enc as J
+
+    rng = np.random.default_rng(47)
+    datas = []
+    for h, w, nc, amp, qlo in [(40, 56, 1, 1023, 1), (64, 48, 3, 60, 150), (24, 200, 3, 400, 20)]:
+        rows, cols = -(-h // 8), -(-w // 8)
+        planes = []
+        for _ in range(nc):
+            z = rng.integers(-amp, amp + 1, (rows, cols, 64))
+            z[:, :, 0] = rng.integers(-900, 901, (rows, cols))
+            z[rng.random((rows, cols)) < 0.3] //= 64  # blocks inside the 32-bit range beside them
+            planes.append(z)
+        q = rng.integers(qlo, 256, 64)
+        datas.append(J.encode(np.zeros((h, w, nc) if nc == 3 else (h, w), np.uint8), q=q, coefs=planes))
+    datas.append(_encode(_smooth(rng, 90, 70), quality=90))
+    _check_identity(datas, pillow=False)
