@@ -3,6 +3,10 @@
 // or written to device destinations, JPEG batches finished on the device.
 #include "capi_internal.h"
 
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <functional>
 
@@ -160,15 +164,49 @@ class Helpers {
   int outstanding_ = 0;  // helpers asked for by the calls in flight
 };
 
+// The CPUs this process may keep busy: the affinity mask, capped by a cgroup
+// CPU quota (v2 cpu.max, v1 cpu.cfs_quota_us) -- a container's share, which
+// the mask does not show: the GPU boxes give every process the whole
+// machine's mask and a 16-CPU quota, and sizing helpers by the mask put
+// 16 prefetch workers x 8 staging threads on 16 CPUs -- and by
+// OMP_NUM_THREADS when the environment sets it (the boxes' per-GPU share).
+// MXD_HOST_CPUS overrides all of it.
+int host_cpu_budget() {
+  if (const char* e = std::getenv("MXD_HOST_CPUS"))
+    if (std::atoi(e) > 0) return std::atoi(e);
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  auto cap = [&](double quota, double period) {
+    if (quota > 0 && period > 0) n = std::min(n, std::max(1, (int)std::ceil(quota / period)));
+  };
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    double period = 0;
+    if (std::fscanf(f, "%31s %lf", q, &period) == 2 && std::strcmp(q, "max") != 0) cap(std::atof(q), period);
+    std::fclose(f);
+  } else if (FILE* g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    double quota = -1, period = 0;
+    if (std::fscanf(g, "%lf", &quota) != 1) quota = -1;
+    std::fclose(g);
+    if (FILE* h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (std::fscanf(h, "%lf", &period) != 1) period = 0;
+      std::fclose(h);
+    }
+    cap(quota, period);
+  }
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int k = std::atoi(e);
+    if (k > 0) n = std::min(n, k);
+  }
+  return std::max(1, n);
+}
+
 template <class F>
 void parallel_items(int32_t first, int32_t end, int64_t bytes, F&& f) {
   const int32_t n = end - first;
-  static const int hw = [] {  // the cores this process may run on (a container's share, not the machine)
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    if (sched_getaffinity(0, sizeof set, &set) == 0) return std::max(1, CPU_COUNT(&set));
-    return std::max(1, (int)std::thread::hardware_concurrency());
-  }();
+  static const int hw = host_cpu_budget();
   int t = std::min<int64_t>({8, hw / std::max(1, g_host_calls.load()), n, bytes >> 20});
   if (t <= 1) {
     for (int32_t i = first; i < end; i++) f(i);
