@@ -36,7 +36,8 @@ extern "C" {
  * entropy decode pending), mxd_jpeg_coefs_entropy_pending,
  * mxd_device_synchronize, and the tuning knobs MXD_TUNE_HUFF_BITS,
  * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS,
- * MXD_TUNE_HUFF_JOB. */
+ * MXD_TUNE_HUFF_JOB, MXD_TUNE_JPEG_RGB, mxd_jpeg_plane_sources,
+ * mxd_host_stats, mxd_jpeg_coefs_load. */
 #define MXD_ABI_VERSION 5
 
 enum mxd_status {
@@ -328,6 +329,14 @@ int mxd_jpeg_coefs_decode(const uint8_t* data, size_t size, mxd_jpeg_coefs** out
  * The bytes are copied (`data` may be freed after the call); every route
  * gives mxd_jpeg_decode's bytes. */
 int mxd_jpeg_coefs_parse(const uint8_t* data, size_t size, int32_t device_entropy, mxd_jpeg_coefs** out);
+/* mxd_jpeg_coefs_parse of the regular file at `path`, read straight into the
+ * handle's own copy (one open, one read sized by fstat: the file-loading
+ * half of op/LoadImage.cpp:23-48 for JPEGs).  MXD_OK with *out = NULL when
+ * the file does not start with the JPEG signature (FF D8 FF; the caller's
+ * other decoders take it); MXD_ERR_INVALID when it cannot be read or parsed,
+ * or is not a regular file -- read it and call mxd_jpeg_coefs_parse for the
+ * reference's exact message. */
+int mxd_jpeg_coefs_load(const char* path, int32_t device_entropy, mxd_jpeg_coefs** out);
 /* *pending = 1 when the coefficients will come from the device entropy decode. */
 int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending);
 int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs);
@@ -365,6 +374,15 @@ int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int3
  * their sample planes (4:2:0 on a scatter wave kernel, MXD_TUNE_JPEG_RGB 0:
  * no RGB frame) since the last reset; reset != 0 zeroes it after reading. */
 int mxd_jpeg_plane_sources(int64_t* count, int32_t reset);
+
+/* Diagnostics: where a host-side pipeline's time goes, summed over every
+ * thread since the last reset (reset != 0 zeroes them after reading).
+ * out[0] host-path calls (the mxd_*_host / *_to_device batch calls above),
+ * out[1] their images, out[2] their wall time in ns, out[3] the part of it
+ * spent waiting for the device (chunk events and the final drain),
+ * out[4] mxd_jpeg_coefs_parse / mxd_jpeg_coefs_load calls, out[5] their time
+ * in ns (a load's includes its file read). */
+int mxd_host_stats(int64_t* out6, int32_t reset);
 
 /* ---- pixel maps: rotate / affine and channel reduction --
  *

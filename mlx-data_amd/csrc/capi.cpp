@@ -451,7 +451,25 @@ int mxd_jpeg_coefs_decode(const uint8_t* data, size_t size, mxd_jpeg_coefs** out
 int mxd_jpeg_coefs_parse(const uint8_t* data, size_t size, int32_t device_entropy, mxd_jpeg_coefs** out) {
   if (!data || !out) return fail(MXD_ERR_INVALID, "mxd: null argument");
   std::string err;
+  const int64_t t0 = now_ns();
   mxd::jpeg::Coefs* c = mxd::jpeg::parse_coefs(data, size, device_entropy != 0, &err);
+  g_host_stats[4].fetch_add(1, std::memory_order_relaxed);
+  g_host_stats[5].fetch_add(now_ns() - t0, std::memory_order_relaxed);
+  if (!c) return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
+  *out = reinterpret_cast<mxd_jpeg_coefs*>(c);
+  return MXD_OK;
+}
+
+int mxd_jpeg_coefs_load(const char* path, int32_t device_entropy, mxd_jpeg_coefs** out) {
+  if (!path || !out) return fail(MXD_ERR_INVALID, "mxd: null argument");
+  *out = nullptr;
+  std::string err;
+  bool not_jpeg = false;
+  const int64_t t0 = now_ns();
+  mxd::jpeg::Coefs* c = mxd::jpeg::load_coefs(path, device_entropy != 0, &not_jpeg, &err);
+  g_host_stats[4].fetch_add(1, std::memory_order_relaxed);
+  g_host_stats[5].fetch_add(now_ns() - t0, std::memory_order_relaxed);
+  if (not_jpeg) return MXD_OK;
   if (!c) return fail(MXD_ERR_INVALID, "load_jpeg: " + err);
   *out = reinterpret_cast<mxd_jpeg_coefs*>(c);
   return MXD_OK;
@@ -492,6 +510,12 @@ int mxd_jpeg_resize_crop_host(const mxd_jpeg_image* images, int32_t n, int32_t o
 
 int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int32_t out_dtype, int32_t device) {
   return jpeg_path(images, n, out_dtype, device, true);
+}
+
+int mxd_host_stats(int64_t* out6, int32_t reset) {
+  if (!out6) return fail(MXD_ERR_INVALID, "mxd: null out6");
+  for (int i = 0; i < 6; i++) out6[i] = reset ? g_host_stats[i].exchange(0) : g_host_stats[i].load();
+  return MXD_OK;
 }
 
 int mxd_jpeg_plane_sources(int64_t* count, int32_t reset) {

@@ -240,6 +240,10 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
 int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t device, bool dst_device,
               const mxd_jpeg_image* jpeg = nullptr);
 int jpeg_path(const mxd_jpeg_image* jimg, int32_t n, int32_t out_dtype, int32_t device, bool dst_device);
+// mxd_host_stats counters: host-path calls, images, wall ns, device-wait ns,
+// coefficient parses, parse ns
+extern std::atomic<int64_t> g_host_stats[6];
+int64_t now_ns();
 extern std::atomic<int64_t> g_plane_sources;  // images resized from their JPEG sample planes (mxd_jpeg_plane_sources)
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c);
 // Frees the buffers of every idle host-path context (mxd_release_host_buffers).

@@ -3,6 +3,8 @@
 // or written to device destinations, JPEG batches finished on the device.
 #include "capi_internal.h"
 
+#include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -379,6 +381,12 @@ struct JpegChunk {
   // the staged input; their coefficients in dev_in past the staged bytes
   // ([coef_off, dev_end), written by the decode, never copied).
   std::vector<mxd::HuffDev> htabs;
+  struct TableSet {
+    std::array<uint64_t, 8> key;  // device_table serials
+    int n;
+    int32_t first;                // in htabs
+  };
+  std::vector<TableSet> table_sets;
   std::vector<mxd::HuffImgDev> himgs;
   std::vector<mxd::HuffSegDev> hsegs;
   std::vector<mxd::HuffJobDev> hjobs;
@@ -398,6 +406,11 @@ struct JpegChunk {
 };
 
 std::atomic<int64_t> g_plane_sources{0};
+std::atomic<int64_t> g_host_stats[6] = {};
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_cast<const mxd::jpeg::Coefs*>(c); }
 
@@ -427,7 +440,6 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       h.comp_h[k] = (int8_t)info.comp[k].h;
       h.comp_v[k] = (int8_t)info.comp[k].v;
     }
-    h.tables = (int32_t)c.htabs.size();
     h.ntables = es.ntables;
     h.bpm = es.bpm;
     h.mcux = es.mcux;
@@ -441,10 +453,26 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       h.blk_dx[j] = (int8_t)es.blk_dx[j];
       h.blk_dy[j] = (int8_t)es.blk_dy[j];
     }
-    for (int t = 0; t < es.ntables; t++) {
-      c.htabs.emplace_back();
-      mxd::jpeg::device_table(coefs_of(jimg[i].coefs), es.table_class[t], es.table_id[t], &c.htabs.back());
-      c.huff_search = c.huff_search || c.htabs.back().search != 0;
+    // the image's tables (consecutive from h.tables): a set an earlier image
+    // of the chunk already staged is shared (files from one encoder carry the
+    // same tables: one set per C4 batch instead of 128 x ~50 KB staged)
+    {
+      std::array<uint64_t, 8> key{};
+      for (int t = 0; t < es.ntables; t++)
+        key[t] = mxd::jpeg::device_table(coefs_of(jimg[i].coefs), es.table_class[t], es.table_id[t], nullptr);
+      int32_t at = -1;
+      for (const auto& ts : c.table_sets)
+        if (ts.n == es.ntables && ts.key == key) at = ts.first;
+      if (at < 0) {
+        at = (int32_t)c.htabs.size();
+        c.table_sets.push_back({key, es.ntables, at});
+        for (int t = 0; t < es.ntables; t++) {
+          c.htabs.emplace_back();
+          mxd::jpeg::device_table(coefs_of(jimg[i].coefs), es.table_class[t], es.table_id[t], &c.htabs.back());
+          c.huff_search = c.huff_search || c.htabs.back().search != 0;
+        }
+      }
+      h.tables = at;
     }
     // subsequence length: kHuffMinBits (MXD_TUNE_HUFF_BITS overrides it;
     // a multiple of 32); segments of any length split over several jobs
@@ -610,8 +638,15 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   DeviceGuard g(device);
   g_host_calls.fetch_add(1);
   struct CallCount {
-    ~CallCount() { g_host_calls.fetch_sub(1); }
-  } call_count;
+    int64_t t0 = now_ns(), n;
+    ~CallCount() {
+      g_host_calls.fetch_sub(1);
+      g_host_stats[0].fetch_add(1, std::memory_order_relaxed);
+      g_host_stats[1].fetch_add(n, std::memory_order_relaxed);
+      g_host_stats[2].fetch_add(now_ns() - t0, std::memory_order_relaxed);
+    }
+  } call_count{now_ns(), n};
+  auto waited = [](int64_t t0) { g_host_stats[3].fetch_add(now_ns() - t0, std::memory_order_relaxed); };
   // Per image: the staged footprint (columns from x0, 16-byte aligned so both
   // kernel families read it as they would the whole image) and its offsets.
   struct Stage {
@@ -700,8 +735,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   struct Drain {
     HostCtx& c;
     ~Drain() {
+      const int64_t t0 = now_ns();
       for (Slot& sl : c.slot)
         if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+      g_host_stats[3].fetch_add(now_ns() - t0, std::memory_order_relaxed);
     }
   } drain{ctx};
   for (Slot& sl : ctx.slot)
@@ -709,7 +746,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   int pending[2] = {-1, -1};  // chunk in flight on each slot
   auto copy_out = [&](int k) -> int {
     Slot& sl = ctx.slot[k & 1];
+    const int64_t t0 = now_ns();
     MXD_HIP(hipEventSynchronize(sl.done));
+    waited(t0);
     pending[k & 1] = -1;
     if (sl.huff_err && *sl.huff_err) {
       *sl.huff_err = 0;
@@ -788,14 +827,15 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const Stage& s = st[i];
       if (jpeg) {
         if (s.pending) {
-          // the image's entropy-coded segments, unstuffed, zero padded
+          // the image's entropy-coded segments, unstuffed, zero padded (the
+          // marker parse counted the bytes: HuffSegDev::bits; removing the
+          // stuffing on the device instead measured slower)
           const int32_t f = jc.seg_first[i - chunks[k].first];
           for (int32_t q = f; q < f + jc.seg_count[i - chunks[k].first]; q++) {
             const JpegChunk::Raw& r = jc.raw[q];
             uint8_t* to = sl.pin_in + jc.words_off + r.at;
             const int64_t n = mxd::jpeg::unstuff(r.b, r.e, to);
             std::memset(to + n, 0, (size_t)(((r.e - r.b + 4 + 15) & ~(int64_t)15) - n));
-            jc.hsegs[q].bits = (int32_t)std::min<int64_t>(8 * n, INT32_MAX);
           }
           return;
         }

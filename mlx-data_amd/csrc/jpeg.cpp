@@ -28,7 +28,12 @@
 
 #include "jpeghuff.h"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -1452,7 +1457,10 @@ int Decoder::color_space() const {
 
 struct Coefs {
   Decoder d;
-  std::vector<uint8_t> file;  // parse_coefs with a pending entropy decode: the file, for the segments
+  // parse_coefs / load_coefs with a pending entropy decode: the file, for the
+  // segments (not value-initialised: load_coefs reads straight into it)
+  std::unique_ptr<uint8_t[]> file;
+  size_t file_size = 0;
   Coefs(const uint8_t* data, size_t size) : d(data, size) {}
 };
 
@@ -1482,13 +1490,14 @@ Coefs* decode_coefs(const uint8_t* data, size_t size, std::string* err) {
   }
 }
 
-Coefs* parse_coefs(const uint8_t* data, size_t size, bool device_entropy, std::string* err) {
-  if (!device_entropy) return decode_coefs(data, size, err);
+namespace {
+// parse_coefs on a Coefs that already holds the file (c->file, c->file_size).
+Coefs* parse_held(std::unique_ptr<Coefs> c, std::string* err) {
+  const uint8_t* data = c->file.get();
+  const size_t size = c->file_size;
   try {
-    auto c = std::make_unique<Coefs>(nullptr, 0);
-    c->file.assign(data, data + size);
     Decoder& d = c->d;
-    d.data = c->file.data();
+    d.data = data;
     d.size = size;
     d.device_entropy = true;
     d.parse();
@@ -1509,6 +1518,67 @@ Coefs* parse_coefs(const uint8_t* data, size_t size, bool device_entropy, std::s
     if (err) *err = "Insufficient memory";
     return nullptr;
   }
+}
+}  // namespace
+
+Coefs* parse_coefs(const uint8_t* data, size_t size, bool device_entropy, std::string* err) {
+  if (!device_entropy) return decode_coefs(data, size, err);
+  std::unique_ptr<Coefs> c;
+  try {
+    c = std::make_unique<Coefs>(nullptr, 0);
+    c->file.reset(new uint8_t[size ? size : 1]);
+  } catch (const std::bad_alloc&) {
+    if (err) *err = "Insufficient memory";
+    return nullptr;
+  }
+  std::memcpy(c->file.get(), data, size);
+  c->file_size = size;
+  return parse_held(std::move(c), err);
+}
+
+Coefs* load_coefs(const char* path, bool device_entropy, bool* not_jpeg, std::string* err) {
+  *not_jpeg = false;
+  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    if (err) *err = "could not load <" + std::string(path) + ">";
+    return nullptr;
+  }
+  struct Close {
+    int fd;
+    ~Close() { ::close(fd); }
+  } close_fd{fd};
+  struct stat st;
+  if (::fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < 3) {
+    if (err) *err = "not a regular file";
+    return nullptr;  // the caller's general path reads it
+  }
+  std::unique_ptr<Coefs> c;
+  try {
+    c = std::make_unique<Coefs>(nullptr, 0);
+    c->file.reset(new uint8_t[(size_t)st.st_size]);
+  } catch (const std::bad_alloc&) {
+    if (err) *err = "Insufficient memory";
+    return nullptr;
+  }
+  uint8_t* buf = c->file.get();
+  size_t got = 0;
+  while (got < (size_t)st.st_size) {
+    const ssize_t r = ::read(fd, buf + got, (size_t)st.st_size - got);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) break;
+    got += (size_t)r;
+    if (got >= 3 && got - (size_t)r < 3 && !is_jpeg(buf, got)) {
+      *not_jpeg = true;
+      return nullptr;
+    }
+  }
+  if (got != (size_t)st.st_size) {
+    if (err) *err = "short read";
+    return nullptr;
+  }
+  c->file_size = got;
+  if (!device_entropy) return decode_coefs(buf, got, err);
+  return parse_held(std::move(c), err);
 }
 
 void free_coefs(Coefs* c) { delete c; }
@@ -1550,30 +1620,36 @@ EntropyScan entropy_scan(const Coefs* c) {
   return e;
 }
 
-void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
+uint64_t device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   const Huff& h = cls ? c->d.ac[table_id] : c->d.dc[table_id];
-  HuffDev& o = *static_cast<HuffDev*>(huff_dev);
   // per-thread cache of built tables (a batch's files mostly share theirs),
   // keyed by the class and the derived code: maxcode, valoffset and the symbol values
   struct Entry {
     int32_t maxcode[18], valoffset[18];
     uint8_t vals[256];
     int nvals = -1, cls = -1;
+    uint64_t serial = 0;  // this thread's build number: equal serials, equal tables
     HuffDev d;
   };
   constexpr int kEntries = 8;
   thread_local std::unique_ptr<Entry[]> cache;
   thread_local int next = 0;
+  thread_local uint64_t builds = 0;
   if (!cache) cache.reset(new Entry[kEntries]);
   for (int k = 0; k < kEntries; k++) {
     const Entry& e = cache[k];
     if (e.nvals == h.nvals && e.cls == cls && std::memcmp(e.maxcode, h.maxcode, sizeof e.maxcode) == 0 &&
         std::memcmp(e.valoffset, h.valoffset, sizeof e.valoffset) == 0 &&
         std::memcmp(e.vals, h.vals, (size_t)h.nvals) == 0) {
-      o = e.d;
-      return;
+      if (huff_dev) *static_cast<HuffDev*>(huff_dev) = e.d;
+      return e.serial;
     }
   }
+  // built in the cache entry it replaces
+  Entry& e = cache[next];
+  next = (next + 1) % kEntries;
+  e.nvals = -1;
+  HuffDev& o = e.d;
   std::memset(&o, 0, sizeof o);
   // The code starting a 16-bit pattern: its length and symbol, jdhuff.c
   // jpeg_huff_decode's search (the shortest l whose l-bit prefix is <=
@@ -1632,14 +1708,14 @@ void device_table(const Coefs* c, int cls, int table_id, void* huff_dev) {
   std::memcpy(o.maxcode, h.maxcode, sizeof o.maxcode);
   std::memcpy(o.valoffset, h.valoffset, sizeof o.valoffset);
   std::memcpy(o.vals, h.vals, sizeof o.vals);
-  Entry& e = cache[next];
-  next = (next + 1) % kEntries;
   std::memcpy(e.maxcode, h.maxcode, sizeof e.maxcode);
   std::memcpy(e.valoffset, h.valoffset, sizeof e.valoffset);
   std::memcpy(e.vals, h.vals, (size_t)h.nvals);
   e.nvals = h.nvals;
   e.cls = cls;
-  e.d = o;
+  e.serial = ++builds;
+  if (huff_dev) *static_cast<HuffDev*>(huff_dev) = o;
+  return e.serial;
 }
 
 // Mirrors Bits::fill's byte rules on a segment that ends at its marker's 0xFF.
@@ -1698,7 +1774,7 @@ bool finish(const Coefs* c, uint8_t* dst, int64_t dst_stride, std::string* err) 
   try {
     if (c->d.pending) {
       // the entropy decode was left to the device: run it here now
-      std::unique_ptr<Coefs> h(decode_coefs(c->file.data(), c->file.size(), err));
+      std::unique_ptr<Coefs> h(decode_coefs(c->file.get(), c->file_size, err));
       if (!h) return false;
       h->d.output(dst, dst_stride);
       return true;

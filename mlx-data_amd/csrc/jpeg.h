@@ -57,6 +57,13 @@ Coefs* decode_coefs(const uint8_t* data, size_t size, std::string* err);
 // Any other file is entropy-decoded here as by decode_coefs.  The file is
 // copied: `data` need not outlive the call.
 Coefs* parse_coefs(const uint8_t* data, size_t size, bool device_entropy, std::string* err);
+// parse_coefs of the file at `path`, read straight into the Coefs' own copy
+// (one open, a read sized by fstat, no intermediate buffer).  nullptr and
+// *not_jpeg when the file does not start with the JPEG signature; nullptr
+// with *err on any other failure (open / read / parse, or not a regular
+// file) -- callers needing the reference's exact messages rerun their general
+// path then.
+Coefs* load_coefs(const char* path, bool device_entropy, bool* not_jpeg, std::string* err);
 void free_coefs(Coefs* c);
 CoefInfo coef_info(const Coefs* c);
 // Host finish into height rows of width*3 bytes at dst_stride (thread-safe);
@@ -80,8 +87,11 @@ struct EntropyScan {
   int table_class[8], table_id[8];  // 0 DC / 1 AC, DHT index
 };
 EntropyScan entropy_scan(const Coefs* c);
-// The derived table `table_id` of class `cls` in the device layout (jpeghuff.h HuffDev).
-void device_table(const Coefs* c, int cls, int table_id, void* huff_dev);
+// The derived table `table_id` of class `cls` in the device layout (jpeghuff.h
+// HuffDev) into huff_dev (nullptr: only made ready).  Returns its serial in a
+// small per-thread cache of built tables: two calls on one thread that
+// return the same serial gave the same table.
+uint64_t device_table(const Coefs* c, int cls, int table_id, void* huff_dev);
 // Unstuffed bytes of the raw segment [b, e) (0xFF 0x00 -> 0xFF, fill 0xFF
 // bytes dropped) into dst (>= e - b bytes); returns their count.
 int64_t unstuff(const uint8_t* b, const uint8_t* e, uint8_t* dst);

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -212,6 +213,31 @@ mxd_jpeg_image jpeg_desc(const ImagePlan& p, const JpegSource& j, void* dst, int
 // decode + resize call (the GPU finishes the decode), the rest in one resize
 // call.  Returns the C ABI status (message in mxd_last_error()).
 std::atomic<int64_t> g_run_calls{0}, g_run_jpeg{0};  // diagnostics (run_on_stats)
+
+// Diagnostics (pipe_stats): ns summed over threads -- LoadImage::apply_key,
+// every StreamTransform op (LoadImage included), StreamBatch's upstream
+// fetches, its merge_batch, FromBuffer::next -- and the LoadImage count.
+// One cache line of counters per thread (up to 64 lines, shared beyond), so
+// prefetch workers do not contend on them.
+struct alignas(64) PipeLine {
+  std::atomic<int64_t> v[6];
+};
+PipeLine g_pipe_ns[64];
+std::atomic<int> g_pipe_threads{0};
+std::atomic<int64_t>* pipe_counters() {
+  thread_local const int k = g_pipe_threads.fetch_add(1) & 63;
+  return g_pipe_ns[k].v;
+}
+int64_t pipe_now() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+struct PipeTimer {
+  int slot;
+  int64_t t0 = pipe_now();
+  explicit PipeTimer(int k) : slot(k) {}
+  ~PipeTimer() { pipe_counters()[slot].fetch_add(pipe_now() - t0, std::memory_order_relaxed); }
+};
 
 int run_on(const Job* jobs, size_t n, int32_t dtype, int device, bool dst_device) {
   g_run_calls.fetch_add(1);
@@ -905,6 +931,8 @@ std::string jpeg_error() {
 // FF D8 FF) through the native decoder (ImageJPEG.cpp:99-232 semantics),
 // anything else through the installed stb_image-rules hook.
 std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) const {
+  PipeTimer timer(0);
+  pipe_counters()[5].fetch_add(1, std::memory_order_relaxed);
   if (x->device() >= 0) throw std::runtime_error("LoadImage: device-resident array expected on host");
   std::string path;
   if (!from_memory_) {
@@ -915,74 +943,91 @@ std::shared_ptr<Array> LoadImage::apply_key(const std::shared_ptr<Array>& x) con
     else if (!path.empty()) path = (path.back() == '/' ? path : path + "/") + filename;
     else path = filename;
   }
-  std::vector<uint8_t> file;
-  const uint8_t* bytes = nullptr;
-  size_t nbytes = 0;
-  if (from_memory_) {
-    bytes = static_cast<const uint8_t*>(x->data());
-    nbytes = (size_t)x->nbytes();
-  } else if (info_) {
-    // core::image::info -> stbi_info (ImageIO.cpp:26-32): the header only;
-    // (0, 0) when the file cannot be opened or parsed.  A JPEG's frame header
-    // follows its APP segments, so a short prefix is read first.
-    constexpr size_t kHead = 1 << 18;
-    if (!read_prefix(path, kHead, &file)) {
-      auto out = std::make_shared<Array>(DType::Int64, std::vector<int64_t>{2});
-      static_cast<int64_t*>(out->data())[0] = static_cast<int64_t*>(out->data())[1] = 0;
-      return out;
+  // The deferred image of a parsed JPEG (the GPU finishes it in the batch).
+  auto deferred = [](mxd_jpeg_coefs* c) {
+    auto src = std::make_shared<const JpegSource>(c);
+    int32_t cw = 0, ch = 0, dev_ok = 0;
+    check(mxd_jpeg_coefs_info(c, &cw, &ch, &dev_ok));
+    auto out = std::make_shared<Array>(src, ch, cw);
+    if (!dev_ok) out->data();  // CMYK / YCCK: the host finishes it now
+    return out;
+  };
+  if (!from_memory_ && !info_ && device_decode()) {
+    // the file read straight into the parsed handle; anything unusual (not
+    // readable, not a regular file, a parse error) takes the general path
+    // below, which gives the reference's messages
+    mxd_jpeg_coefs* c = nullptr;
+    if (mxd_jpeg_coefs_load(path.c_str(), device_entropy() ? 1 : 0, &c) == MXD_OK) {
+      if (c) return deferred(c);
+      goto not_jpeg;
     }
-    int32_t w = 0, h = 0, c = 0;
-    if (mxd_is_jpeg(file.data(), file.size()) && file.size() == kHead &&
-        mxd_jpeg_info(file.data(), file.size(), &w, &h, &c) != MXD_OK)
-      file = read_file(path);  // frame header past the prefix
-    bytes = file.data();
-    nbytes = file.size();
-  } else {
-    // load_jpeg's signature check (ImageJPEG.cpp:74-86) first: only JPEGs are
-    // read here, anything else goes to the stb_image hook by path.
-    // One open: the signature, then (a JPEG) the rest of the file.
-    Fd f(path);
-    if (f.fd < 0 || !read_to(f.fd, 3, &file)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
-    if (mxd_is_jpeg(file.data(), file.size())) {
-      if (!read_to(f.fd, SIZE_MAX, &file)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+  }
+  {
+    std::vector<uint8_t> file;
+    const uint8_t* bytes = nullptr;
+    size_t nbytes = 0;
+    if (from_memory_) {
+      bytes = static_cast<const uint8_t*>(x->data());
+      nbytes = (size_t)x->nbytes();
+    } else if (info_) {
+      // core::image::info -> stbi_info (ImageIO.cpp:26-32): the header only;
+      // (0, 0) when the file cannot be opened or parsed.  A JPEG's frame header
+      // follows its APP segments, so a short prefix is read first.
+      constexpr size_t kHead = 1 << 18;
+      if (!read_prefix(path, kHead, &file)) {
+        auto out = std::make_shared<Array>(DType::Int64, std::vector<int64_t>{2});
+        static_cast<int64_t*>(out->data())[0] = static_cast<int64_t*>(out->data())[1] = 0;
+        return out;
+      }
+      int32_t w = 0, h = 0, c = 0;
+      if (mxd_is_jpeg(file.data(), file.size()) && file.size() == kHead &&
+          mxd_jpeg_info(file.data(), file.size(), &w, &h, &c) != MXD_OK)
+        file = read_file(path);  // frame header past the prefix
       bytes = file.data();
       nbytes = file.size();
+    } else {
+      // load_jpeg's signature check (ImageJPEG.cpp:74-86) first: only JPEGs are
+      // read here, anything else goes to the stb_image hook by path.
+      // One open: the signature, then (a JPEG) the rest of the file.
+      Fd f(path);
+      if (f.fd < 0 || !read_to(f.fd, 3, &file)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+      if (mxd_is_jpeg(file.data(), file.size())) {
+        if (!read_to(f.fd, SIZE_MAX, &file)) throw std::runtime_error("load_jpeg: could not load <" + path + ">");
+        bytes = file.data();
+        nbytes = file.size();
+      }
     }
-  }
-  const std::string where = from_memory_ ? std::string("from memory") : "<" + path + ">";
-  if (bytes && mxd_is_jpeg(bytes, nbytes)) {
-    int32_t w = 0, h = 0, c = 0;
-    const bool ok = mxd_jpeg_info(bytes, nbytes, &w, &h, &c) == MXD_OK;
-    if (info_) {
-      // stbi_info: (w, h), zeros when the header cannot be read
-      auto out = std::make_shared<Array>(DType::Int64, std::vector<int64_t>{2});
-      static_cast<int64_t*>(out->data())[0] = ok ? w : 0;
-      static_cast<int64_t*>(out->data())[1] = ok ? h : 0;
+    const std::string where = from_memory_ ? std::string("from memory") : "<" + path + ">";
+    if (bytes && mxd_is_jpeg(bytes, nbytes)) {
+      int32_t w = 0, h = 0, c = 0;
+      const bool ok = mxd_jpeg_info(bytes, nbytes, &w, &h, &c) == MXD_OK;
+      if (info_) {
+        // stbi_info: (w, h), zeros when the header cannot be read
+        auto out = std::make_shared<Array>(DType::Int64, std::vector<int64_t>{2});
+        static_cast<int64_t*>(out->data())[0] = ok ? w : 0;
+        static_cast<int64_t*>(out->data())[1] = ok ? h : 0;
+        return out;
+      }
+      if (!ok) throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
+      if (device_decode()) {
+        // markers only (the Huffman decode too runs on the GPU, csrc/jpeghuff.hip)
+        // when the file qualifies, else the entropy decode here; the GPU
+        // finishes it in the batch launch
+        mxd_jpeg_coefs* c = nullptr;
+        if (mxd_jpeg_coefs_parse(bytes, nbytes, device_entropy() ? 1 : 0, &c) != MXD_OK)
+          throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
+        return deferred(c);
+      }
+      auto out = std::make_shared<Array>(DType::UInt8, std::vector<int64_t>{h, w, 3}, alloc_bytes((int64_t)h * w * 3));
+      if (mxd_jpeg_decode(bytes, nbytes, static_cast<uint8_t*>(out->data()), (int64_t)w * 3, w, h) != MXD_OK) {
+        const std::string e = jpeg_error();
+        throw std::runtime_error("load_jpeg: could not load " + where + " (" +
+                                 (e == "unhandled format" ? e : e) + ")");
+      }
       return out;
     }
-    if (!ok) throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
-    if (device_decode()) {
-      // markers only (the Huffman decode too runs on the GPU, csrc/jpeghuff.hip)
-      // when the file qualifies, else the entropy decode here; the GPU
-      // finishes it in the batch launch
-      mxd_jpeg_coefs* c = nullptr;
-      if (mxd_jpeg_coefs_parse(bytes, nbytes, device_entropy() ? 1 : 0, &c) != MXD_OK)
-        throw std::runtime_error("load_jpeg: could not load " + where + " (" + jpeg_error() + ")");
-      auto src = std::make_shared<const JpegSource>(c);
-      int32_t cw = 0, ch = 0, dev_ok = 0;
-      check(mxd_jpeg_coefs_info(c, &cw, &ch, &dev_ok));
-      auto out = std::make_shared<Array>(src, ch, cw);
-      if (!dev_ok) out->data();  // CMYK / YCCK: the host finishes it now
-      return out;
-    }
-    auto out = std::make_shared<Array>(DType::UInt8, std::vector<int64_t>{h, w, 3}, alloc_bytes((int64_t)h * w * 3));
-    if (mxd_jpeg_decode(bytes, nbytes, static_cast<uint8_t*>(out->data()), (int64_t)w * 3, w, h) != MXD_OK) {
-      const std::string e = jpeg_error();
-      throw std::runtime_error("load_jpeg: could not load " + where + " (" +
-                               (e == "unhandled format" ? e : e) + ")");
-    }
-    return out;
   }
+not_jpeg:
   ImageDecoder dec;
   {
     std::lock_guard<std::mutex> lk(g_dec_mu);
@@ -1165,6 +1210,13 @@ DevicePool& device_pool() {
 }  // namespace
 
 size_t device_pool_bytes(int device) { return device_pool().cached(device); }
+
+std::vector<int64_t> pipe_stats(bool reset) {
+  std::vector<int64_t> r(6, 0);
+  for (PipeLine& l : g_pipe_ns)
+    for (int i = 0; i < 6; i++) r[i] += reset ? l.v[i].exchange(0) : l.v[i].load();
+  return r;
+}
 
 std::pair<int64_t, int64_t> run_on_stats(bool reset) {
   const std::pair<int64_t, int64_t> r{g_run_calls.load(), g_run_jpeg.load()};
@@ -1435,6 +1487,7 @@ Sample BufferBatch::get(int64_t idx) const {
 // ------------------------------------------------------------------ streams
 // stream/FromBuffer.cpp:12-30
 Sample FromBuffer::next() const {
+  PipeTimer timer(4);
   int64_t idx = -1;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -1454,6 +1507,7 @@ Sample StreamTransform::next() const {
   while (res.empty()) {
     Sample s = s_->next();
     if (s.empty()) break;
+    PipeTimer timer(1);
     res = op_->apply(s);
   }
   return res;
@@ -1468,11 +1522,15 @@ StreamBatch::StreamBatch(std::shared_ptr<Stream> s, int64_t batch_size, std::uno
 
 Sample StreamBatch::next() const {
   std::vector<Sample> samples;
-  for (int64_t i = 0; i < bs_; i++) {
-    Sample s = s_->next();
-    if (s.empty()) break;
-    samples.push_back(std::move(s));
+  {
+    PipeTimer timer(2);
+    for (int64_t i = 0; i < bs_; i++) {
+      Sample s = s_->next();
+      if (s.empty()) break;
+      samples.push_back(std::move(s));
+    }
   }
+  PipeTimer timer(3);
   return samples.empty() ? Sample() : merge_batch(samples, pad_, dims_, out_);
 }
 

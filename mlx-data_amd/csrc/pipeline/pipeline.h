@@ -136,6 +136,7 @@ size_t device_pool_bytes(int device);
 // Per-device batch calls made (fused launches, one per device slice) and the
 // JPEG images they carried since the last reset (diagnostics, tests).
 std::pair<int64_t, int64_t> run_on_stats(bool reset);
+std::vector<int64_t> pipe_stats(bool reset);  // diagnostics: see pipeline.cpp g_pipe_ns
 
 // ---------------------------------------------------------------- state
 struct State {

@@ -513,6 +513,7 @@ PYBIND11_MODULE(_pipeline, m) {
   m.def("device_decode", &device_decode);
   m.def("_device_pool_bytes", &device_pool_bytes, py::arg("device"));
   m.def("_run_on_stats", &run_on_stats, py::arg("reset") = false);
+  m.def("_pipe_stats", &pipe_stats, py::arg("reset") = false);
 
   // The decoder holds a Python callable: drop it before the interpreter goes.
   py::module_::import("atexit").attr("register")(py::cpp_function([] { set_image_decoder(nullptr); }));

@@ -30,9 +30,9 @@ EXPORTS = (
     "mxd_release_host_buffers",
     "mxd_rotate_geometry", "mxd_channel_reduction_preset", "mxd_pixmap_batch", "mxd_pixmap_host",
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
-    "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
+    "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_load", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
     "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
-    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources",
+    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources", "mxd_host_stats",
 )
 
 MXD_AFFINE = 0
@@ -274,13 +274,16 @@ class JpegCoefs:
     Huffman decode too is left to the GPU when the file qualifies
     (``entropy_pending``)."""
 
-    def __init__(self, data, device_entropy=False):
-        buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
-        h = ctypes.c_void_p()
-        if device_entropy:
+    def __init__(self, data, device_entropy=False, _handle=None):
+        h = ctypes.c_void_p(_handle)
+        if _handle is not None:
+            pass
+        elif device_entropy:
+            buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
             check(lib().mxd_jpeg_coefs_parse(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes), 1,
                                              ctypes.byref(h)))
         else:
+            buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
             check(lib().mxd_jpeg_coefs_decode(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes),
                                               ctypes.byref(h)))
         self.handle = h.value
@@ -291,6 +294,14 @@ class JpegCoefs:
         check(lib().mxd_jpeg_coefs_info(ctypes.c_void_p(self.handle), ctypes.byref(w), ctypes.byref(hh),
                                         ctypes.byref(ok)))
         self.width, self.height, self.device_ok = w.value, hh.value, bool(ok.value)
+
+    @classmethod
+    def load(cls, path, device_entropy=True):
+        """mxd_jpeg_coefs_load: the file at `path` read straight into the
+        handle; None when it does not start with the JPEG signature."""
+        h = ctypes.c_void_p()
+        check(lib().mxd_jpeg_coefs_load(os.fsencode(path), 1 if device_entropy else 0, ctypes.byref(h)))
+        return None if not h.value else cls(None, _handle=h.value)
 
     def finish(self):
         """Host finish: (H, W, 3) uint8, the bytes jpeg_decode gives."""
@@ -334,6 +345,16 @@ def jpeg_plane_sources(reset=False):
     c = ctypes.c_int64()
     check(lib().mxd_jpeg_plane_sources(ctypes.byref(c), 1 if reset else 0))
     return c.value
+
+
+def host_stats(reset=False):
+    """Host-side time split since the last reset (mxd_host_stats): a dict of
+    host-path calls, images, wall / device-wait seconds, coefficient parses
+    and their seconds (summed over threads)."""
+    v = (ctypes.c_int64 * 6)()
+    check(lib().mxd_host_stats(v, 1 if reset else 0))
+    return {"calls": v[0], "images": v[1], "call_s": v[2] * 1e-9, "wait_s": v[3] * 1e-9,
+            "parses": v[4], "parse_s": v[5] * 1e-9}
 
 
 def jpeg_resize_crop_to_device(images, n, out_dtype, device=0):

@@ -144,6 +144,31 @@ def word_source(request):
     capi.set_tuning(capi.MXD_TUNE_HUFF_GLOBAL, prev)
 
 
+def test_fill_bytes_before_markers(word_source):
+    """0xFF fill bytes before restart markers and EOI (legal padding no
+    Pillow file carries) are dropped like jdhuff.c drops them: the device
+    decode equals the host decoder and Pillow."""
+    rng = np.random.default_rng(12)
+    datas = []
+    for i in range(4):
+        d = _encode(_smooth(rng, 120 + 40 * i, 170), quality=80 + 4 * i, subsampling=i % 3,
+                    restart_marker_blocks=1 + i)
+        s, e = _ecs_range(d)
+        body = bytearray()
+        k = s
+        while k < e:  # before every RSTn marker: one to three fill bytes
+            if d[k] == 0xFF and 0xD0 <= d[k + 1] <= 0xD7:
+                body += b"\xff" * (1 + (k % 3))
+                body += d[k:k + 2]
+                k += 2
+                continue
+            body.append(d[k])
+            k += 1
+        datas.append(d[:s] + bytes(body) + b"\xff\xff" + d[e:])
+    coefs = _check_identity(datas)
+    assert all(c.entropy_pending for c in coefs)
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_encoded_sweep_identity(seed, word_source):
     coefs = _check_identity(_sweep(seed))

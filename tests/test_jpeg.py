@@ -193,6 +193,35 @@ def test_device_entropy_parse_routes_and_host_finish():
             assert np.array_equal(c.finish(), GOLD[f"{k}_rgb"]), k
 
 
+def test_coefs_load_reads_files_like_parse(tmp_path):
+    """mxd_jpeg_coefs_load (the pipeline's LoadImage on device decode): the
+    file read straight into the handle gives mxd_jpeg_coefs_parse's routes and
+    bytes; a file without the JPEG signature gives no handle (the caller's
+    other decoders take it); unreadable / broken files are errors."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(78)
+    for i, kw in enumerate([dict(quality=90), dict(quality=70, progressive=True), dict(quality=85, subsampling=0,
+                                                                                       restart_marker_blocks=2)]):
+        b = io.BytesIO()
+        Image.fromarray(_smooth(rng, 60 + i, 83, 3)).save(b, "JPEG", **kw)
+        p = tmp_path / f"f{i}.jpg"
+        p.write_bytes(b.getvalue())
+        for dev in (True, False):
+            c = capi.JpegCoefs.load(str(p), device_entropy=dev)
+            ref = capi.JpegCoefs(b.getvalue(), device_entropy=dev)
+            assert (c.width, c.height, c.entropy_pending) == (ref.width, ref.height, ref.entropy_pending), (i, dev)
+            assert np.array_equal(c.finish(), ref.finish()), (i, dev)
+    png = tmp_path / "x.png"
+    Image.fromarray(_smooth(rng, 8, 8, 3)).save(png)
+    assert capi.JpegCoefs.load(str(png)) is None
+    with pytest.raises(capi.MxdError, match="could not load"):
+        capi.JpegCoefs.load(str(tmp_path / "missing.jpg"))
+    bad = tmp_path / "bad.jpg"
+    bad.write_bytes(b"\xff\xd8\xff\xe0\x00\x10JFIF" + bytes(40))
+    with pytest.raises(capi.MxdError):
+        capi.JpegCoefs.load(str(bad))
+
+
 def test_device_entropy_tables_after_the_scan_go_to_the_host():
     """a DHT or DRI between the recorded scan and EOI must not
     reach the device decode (the host decodes the scan at its SOS with the

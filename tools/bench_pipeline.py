@@ -70,6 +70,11 @@ def make_files(root, name, n):
     return files
 
 
+def _pipe_stats(reset):
+    from mlx_data_amd import _pipeline
+    return _pipeline._pipe_stats(reset)
+
+
 def run_surface(files, batch, workers, variant, repeat=1):
     from mlx_data_amd import data as dx
 
@@ -156,6 +161,7 @@ def main():
     ap.add_argument("--cpu-images", type=int, default=512, help="files the CPU restatement runs over")
     ap.add_argument("--min-seconds", type=float, default=5.0, help="least duration of a timed surface run")
     ap.add_argument("--min-batches", type=int, default=16, help="least batches per worker of a timed surface run")
+    ap.add_argument("--stats", action="store_true", help="add mxd_host_stats of the timed run to GPU legs' lines")
     ap.add_argument("--tune", default="", help="tuning knobs for the GPU legs, e.g. HUFF_GLOBAL=1,HUFF_BITS=1024 "
                     "(capi.set_tuning; MXD_TUNE_<name>)")
     args = ap.parse_args()
@@ -187,6 +193,10 @@ def main():
                         nw, tw = run_surface(fl[:min(len(fl), 2 * B * w)], B, w, v)
                         want = max(args.min_seconds * nw / tw, args.min_batches * B * w)
                         repeat = max(1, int(np.ceil(want / len(fl))))
+                        if args.stats:
+                            from mlx_data_amd import capi
+                            capi.host_stats(reset=True)
+                            _pipe_stats(True)
                         n, dt = run_surface(fl, B, w, v, repeat)
                         # the warm-up's rate underestimates the steady one: rerun
                         # longer until the timed run itself lasts >= --min-seconds
@@ -194,11 +204,23 @@ def main():
                             if dt >= args.min_seconds:
                                 break
                             repeat = max(repeat + 1, int(np.ceil(repeat * 1.25 * args.min_seconds / dt)))
+                            if args.stats:
+                                capi.host_stats(reset=True)
+                                _pipe_stats(True)
                             n, dt = run_surface(fl, B, w, v, repeat)
                     rec = dict(dataset=name, variant=v, workers=w, images=n, seconds=round(dt, 3),
                                images_per_s=round(n / dt, 1), batch=B)
                     if tune and v != "cpu":
                         rec["tune"] = tune
+                    if args.stats and v != "cpu":
+                        hs = capi.host_stats(reset=True)
+                        # per image, microseconds (summed over worker threads)
+                        rec["host_us_per_image"] = {k: round(hs[k] / max(1, n) * 1e6, 2)
+                                                    for k in ("call_s", "wait_s", "parse_s")}
+                        rec["host_calls"] = hs["calls"]
+                        ps = _pipe_stats(True)
+                        rec["pipe_us_per_image"] = {k: round(ps[i] / max(1, n) / 1e3, 2) for i, k in enumerate(
+                            ("load_image", "transforms", "batch_fetch", "batch_merge", "from_buffer"))}
                     print(json.dumps(rec), flush=True)
 
 
