@@ -160,6 +160,29 @@ def test_load_image_uses_native_decoder(tmp_path):
         dx.buffer_from_vector([dict(m=bad)]).load_image("m", from_memory=True)[0]
 
 
+def test_host_and_pipeline_stats_count(tmp_path):
+    """The diagnostics bench_pipeline --stats reads: mxd_host_stats counts
+    marker parses / loads (and resets), the pipeline's stage timers count
+    load_image calls and time the batch's fetches."""
+    from mlx_data_amd import _pipeline
+    from mlx_data_amd import data as dx
+
+    raw = GOLD["caltech_300x200_jpg"]
+    (tmp_path / "x.jpg").write_bytes(raw.tobytes())
+    capi.host_stats(reset=True)
+    capi.JpegCoefs(raw.tobytes(), device_entropy=True)
+    capi.JpegCoefs.load(str(tmp_path / "x.jpg"))
+    hs = capi.host_stats(reset=True)
+    assert hs["parses"] == 2 and hs["parse_s"] > 0
+    assert capi.host_stats()["parses"] == 0
+    _pipeline._pipe_stats(True)
+    d = dx.buffer_from_vector([dict(f=b"x.jpg")] * 6).to_stream().load_image("f", prefix=str(tmp_path)).batch(3)
+    assert sum(1 for _ in d) == 2
+    ps = _pipeline._pipe_stats(True)
+    assert ps[5] == 6 and ps[0] > 0 and ps[2] >= ps[0] and ps[1] >= ps[0]
+    assert _pipeline._pipe_stats(False)[5] == 0
+
+
 def test_device_entropy_parse_routes_and_host_finish():
     """mxd_jpeg_coefs_parse(device_entropy=1) (CPU half of the device entropy
     decode, csrc/jpeghuff.h): baseline one-scan files are only parsed
