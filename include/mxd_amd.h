@@ -297,8 +297,9 @@ int mxd_jpeg_info(const uint8_t* data, size_t size, int32_t* width, int32_t* hei
 
 /* Decodes into dst: height rows of width*3 bytes, dst_stride bytes apart (any
  * host memory, e.g. pinned staging from mxd_malloc_pinned).  width/height
- * must be mxd_jpeg_info's.  MXD_ERR_INVALID with libjpeg's message on corrupt
- * or unsupported data. */
+ * must be mxd_jpeg_info's.  Baseline, extended and progressive frames,
+ * Huffman or arithmetic coded (SOF0-2, SOF9-10).  MXD_ERR_INVALID with
+ * libjpeg's message on corrupt or unsupported data. */
 int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, int32_t width,
                     int32_t height);
 
@@ -306,7 +307,8 @@ int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_
  * "later a device-side decode") ---------------------------------------------
  *
  * The same decode in two halves: mxd_jpeg_coefs_decode runs the host part
- * (markers + Huffman entropy decode, every error mxd_jpeg_decode reports)
+ * (markers + Huffman or arithmetic entropy decode, every error
+ * mxd_jpeg_decode reports)
  * and keeps the quantised DCT coefficients; dequantisation + ISLOW IDCT,
  * chroma upsampling and colour conversion run later -- on the host
  * (mxd_jpeg_coefs_finish) or on the GPU inside mxd_jpeg_resize_crop_host /

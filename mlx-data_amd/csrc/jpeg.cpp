@@ -64,10 +64,10 @@ std::string hex2(int v) {
   return std::string("0x") + d[(v >> 4) & 15] + d[v & 15];
 }
 
-// SOF markers other than 0xC0-0xC2: arithmetic coding (0xC9-0xCB, 0xCD-0xCF)
-// and lossless / hierarchical processes are not decoded here.
+// SOF markers other than 0xC0-0xC2 and 0xC9-0xCA (sequential / progressive
+// arithmetic coding): lossless and hierarchical processes are not decoded
+// here.
 [[noreturn]] void unsupported_sof(int m) {
-  if ((m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) fail("Sorry, arithmetic coding is not supported");
   fail("Unsupported JPEG process: SOF type " + hex2(m));
 }
 
@@ -420,6 +420,164 @@ struct Bits {
 
 
 // ---------------------------------------------------------------- IDCT
+// ---------------------------------------------------------------- arithmetic
+// T.81 Table D.2 (Qe, next state after an MPS, after an LPS, MPS switch on
+// an LPS) and a 114th state: Table F.5's fixed estimate for the AC sign.
+struct QeState {
+  uint16_t qe;
+  uint8_t nmps, nlps, sw;
+};
+constexpr QeState kQe[114] = {
+    {0x5A1D, 1, 1, 1},    {0x2586, 2, 14, 0},   {0x1114, 3, 16, 0},   {0x080B, 4, 18, 0},   {0x03D8, 5, 20, 0},
+    {0x01DA, 6, 23, 0},   {0x00E5, 7, 25, 0},   {0x006F, 8, 28, 0},   {0x0036, 9, 30, 0},   {0x001A, 10, 33, 0},
+    {0x000D, 11, 35, 0},  {0x0006, 12, 9, 0},   {0x0003, 13, 10, 0},  {0x0001, 13, 12, 0},  {0x5A7F, 15, 15, 1},
+    {0x3F25, 16, 36, 0},  {0x2CF2, 17, 38, 0},  {0x207C, 18, 39, 0},  {0x17B9, 19, 40, 0},  {0x1182, 20, 42, 0},
+    {0x0CEF, 21, 43, 0},  {0x09A1, 22, 45, 0},  {0x072F, 23, 46, 0},  {0x055C, 24, 48, 0},  {0x0406, 25, 49, 0},
+    {0x0303, 26, 51, 0},  {0x0240, 27, 52, 0},  {0x01B1, 28, 54, 0},  {0x0144, 29, 56, 0},  {0x00F5, 30, 57, 0},
+    {0x00B7, 31, 59, 0},  {0x008A, 32, 60, 0},  {0x0068, 33, 62, 0},  {0x004E, 34, 63, 0},  {0x003B, 35, 32, 0},
+    {0x002C, 9, 33, 0},   {0x5AE1, 37, 37, 1},  {0x484C, 38, 64, 0},  {0x3A0D, 39, 65, 0},  {0x2EF1, 40, 67, 0},
+    {0x261F, 41, 68, 0},  {0x1F33, 42, 69, 0},  {0x19A8, 43, 70, 0},  {0x1518, 44, 72, 0},  {0x1177, 45, 73, 0},
+    {0x0E74, 46, 74, 0},  {0x0BFB, 47, 75, 0},  {0x09F8, 48, 77, 0},  {0x0861, 49, 78, 0},  {0x0706, 50, 79, 0},
+    {0x05CD, 51, 48, 0},  {0x04DE, 52, 50, 0},  {0x040F, 53, 50, 0},  {0x0363, 54, 51, 0},  {0x02D4, 55, 52, 0},
+    {0x025C, 56, 53, 0},  {0x01F8, 57, 54, 0},  {0x01A4, 58, 55, 0},  {0x0160, 59, 56, 0},  {0x0125, 60, 57, 0},
+    {0x00F6, 61, 58, 0},  {0x00CB, 62, 59, 0},  {0x00AB, 63, 61, 0},  {0x008F, 32, 61, 0},  {0x5B12, 65, 65, 1},
+    {0x4D04, 66, 80, 0},  {0x412C, 67, 81, 0},  {0x37D8, 68, 82, 0},  {0x2FE8, 69, 83, 0},  {0x293C, 70, 84, 0},
+    {0x2379, 71, 86, 0},  {0x1EDF, 72, 87, 0},  {0x1AA9, 73, 87, 0},  {0x174E, 74, 72, 0},  {0x1424, 75, 72, 0},
+    {0x119C, 76, 74, 0},  {0x0F6B, 77, 74, 0},  {0x0D51, 78, 75, 0},  {0x0BB6, 79, 77, 0},  {0x0A40, 48, 77, 0},
+    {0x5832, 81, 80, 1},  {0x4D1C, 82, 88, 0},  {0x438E, 83, 89, 0},  {0x3BDD, 84, 90, 0},  {0x34EE, 85, 91, 0},
+    {0x2EAE, 86, 92, 0},  {0x299A, 87, 93, 0},  {0x2516, 71, 86, 0},  {0x5570, 89, 88, 1},  {0x4CA9, 90, 95, 0},
+    {0x44D9, 91, 96, 0},  {0x3E22, 92, 97, 0},  {0x3824, 93, 99, 0},  {0x32B4, 94, 99, 0},  {0x2E17, 86, 93, 0},
+    {0x56A8, 96, 95, 1},  {0x4F46, 97, 101, 0}, {0x47E5, 98, 102, 0}, {0x41CF, 99, 103, 0}, {0x3C3D, 100, 104, 0},
+    {0x375E, 93, 99, 0},  {0x5231, 102, 105, 0}, {0x4C0F, 103, 106, 0}, {0x4639, 104, 107, 0}, {0x415E, 99, 103, 0},
+    {0x5627, 106, 105, 1}, {0x50E7, 107, 108, 0}, {0x4B85, 103, 109, 0}, {0x5597, 109, 110, 0}, {0x504F, 107, 111, 0},
+    {0x5A10, 111, 110, 1}, {0x5522, 109, 112, 0}, {0x59EB, 111, 112, 1}, {0x5A1D, 113, 113, 0}};
+constexpr uint8_t kFixedState = 113;
+
+// The QM decoder (T.81 D.2: INITDEC, DECODE with its conditional exchanges,
+// RENORMD, BYTEIN) over one scan's data.  A statistics bin is a byte: the MPS
+// in bit 7, the state index below.  C holds the code bits aligned to A << CT;
+// CT < 0 at a segment's start takes the first two bytes in.  At a marker (or
+// the end of the data) the input is zeros from then on, as T.81 allows and
+// jdarith.c does.  `failed`: a spectral or magnitude overflow in this
+// interval (corrupt data) -- its remaining blocks are left zero.
+struct Arith {
+  const uint8_t* p = nullptr;
+  const uint8_t* end = nullptr;
+  bool at_marker = false;  // p at the 0xFF of the marker the data ran into
+  uint64_t c = 0;
+  uint32_t a = 0;
+  int ct = -16;
+  bool failed = false;
+  uint8_t dc_stats[16][64], ac_stats[16][256];
+  uint8_t fixed = kFixedState;
+
+  int byte_in() {
+    if (at_marker || p >= end) {
+      at_marker = true;
+      return 0;
+    }
+    const uint8_t b = *p;
+    if (b != 0xFF) {
+      p++;
+      return b;
+    }
+    const uint8_t* q = p + 1;
+    while (q < end && *q == 0xFF) q++;  // fill bytes
+    if (q < end && *q == 0x00) {
+      p = q + 1;
+      return 0xFF;  // stuffed
+    }
+    p = q - 1;  // the marker's 0xFF
+    at_marker = true;
+    return 0;
+  }
+  void reset() {
+    c = 0;
+    a = 0;
+    ct = -16;
+    failed = false;
+  }
+  int decode(uint8_t& st) {
+    while (a < 0x8000) {
+      if (--ct < 0) {
+        c = (c << 8) | (uint64_t)byte_in();
+        ct += 8;
+        if (ct < 0 && ++ct == 0) a = 0x8000;  // both initial bytes in: A = 0x10000 below
+      }
+      a <<= 1;
+    }
+    int sv = st;
+    const QeState& q = kQe[sv & 0x7F];
+    const uint8_t mps_next = (uint8_t)q.nmps, lps_next = (uint8_t)(q.nlps | (q.sw << 7));
+    a -= q.qe;
+    const uint64_t t = (uint64_t)a << ct;
+    if (c >= t) {  // the lower sub-interval: the LPS, unless it is the larger one
+      c -= t;
+      if (a < q.qe) {
+        st = (uint8_t)((sv & 0x80) ^ mps_next);
+      } else {
+        st = (uint8_t)((sv & 0x80) ^ lps_next);
+        sv ^= 0x80;
+      }
+      a = q.qe;
+    } else if (a < 0x8000) {  // the upper one, renormalising: the MPS, unless exchanged
+      if (a < q.qe) {
+        st = (uint8_t)((sv & 0x80) ^ lps_next);
+        sv ^= 0x80;
+      } else {
+        st = (uint8_t)((sv & 0x80) ^ mps_next);
+      }
+    }
+    return sv >> 7;
+  }
+  // The bins of the scan's tables to state 0 / MPS 0 (scan start, restart).
+  void clear_stats(const int* dc_tbls, const int* ac_tbls, int n) {
+    for (int i = 0; i < n; i++) {
+      if (dc_tbls[i] >= 0) std::memset(dc_stats[dc_tbls[i]], 0, sizeof dc_stats[0]);
+      if (ac_tbls[i] >= 0) std::memset(ac_stats[ac_tbls[i]], 0, sizeof ac_stats[0]);
+    }
+  }
+  // End of a restart interval: the RST marker (Bits::restart's resync
+  // rules), then a fresh coder.
+  void restart(int expected) {
+    Bits b;
+    b.p = p;
+    b.end = end;
+    b.at_marker = at_marker;
+    b.restart(expected);
+    p = b.p;
+    at_marker = b.at_marker;
+    reset();
+  }
+  // Magnitude category and bits of a nonzero value (F.2.4.3, Figures F.23 /
+  // F.24): the first decision in bin `first`, the next ones from `x2` on
+  // (first + 0 again for AC: X1 = SP), the bits 14 bins past the last
+  // category bin.  Returns |v| - 1 (*cat: its top bit, 0 for |v| = 1), or -1
+  // on a magnitude overflow.
+  int magnitude(uint8_t* stats, int first, int x2, bool ac, int* cat) {
+    int i = first;
+    int m = decode(stats[i]);
+    if (m) {
+      if (ac) {
+        if (!decode(stats[i])) goto bits;
+        m <<= 1;
+      }
+      i = x2;
+      while (decode(stats[i])) {
+        if ((m <<= 1) == 0x8000) return -1;
+        i++;
+      }
+    }
+  bits:
+    *cat = m;
+    int v = m;
+    i += 14;
+    while (m >>= 1)
+      if (decode(stats[i])) v |= m;
+    return v;
+  }
+};
+
 constexpr int kConstBits = 13;
 constexpr int kPass1Bits = 2;
 constexpr int32_t FIX_0_298631336 = 2446, FIX_0_390180644 = 3196, FIX_0_541196100 = 4433, FIX_0_765366865 = 6270,
@@ -686,6 +844,9 @@ struct Decoder {
   size_t pos = 0;
   int width = 0, height = 0, ncomp = 0;
   bool progressive = false, baseline_seen = false;
+  bool arith = false;  // arithmetic-coded frame (SOF9 / SOF10)
+  // DAC conditioning (T.81 F.1.4.4.1.4 / F.1.4.4.2.1), defaults L = 0, U = 1, Kx = 5
+  uint8_t arith_dc_l[16], arith_dc_u[16], arith_ac_k[16];
   bool jfif = false, adobe = false;
   int adobe_transform = -1;
   int restart_interval = 0;
@@ -726,7 +887,11 @@ struct Decoder {
     return coefbuf.data() + c.off + ((int64_t)by * c.bw + bx) * 64;
   }
 
-  Decoder(const uint8_t* d, size_t n) : data(d), size(n) {}
+  Decoder(const uint8_t* d, size_t n) : data(d), size(n) {
+    std::memset(arith_dc_l, 0, sizeof arith_dc_l);
+    std::memset(arith_dc_u, 1, sizeof arith_dc_u);
+    std::memset(arith_ac_k, 5, sizeof arith_ac_k);
+  }
 
   int u8() {
     if (pos >= size) fail("Premature end of JPEG file");
@@ -784,6 +949,24 @@ struct Decoder {
     if (len != 0) fail("Bogus marker length");
   }
 
+  // jdmarker.c get_dac: (Tc Tb, value) pairs; DC values are U << 4 | L.
+  void read_dac() {
+    int len = u16() - 2;
+    while (len > 0) {
+      const int index = u8(), val = u8();
+      len -= 2;
+      if (index >= 32) fail("Bogus DAC index " + std::to_string(index));
+      if (index >= 16) {
+        arith_ac_k[index - 16] = (uint8_t)val;
+      } else {
+        arith_dc_l[index] = (uint8_t)(val & 15);
+        arith_dc_u[index] = (uint8_t)(val >> 4);
+        if (arith_dc_l[index] > arith_dc_u[index]) fail("Bogus DAC value " + hex2(val));
+      }
+    }
+    if (len != 0) fail("Bogus marker length");
+  }
+
   void read_sof(int marker) {
     if (frame) fail("Invalid JPEG file structure: two SOF markers");
     const int len = u16();
@@ -794,8 +977,9 @@ struct Decoder {
     if (prec != 8) fail("Unsupported JPEG data precision " + std::to_string(prec));
     if (width <= 0 || height <= 0 || ncomp <= 0 || ncomp > 4) fail("Empty JPEG image (DNL not supported)");
     if (len != 8 + 3 * ncomp) fail("Bogus marker length");
-    progressive = marker == 0xC2;
-    if (progressive && device_entropy) throw NotDevice{};
+    progressive = marker == 0xC2 || marker == 0xCA;
+    arith = marker == 0xC9 || marker == 0xCA;
+    if ((progressive || arith) && device_entropy) throw NotDevice{};
     for (int i = 0; i < ncomp; i++) {
       Component& c = comp[i];
       c.id = u8();
@@ -893,11 +1077,20 @@ struct Decoder {
       // libjpeg only warns here; sequential decoding ignores the fields
     }
     any_scan = true;
+    for (int i = 0; i < ns; i++) sc[i]->dc_pred = 0;
+    eobrun = 0;
+    if (arith) {
+      if (progressive && ah != 0 && al != ah - 1) fail("Invalid progressive parameters");
+      Arith ar;
+      ar.p = data + pos;
+      ar.end = data + size;
+      decode_scan_arith(ar, sc, ns, ss, se, ah, al);
+      pos = (size_t)(ar.p - data);
+      return;
+    }
     Bits bits;
     bits.p = data + pos;
     bits.end = data + size;
-    for (int i = 0; i < ns; i++) sc[i]->dc_pred = 0;
-    eobrun = 0;
     decode_scan(bits, sc, ns, ss, se, ah, al);
     // resume marker parsing where the entropy data ended
     pos = (size_t)(bits.p - data);
@@ -969,8 +1162,9 @@ struct Decoder {
     pending = true;
   }
 
-  template <class F>
-  void for_each_mcu(Bits& bits, Component** sc, int ns, F&& decode_block) {
+  // R: Bits or Arith (restart(), insufficient)
+  template <class R, class F>
+  void for_each_mcu(R& bits, Component** sc, int ns, F&& decode_block) {
     int restarts_left = restart_interval, next_rst = 0;
     auto restart_check = [&]() {
       if (restart_interval) {
@@ -1123,6 +1317,139 @@ struct Decoder {
     });
   }
 
+  // One arithmetic-coded scan (T.81 F.2.4 / G.2: jdarith.c's decode_mcu,
+  // decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine).  The
+  // statistics of the scan's tables, the DC predictions and contexts start
+  // over at the scan and at every restart; a spectral or magnitude overflow
+  // (corrupt data) leaves the rest of its restart interval's blocks alone.
+  void decode_scan_arith(Arith& ar, Component** sc, int ns, int ss, int se, int ah, int al) {
+    const bool dc_stats = !progressive || (ss == 0 && ah == 0);
+    const bool ac_stats = !progressive || ss != 0;
+    int dct[4], act[4];
+    for (int i = 0; i < ns; i++) {
+      dct[i] = dc_stats ? sc[i]->dc_tbl : -1;
+      act[i] = ac_stats ? sc[i]->ac_tbl : -1;
+      if (!progressive) {
+        std::memcpy(sc[i]->q, quant(*sc[i]), sizeof sc[i]->q);  // latched at the scan
+        sc[i]->coded = true;
+      }
+    }
+    int dc_ctx[4] = {0, 0, 0, 0};
+    int gen = 0, seen = -1;  // restarts seen by the coder / by the block loop
+    struct Restarting {
+      Arith& ar;
+      int& gen;
+      bool insufficient = false;
+      void restart(int expected) {
+        ar.restart(expected);
+        gen++;
+      }
+    } rd{ar, gen};
+    auto fresh = [&]() {
+      if (seen == gen) return;
+      seen = gen;
+      ar.clear_stats(dct, act, ns);
+      for (int i = 0; i < 4; i++) dc_ctx[i] = 0;
+    };
+    // F.2.4.1: a DC difference in the context of the component's last one
+    auto dc_diff = [&](Component& c) -> bool {
+      const int ci = (int)(&c - comp), t = c.dc_tbl;
+      uint8_t* st = ar.dc_stats[t];
+      const int s0 = dc_ctx[ci];
+      if (!ar.decode(st[s0])) {
+        dc_ctx[ci] = 0;
+        return true;
+      }
+      const int sign = ar.decode(st[s0 + 1]);
+      int cat;
+      const int v = ar.magnitude(st, s0 + 2 + sign, 20, false, &cat);
+      if (v < 0) return false;
+      if (cat < (1 << arith_dc_l[t]) >> 1) dc_ctx[ci] = 0;
+      else if (cat > (1 << arith_dc_u[t]) >> 1) dc_ctx[ci] = 12 + 4 * sign;
+      else dc_ctx[ci] = 4 + 4 * sign;
+      c.dc_pred = (c.dc_pred + (sign ? -(v + 1) : v + 1)) & 0xffff;
+      return true;
+    };
+    // F.2.4.2 / G.2: the AC coefficients k0..k1 of a first (or only) scan
+    auto ac_first = [&](Component& c, int16_t* blk, int k0, int k1, int shift) -> bool {
+      const int t = c.ac_tbl;
+      uint8_t* st = ar.ac_stats[t];
+      int k = k0 - 1;
+      do {
+        int i = 3 * k;
+        if (ar.decode(st[i])) break;  // end of block
+        for (;;) {
+          k++;
+          if (ar.decode(st[i + 1])) break;
+          i += 3;
+          if (k >= k1) return false;  // spectral overflow
+        }
+        const int sign = ar.decode(ar.fixed);
+        int cat;
+        const int v = ar.magnitude(st, i + 2, k <= arith_ac_k[t] ? 189 : 217, true, &cat);
+        if (v < 0) return false;
+        blk[kNatural[k]] = (int16_t)((uint32_t)(sign ? -(v + 1) : v + 1) << shift);
+      } while (k < k1);
+      return true;
+    };
+    if (!progressive) {
+      int16_t local[64];
+      for_each_mcu(rd, sc, ns, [&](Component& c, int bx, int by, bool) {
+        fresh();
+        int16_t* blk = defer ? cblk(c, bx, by) : local;
+        if (!defer) std::memset(blk, 0, 64 * sizeof(int16_t));
+        if (!ar.failed) {
+          if (!dc_diff(c)) ar.failed = true;
+          else {
+            blk[0] = (int16_t)c.dc_pred;
+            if (!ac_first(c, blk, 1, 63, 0)) ar.failed = true;  // (a sequential scan's Ss / Se / Al are ignored)
+          }
+        }
+        if (!defer) idct_block(blk, c.q, c.plane.data() + ((size_t)by * 8 * c.bw * 8) + (size_t)bx * 8, c.bw * 8);
+      });
+      return;
+    }
+    const int p1 = 1 << al, m1 = -1 * (1 << al);
+    for_each_mcu(rd, sc, ns, [&](Component& c, int bx, int by, bool) {
+      fresh();
+      if (ar.failed) return;
+      int16_t* blk = cblk(c, bx, by);
+      if (ss == 0 && ah == 0) {
+        if (!dc_diff(c)) ar.failed = true;
+        else blk[0] = (int16_t)((uint32_t)c.dc_pred << al);
+      } else if (ss == 0) {
+        if (ar.decode(ar.fixed)) blk[0] = (int16_t)(blk[0] | p1);
+      } else if (ah == 0) {
+        if (!ac_first(c, blk, ss, se, al)) ar.failed = true;
+      } else {
+        uint8_t* st = ar.ac_stats[c.ac_tbl];
+        int kex = se;  // the previous stage's end of block
+        while (kex > 0 && !blk[kNatural[kex]]) kex--;
+        for (int k = ss - 1; k < se; k++) {
+          int i = 3 * k;
+          if (k >= kex && ar.decode(st[i])) break;  // end of block
+          for (;;) {
+            int16_t& co = blk[kNatural[k + 1]];
+            if (co) {  // already nonzero: a correction bit
+              if (ar.decode(st[i + 2])) co = (int16_t)(co < 0 ? co + m1 : co + p1);
+              break;
+            }
+            if (ar.decode(st[i + 1])) {  // newly nonzero
+              co = (int16_t)(ar.decode(ar.fixed) ? m1 : p1);
+              break;
+            }
+            i += 3;
+            k++;
+            if (k >= se) {
+              ar.failed = true;  // spectral overflow
+              return;
+            }
+          }
+        }
+      }
+    });
+  }
+
   void parse() {
     if (size < 3 || data[0] != 0xFF || data[1] != 0xD8) fail("Not a JPEG file");
     pos = 2;
@@ -1136,9 +1463,11 @@ struct Decoder {
         case 0xC0:
         case 0xC1:
         case 0xC2:
+        case 0xC9:
+        case 0xCA:
           read_sof(m);
           break;
-        case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE:
+        case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xCB: case 0xCD: case 0xCE:
         case 0xCF:
           unsupported_sof(m);
         case 0xC4:
@@ -1149,7 +1478,8 @@ struct Decoder {
           read_dht();
           break;
         case 0xCC:
-          fail("Sorry, arithmetic coding is not supported");
+          read_dac();
+          break;
         case 0xDB:
           read_dqt();
           break;
@@ -1802,13 +2132,13 @@ bool info(const uint8_t* data, size_t size, int* width, int* height, int* compon
     for (;;) {
       const int m = d.next_marker();
       if (m < 0) fail("Premature end of JPEG file");
-      if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+      if (m == 0xC0 || m == 0xC1 || m == 0xC2 || m == 0xC9 || m == 0xCA) {
         d.read_sof(m);
         break;
       }
       if (m == 0xD9 || m == 0xDA) fail("Invalid JPEG file structure: SOS before SOF");
       if (m >= 0xD0 && m <= 0xD7) continue;
-      if ((m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) unsupported_sof(m);
+      if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xC9 && m != 0xCA && m != 0xCC) unsupported_sof(m);
       d.skip_segment();
     }
     *width = d.width;

@@ -319,3 +319,19 @@ def test_out_of_range_coefficients_take_the_wide_idct():
         datas.append(J.encode(np.zeros((h, w, nc) if nc == 3 else (h, w), np.uint8), q=q, coefs=planes))
     datas.append(_encode(_smooth(rng, 90, 70), quality=90))
     _check_identity(datas, pillow=False)
+
+
+def test_arithmetic_coded_files_finish_on_the_device():
+    """Arithmetic-coded files (tests/jpeg_arith_enc.py, SOF9 and SOF10) are
+    entropy-decoded on the host (parse_coefs routes them there) and finished
+    by the batch launch beside device-entropy files: equal to the host
+    decoder and to Pillow."""
+    import jpeg_arith_enc as A
+
+    rng = np.random.default_rng(33)
+    datas = [A.encode(_smooth(rng, 70, 90), q=3, restart_mcus=4),
+             A.encode_progressive(_smooth(rng, 64, 100), q=2),
+             _encode(_smooth(rng, 80, 60), quality=90),
+             A.encode(_smooth(rng, 33, 47)[:, :, 0], q=5, dac=(1, 6, 9))]
+    coefs = _check_identity(datas)
+    assert [c.entropy_pending for c in coefs] == [False, False, True, False]

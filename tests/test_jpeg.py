@@ -123,10 +123,10 @@ def _segment(marker, payload):
 def test_errors_carry_libjpeg_messages():
     with pytest.raises(capi.MxdError, match="Not a JPEG file"):
         capi.jpeg_info(b"\x89PNG\r\n\x1a\n" + bytes(32))
-    # arithmetic-coded frame (SOF9)
-    sof9 = b"\xff\xd8" + _segment(0xC9, bytes([8, 0, 8, 0, 8, 1, 1, 0x11, 0]))
-    with pytest.raises(capi.MxdError, match="arithmetic"):
-        capi.jpeg_info(sof9)
+    # a hierarchical (differential) frame, which libjpeg-turbo does not decode
+    sof13 = b"\xff\xd8" + _segment(0xCD, bytes([8, 0, 8, 0, 8, 1, 1, 0x11, 0]))
+    with pytest.raises(capi.MxdError, match="Unsupported JPEG process: SOF type 0xcd"):
+        capi.jpeg_info(sof13)
     # 12-bit precision
     sof1_12 = b"\xff\xd8" + _segment(0xC1, bytes([12, 0, 8, 0, 8, 1, 1, 0x11, 0]))
     with pytest.raises(capi.MxdError, match="precision"):
@@ -154,9 +154,9 @@ def test_load_image_uses_native_decoder(tmp_path):
     grey = dx.buffer_from_vector([dict(m=GOLD["grey_jpg"])]).load_image("m", from_memory=True)[0]["m"]
     assert np.array_equal(grey, GOLD["grey_rgb"]) and grey.shape[2] == 3
     bad = np.frombuffer(bytes(raw[:200]) + b"\xff\xd9", np.uint8)
-    bad = np.concatenate([bad[:2], np.frombuffer(b"\xff\xc9\x00\x0b\x08\x00\x08\x00\x08\x01\x01\x11\x00", np.uint8),
+    bad = np.concatenate([bad[:2], np.frombuffer(b"\xff\xcd\x00\x0b\x08\x00\x08\x00\x08\x01\x01\x11\x00", np.uint8),
                           bad[2:]])
-    with pytest.raises(RuntimeError, match=r"load_jpeg: could not load from memory \(.*arithmetic"):
+    with pytest.raises(RuntimeError, match=r"load_jpeg: could not load from memory \(Unsupported JPEG process"):
         dx.buffer_from_vector([dict(m=bad)]).load_image("m", from_memory=True)[0]
 
 
@@ -181,6 +181,90 @@ def test_host_and_pipeline_stats_count(tmp_path):
     ps = _pipeline._pipe_stats(True)
     assert ps[5] == 6 and ps[0] > 0 and ps[2] >= ps[0] and ps[1] >= ps[0]
     assert _pipeline._pipe_stats(False)[5] == 0
+
+
+def _arith_cases(seed, n, progressive):
+    import jpeg_arith_enc as A
+
+    rng = np.random.default_rng(seed)
+    for t in range(n):
+        h, w = int(rng.integers(1, 90)), int(rng.integers(1, 90))
+        grey = t % 4 == 3
+        if t % 2:
+            img = rng.integers(0, 256, (h, w) if grey else (h, w, 3), dtype=np.uint8)
+        else:
+            img = _smooth(rng, h, w, 1 if grey else 3)
+            img = img[:, :, 0] if grey else img
+        kw = dict(q=int(rng.integers(1, 30)))
+        if t % 3 == 0:
+            kw["restart_mcus"] = int(rng.integers(1, 5))
+        if t % 5 == 0:  # DAC conditioning other than the defaults
+            kw["dac"] = (int(rng.integers(0, 4)), int(rng.integers(4, 16)), int(rng.integers(1, 63)))
+        yield (A.encode_progressive if progressive else A.encode)(img, **kw), kw
+
+
+@pytest.mark.parametrize("progressive", [False, True])
+def test_arithmetic_coded_files_match_pillow(progressive):
+    """Arithmetic-coded JPEGs (SOF9 sequential, SOF10 progressive; the
+    reference's libjpeg-turbo build decodes them, super/CMakeLists.txt):
+    tests/jpeg_arith_enc.py writes them from T.81's QM coder and statistical
+    models -- Pillow decodes every one to the pixels of the same
+    coefficients Huffman-coded (the encoder is right) -- and the host decoder
+    gives Pillow's bytes: noise and smooth images, grey and 4:4:4, restart
+    intervals, DAC conditioning.  They are entropy-decoded on the host on the
+    device route too (parse_coefs)."""
+    Image = pytest.importorskip("PIL.Image")
+
+    for i, (data, kw) in enumerate(_arith_cases(31 + progressive, 24, progressive)):
+        pil = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+        assert np.array_equal(capi.jpeg_decode(data), pil), (i, kw)
+        if i < 4:  # the encoder: the same coefficients Huffman-coded decode alike
+            c = capi.JpegCoefs(data, device_entropy=True)
+            assert not c.entropy_pending and np.array_equal(c.finish(), pil), (i, kw)
+
+
+def test_truncated_progressive_arithmetic_files_match_pillow():
+    """Progressive arithmetic-coded files cut between scans and inside their
+    entropy-coded data (an EOI appended, as libjpeg's memory source fakes
+    one): past a cut the decoder reads zeros (T.81 allows a marker inside
+    arithmetic-coded data) and block smoothing fills what later scans would
+    have held; Pillow's bytes for every cut between scans.  A cut inside a
+    scan decodes the rest of it from zeros, which can leave coefficients far
+    outside any 8-bit image's range; where the IDCT's 16-bit SIMD
+    dequantisation in Pillow's libjpeg-turbo then departs from jidctint.c
+    (test_gpu_jpeg_entropy.py's out-of-range test) a few pixels differ, so
+    those cuts must match in all but a few percent of files."""
+    Image = pytest.importorskip("PIL.Image")
+    ImageFile = pytest.importorskip("PIL.ImageFile")
+    import jpeg_arith_enc as A
+
+    prev = ImageFile.LOAD_TRUNCATED_IMAGES
+    ImageFile.LOAD_TRUNCATED_IMAGES = True
+    try:
+        rng = np.random.default_rng(9)
+        between = inside = inside_bad = 0
+        for t in range(12):
+            h, w = int(rng.integers(16, 120)), int(rng.integers(16, 120))
+            d = A.encode_progressive(_smooth(rng, h, w, 3), q=int(rng.integers(1, 12)),
+                                     restart_mcus=3 if t % 3 == 0 else 0)
+            sos = [i for i in range(len(d) - 1) if d[i] == 0xFF and d[i + 1] == 0xDA]
+            hdr = [i + 2 + int.from_bytes(d[i + 2:i + 4], "big") for i in sos]  # each scan's data start
+            for cut in sos[1:]:
+                m = d[:cut] + b"\xff\xd9"
+                want = np.asarray(Image.open(io.BytesIO(m)).convert("RGB"))
+                assert np.array_equal(capi.jpeg_decode(m), want), (t, cut)
+                between += 1
+            for a, b in zip(hdr, sos[1:] + [len(d) - 2]):
+                if b - a <= 3:
+                    continue
+                m = d[:int(rng.integers(a + 1, b - 1))] + b"\xff\xd9"
+                want = np.asarray(Image.open(io.BytesIO(m)).convert("RGB"))
+                inside += 1
+                inside_bad += not np.array_equal(capi.jpeg_decode(m), want)
+        assert between > 100 and inside > 100
+        assert inside_bad <= 0.03 * inside, (inside_bad, inside)
+    finally:
+        ImageFile.LOAD_TRUNCATED_IMAGES = prev
 
 
 def test_device_entropy_parse_routes_and_host_finish():
