@@ -297,8 +297,9 @@ int mxd_jpeg_info(const uint8_t* data, size_t size, int32_t* width, int32_t* hei
 
 /* Decodes into dst: height rows of width*3 bytes, dst_stride bytes apart (any
  * host memory, e.g. pinned staging from mxd_malloc_pinned).  width/height
- * must be mxd_jpeg_info's.  Baseline, extended and progressive frames,
- * Huffman or arithmetic coded (SOF0-2, SOF9-10).  MXD_ERR_INVALID with
+ * must be mxd_jpeg_info's.  Baseline, extended, progressive and (8-bit)
+ * lossless frames, Huffman or arithmetic coded (SOF0-3, SOF9-10).
+ * MXD_ERR_INVALID with
  * libjpeg's message on corrupt or unsupported data. */
 int mxd_jpeg_decode(const uint8_t* data, size_t size, uint8_t* dst, int64_t dst_stride, int32_t width,
                     int32_t height);

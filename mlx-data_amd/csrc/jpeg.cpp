@@ -844,7 +844,8 @@ struct Decoder {
   size_t pos = 0;
   int width = 0, height = 0, ncomp = 0;
   bool progressive = false, baseline_seen = false;
-  bool arith = false;  // arithmetic-coded frame (SOF9 / SOF10)
+  bool arith = false;     // arithmetic-coded frame (SOF9 / SOF10)
+  bool lossless = false;  // lossless Huffman-coded frame (SOF3): samples, no DCT
   // DAC conditioning (T.81 F.1.4.4.1.4 / F.1.4.4.2.1), defaults L = 0, U = 1, Kx = 5
   uint8_t arith_dc_l[16], arith_dc_u[16], arith_ac_k[16];
   bool jfif = false, adobe = false;
@@ -979,7 +980,8 @@ struct Decoder {
     if (len != 8 + 3 * ncomp) fail("Bogus marker length");
     progressive = marker == 0xC2 || marker == 0xCA;
     arith = marker == 0xC9 || marker == 0xCA;
-    if ((progressive || arith) && device_entropy) throw NotDevice{};
+    lossless = marker == 0xC3;
+    if ((progressive || arith || lossless) && device_entropy) throw NotDevice{};
     for (int i = 0; i < ncomp; i++) {
       Component& c = comp[i];
       c.id = u8();
@@ -1004,10 +1006,10 @@ struct Decoder {
       c.bh = mcuy * c.v;
       c.off = total;
       total += (int64_t)c.bw * c.bh * 64;
-      if (!progressive && !defer && !device_entropy) c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
+      if ((lossless || (!progressive && !defer)) && !device_entropy) c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
     }
-    coef_total = total;
-    if ((progressive || defer) && !device_entropy) coefbuf.assign((size_t)total, 0);
+    coef_total = lossless ? 0 : total;
+    if ((progressive || defer) && !lossless && !device_entropy) coefbuf.assign((size_t)total, 0);
     for (auto& row : coef_bits)
       for (int& b : row) b = -1;
     frame = true;
@@ -1079,6 +1081,16 @@ struct Decoder {
     any_scan = true;
     for (int i = 0; i < ns; i++) sc[i]->dc_pred = 0;
     eobrun = 0;
+    if (lossless) {
+      // jdlossls.c start_pass: a predictor 1..7, Se 0, Ah 0, Al below the precision
+      if (ss < 1 || ss > 7 || se != 0 || ah != 0 || al >= 8) fail("Invalid progressive parameters");
+      Bits bits;
+      bits.p = data + pos;
+      bits.end = data + size;
+      decode_scan_lossless(bits, sc, ns, ss, al);
+      pos = (size_t)(bits.p - data);
+      return;
+    }
     if (arith) {
       if (progressive && ah != 0 && al != ah - 1) fail("Invalid progressive parameters");
       Arith ar;
@@ -1317,6 +1329,100 @@ struct Decoder {
     });
   }
 
+  // One lossless scan (T.81 H.1.2; jdlossls.c / jdlhuff.c / jdpred.c): per
+  // sample a Huffman-coded difference category (DC tables, 0..16; 16 is
+  // 32768 with no extra bits) and value, added modulo 2^16 to the
+  // prediction from the component's reconstructed neighbours -- Ra (left), Rb
+  // (above), Rc (above left) through predictor `psv` -- except on the first
+  // line of the scan or of a restart interval (Ra; its first sample
+  // 2^(P - Pt - 1)) and in the first column (Rb).  The output sample is the
+  // reconstruction << Pt (8 bits).  An MCU holds h x v samples of each
+  // component (interleaved) or one sample (one component).
+  void decode_scan_lossless(Bits& bits, Component** sc, int ns, int psv, int pt) {
+    for (int i = 0; i < ns; i++) {
+      const Huff& h = dc[sc[i]->dc_tbl];
+      if (!h.present) fail("Huffman table was not defined");
+      for (int k = 0; k < h.nvals; k++)
+        if (h.vals[k] > 16) fail("Bogus Huffman table definition");
+      sc[i]->coded = true;
+    }
+    const int mx_n = ns == 1 ? sc[0]->dw : (width + max_h - 1) / max_h;
+    const int my_n = ns == 1 ? sc[0]->dh : (height + max_v - 1) / max_v;
+    // reconstructed samples per component, on its MCU-padded sample grid
+    std::vector<int32_t> rec[4];
+    int gw[4], row0[4];
+    for (int i = 0; i < ns; i++) {
+      const int hh = ns == 1 ? 1 : sc[i]->h, vv = ns == 1 ? 1 : sc[i]->v;
+      gw[i] = mx_n * hh;
+      rec[i].assign((size_t)gw[i] * my_n * vv, 0);
+      row0[i] = 0;
+    }
+    const int init = 1 << (8 - pt - 1);
+    auto predict = [&](int i, int x, int y) -> int {
+      const int32_t* r = rec[i].data();
+      const int w = gw[i];
+      if (y == row0[i]) return x == 0 ? init : r[(size_t)y * w + x - 1];
+      if (x == 0) return r[(size_t)(y - 1) * w];
+      const int ra = r[(size_t)y * w + x - 1], rb = r[(size_t)(y - 1) * w + x], rc = r[(size_t)(y - 1) * w + x - 1];
+      switch (psv) {
+        case 1: return ra;
+        case 2: return rb;
+        case 3: return rc;
+        case 4: return ra + rb - rc;
+        case 5: return ra + ((rb - rc) >> 1);
+        case 6: return rb + ((ra - rc) >> 1);
+        default: return (ra + rb) >> 1;
+      }
+    };
+    // Data running out (jdlhuff.c decode_mcus, per MCU row): the row it runs
+    // out in decodes on from zero bits; every later row (until a restart
+    // marker clears the flag) gets zero differences with the predictor
+    // restarted, i.e. uniform grey.
+    int restarts_left = restart_interval, next_rst = 0;
+    bool skip = false;
+    for (int my = 0; my < my_n; my++)
+      for (int mx = 0; mx < mx_n; mx++) {
+        if (restart_interval) {
+          if (restarts_left == 0) {
+            bits.restart(next_rst);
+            next_rst = (next_rst + 1) & 7;
+            for (int i = 0; i < ns; i++) row0[i] = my * (ns == 1 ? 1 : sc[i]->v);
+            restarts_left = restart_interval;
+          }
+          restarts_left--;
+        }
+        if (mx == 0) {
+          skip = bits.insufficient;
+          if (skip)
+            for (int i = 0; i < ns; i++) row0[i] = my * (ns == 1 ? 1 : sc[i]->v);
+        }
+        for (int i = 0; i < ns; i++) {
+          const int hh = ns == 1 ? 1 : sc[i]->h, vv = ns == 1 ? 1 : sc[i]->v;
+          const Huff& h = dc[sc[i]->dc_tbl];
+          for (int v = 0; v < vv; v++)
+            for (int u = 0; u < hh; u++) {
+              const int x = mx * hh + u, y = my * vv + v;
+              int diff = 0;
+              if (!skip) {
+                const int s = bits.decode(h);
+                if (s == 16) diff = -32768;
+                else if (s) diff = extend(bits.get(s), s);
+              }
+              rec[i][(size_t)y * gw[i] + x] = (predict(i, x, y) + diff) & 0xFFFF;
+            }
+        }
+      }
+    // the samples (<< Pt, 8 bits) into the planes the output reads
+    for (int i = 0; i < ns; i++) {
+      Component& c = *sc[i];
+      const int rows = (int)(rec[i].size() / gw[i]);
+      const int stride = c.bw * 8;
+      for (int y = 0; y < rows && y < c.bh * 8; y++)
+        for (int x = 0; x < gw[i] && x < stride; x++)
+          c.plane[(size_t)y * stride + x] = (uint8_t)(rec[i][(size_t)y * gw[i] + x] << pt);
+    }
+  }
+
   // One arithmetic-coded scan (T.81 F.2.4 / G.2: jdarith.c's decode_mcu,
   // decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine).  The
   // statistics of the scan's tables, the DC predictions and contexts start
@@ -1463,11 +1569,12 @@ struct Decoder {
         case 0xC0:
         case 0xC1:
         case 0xC2:
+        case 0xC3:
         case 0xC9:
         case 0xCA:
           read_sof(m);
           break;
-        case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xCB: case 0xCD: case 0xCE:
+        case 0xC5: case 0xC6: case 0xC7: case 0xCB: case 0xCD: case 0xCE:
         case 0xCF:
           unsupported_sof(m);
         case 0xC4:
@@ -1713,7 +1820,7 @@ struct Decoder {
   // carried, as the in-place planes keep).
   const uint8_t* samples(int i, std::vector<uint8_t>& store) const {
     const Component& c = comp[i];
-    if (!progressive && !defer) return c.plane.data();
+    if (lossless || (!progressive && !defer)) return c.plane.data();
     store.assign((size_t)c.bw * 8 * c.bh * 8, 0);
     if (c.coded)
       for (int by = 0; by < c.bh; by++)
@@ -1769,6 +1876,12 @@ struct Decoder {
 // jdapimin.c default_decompress_parms
 int Decoder::color_space() const {
   if (ncomp == 1) return 0;
+  if (lossless) {
+    // libjpeg-turbo: no colour conversion in lossless mode -- RGB / CMYK
+    // unless a JFIF or Adobe marker declares YCbCr / YCCK, which it refuses
+    if (jfif || (adobe && adobe_transform != 0)) fail("Unsupported color conversion request");
+    return ncomp == 3 ? 2 : ncomp == 4 ? 3 : -1;
+  }
   if (ncomp == 3) {
     if (jfif) return 1;
     if (adobe) return adobe_transform == 0 ? 2 : 1;
@@ -2096,7 +2209,7 @@ CoefInfo coef_info(const Coefs* c) {
     p.off = k.off;
     p.q = k.q;
   }
-  r.device_ok = d.ncomp == 1 || (d.ncomp == 3 && (r.color_space == 1 || r.color_space == 2));
+  r.device_ok = !d.lossless && (d.ncomp == 1 || (d.ncomp == 3 && (r.color_space == 1 || r.color_space == 2)));
   return r;
 }
 
@@ -2132,13 +2245,13 @@ bool info(const uint8_t* data, size_t size, int* width, int* height, int* compon
     for (;;) {
       const int m = d.next_marker();
       if (m < 0) fail("Premature end of JPEG file");
-      if (m == 0xC0 || m == 0xC1 || m == 0xC2 || m == 0xC9 || m == 0xCA) {
+      if (m == 0xC0 || m == 0xC1 || m == 0xC2 || m == 0xC3 || m == 0xC9 || m == 0xCA) {
         d.read_sof(m);
         break;
       }
       if (m == 0xD9 || m == 0xDA) fail("Invalid JPEG file structure: SOS before SOF");
       if (m >= 0xD0 && m <= 0xD7) continue;
-      if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xC9 && m != 0xCA && m != 0xCC) unsupported_sof(m);
+      if (m >= 0xC5 && m <= 0xCF && m != 0xC8 && m != 0xC9 && m != 0xCA && m != 0xCC) unsupported_sof(m);
       d.skip_segment();
     }
     *width = d.width;

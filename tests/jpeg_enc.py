@@ -151,3 +151,60 @@ def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0, coefs=None):
         out += s
     out += b"\xff\xd9"
     return bytes(out)
+
+
+# Lossless difference categories 0..16, all 5-bit codes.
+LOSSLESS_DC = ([0, 0, 0, 0, 17, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0], list(range(17)))
+
+
+def encode_lossless(pixels, psv=1, pt=0, restart_rows=0, table=LOSSLESS_DC, markers=b""):
+    """pixels: (H, W) or (H, W, 3) uint8 -> lossless Huffman-coded JPEG
+    (SOF3, 8-bit, 1x1 sampling, one interleaved scan; T.81 H.1): predictor
+    `psv` (1..7), point transform `pt`, a restart interval of `restart_rows`
+    rows of MCUs, `markers` (e.g. an APP segment) after SOI."""
+    a = pixels if pixels.ndim == 3 else pixels[:, :, None]
+    h, w, nc = a.shape
+    x = a.astype(np.int64) >> pt
+    codes = _codes(table)
+    segs, bits = [], _Bits()
+    r0 = 0
+    for r in range(h):
+        if restart_rows and r and r % restart_rows == 0:
+            bits.flush()
+            segs.append(bytes(bits.out))
+            bits, r0 = _Bits(), r
+        for c in range(w):
+            for i in range(nc):
+                if r == r0:
+                    px = (1 << (8 - pt - 1)) if c == 0 else x[r, c - 1, i]
+                elif c == 0:
+                    px = x[r - 1, c, i]
+                else:
+                    ra, rb, rc = x[r, c - 1, i], x[r - 1, c, i], x[r - 1, c - 1, i]
+                    px = {1: ra, 2: rb, 3: rc, 4: ra + rb - rc, 5: ra + ((rb - rc) >> 1), 6: rb + ((ra - rc) >> 1),
+                          7: (ra + rb) >> 1}[psv]
+                d = (int(x[r, c, i]) - int(px)) & 0xFFFF
+                d = d - 0x10000 if d >= 0x8000 else d
+                s = 0 if d == 0 else 16 if d == -32768 else abs(d).bit_length()
+                bits.put(*codes[s])
+                if 0 < s < 16:
+                    bits.put(d if d > 0 else d - 1, s)
+    bits.flush()
+    segs.append(bytes(bits.out))
+
+    def seg(marker, body):
+        return bytes([0xFF, marker]) + (len(body) + 2).to_bytes(2, "big") + body
+
+    out = bytearray(b"\xff\xd8") + markers
+    out += seg(0xC3, bytes([8]) + h.to_bytes(2, "big") + w.to_bytes(2, "big") + bytes([nc]) +
+               b"".join(bytes([i + 1, 0x11, 0]) for i in range(nc)))
+    out += seg(0xC4, bytes([0x00]) + bytes(table[0]) + bytes(table[1]))
+    if restart_rows:
+        out += seg(0xDD, (restart_rows * w).to_bytes(2, "big"))
+    out += seg(0xDA, bytes([nc]) + b"".join(bytes([i + 1, 0x00]) for i in range(nc)) + bytes([psv, 0, pt]))
+    for i, s in enumerate(segs):
+        if i:
+            out += bytes([0xFF, 0xD0 + (i - 1) % 8])
+        out += s
+    out += b"\xff\xd9"
+    return bytes(out)

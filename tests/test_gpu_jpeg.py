@@ -220,6 +220,15 @@ def test_pipeline_device_decode_on_off(variant, tmp_path):
         p = tmp_path / f"{i}.jpg"
         if i % 9 == 4:  # grey
             p.write_bytes(_encode(_smooth(rng, h, w, 1), quality=88))
+        elif i % 9 == 7:  # arithmetic-coded (tests/jpeg_arith_enc.py): host entropy decode
+            import jpeg_arith_enc as A
+
+            img = _smooth(rng, h // 4 + 8, w // 4 + 8)
+            p.write_bytes(A.encode_progressive(img, q=3) if i % 2 else A.encode(img, q=3, restart_mcus=5))
+        elif i % 9 == 8:  # lossless (SOF3): the host finishes it
+            import jpeg_enc as J
+
+            p.write_bytes(J.encode_lossless(_smooth(rng, h // 4 + 8, w // 4 + 8), psv=1 + i % 7))
         else:
             p.write_bytes(_encode(_smooth(rng, h, w), quality=88, subsampling=i % 3, progressive=i % 4 == 1))
         samples.append(dict(image=str(p).encode(), label=i))

@@ -267,6 +267,54 @@ def test_truncated_progressive_arithmetic_files_match_pillow():
         ImageFile.LOAD_TRUNCATED_IMAGES = prev
 
 
+def test_lossless_files_match_pillow():
+    """Lossless Huffman-coded JPEGs (SOF3, 8-bit; libjpeg-turbo 3.x, the
+    reference's build, decodes them): tests/jpeg_enc.py encode_lossless writes
+    every predictor 1..7, point transforms, restart intervals, grey and
+    three-component files; the decoder gives Pillow's bytes on each, on files
+    cut inside their data (the row the data runs out in decodes on from zero
+    bits, later rows are uniform grey, as jdlhuff.c does), and refuses a
+    JFIF-marked (YCbCr) one as libjpeg-turbo does (no colour conversion in
+    lossless mode).  Such files finish on the host on the device route."""
+    Image = pytest.importorskip("PIL.Image")
+    ImageFile = pytest.importorskip("PIL.ImageFile")
+    import jpeg_enc as J
+
+    rng = np.random.default_rng(5)
+    cut_files = []
+    for t in range(28):
+        h, w = int(rng.integers(1, 60)), int(rng.integers(1, 60))
+        grey = t % 3 == 2
+        if t % 2:
+            img = rng.integers(0, 256, (h, w) if grey else (h, w, 3), dtype=np.uint8)
+        else:
+            img = _smooth(rng, h, w, 1 if grey else 3)
+            img = img[:, :, 0] if grey else img
+        kw = dict(psv=1 + t % 7, pt=int(rng.integers(1, 4)) if t % 4 == 0 else 0,
+                  restart_rows=int(rng.integers(1, 4)) if t % 5 == 0 and h > 1 else 0)
+        data = J.encode_lossless(img, **kw)
+        pil = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+        assert np.array_equal(capi.jpeg_decode(data), pil), (t, kw)
+        if t % 2 == 0 and h >= 8:
+            cut_files.append(data)
+        if t < 3:
+            c = capi.JpegCoefs(data, device_entropy=True)
+            assert not c.entropy_pending and not c.device_ok and np.array_equal(c.finish(), pil)
+    prev = ImageFile.LOAD_TRUNCATED_IMAGES
+    ImageFile.LOAD_TRUNCATED_IMAGES = True
+    try:
+        for data in cut_files:
+            sos = data.index(b"\xff\xda")
+            for cut in rng.integers(sos + 14, len(data) - 2, 4):
+                m = data[:int(cut)] + b"\xff\xd9"
+                assert np.array_equal(capi.jpeg_decode(m), np.asarray(Image.open(io.BytesIO(m)).convert("RGB")))
+    finally:
+        ImageFile.LOAD_TRUNCATED_IMAGES = prev
+    jfif = _segment(0xE0, b"JFIF\x00\x01\x01\x00\x00\x01\x00\x01\x00\x00")
+    with pytest.raises(capi.MxdError, match="Unsupported color conversion request"):
+        capi.jpeg_decode(J.encode_lossless(_smooth(rng, 9, 9, 3), markers=jfif))
+
+
 def test_device_entropy_parse_routes_and_host_finish():
     """mxd_jpeg_coefs_parse(device_entropy=1) (CPU half of the device entropy
     decode, csrc/jpeghuff.h): baseline one-scan files are only parsed

@@ -56,9 +56,9 @@ def _segment(marker, payload):
 def test_errors_from_the_entropy_decode():
     with pytest.raises(capi.MxdError, match="Not a JPEG file"):
         capi.JpegCoefs(b"\x89PNG\r\n\x1a\n" + bytes(32))
-    sof3 = b"\xff\xd8" + _segment(0xC3, bytes([8, 0, 8, 0, 8, 1, 1, 0x11, 0]))  # lossless: not decoded
-    with pytest.raises(capi.MxdError, match="Unsupported JPEG process: SOF type 0xc3"):
-        capi.JpegCoefs(sof3)
+    sof7 = b"\xff\xd8" + _segment(0xC7, bytes([8, 0, 8, 0, 8, 1, 1, 0x11, 0]))  # differential lossless
+    with pytest.raises(capi.MxdError, match="Unsupported JPEG process: SOF type 0xc7"):
+        capi.JpegCoefs(sof7)
     sof9 = b"\xff\xd8" + _segment(0xC9, bytes([8, 0, 8, 0, 8, 1, 1, 0x11, 0]))  # arithmetic, no scan
     with pytest.raises(capi.MxdError, match="Premature end of JPEG file"):
         capi.JpegCoefs(sof9)
