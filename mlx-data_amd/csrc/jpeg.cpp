@@ -144,7 +144,7 @@ void build_huff(Huff& h, const uint8_t* bits /* [17], bits[0] unused */, const u
         f = FastAC{0, (uint8_t)(r == 15 ? 15 : kEob), (uint8_t)l};
       } else if (l + sz <= kLook) {
         const int v = (i >> (kLook - l - sz)) & ((1 << sz) - 1);
-        f = FastAC{(int16_t)(v < (1 << (sz - 1)) ? v + ((-1) << sz) + 1 : v), (uint8_t)r, (uint8_t)(l + sz)};
+        f = FastAC{(int16_t)(v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v), (uint8_t)r, (uint8_t)(l + sz)};
       }
     }
     h.fac[i] = f;
@@ -182,7 +182,7 @@ void cached_huff(Huff& h, const uint8_t* bits, const uint8_t* vals, int nvals) {
   e.h = h;
 }
 
-inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v + ((-1) << s) + 1 : v; }
+inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
 // Entropy-coded segment reader: stops at a marker; bits needed past it are
 // zeros and set `insufficient` (jdhuff.c jpeg_fill_bit_buffer).
@@ -397,7 +397,7 @@ struct Bits {
     buf = 0;
     cnt = 0;
     for (;;) {
-      const int m = p < end && at_marker ? p[1] : find_marker();
+      const int m = at_marker && p + 1 < end ? p[1] : find_marker();
       at_marker = true;
       int action;
       if (m < 0xC0) action = 2;
@@ -1123,7 +1123,8 @@ struct Decoder {
     if (scans++ > 0 || progressive || ns != ncomp || (ncomp != 1 && ncomp != 3)) throw NotDevice{};
     int bpm = 0;
     for (int i = 0; i < ns; i++) {
-      if (!dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present) fail("Huffman table was not defined");
+      if (sc[i]->dc_tbl > 3 || sc[i]->ac_tbl > 3 || !dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present)
+          fail("Huffman table was not defined");
       check_dc_table(dc[sc[i]->dc_tbl]);
       std::memcpy(sc[i]->q, quant(*sc[i]), sizeof sc[i]->q);  // latched at the scan
       sc[i]->coded = true;
@@ -1217,7 +1218,8 @@ struct Decoder {
   void decode_scan(Bits& bits, Component** sc, int ns, int ss, int se, int ah, int al) {
     if (!progressive) {
       for (int i = 0; i < ns; i++) {
-        if (!dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present) fail("Huffman table was not defined");
+        if (sc[i]->dc_tbl > 3 || sc[i]->ac_tbl > 3 || !dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present)
+          fail("Huffman table was not defined");
         check_dc_table(dc[sc[i]->dc_tbl]);
         std::memcpy(sc[i]->q, quant(*sc[i]), sizeof sc[i]->q);  // latched at the scan
         sc[i]->coded = true;
@@ -1236,7 +1238,7 @@ struct Decoder {
     if (ss == 0) {
       if (ah == 0)
         for (int i = 0; i < ns; i++)
-          if (!dc[sc[i]->dc_tbl].present) fail("Huffman table was not defined");
+          if (sc[i]->dc_tbl > 3 || !dc[sc[i]->dc_tbl].present) fail("Huffman table was not defined");
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
         int16_t* blk = cblk(c, bx, by);
         if (ah == 0) {
@@ -1253,7 +1255,7 @@ struct Decoder {
       return;
     }
     Component& c0 = *sc[0];
-    if (!ac[c0.ac_tbl].present) fail("Huffman table was not defined");
+    if (c0.ac_tbl > 3 || !ac[c0.ac_tbl].present) fail("Huffman table was not defined");
     const Huff& ha = ac[c0.ac_tbl];
     if (ah == 0) {
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
@@ -1340,8 +1342,8 @@ struct Decoder {
   // component (interleaved) or one sample (one component).
   void decode_scan_lossless(Bits& bits, Component** sc, int ns, int psv, int pt) {
     for (int i = 0; i < ns; i++) {
+      if (sc[i]->dc_tbl > 3 || !dc[sc[i]->dc_tbl].present) fail("Huffman table was not defined");
       const Huff& h = dc[sc[i]->dc_tbl];
-      if (!h.present) fail("Huffman table was not defined");
       for (int k = 0; k < h.nvals; k++)
         if (h.vals[k] > 16) fail("Bogus Huffman table definition");
       sc[i]->coded = true;
