@@ -418,8 +418,10 @@ int64_t rgb_pitch(int32_t w) { return (((int64_t)w * 3 + 63) & ~(int64_t)63) + 6
 
 // Lays out the chunk [first, end) of a JPEG batch whose coefficients are staged
 // at in_off[i]; the tables follow at `tables_at`.
+// foot[i]: image i's resize footprint (x0, x1, y0, y1, inclusive, in image
+// pixels; the whole image when unknown).
 void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const std::vector<int64_t>& in_off,
-                int64_t tables_at, JpegChunk* out) {
+                int64_t tables_at, const std::vector<std::array<int32_t, 4>>& foot, JpegChunk* out) {
   JpegChunk& c = *out;
   c = JpegChunk();
   auto up = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
@@ -572,6 +574,16 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       p.qtab = (int32_t)c.qtabs.size();
       p.coded = cp.coded ? 1 : 0;
       p.zigzag = pend_rel[i - first] >= 0 ? 1 : 0;  // decoded by jpeg_huff: zig-zag order
+      {
+        // the footprint on this component's sample grid, one sample wider on
+        // each side (fancy upsampling reads a neighbour), in whole blocks
+        const int hx = info.max_h / cp.h, vx = info.max_v / cp.v;
+        const std::array<int32_t, 4>& f = foot[i];
+        p.bx0 = std::max(0, (f[0] / hx - 1) / 8);
+        p.bx1 = std::min(cp.bw, (f[1] / hx + 1) / 8 + 1);
+        p.by0 = std::max(0, (f[2] / vx - 1) / 8);
+        p.by1 = std::min(cp.bh, (f[3] / vx + 1) / 8 + 1);
+      }
       c.qtabs.insert(c.qtabs.end(), cp.q, cp.q + 64);
       c.planes.push_back(p);
       m.plane[k] = c.samples;
@@ -589,7 +601,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
                   : h2 && v2 && cp.dw > 2 ? mxd::kUpH2V2
                                           : mxd::kUpRep;
       c.samples += up((int64_t)cp.bw * 8 * cp.bh * 8, 256);
-      c.nblocks += ((int64_t)cp.bw * cp.bh + 63) & ~(int64_t)63;  // jpeg_idct: a wave stays in one plane
+      // jpeg_idct's threads: the plane's needed rectangle, padded to a wave
+      // (a wave stays in one plane)
+      c.nblocks += ((int64_t)std::max(0, p.bx1 - p.bx0) * std::max(0, p.by1 - p.by0) + 63) & ~(int64_t)63;
     }
     m.out = c.mid_bytes;  // relative to rgb_off, fixed below
     c.mid_bytes += up((int64_t)m.pitch * m.height, 256);
@@ -791,8 +805,19 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     int64_t dev_in_bytes = 0;
     if (jpeg) {
       std::vector<int64_t> off(n, 0);
-      for (int32_t i = chunks[k].first; i < chunks[k].second; i++) off[i] = st[i].in_off;
-      jpeg_chunk(jpeg, chunks[k].first, chunks[k].second, off, in_bytes, &jc);
+      std::vector<std::array<int32_t, 4>> foot(n);
+      for (int32_t i = chunks[k].first; i < chunks[k].second; i++) {
+        off[i] = st[i].in_off;
+        // the resize's source footprint in the window, as image pixels
+        const mxd_image& im = images[i];
+        const DevTable *xt = nullptr, *yt = nullptr;
+        int32_t xl = 0, xh = im.src_w - 1, yl = 0, yh = im.src_h - 1;
+        if (tables().get(device, im.src_w, im.resize_w, &xt) == MXD_OK &&
+            tables().get(device, im.src_h, im.resize_h, &yt) == MXD_OK)
+          footprint(*xt, *yt, im, &xl, &xh, &yl, &yh);
+        foot[i] = {jpeg[i].win_x + xl, jpeg[i].win_x + xh, jpeg[i].win_y + yl, jpeg[i].win_y + yh};
+      }
+      jpeg_chunk(jpeg, chunks[k].first, chunks[k].second, off, in_bytes, foot, &jc);
       in_bytes = in_staged = jc.end;  // coefficients, then the chunk's tables, in one copy
       dev_in_bytes = jc.dev_end;      // + the device-decoded coefficients
       if (int rc = grow_device(&sl.dev_mid, &sl.dev_mid_cap, jc.mid_bytes)) return rc;

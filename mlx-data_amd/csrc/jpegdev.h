@@ -21,6 +21,10 @@ struct JpegPlaneDev {
   int32_t qtab;         // first entry of its quantisation table (uint16 elements)
   int32_t coded;        // 0: no scan carried it, its samples are 0
   int32_t zigzag;       // 1: each block's coefficients in zig-zag order (the device entropy decode's), 0: natural
+  // the blocks the resize can read ([bx0, bx1) x [by0, by1): its source
+  // footprint, widened by the upsampling's reach): jpeg_idct's threads cover
+  // this rectangle only (first_block numbers them), the rest is never read
+  int32_t bx0, bx1, by0, by1;
   int32_t pad;
 };
 

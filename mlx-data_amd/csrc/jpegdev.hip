@@ -147,8 +147,10 @@ __global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coe
   lo = __builtin_amdgcn_readfirstlane(lo);
   const JpegPlaneDev p = planes[lo];
   const i64 b = g - p.first_block;
-  if (b >= (i64)p.bw * p.bh) return;  // the plane's padding
-  const int by = (int)((uint32_t)b / (uint32_t)p.bw), bx = (int)b - by * p.bw;  // (a plane holds < 2^31 blocks)
+  const int rw = p.bx1 - p.bx0;
+  if (b >= (i64)rw * (p.by1 - p.by0)) return;  // the plane's padding
+  const int ry = (int)((uint32_t)b / (uint32_t)rw);  // (a plane holds < 2^31 blocks)
+  const int by = p.by0 + ry, bx = p.bx0 + ((int)b - ry * rw);
   const int stride = p.bw * 8;
   uint8_t* out = samples + p.out + (i64)by * 8 * stride + bx * 8;
   if (!p.coded) {
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256) void jpeg_idct(const int16_t* __restrict__ coe
   }
   int32_t d[64];
   {
-    const int4* cp = reinterpret_cast<const int4*>(coef + p.coef + b * 64);
+    const int4* cp = reinterpret_cast<const int4*>(coef + p.coef + ((i64)by * p.bw + bx) * 64);
     const uint16_t* q = qt + p.qtab;  // uniform: scalar loads
     const bool zz = p.zigzag != 0;
     int32_t cw[64];  // the block's 64 stored coefficients, in storage order
