@@ -17,7 +17,8 @@ import pytest
 
 from mlx_data_amd import capi
 
-GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "jpeg.npz"))
+GOLD_PATH = os.path.join(os.path.dirname(__file__), "golden", "jpeg.npz")
+GOLD = np.load(GOLD_PATH)
 CASES = sorted(k[:-4] for k in GOLD.files if k.endswith("_jpg"))
 
 
@@ -433,3 +434,34 @@ def test_deep_huffman_tables_host_decode_matches_pillow():
         c = capi.JpegCoefs(d, device_entropy=True)
         assert c.entropy_pending
         assert np.array_equal(c.finish(), want)
+
+
+def test_scalar_byte_scans_match_avx512(tmp_path):
+    """The marker parse's and unstuff's AVX-512 forms (chosen when the CPU
+    has them) and the scalar ones (MXD_NO_AVX512=1, in a child process) give
+    the same segment split and the same decodes: every fixture, through the
+    markers-only parse and the host finish, digested in both processes."""
+    import subprocess
+    import sys
+
+    script = (
+        "import hashlib, sys, numpy as np\n"
+        "sys.path.insert(0, %r)\n"
+        "from mlx_data_amd import capi\n"
+        "g = np.load(%r)\n"
+        "h = hashlib.sha256()\n"
+        "for k in sorted(f for f in g.files if f.endswith('_jpg')):\n"
+        "    d = g[k].tobytes()\n"
+        "    try:\n"
+        "        c = capi.JpegCoefs(d, device_entropy=True)\n"
+        "        h.update(bytes([c.entropy_pending])); h.update(c.finish().tobytes())\n"
+        "    except capi.MxdError as e:\n"
+        "        h.update(str(e).encode())\n"
+        "print(h.hexdigest())\n") % (os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "mlx-data_amd"), GOLD_PATH)
+    out = {}
+    for flag in ("0", "1"):
+        env = dict(os.environ, MXD_NO_AVX512=flag)
+        out[flag] = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True,
+                                   check=True, timeout=300).stdout.strip()
+    assert out["0"] == out["1"] and len(out["0"]) == 64
