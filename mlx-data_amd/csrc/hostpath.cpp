@@ -818,7 +818,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         foot[i] = {jpeg[i].win_x + xl, jpeg[i].win_x + xh, jpeg[i].win_y + yl, jpeg[i].win_y + yh};
       }
       jpeg_chunk(jpeg, chunks[k].first, chunks[k].second, off, in_bytes, foot, &jc);
-      in_bytes = in_staged = jc.end;  // coefficients, then the chunk's tables, in one copy
+      // coefficients, then the chunk's tables, then the entropy decode's
+      // publication records and launch control (zeros), in one copy
+      in_bytes = in_staged = jc.hjobs.empty() ? jc.end : jc.coef_off;
       dev_in_bytes = jc.dev_end;      // + the device-decoded coefficients
       if (int rc = grow_device(&sl.dev_mid, &sl.dev_mid_cap, jc.mid_bytes)) return rc;
     }
@@ -946,15 +948,27 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     if (jpeg) {  // (after the fused-source decisions above)
       std::memcpy(sl.pin_in + jc.imgs_off, jc.imgs.data(), jc.imgs.size() * sizeof(mxd::JpegImgDev));
       std::memcpy(sl.pin_in + jc.ycc_off, jc.ycc.data(), jc.ycc.size() * sizeof(mxd::YccDev));
+      if (!jc.hjobs.empty()) {
+        // the entropy decode's publication records and launch control, staged
+        // zero (one copy with the rest instead of a fill), the error word's
+        // page-locked host twin in the control record
+        if (!sl.huff_err) {
+          MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.huff_err), 64, hipHostMallocDefault));
+          *sl.huff_err = 0;
+        }
+        std::memset(sl.pin_in + jc.pub_off, 0, (size_t)(jc.coef_off - jc.pub_off));
+        mxd::HuffCtlDev ctl{};
+        ctl.err_host = const_cast<int32_t*>(reinterpret_cast<const int32_t*>(host_device_ptr(sl.huff_err)));
+        std::memcpy(sl.pin_in + jc.pub_off + jc.hjobs.size() * sizeof(mxd::HuffPubDev), &ctl, sizeof ctl);
+      }
     }
     if (in_staged > 0 && !pin_in_dev)
       MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
     if (jpeg) {
       if (!jc.hjobs.empty()) {
-        // the jobs' publication records and the ticket start zero (the
-        // decode zeroes every block it starts, and the blocks insufficient
-        // data leaves undecoded)
-        MXD_HIP(hipMemsetAsync(sl.dev_in + jc.pub_off, 0, (size_t)(jc.coef_off - jc.pub_off), sl.stream));
+        // (the publication records and the ticket came zero with the staged
+        // copy; the decode zeroes every block it starts, and the blocks
+        // insufficient data leaves undecoded)
         auto* pub = reinterpret_cast<mxd::HuffPubDev*>(sl.dev_in + jc.pub_off);
         auto* ctl = reinterpret_cast<mxd::HuffCtlDev*>(pub + jc.hjobs.size());
         if (mxd::launch_jpeg_huff(reinterpret_cast<const uint32_t*>(sl.dev_in + jc.words_off),
@@ -965,8 +979,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                   (int32_t)jc.hjobs.size(), jc.huff_threads, jc.huff_lds, pub, ctl,
                                   reinterpret_cast<int16_t*>(sl.dev_in), jc.huff_search, sl.stream))
           return fail(MXD_ERR_DEVICE, std::string("jpeg entropy decode launch: ") + hipGetErrorString(hipGetLastError()));
-        if (!sl.huff_err) MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.huff_err), 64, hipHostMallocDefault));
-        MXD_HIP(hipMemcpyAsync(sl.huff_err, &ctl->error, sizeof(int32_t), hipMemcpyDeviceToHost, sl.stream));
+        // (a job that gives up sets *sl.huff_err itself: no copy back)
 #ifdef MXD_HUFF_STAMPS
         // diagnostic build: the jobs' phase stamps (jpeghuff.hip) appended to $MXD_HUFF_STAMPS_FILE
         if (const char* path = getenv("MXD_HUFF_STAMPS_FILE")) {

@@ -159,12 +159,15 @@ struct HuffPubDev {
 constexpr uint64_t kHuffValid = (uint64_t)1 << 63;
 static_assert(sizeof(HuffPubDev) == 8 * kHuffPubWords, "HuffPubDev layout");
 
-// Launch control (device memory, zeroed before the launch): the job ticket
-// counter and an error word (1: a job gave up waiting for its predecessor).
+// Launch control (device memory, staged zero before the launch): the job
+// ticket counter, an error word (1: a job gave up waiting for its
+// predecessor) and, when not null, a page-locked host word the error is
+// also written to (the host reads it after the launch with no copy back).
 struct HuffCtlDev {
   int32_t ticket, error;
-  int32_t pad[2];
+  int32_t* err_host;
 };
+static_assert(sizeof(HuffCtlDev) == 16, "HuffCtlDev layout");
 
 // Shortest subsequence (bits): a decoder that starts mid-stream needs some
 // symbols to fall into step.

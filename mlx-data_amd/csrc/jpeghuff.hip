@@ -584,6 +584,7 @@ __device__ uint64_t wait_pub(const HuffPubDev* p, int i, HuffCtlDev* ctl) {
     __builtin_amdgcn_s_sleep(8);
   }
   __hip_atomic_store(&ctl->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (int32_t* h = ctl->err_host) __hip_atomic_store(h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return 0;
 }
 
