@@ -377,6 +377,95 @@ struct Bits {
     cnt = n;
   }
 
+  // One block of a progressive AC refinement scan (jdphuff.c
+  // decode_mcu_AC_refine: new coefficients of +-p1 / m1 placed after r
+  // still-zero ones, a correction bit for every nonzero one passed, EOB runs
+  // correcting the rest of the band) with the bit buffer in registers as in
+  // block_seq: refilled to >= 57 bits whenever fewer than 32 remain (a symbol,
+  // its sign and an EOB run's bits take <= 30), per correction bit when
+  // empty.  Bits past the segment's end are zeros and mark the data
+  // insufficient, as consume() does.
+  void block_refine(const Huff& ha, int16_t* blk, int ss, int se, int p1, int m1, int& eobrun) {
+    uint64_t b = buf;
+    int n = cnt;
+    auto refill = [&]() {
+      if (!at_marker && end - p >= 8 && n >= 0) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        const uint64_t x = ~w;
+        if (((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) == 0) {
+          const int k = (64 - n) >> 3;
+          b |= (__builtin_bswap64(w) >> (64 - 8 * k)) << (64 - n - 8 * k);
+          p += k;
+          n += 8 * k;
+          return;
+        }
+      }
+      if (n < 0) return;  // past the end: only zeros follow
+      buf = b;
+      cnt = n;
+      fill();
+      b = buf;
+      n = cnt;
+    };
+    auto bit = [&]() {
+      if (n < 1) refill();
+      const int v = (int)(b >> 63);
+      b <<= 1;
+      n -= 1;
+      return v;
+    };
+    auto fix = [&](int16_t& co) {
+      if (bit() && (co & p1) == 0) co = (int16_t)(co >= 0 ? co + p1 : co + m1);
+    };
+    int k = ss;
+    if (eobrun == 0) {
+      for (; k <= se; k++) {
+        if (n < 32) refill();
+        const int rs = decode_slow(ha, b, n);
+        int r = rs >> 4;
+        int s = rs & 15;
+        if (s) {
+          s = (int)(b >> 63) ? p1 : m1;
+          b <<= 1;
+          n -= 1;
+        } else if (r != 15) {
+          eobrun = 1 << r;
+          if (r) {
+            eobrun += (int)(b >> (64 - r));
+            b <<= r;
+            n -= r;
+          }
+          break;
+        }
+        do {
+          int16_t& co = blk[kNatural[k]];
+          if (co != 0) {
+            fix(co);
+          } else {
+            if (--r < 0) break;
+          }
+          k++;
+        } while (k <= se);
+        if (s) blk[kNatural[k]] = (int16_t)s;
+      }
+    }
+    if (eobrun > 0) {
+      for (; k <= se; k++) {
+        int16_t& co = blk[kNatural[k]];
+        if (co != 0) fix(co);
+      }
+      eobrun--;
+    }
+    if (n < 0) {
+      insufficient = true;
+      n = 0;
+      b = 0;
+    }
+    buf = b;
+    cnt = n;
+  }
+
   // Next marker from p: p at its 0xFF, returns its code; 0xD9 (EOI) at the
   // end of the data, as libjpeg's sources insert a fake EOI there.
   int find_marker() {
@@ -1283,8 +1372,10 @@ struct Decoder {
     // progressive (jdphuff.c)
     if (ss == 0) {
       if (ah == 0)
-        for (int i = 0; i < ns; i++)
+        for (int i = 0; i < ns; i++) {
           if (sc[i]->dc_tbl > 3 || !dc[sc[i]->dc_tbl].present) fail("Huffman table was not defined");
+          check_dc_table(dc[sc[i]->dc_tbl]);  // (jdphuff.c derives DC tables with the DC check too)
+        }
       for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
         int16_t* blk = cblk(c, bx, by);
         if (ah == 0) {
@@ -1340,40 +1431,7 @@ struct Decoder {
     }
     const int p1 = 1 << al, m1 = -1 * (1 << al);
     for_each_mcu(bits, sc, ns, [&](Component& c, int bx, int by, bool skip) {
-      if (skip) return;
-      int16_t* blk = cblk(c, bx, by);
-      int k = ss;
-      if (eobrun == 0) {
-        for (; k <= se; k++) {
-          const int rs = bits.decode(ha);
-          int r = rs >> 4;
-          int s = rs & 15;
-          if (s) {
-            s = bits.get(1) ? p1 : m1;
-          } else if (r != 15) {
-            eobrun = 1 << r;
-            if (r) eobrun += bits.get(r);
-            break;
-          }
-          do {
-            int16_t& co = blk[kNatural[k]];
-            if (co != 0) {
-              if (bits.get(1) && (co & p1) == 0) co = (int16_t)(co >= 0 ? co + p1 : co + m1);
-            } else {
-              if (--r < 0) break;
-            }
-            k++;
-          } while (k <= se);
-          if (s) blk[kNatural[k]] = (int16_t)s;
-        }
-      }
-      if (eobrun > 0) {
-        for (; k <= se; k++) {
-          int16_t& co = blk[kNatural[k]];
-          if (co != 0 && bits.get(1) && (co & p1) == 0) co = (int16_t)(co >= 0 ? co + p1 : co + m1);
-        }
-        eobrun--;
-      }
+      if (!skip) bits.block_refine(ha, cblk(c, bx, by), ss, se, p1, m1, eobrun);
     });
   }
 
