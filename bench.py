@@ -789,14 +789,30 @@ def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False):
             bp.run_surface(files, batch, workers, variant, 2 * workers)  # warm: contexts, pools, tables
             repeat = 4 * workers
             for _ in range(4):
+                capi.host_stats(reset=True)
+                bp._pipe_stats(True)
                 n, dt = bp.run_surface(files, batch, workers, variant, repeat)
                 if dt >= min_s:
                     break
                 repeat = int(np.ceil(repeat * 1.2 * min_s / max(dt, 1e-3)))
-            return round(n / dt, 1), n, round(dt, 3)
+            return round(n / dt, 1), n, round(dt, 3), host_split(n, dt)
 
-        value, n, dt = leg("device")
-        hostent, n2, dt2 = leg("device_hostent")
+        def host_split(n, dt):
+            """Where the worker threads' time went in the timed run (microseconds
+            per image, summed over threads): what bounds the pipeline."""
+            hs = capi.host_stats(reset=True)
+            ps = bp._pipe_stats(True)
+            fetch, merge = ps[2] / n / 1e3, ps[3] / n / 1e3  # batch_fetch includes load_image + transforms
+            busy = (fetch + merge) * n * 1e-6 / (workers * dt)
+            wait = hs["wait_s"] / n * 1e6
+            return {"load_image_us": round(ps[0] / n / 1e3, 2), "fetch_us": round(fetch, 2),
+                    "batch_call_us": round(merge, 2), "device_wait_us": round(wait, 2),
+                    "worker_busy": round(busy, 3), "device_wait_share": round(wait / max(fetch + merge, 1e-9), 3),
+                    "bound": ("host workers" if busy >= 0.85 and wait < 0.5 * (fetch + merge - wait)
+                              else "device calls" if busy >= 0.85 else "feed (workers idle)")}
+
+        value, n, dt, split = leg("device")
+        hostent, n2, dt2, split2 = leg("device_hostent")
         cpu = None
         if not no_cpu:
             sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -824,6 +840,7 @@ def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False):
     return {"value": value, "unit": "images/s", "images": n, "seconds": dt, "workers": workers, "cores": cores,
             "batch": batch, "files": len(files), "file_mb": round(mb, 2),
             "host_entropy_value": hostent, "host_entropy_seconds": dt2, "cpu_restatement": cpu,
+            "host_split": split, "host_entropy_split": split2,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "devices": dx.devices(),
             "device_entropy": dx.device_entropy(), "abi": capi.lib().mxd_abi_version(),
             "chain": "files -> load_image -> image_resize_smallest_side(256) -> image_center_crop(224, 224) -> "
