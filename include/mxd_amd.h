@@ -340,7 +340,9 @@ int mxd_jpeg_coefs_parse(const uint8_t* data, size_t size, int32_t device_entrop
  * or is not a regular file -- read it and call mxd_jpeg_coefs_parse for the
  * reference's exact message. */
 int mxd_jpeg_coefs_load(const char* path, int32_t device_entropy, mxd_jpeg_coefs** out);
-/* *pending = 1 when the coefficients will come from the device entropy decode. */
+/* *pending = 1 when the coefficients will come from the device entropy decode
+ * of a sequential file's one scan, 2 when from the device decode of every scan
+ * of a progressive file (round 5), 0 when the host decoded them. */
 int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending);
 int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs);
 

@@ -959,6 +959,15 @@ size_t scan_to_marker_avx512(const uint8_t* data, size_t p, size_t size, int64_t
   return scan_to_marker_scalar(data, p, size, dropped);
 }
 
+static_assert(kLook == kProgLook, "ProgTabDev copies Huff::look");
+
+// Progressive files' scans decoded on the device (jpeghuff.h jpeg_prog);
+// MXD_NO_DEVICE_PROGRESSIVE=1 leaves them to the host entropy decode (A/Bs).
+bool device_progressive() {
+  static const bool on = !(std::getenv("MXD_NO_DEVICE_PROGRESSIVE") && std::atoi(std::getenv("MXD_NO_DEVICE_PROGRESSIVE")) == 1);
+  return on;
+}
+
 bool have_avx512_bytes() {  // (MXD_NO_AVX512=1: the scalar forms, for A/Bs)
   static const bool ok = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vbmi2") &&
                          !(std::getenv("MXD_NO_AVX512") && std::atoi(std::getenv("MXD_NO_AVX512")) == 1);
@@ -1013,6 +1022,13 @@ struct Decoder {
   bool device_entropy = false;
   bool pending = false;
   int scans = 0;
+  // device_entropy on a progressive Huffman file: every scan recorded
+  // (record_prog_scan), its tables snapshotted; pending once parse_held finds
+  // the progression complete (jpeghuff.h jpeg_prog)
+  bool prog_dev = false;
+  bool eoi = false;
+  std::vector<ProgScan> prog;
+  std::vector<ProgTabDev> prog_tabs;
   std::vector<int64_t> seg_begin, seg_end;
   std::vector<int64_t> seg_bytes;  // unstuffed bytes of each segment (what unstuff() writes)
   int scan_ns = 0;
@@ -1127,7 +1143,9 @@ struct Decoder {
     progressive = marker == 0xC2 || marker == 0xCA;
     arith = marker == 0xC9 || marker == 0xCA;
     lossless = marker == 0xC3;
-    if ((progressive || arith || lossless) && device_entropy) throw NotDevice{};
+    if ((arith || lossless) && device_entropy) throw NotDevice{};
+    prog_dev = progressive && device_entropy;
+    if (prog_dev && !device_progressive()) throw NotDevice{};
     for (int i = 0; i < ncomp; i++) {
       Component& c = comp[i];
       c.id = u8();
@@ -1206,7 +1224,8 @@ struct Decoder {
     const int ss = u8(), se = u8(), a = u8();
     const int ah = a >> 4, al = a & 15;
     if (device_entropy) {
-      record_scan(sc, ns);
+      if (prog_dev) record_prog_scan(sc, ns, ss, se, ah, al);
+      else record_scan(sc, ns);
       any_scan = true;
       return;
     }
@@ -1280,8 +1299,17 @@ struct Decoder {
     if (bpm > 10) throw NotDevice{};  // libjpeg: "Sampling factors too large for interleaved scan"
     scan_ns = ns;
     scan_mcus = ns == 1 ? (int64_t)sc[0]->wib * sc[0]->hib : (int64_t)mcux * mcuy;
-    // segments: split the entropy-coded data at its restart markers
-    const int64_t nseg = restart_interval ? (scan_mcus + restart_interval - 1) / restart_interval : 1;
+    record_segments(scan_mcus);
+    pending = true;
+  }
+
+  // The entropy-coded data from pos split at its restart markers (RST0..7 in
+  // sequence, one per interval) into seg_begin / seg_end / seg_bytes; pos
+  // left at the marker after the data.  Data not ending at a marker, or
+  // markers out of sequence: NotDevice.
+  void record_segments(int64_t mcus) {
+    const int64_t nseg = restart_interval ? (mcus + restart_interval - 1) / restart_interval : 1;
+    const int64_t seg0 = (int64_t)seg_begin.size();
     size_t p = pos, b = pos;
     int next_rst = 0;
     int64_t dropped = 0;  // bytes unstuff() drops: the 0x00 of 0xFF 0x00, fill 0xFF bytes
@@ -1297,7 +1325,7 @@ struct Decoder {
       seg_bytes.push_back((int64_t)(p - b) - dropped);
       dropped = 0;
       if (m >= 0xD0 && m <= 0xD7) {
-        if (!restart_interval || m != 0xD0 + next_rst || (int64_t)seg_begin.size() >= nseg) throw NotDevice{};
+        if (!restart_interval || m != 0xD0 + next_rst || (int64_t)seg_begin.size() - seg0 >= nseg) throw NotDevice{};
         next_rst = (next_rst + 1) & 7;
         p += 2;
         b = p;
@@ -1305,9 +1333,66 @@ struct Decoder {
       }
       break;  // the marker after the scan
     }
-    if ((int64_t)seg_begin.size() != nseg) throw NotDevice{};
+    if ((int64_t)seg_begin.size() - seg0 != nseg) throw NotDevice{};
     pos = seg_end.back();  // marker parsing resumes at the marker
-    pending = true;
+  }
+
+  // One scan of a progressive file for the device (jpeghuff.h jpeg_prog):
+  // parameters, progression status (as read_sos keeps it for the host
+  // decode), table snapshots and segments.  Whatever the host decoder would
+  // refuse, or that the device decode does not cover, throws NotDevice (the
+  // host decodes the file and reports its own error).
+  void record_prog_scan(Component** sc, int ns, int ss, int se, int ah, int al) {
+    if (ncomp != 1 && ncomp != 3) throw NotDevice{};
+    if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || ah > 13 || al > 13) throw NotDevice{};
+    input_scans++;
+    for (int i = 0; i < ns; i++) {
+      const int ci = (int)(sc[i] - comp);
+      for (int k = std::min(ss, 1); k <= std::min(std::max(se, 9), 9); k++)
+        coef_bits[4 + ci][k] = input_scans > 1 ? coef_bits[ci][k] : 0;
+      for (int k = ss; k <= std::min(se, 9); k++) coef_bits[ci][k] = al;
+    }
+    ProgScan r{};
+    r.ns = ns;
+    r.ss = ss;
+    r.se = se;
+    r.ah = ah;
+    r.al = al;
+    r.rst = restart_interval;
+    int bpm = 0;
+    for (int i = 0; i < 4; i++) r.tab[i] = -1;
+    auto snapshot = [&](const Huff& h) {
+      ProgTabDev t;
+      std::memset(&t, 0, sizeof t);
+      std::memcpy(t.look, h.look, sizeof t.look);
+      std::memcpy(t.maxcode, h.maxcode, sizeof t.maxcode);
+      std::memcpy(t.valoffset, h.valoffset, sizeof t.valoffset);
+      std::memcpy(t.vals, h.vals, (size_t)h.nvals);
+      for (size_t q = 0; q < prog_tabs.size(); q++)
+        if (std::memcmp(&prog_tabs[q], &t, sizeof t) == 0) return (int)q;
+      prog_tabs.push_back(t);
+      return (int)prog_tabs.size() - 1;
+    };
+    for (int i = 0; i < ns; i++) {
+      Component& c = *sc[i];
+      r.comp[i] = (int)(sc[i] - comp);
+      bpm += ns == 1 ? 1 : c.h * c.v;
+      if (ss == 0 && ah == 0) {
+        if (c.dc_tbl > 3 || !dc[c.dc_tbl].present) throw NotDevice{};
+        for (int q = 0; q < dc[c.dc_tbl].nvals; q++)
+          if (dc[c.dc_tbl].vals[q] > 15) throw NotDevice{};  // check_dc_table's failure
+        r.tab[i] = snapshot(dc[c.dc_tbl]);
+      } else if (ss > 0) {
+        if (c.ac_tbl > 3 || !ac[c.ac_tbl].present) throw NotDevice{};
+        r.tab[i] = snapshot(ac[c.ac_tbl]);
+      }
+    }
+    if (bpm > 10) throw NotDevice{};
+    r.mcus = ns == 1 ? (int64_t)sc[0]->wib * sc[0]->hib : (int64_t)mcux * mcuy;
+    r.seg0 = (int)seg_begin.size();
+    record_segments(r.mcus);
+    r.nseg = (int)seg_begin.size() - r.seg0;
+    prog.push_back(r);
   }
 
   // R: Bits or Arith (restart(), insufficient)
@@ -1706,6 +1791,7 @@ struct Decoder {
           break;
         case 0xD9:
           if (!any_scan) fail("Premature end of JPEG file");
+          eoi = true;
           return;
         case 0xD8:
           fail("Invalid JPEG file structure: two SOI markers");
@@ -1782,11 +1868,14 @@ struct Decoder {
   // (they may change between scans); sequential scans latched theirs.
   void finalize() {
     if (!progressive) return;
+    finalize_quant();
+    smooth_blocks();
+  }
+  void finalize_quant() {
     for (int i = 0; i < ncomp; i++) {
       std::memcpy(comp[i].q, quant(comp[i]), sizeof comp[i].q);
       comp[i].coded = true;
     }
-    smooth_blocks();
   }
 
   // ---- block smoothing (libjpeg's do_block_smoothing, on by default and
@@ -2052,6 +2141,17 @@ Coefs* parse_held(std::unique_ptr<Coefs> c, std::string* err) {
     d.parse();
     if (!d.frame) fail("Invalid JPEG file structure: missing SOF marker");
     if (d.color_space() < 0) fail("unhandled format");
+    if (d.prog_dev) {
+      // every scan recorded: on the device when the file ends at EOI and its
+      // progression leaves the first ten coefficients of every component
+      // exact (libjpeg's block smoothing has nothing to estimate: smoothing_ok)
+      if (!d.eoi || d.prog.empty()) throw NotDevice{};
+      for (int ci = 0; ci < d.ncomp; ci++)
+        for (int k = 0; k < 10; k++)
+          if (d.coef_bits[ci][k] != 0) throw NotDevice{};
+      d.finalize_quant();
+      d.pending = true;
+    }
     if (!d.pending) throw NotDevice{};  // no scan
     // decode_coefs' check: output() reaches it exactly for non-integral factors
     if (d.ncomp > 1)
@@ -2331,6 +2431,7 @@ CoefInfo coef_info(const Coefs* c) {
   r.coef = d.pending ? nullptr : d.coefbuf.data();
   r.coef_count = d.coef_total;
   r.entropy_pending = d.pending;
+  r.entropy_progressive = d.pending && d.prog_dev;
   for (int i = 0; i < d.ncomp; i++) {
     const Component& k = d.comp[i];
     CoefPlane& p = r.comp[i];
@@ -2345,6 +2446,26 @@ CoefInfo coef_info(const Coefs* c) {
     p.q = k.q;
   }
   r.device_ok = !d.lossless && (d.ncomp == 1 || (d.ncomp == 3 && (r.color_space == 1 || r.color_space == 2)));
+  return r;
+}
+
+ProgScans prog_scans(const Coefs* c) {
+  const Decoder& d = c->d;
+  ProgScans r{};
+  r.nscan = (int)d.prog.size();
+  r.scans = d.prog.data();
+  r.ntab = (int)d.prog_tabs.size();
+  r.tabs = d.prog_tabs.data();
+  r.seg_begin = d.seg_begin.data();
+  r.seg_end = d.seg_end.data();
+  r.seg_bytes = d.seg_bytes.data();
+  r.data = d.data;
+  r.mcux = d.mcux;
+  r.mcuy = d.mcuy;
+  for (int i = 0; i < d.ncomp && i < 4; i++) {
+    r.wib[i] = d.comp[i].wib;
+    r.hib[i] = d.comp[i].hib;
+  }
   return r;
 }
 

@@ -924,6 +924,439 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     decode_job<GlobalReader, SEARCH>(words + job.word0, sh, tab, seg, nsub, coef, pub, ctl);
 }
 
+
+// ---------------------------------------------------------------- progressive
+// jpeg_prog (jpeghuff.h): one wave per image; the scans of a phase run on
+// the lanes of their components, each scan in the host decoder's order of
+// operations (jpeg.cpp Decoder::decode_scan, jdphuff.c), so the coefficients
+// are the host's bit for bit.
+
+// jpeg_natural_order with libjpeg's 16 extra entries (a corrupt run past 63
+// lands on 63)
+__device__ constexpr int8_t kNat80[80] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
+    6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
+    39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+struct ProgShared {
+  ProgTabDev tab[kProgSlots];
+  int8_t nat[80];
+};
+
+// One symbol (jpeg.cpp Bits::decode: the 9-bit lookahead, then the canonical
+// search; no code within 16 bits: 16 bits consumed, symbol 0)
+__device__ __forceinline__ int prog_sym(GlobalReader& r, const ProgTabDev& t) {
+  const uint32_t w = r.win();
+  const int e = t.look[w >> (32 - kProgLook)];
+  if (e) {
+    r.advance(e >> 8);
+    return e & 0xff;
+  }
+  int l = kProgLook + 1;
+  while (l <= 16 && (int32_t)(w >> (32 - l)) > t.maxcode[l]) l++;
+  if (l > 16) {
+    r.advance(16);
+    return 0;
+  }
+  r.advance(l);
+  return t.vals[((int32_t)(w >> (32 - l)) + t.valoffset[l]) & 0xff];
+}
+__device__ __forceinline__ int prog_get(GlobalReader& r, int n) {  // n <= 16
+  const int v = n ? (int)(r.win() >> (32 - n)) : 0;
+  r.advance(n);
+  return v;
+}
+__device__ __forceinline__ int prog_extend(int v, int s) { return s ? extend_nz((uint32_t)v, s) : 0; }
+
+// Per-component fields picked by selects (a dynamic index into the image
+// record would put it in scratch memory, a load per use)
+template <class T>
+__device__ __forceinline__ T pick3(const T (&a)[3], int c) {
+  return c == 0 ? a[0] : c == 1 ? a[1] : a[2];
+}
+struct CompGeom {
+  int64_t base;  // first coefficient of the component's plane
+  int32_t bw, wib, h, v;
+  __device__ __forceinline__ CompGeom(const ProgImgDev& im, int c)
+      : base(im.coef + pick3(im.plane, c)), bw(pick3(im.bw, c)), wib(pick3(im.wib, c)), h(pick3(im.h, c)),
+        v(pick3(im.v, c)) {}
+};
+
+struct ProgSeg {
+  GlobalReader r;
+  int32_t bits;
+  __device__ __forceinline__ void open(const uint32_t* words, const ProgSegDev& sg) {
+    bits = sg.bits;
+    r.init(words, (int32_t)sg.word, (bits + 31) >> 5, 0);
+    r.seek(0);
+  }
+  // libjpeg's insufficient data: some symbol read past the segment's end
+  __device__ __forceinline__ bool out() const { return r.pos() > bits; }
+};
+
+// DC first (Ah = 0), any number of components, on one lane.
+__device__ void prog_dc_first(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+                              const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
+  const int ns = sc.ns;
+  const CompGeom g0(im, sc.comp[0]), g1(im, sc.comp[1]), g2(im, sc.comp[2]);
+  const int t0 = sc.slot[0], t1 = sc.slot[1], t2 = sc.slot[2];
+  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
+  const int mult = 1 << sc.al;
+  const int64_t row = ns == 1 ? g0.wib : im.mcux;
+  for (int s = 0; s < sc.nseg; s++) {
+    ProgSeg g;
+    g.open(words, segs[sc.seg0 + s]);
+    int pred0 = 0, pred1 = 0, pred2 = 0;
+    const int64_t m0 = (int64_t)s * per, m1 = min(sc.mcus, m0 + per);
+    int64_t my = m0 / row, mx = m0 - my * row;
+    for (int64_t m = m0; m < m1; m++) {
+      if (g.out()) break;
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        if (i >= ns) break;
+        const CompGeom& cg = i == 0 ? g0 : i == 1 ? g1 : g2;
+        const ProgTabDev& t = sh.tab[i == 0 ? t0 : i == 1 ? t1 : t2];
+        int& pred = i == 0 ? pred0 : i == 1 ? pred1 : pred2;
+        const int nh = ns > 1 ? cg.h : 1, nv = ns > 1 ? cg.v : 1;
+        for (int y = 0; y < nv; y++)
+          for (int x = 0; x < nh; x++) {
+            const int z = prog_sym(g.r, t);
+            pred += prog_extend(prog_get(g.r, z), z);
+            const int64_t bx = mx * nh + x, by = my * nv + y;
+            coef[cg.base + (by * cg.bw + bx) * 64] = (int16_t)(pred * mult);
+          }
+      }
+      if (++mx == row) {
+        mx = 0;
+        my++;
+      }
+    }
+  }
+}
+
+// AC first (Ah = 0) of one component.
+__device__ void prog_ac_first(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+                              const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
+  const CompGeom cg(im, sc.comp[0]);
+  const ProgTabDev& t = sh.tab[sc.slot[0]];
+  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
+  const int ss = sc.ss, se = sc.se, al = sc.al;
+  for (int s = 0; s < sc.nseg; s++) {
+    ProgSeg g;
+    g.open(words, segs[sc.seg0 + s]);
+    int eobrun = 0;
+    const int64_t m0 = (int64_t)s * per, m1 = min(sc.mcus, m0 + per);
+    int64_t by = m0 / cg.wib, bx = m0 - by * cg.wib;
+    for (int64_t m = m0; m < m1; m++) {
+      if (g.out()) break;
+      int16_t* blk = coef + cg.base + (by * cg.bw + bx) * 64;
+      if (++bx == cg.wib) {
+        bx = 0;
+        by++;
+      }
+      if (eobrun > 0) {
+        eobrun--;
+        continue;
+      }
+      for (int k = ss; k <= se; k++) {
+        const int rs = prog_sym(g.r, t);
+        const int r = rs >> 4, z = rs & 15;
+        if (z) {
+          k += r;
+          blk[sh.nat[k]] = (int16_t)(prog_extend(prog_get(g.r, z), z) * (1 << al));
+        } else if (r == 15) {
+          k += 15;
+        } else {
+          eobrun = 1 << r;
+          if (r) eobrun += prog_get(g.r, r);
+          eobrun--;
+          break;
+        }
+      }
+    }
+  }
+}
+
+// AC refinement (Ah != 0) of one component (jpeg.cpp Bits::block_refine),
+// in three steps so that the lane decoding the symbols never waits on
+// coefficient memory:
+//   1. (every lane) each block's nonzero history as a 64-bit mask in zigzag
+//      order into the image's aux area, its delta record zeroed;
+//   2. (the scan's lane) the symbols: per symbol the zero-history positions
+//      it skips and the position of a new coefficient found with mask
+//      arithmetic, the correction bits of the nonzero positions passed read
+//      together (they come in position order: one bit per nonzero position
+//      of the band, EOB runs included) -- per block a delta record (the
+//      correction bits packed, new positions, their signs);
+//   3. (every lane) the deltas applied to the blocks (jpeg.cpp's fix(): a
+//      correction bit adds p1 / m1 to a coefficient whose Al bit is clear).
+__device__ __forceinline__ uint64_t zz_band(int a, int b) {  // zigzag positions a..b (empty when a > b)
+  return a > b ? 0ull : (~0ull >> (63 - b)) & (~0ull << a);
+}
+struct ProgAux {  // the image's aux area: per block of the image (coefficient block index)
+  uint64_t* mask;   // nonzero history
+  uint64_t* delta;  // 3 per block: correction bits (first read at the top), new positions, their signs
+  __device__ __forceinline__ ProgAux(const ProgImgDev& im, int16_t* coef) {
+    mask = reinterpret_cast<uint64_t*>(coef + im.aux);
+    delta = mask + im.coef_count / 64;
+  }
+};
+
+__device__ void prog_refine_masks(const ProgImgDev& im, const ProgScanDev& sc, int16_t* coef) {
+  const CompGeom cg(im, sc.comp[0]);
+  const ProgAux ax(im, coef);
+  const int64_t g0 = (cg.base - im.coef) / 64, n = (int64_t)cg.wib * pick3(im.hib, sc.comp[0]);
+  for (int64_t q = threadIdx.x; q < n; q += 64) {
+    const int64_t by = q / cg.wib, bx = q - by * cg.wib, g = g0 + by * cg.bw + bx;
+    const uint4* p = reinterpret_cast<const uint4*>(coef + cg.base + (by * cg.bw + bx) * 64);
+    uint32_t w[32];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint4 v = p[u];
+      w[4 * u] = v.x;
+      w[4 * u + 1] = v.y;
+      w[4 * u + 2] = v.z;
+      w[4 * u + 3] = v.w;
+    }
+    uint64_t nz = 0;
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+      const int nn = kNat80[k];
+      nz |= (uint64_t)(((w[nn >> 1] >> ((nn & 1) * 16)) & 0xffffu) != 0) << k;
+    }
+    ax.mask[g] = nz;
+    ax.delta[3 * g] = ax.delta[3 * g + 1] = ax.delta[3 * g + 2] = 0;
+  }
+}
+
+__device__ __forceinline__ void prog_bits(GlobalReader& r, int c, uint64_t& acc) {  // c <= 63 bits appended
+  while (c > 0) {
+    const int n = min(c, 16);
+    acc = (acc << n) | (uint64_t)prog_get(r, n);
+    c -= n;
+  }
+}
+
+__device__ void prog_ac_refine(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+                               const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
+  const CompGeom cg(im, sc.comp[0]);
+  const ProgAux ax(im, coef);
+  const ProgTabDev& t = sh.tab[sc.slot[0]];
+  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
+  const int ss = sc.ss, se = sc.se;
+  const int64_t g0 = (cg.base - im.coef) / 64;
+  const int wib = cg.wib;
+  constexpr int kAhead = 8;  // masks loaded ahead of the block being decoded
+  for (int s = 0; s < sc.nseg; s++) {
+    ProgSeg g;
+    g.open(words, segs[sc.seg0 + s]);
+    int eobrun = 0;
+    const int64_t m0 = (int64_t)s * per, m1b = min(sc.mcus, m0 + per);
+    int64_t by = m0 / wib, bx = m0 - by * wib;
+    // a ring of the next kAhead blocks' masks (block m + u at ring[u])
+    uint64_t ring[kAhead];
+    int64_t fy = by, fx = bx;  // the block the next ring load reads
+    auto fetch = [&](int64_t m) -> uint64_t {
+      uint64_t v = 0;
+      if (m < m1b) v = ax.mask[g0 + fy * cg.bw + fx];
+      if (++fx == wib) {
+        fx = 0;
+        fy++;
+      }
+      return v;
+    };
+#pragma unroll
+    for (int u = 0; u < kAhead; u++) ring[u] = fetch(m0 + u);
+    for (int64_t m = m0; m < m1b; m++) {
+      if (g.out()) break;
+      const uint64_t nz = ring[0];
+#pragma unroll
+      for (int u = 0; u + 1 < kAhead; u++) ring[u] = ring[u + 1];
+      ring[kAhead - 1] = fetch(m + kAhead);
+      const int64_t gb = g0 + by * cg.bw + bx;
+      if (++bx == wib) {
+        bx = 0;
+        by++;
+      }
+      uint64_t acc = 0, newm = 0, negm = 0;
+      int k = ss;
+      if (eobrun == 0) {
+        for (; k <= se; k++) {
+          const int rs = prog_sym(g.r, t);
+          const int r = rs >> 4, z = rs & 15;
+          int neg = 0;
+          if (z) {
+            neg = prog_get(g.r, 1) ? 0 : 1;
+          } else if (r != 15) {
+            eobrun = 1 << r;
+            if (r) eobrun += prog_get(g.r, r);
+            break;
+          }
+          // past r zero-history positions to the next one (the new
+          // coefficient's place), or to the band's end
+          uint64_t zeros = ~nz & zz_band(k, se);
+          for (int q = 0; q < r && zeros; q++) zeros &= zeros - 1;
+          const int p = zeros ? __builtin_ctzll(zeros) : se + 1;
+          prog_bits(g.r, __builtin_popcountll(nz & zz_band(k, p - 1)), acc);
+          k = p;
+          if (z) {  // k <= 64; 64 is libjpeg's extra entry: natural position 63
+            const uint64_t bit = (uint64_t)1 << min(k, 63);
+            newm |= bit;
+            negm = neg ? negm | bit : negm & ~bit;
+          }
+        }
+      }
+      if (eobrun > 0) {
+        prog_bits(g.r, __builtin_popcountll(nz & zz_band(k, se)), acc);
+        eobrun--;
+      }
+      if (acc | newm) {
+        ax.delta[3 * gb] = acc;
+        ax.delta[3 * gb + 1] = newm;
+        ax.delta[3 * gb + 2] = negm;
+      }
+    }
+  }
+}
+
+__device__ void prog_refine_apply(const ProgImgDev& im, const ProgScanDev& sc, int16_t* coef) {
+  const CompGeom cg(im, sc.comp[0]);
+  const ProgAux ax(im, coef);
+  const int64_t g0 = (cg.base - im.coef) / 64, n = (int64_t)cg.wib * pick3(im.hib, sc.comp[0]);
+  const int p1 = 1 << sc.al, m1 = -(1 << sc.al);
+  const uint64_t band = zz_band(sc.ss, sc.se);
+  for (int64_t q = threadIdx.x; q < n; q += 64) {
+    const int64_t by = q / cg.wib, bx = q - by * cg.wib, g = g0 + by * cg.bw + bx;
+    const uint64_t acc = ax.delta[3 * g], newm = ax.delta[3 * g + 1], negm = ax.delta[3 * g + 2];
+    if (!(acc | newm)) continue;
+    const uint64_t nzb = ax.mask[g] & band;
+    int rem = __builtin_popcountll(nzb);
+    uint4* p = reinterpret_cast<uint4*>(coef + cg.base + (by * cg.bw + bx) * 64);
+    uint32_t w[32];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint4 v = p[u];
+      w[4 * u] = v.x;
+      w[4 * u + 1] = v.y;
+      w[4 * u + 2] = v.z;
+      w[4 * u + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+      const int nn = kNat80[k];
+      const int sh16 = (nn & 1) * 16;
+      int v = (int16_t)(w[nn >> 1] >> sh16);
+      if ((nzb >> k) & 1) {
+        rem--;
+        if (((acc >> rem) & 1) && (v & p1) == 0) v = v >= 0 ? v + p1 : v + m1;
+      }
+      if ((newm >> k) & 1) v = ((negm >> k) & 1) ? m1 : p1;
+      w[nn >> 1] = (w[nn >> 1] & ~(0xffffu << sh16)) | (((uint32_t)v & 0xffffu) << sh16);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) p[u] = make_uint4(w[4 * u], w[4 * u + 1], w[4 * u + 2], w[4 * u + 3]);
+  }
+}
+
+// DC refinement: one bit per block in scan order, no Huffman code; spread
+// over the wave's lanes (bits past a segment's end are zeros: no change).
+__device__ void prog_dc_refine(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+                               const ProgSegDev* segs, int16_t* coef) {
+  const int ns = sc.ns;
+  const CompGeom g0(im, sc.comp[0]), g1(im, sc.comp[1]), g2(im, sc.comp[2]);
+  const int n0 = ns > 1 ? g0.h * g0.v : 1, n1 = ns > 1 ? g1.h * g1.v : 0, n2 = ns > 2 ? g2.h * g2.v : 0;
+  const int bpm = n0 + n1 + n2;
+  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
+  const int16_t p1 = (int16_t)(1 << sc.al);
+  const uint8_t* bytes = reinterpret_cast<const uint8_t*>(words);
+  for (int s = 0; s < sc.nseg; s++) {
+    const ProgSegDev sg = segs[sc.seg0 + s];
+    const int64_t m0 = (int64_t)s * per, nm = min(sc.mcus, m0 + per) - m0;
+    const int64_t nb = min(nm * bpm, (int64_t)sg.bits);  // blocks with a bit of data
+    for (int64_t q = threadIdx.x; q < nb; q += 64) {
+      if (!((bytes[sg.word * 4 + (q >> 3)] >> (7 - (q & 7))) & 1)) continue;
+      const int64_t m = m0 + q / bpm;
+      int j = (int)(q % bpm);
+      const int i = j < n0 ? 0 : j < n0 + n1 ? 1 : 2;
+      j -= i == 0 ? 0 : i == 1 ? n0 : n0 + n1;
+      const CompGeom& cg = i == 0 ? g0 : i == 1 ? g1 : g2;
+      int64_t bx, by;
+      if (ns == 1) {
+        by = m / cg.wib;
+        bx = m - by * cg.wib;
+      } else {
+        const int64_t my = m / im.mcux, mx = m - my * im.mcux;
+        const int dy = j / cg.h;
+        bx = mx * cg.h + (j - dy * cg.h);
+        by = my * cg.v + dy;
+      }
+      int16_t* d = coef + cg.base + (by * cg.bw + bx) * 64;
+      *d = (int16_t)(*d | p1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ words, const ProgTabDev* __restrict__ tabs,
+                                                const ProgImgDev* __restrict__ imgs,
+                                                const ProgScanDev* __restrict__ scans,
+                                                const ProgSegDev* __restrict__ segs, int16_t* __restrict__ coef) {
+  __shared__ ProgShared sh;
+  const ProgImgDev im = imgs[blockIdx.x];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 80; i += 64) sh.nat[i] = kNat80[i];
+  {
+    uint4* z = reinterpret_cast<uint4*>(coef + im.coef);
+    const int64_t n16 = im.coef_count / 8;
+    for (int64_t i = lane; i < n16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  for (int ph = 0; ph < im.nphase; ph++) {
+    // the phase's tables into their slots, refinement masks (the whole wave)
+    bool refine_all = false, refine_ac = false;
+    for (int si = im.scan0; si < im.scan0 + im.nscan; si++) {
+      const ProgScanDev& sc = scans[si];
+      if (sc.phase != ph) continue;
+      refine_all = refine_all || sc.lane < 0;
+      for (int j = 0; j < sc.ns; j++) {
+        if (sc.tab[j] < 0) continue;
+        const uint4* from = reinterpret_cast<const uint4*>(tabs + sc.tab[j]);
+        uint4* to = reinterpret_cast<uint4*>(&sh.tab[sc.slot[j]]);
+        for (int q = lane; q < (int)(sizeof(ProgTabDev) / 16); q += 64) to[q] = from[q];
+      }
+      if (sc.ss > 0 && sc.ah != 0) {
+        prog_refine_masks(im, sc, coef);
+        refine_ac = true;
+      }
+    }
+    __syncthreads();
+    if (refine_all) {
+      for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
+        if (scans[si].phase == ph) prog_dc_refine(words, im, scans[si], segs, coef);
+    } else {
+      // each component's scans of the phase on its lane, in file order
+      int steps = 0;
+      for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
+        if (scans[si].phase == ph) steps = max(steps, scans[si].step + 1);
+      for (int st = 0; st < steps; st++) {
+        int mine = -1;
+        for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
+          if (scans[si].phase == ph && scans[si].lane == lane && scans[si].step == st) mine = si;
+        if (mine < 0) continue;
+        const ProgScanDev sc = scans[mine];
+        if (sc.ss == 0) prog_dc_first(words, im, sc, segs, sh, coef);
+        else if (sc.ah == 0) prog_ac_first(words, im, sc, segs, sh, coef);
+        else prog_ac_refine(words, im, sc, segs, sh, coef);
+      }
+    }
+    __syncthreads();
+    if (refine_ac) {
+      for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
+        if (scans[si].phase == ph && scans[si].ss > 0 && scans[si].ah != 0) prog_refine_apply(im, scans[si], coef);
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace
 
 int64_t jpeg_huff_lds_budget() { return 160 * 1024 - (int64_t)sizeof(Shared) - 1024; }
@@ -959,6 +1392,14 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
   if (set_rc[dev]) return -1;
   hipLaunchKernelGGL(k, dim3(njobs), dim3(threads), (size_t)lds_bytes, reinterpret_cast<hipStream_t>(stream), words,
                      tables, imgs, segs, jobs, pub, ctl, coef);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_jpeg_prog(const uint32_t* words, const ProgTabDev* tabs, const ProgImgDev* imgs, const ProgScanDev* scans,
+                     const ProgSegDev* segs, int32_t nimg, int16_t* coef, void* stream) {
+  if (nimg <= 0) return 0;
+  hipLaunchKernelGGL(jpeg_prog, dim3(nimg), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), words, tabs, imgs,
+                     scans, segs, coef);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

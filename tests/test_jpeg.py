@@ -318,9 +318,10 @@ def test_lossless_files_match_pillow():
 
 def test_device_entropy_parse_routes_and_host_finish():
     """mxd_jpeg_coefs_parse(device_entropy=1) (CPU half of the device entropy
-    decode, csrc/jpeghuff.h): baseline one-scan files are only parsed
-    (entropy_pending), every other file is entropy-decoded on the host; either
-    way the host finish gives the decoder's bytes (Pillow's libjpeg-turbo)."""
+    decode, csrc/jpeghuff.h): baseline one-scan files and complete progressive
+    files are only parsed (entropy_pending; entropy_progressive for the
+    latter), every other file is entropy-decoded on the host; either way the
+    host finish gives the decoder's bytes (Pillow's libjpeg-turbo)."""
     Image = pytest.importorskip("PIL.Image")
     rng = np.random.default_rng(77)
     for i in range(24):
@@ -337,14 +338,16 @@ def test_device_entropy_parse_routes_and_host_finish():
         Image.fromarray(a[:, :, 0] if grey else a).save(b, "JPEG", **kw)
         data = b.getvalue()
         c = capi.JpegCoefs(data, device_entropy=True)
-        assert c.entropy_pending == (not prog), (i, kw)
+        assert c.entropy_pending and c.entropy_progressive == prog, (i, kw)
         assert np.array_equal(c.finish(), np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))), (i, kw)
-    # fixtures: progressive / CMYK / truncated files are decoded on the host
+    # fixtures: CMYK / truncated files are decoded on the host
     for k in [k[:-4] for k in GOLD.files if k.endswith("_jpg")]:
         data = bytes(GOLD[f"{k}_jpg"])
         c = capi.JpegCoefs(data, device_entropy=True)
-        if ("prog" in k and "prog0" not in k) or "cmyk" in k or "trunc" in k:
+        if "cmyk" in k or "trunc" in k:
             assert not c.entropy_pending, k
+        if "prog" in k and "prog0" not in k and "trunc" not in k:
+            assert c.entropy_progressive, k
         if c.device_ok:
             assert np.array_equal(c.finish(), GOLD[f"{k}_rgb"]), k
 

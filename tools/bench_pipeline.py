@@ -22,6 +22,7 @@ Variants per worker count:
 Datasets (synthetic stand-ins, seeded smooth noise, Pillow q=90 JPEGs):
   c1  300x200 / 200x300 (Caltech-101-like), batch 32
   c4  500x375 / 375x500 / 500x333 (ImageNet-like), batch 128
+  c4p the c4 files saved progressive
 Each surface point iterates the file list as many times as it takes to run
 >= --min-seconds (default 5 s) with >= --min-batches (16) batches per worker.
 Prints one JSON line per (dataset, variant, workers)."""
@@ -42,6 +43,8 @@ sys.path[:0] = [os.path.join(REPO, "mlx-data_amd"), os.path.join(REPO, "oracle")
 DATASETS = {
     "c1": dict(sizes=[(300, 200), (300, 200), (200, 300)], batch=32),
     "c4": dict(sizes=[(500, 375), (375, 500), (500, 333)], batch=128),
+    # c4's files saved progressive (libjpeg's default progression, optimised tables)
+    "c4p": dict(sizes=[(500, 375), (375, 500), (500, 333)], batch=128, progressive=True),
 }
 
 
@@ -57,7 +60,7 @@ def smooth(rng, h, w):
 def make_files(root, name, n):
     from PIL import Image
 
-    rng = np.random.default_rng({"c1": 11, "c4": 2}[name])
+    rng = np.random.default_rng({"c1": 11, "c4": 2, "c4p": 2}[name])
     sizes = DATASETS[name]["sizes"]
     files = []
     for i in range(n):
@@ -65,7 +68,7 @@ def make_files(root, name, n):
         d = os.path.join(root, name, f"class{i % 16}")
         os.makedirs(d, exist_ok=True)
         p = os.path.join(d, f"img{i}.jpg")
-        Image.fromarray(smooth(rng, h, w)).save(p, quality=90)
+        Image.fromarray(smooth(rng, h, w)).save(p, quality=90, progressive=DATASETS[name].get("progressive", False))
         files.append(p)
     return files
 
