@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 
 #include "jpeghuff.h"
 
@@ -945,7 +946,8 @@ struct ProgShared {
 
 // One symbol (jpeg.cpp Bits::decode: the 9-bit lookahead, then the canonical
 // search; no code within 16 bits: 16 bits consumed, symbol 0)
-__device__ __forceinline__ int prog_sym(GlobalReader& r, const ProgTabDev& t) {
+template <class R>
+__device__ __forceinline__ int prog_sym(R& r, const ProgTabDev& t) {
   const uint32_t w = r.win();
   const int e = t.look[w >> (32 - kProgLook)];
   if (e) {
@@ -961,7 +963,8 @@ __device__ __forceinline__ int prog_sym(GlobalReader& r, const ProgTabDev& t) {
   r.advance(l);
   return t.vals[((int32_t)(w >> (32 - l)) + t.valoffset[l]) & 0xff];
 }
-__device__ __forceinline__ int prog_get(GlobalReader& r, int n) {  // n <= 16
+template <class R>
+__device__ __forceinline__ int prog_get(R& r, int n) {  // n <= 16
   const int v = n ? (int)(r.win() >> (32 - n)) : 0;
   r.advance(n);
   return v;
@@ -982,12 +985,30 @@ struct CompGeom {
         v(pick3(im.v, c)) {}
 };
 
+// Where a lane's scan reads its segments: the words in device memory, or
+// (at >= 0) the copy the wave staged in LDS for the phase -- each segment's
+// words byte-swapped and followed by a zero word, the scan's segments one
+// after another from `at` (an LDS read has no wait on outstanding stores,
+// while a device-memory reader's refills wait for every memory operation in
+// flight: the coefficient stores included)
+struct ProgSrc {
+  const uint32_t* words;
+  const uint32_t* lds;
+  int32_t at;
+};
+template <class R>
 struct ProgSeg {
-  GlobalReader r;
+  R r;
   int32_t bits;
-  __device__ __forceinline__ void open(const uint32_t* words, const ProgSegDev& sg) {
+  __device__ __forceinline__ void open(const ProgSrc& src, const ProgSegDev& sg, int32_t& at) {
     bits = sg.bits;
-    r.init(words, (int32_t)sg.word, (bits + 31) >> 5, 0);
+    const int32_t nw = (bits + 31) >> 5;
+    if constexpr (std::is_same<R, GlobalReader>::value) {
+      r.init(src.words, (int32_t)sg.word, nw, 0);
+    } else {
+      r.init(src.lds, at, nw, nw);
+      at += nw + 1;
+    }
     r.seek(0);
   }
   // libjpeg's insufficient data: some symbol read past the segment's end
@@ -995,8 +1016,10 @@ struct ProgSeg {
 };
 
 // DC first (Ah = 0), any number of components, on one lane.
-__device__ void prog_dc_first(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+template <class R>
+__device__ void prog_dc_first(const ProgSrc& src, const ProgImgDev& im, const ProgScanDev& sc,
                               const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
+  int32_t at = src.at;
   const int ns = sc.ns;
   const CompGeom g0(im, sc.comp[0]), g1(im, sc.comp[1]), g2(im, sc.comp[2]);
   const int t0 = sc.slot[0], t1 = sc.slot[1], t2 = sc.slot[2];
@@ -1004,8 +1027,8 @@ __device__ void prog_dc_first(const uint32_t* words, const ProgImgDev& im, const
   const int mult = 1 << sc.al;
   const int64_t row = ns == 1 ? g0.wib : im.mcux;
   for (int s = 0; s < sc.nseg; s++) {
-    ProgSeg g;
-    g.open(words, segs[sc.seg0 + s]);
+    ProgSeg<R> g;
+    g.open(src, segs[sc.seg0 + s], at);
     int pred0 = 0, pred1 = 0, pred2 = 0;
     const int64_t m0 = (int64_t)s * per, m1 = min(sc.mcus, m0 + per);
     int64_t my = m0 / row, mx = m0 - my * row;
@@ -1035,15 +1058,17 @@ __device__ void prog_dc_first(const uint32_t* words, const ProgImgDev& im, const
 }
 
 // AC first (Ah = 0) of one component.
-__device__ void prog_ac_first(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+template <class R>
+__device__ void prog_ac_first(const ProgSrc& src, const ProgImgDev& im, const ProgScanDev& sc,
                               const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
+  int32_t at = src.at;
   const CompGeom cg(im, sc.comp[0]);
   const ProgTabDev& t = sh.tab[sc.slot[0]];
   const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
   const int ss = sc.ss, se = sc.se, al = sc.al;
   for (int s = 0; s < sc.nseg; s++) {
-    ProgSeg g;
-    g.open(words, segs[sc.seg0 + s]);
+    ProgSeg<R> g;
+    g.open(src, segs[sc.seg0 + s], at);
     int eobrun = 0;
     const int64_t m0 = (int64_t)s * per, m1 = min(sc.mcus, m0 + per);
     int64_t by = m0 / cg.wib, bx = m0 - by * cg.wib;
@@ -1129,7 +1154,8 @@ __device__ void prog_refine_masks(const ProgImgDev& im, const ProgScanDev& sc, i
   }
 }
 
-__device__ __forceinline__ void prog_bits(GlobalReader& r, int c, uint64_t& acc) {  // c <= 63 bits appended
+template <class R>
+__device__ __forceinline__ void prog_bits(R& r, int c, uint64_t& acc) {  // c <= 63 bits appended
   while (c > 0) {
     const int n = min(c, 16);
     acc = (acc << n) | (uint64_t)prog_get(r, n);
@@ -1137,8 +1163,10 @@ __device__ __forceinline__ void prog_bits(GlobalReader& r, int c, uint64_t& acc)
   }
 }
 
-__device__ void prog_ac_refine(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
+template <class R>
+__device__ void prog_ac_refine(const ProgSrc& src, const ProgImgDev& im, const ProgScanDev& sc,
                                const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
+  int32_t at = src.at;
   const CompGeom cg(im, sc.comp[0]);
   const ProgAux ax(im, coef);
   const ProgTabDev& t = sh.tab[sc.slot[0]];
@@ -1148,8 +1176,8 @@ __device__ void prog_ac_refine(const uint32_t* words, const ProgImgDev& im, cons
   const int wib = cg.wib;
   constexpr int kAhead = 8;  // masks loaded ahead of the block being decoded
   for (int s = 0; s < sc.nseg; s++) {
-    ProgSeg g;
-    g.open(words, segs[sc.seg0 + s]);
+    ProgSeg<R> g;
+    g.open(src, segs[sc.seg0 + s], at);
     int eobrun = 0;
     const int64_t m0 = (int64_t)s * per, m1b = min(sc.mcus, m0 + per);
     int64_t by = m0 / wib, bx = m0 - by * wib;
@@ -1296,11 +1324,16 @@ __device__ void prog_dc_refine(const uint32_t* words, const ProgImgDev& im, cons
   }
 }
 
+constexpr int kProgLdsWords = 12288;  // the phase's staged segments (48 KB of dynamic LDS)
+constexpr int kProgScansLds = 64;     // scans of an image that can be staged
+
 __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ words, const ProgTabDev* __restrict__ tabs,
                                                 const ProgImgDev* __restrict__ imgs,
                                                 const ProgScanDev* __restrict__ scans,
                                                 const ProgSegDev* __restrict__ segs, int16_t* __restrict__ coef) {
   __shared__ ProgShared sh;
+  __shared__ int32_t scan_at[kProgScansLds];
+  extern __shared__ uint32_t staged[];
   const ProgImgDev im = imgs[blockIdx.x];
   const int lane = threadIdx.x;
   for (int i = lane; i < 80; i += 64) sh.nat[i] = kNat80[i];
@@ -1328,6 +1361,25 @@ __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ wor
         refine_ac = true;
       }
     }
+    // the phase's Huffman-coded segments into LDS while they fit
+    {
+      int32_t at = 0;
+      for (int si = im.scan0; si < im.scan0 + im.nscan && si - im.scan0 < kProgScansLds; si++) {
+        const ProgScanDev& sc = scans[si];
+        if (sc.phase != ph || sc.lane < 0) continue;
+        int64_t need = 0;
+        for (int q = sc.seg0; q < sc.seg0 + sc.nseg; q++) need += ((segs[q].bits + 31) >> 5) + 1;
+        const bool fits = at + need <= kProgLdsWords;
+        if (lane == 0) scan_at[si - im.scan0] = fits ? at : -1;
+        if (!fits) continue;
+        for (int q = sc.seg0; q < sc.seg0 + sc.nseg; q++) {
+          const int32_t nw = (segs[q].bits + 31) >> 5;
+          const uint32_t* from = words + segs[q].word;
+          for (int u = lane; u <= nw; u += 64) staged[at + u] = u < nw ? __builtin_bswap32(from[u]) : 0u;
+          at += nw + 1;
+        }
+      }
+    }
     __syncthreads();
     if (refine_all) {
       for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
@@ -1343,9 +1395,16 @@ __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ wor
           if (scans[si].phase == ph && scans[si].lane == lane && scans[si].step == st) mine = si;
         if (mine < 0) continue;
         const ProgScanDev sc = scans[mine];
-        if (sc.ss == 0) prog_dc_first(words, im, sc, segs, sh, coef);
-        else if (sc.ah == 0) prog_ac_first(words, im, sc, segs, sh, coef);
-        else prog_ac_refine(words, im, sc, segs, sh, coef);
+        const ProgSrc src{words, staged, mine - im.scan0 < kProgScansLds ? scan_at[mine - im.scan0] : -1};
+        if (src.at >= 0) {
+          if (sc.ss == 0) prog_dc_first<LdsReader<true>>(src, im, sc, segs, sh, coef);
+          else if (sc.ah == 0) prog_ac_first<LdsReader<true>>(src, im, sc, segs, sh, coef);
+          else prog_ac_refine<LdsReader<true>>(src, im, sc, segs, sh, coef);
+        } else {
+          if (sc.ss == 0) prog_dc_first<GlobalReader>(src, im, sc, segs, sh, coef);
+          else if (sc.ah == 0) prog_ac_first<GlobalReader>(src, im, sc, segs, sh, coef);
+          else prog_ac_refine<GlobalReader>(src, im, sc, segs, sh, coef);
+        }
       }
     }
     __syncthreads();
@@ -1398,8 +1457,8 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
 int launch_jpeg_prog(const uint32_t* words, const ProgTabDev* tabs, const ProgImgDev* imgs, const ProgScanDev* scans,
                      const ProgSegDev* segs, int32_t nimg, int16_t* coef, void* stream) {
   if (nimg <= 0) return 0;
-  hipLaunchKernelGGL(jpeg_prog, dim3(nimg), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), words, tabs, imgs,
-                     scans, segs, coef);
+  hipLaunchKernelGGL(jpeg_prog, dim3(nimg), dim3(64), (size_t)kProgLdsWords * 4, reinterpret_cast<hipStream_t>(stream),
+                     words, tabs, imgs, scans, segs, coef);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
