@@ -26,6 +26,7 @@
 // measured in profiles/r04/ and described in DESIGN.md section 8.)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 
@@ -1330,7 +1331,8 @@ constexpr int kProgScansLds = 64;     // scans of an image that can be staged
 __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ words, const ProgTabDev* __restrict__ tabs,
                                                 const ProgImgDev* __restrict__ imgs,
                                                 const ProgScanDev* __restrict__ scans,
-                                                const ProgSegDev* __restrict__ segs, int16_t* __restrict__ coef) {
+                                                const ProgSegDev* __restrict__ segs, int16_t* __restrict__ coef,
+                                                int skip) {
   __shared__ ProgShared sh;
   __shared__ int32_t scan_at[kProgScansLds];
   extern __shared__ uint32_t staged[];
@@ -1396,6 +1398,8 @@ __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ wor
         if (mine < 0) continue;
         const ProgScanDev sc = scans[mine];
         const ProgSrc src{words, staged, mine - im.scan0 < kProgScansLds ? scan_at[mine - im.scan0] : -1};
+        const int kind = sc.ss == 0 ? 1 : sc.ah == 0 ? 2 : 4;
+        if (skip & kind) continue;  // (diagnostic: MXD_PROG_SKIP, timing breakdowns only)
         if (src.at >= 0) {
           if (sc.ss == 0) prog_dc_first<LdsReader<true>>(src, im, sc, segs, sh, coef);
           else if (sc.ah == 0) prog_ac_first<LdsReader<true>>(src, im, sc, segs, sh, coef);
@@ -1457,8 +1461,11 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
 int launch_jpeg_prog(const uint32_t* words, const ProgTabDev* tabs, const ProgImgDev* imgs, const ProgScanDev* scans,
                      const ProgSegDev* segs, int32_t nimg, int16_t* coef, void* stream) {
   if (nimg <= 0) return 0;
+  // MXD_PROG_SKIP (diagnostic; wrong output): bit 0 skips DC-first scans,
+  // bit 1 AC-first, bit 2 AC refinements -- tools/prog_breakdown.py times them
+  static const int skip = std::getenv("MXD_PROG_SKIP") ? std::atoi(std::getenv("MXD_PROG_SKIP")) : 0;
   hipLaunchKernelGGL(jpeg_prog, dim3(nimg), dim3(64), (size_t)kProgLdsWords * 4, reinterpret_cast<hipStream_t>(stream),
-                     words, tabs, imgs, scans, segs, coef);
+                     words, tabs, imgs, scans, segs, coef, skip);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
