@@ -986,6 +986,42 @@ struct CompGeom {
         v(pick3(im.v, c)) {}
 };
 
+// One lane's bit reader over a segment staged in LDS (byte-swapped words, a
+// zero word after them): a 64-bit buffer refilled a word at a time when 32 or
+// fewer bits remain, the next word's LDS load issued one refill ahead -- so
+// a step waits on LDS only when its lookup does (LdsReader, built for the
+// many-lane sequential kernel, loads a word per step)
+struct LdsBits {
+  const uint32_t* w;
+  int32_t nw, q;  // words: staged (w[nw] is the zero word), taken into buf
+  uint64_t buf;
+  int32_t cnt;    // bits of buf not yet consumed (33..64 between steps)
+  uint32_t nxt;   // w[q], loaded ahead
+  __device__ __forceinline__ uint32_t word(int32_t i) const { return w[min(i, nw)]; }
+  __device__ __forceinline__ void init(const void* base, int32_t w0, int32_t nwords, int32_t) {
+    w = static_cast<const uint32_t*>(base) + w0;
+    nw = nwords;
+  }
+  __device__ __forceinline__ void seek(int32_t) {  // (segment start only)
+    buf = (uint64_t)word(0) << 32 | word(1);
+    cnt = 64;
+    q = 2;
+    nxt = word(2);
+  }
+  __device__ __forceinline__ uint32_t win() const { return (uint32_t)(buf >> 32); }
+  __device__ __forceinline__ void advance(int n) {  // n <= 31
+    buf <<= n;
+    cnt -= n;
+    if (cnt <= 32) {
+      buf |= (uint64_t)nxt << (32 - cnt);
+      cnt += 32;
+      q++;
+      nxt = word(q);
+    }
+  }
+  __device__ __forceinline__ int32_t pos() const { return q * 32 - cnt; }
+};
+
 // Where a lane's scan reads its segments: the words in device memory, or
 // (at >= 0) the copy the wave staged in LDS for the phase -- each segment's
 // words byte-swapped and followed by a zero word, the scan's segments one
@@ -1401,9 +1437,9 @@ __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ wor
         const int kind = sc.ss == 0 ? 1 : sc.ah == 0 ? 2 : 4;
         if (skip & kind) continue;  // (diagnostic: MXD_PROG_SKIP, timing breakdowns only)
         if (src.at >= 0) {
-          if (sc.ss == 0) prog_dc_first<LdsReader<true>>(src, im, sc, segs, sh, coef);
-          else if (sc.ah == 0) prog_ac_first<LdsReader<true>>(src, im, sc, segs, sh, coef);
-          else prog_ac_refine<LdsReader<true>>(src, im, sc, segs, sh, coef);
+          if (sc.ss == 0) prog_dc_first<LdsBits>(src, im, sc, segs, sh, coef);
+          else if (sc.ah == 0) prog_ac_first<LdsBits>(src, im, sc, segs, sh, coef);
+          else prog_ac_refine<LdsBits>(src, im, sc, segs, sh, coef);
         } else {
           if (sc.ss == 0) prog_dc_first<GlobalReader>(src, im, sc, segs, sh, coef);
           else if (sc.ah == 0) prog_ac_first<GlobalReader>(src, im, sc, segs, sh, coef);
