@@ -80,6 +80,10 @@ import numpy as np  # noqa: E402
 # C4 114-116 k img/s with 4 queues, 146-150 k with 16).  The C2 line does not
 # depend on it (profiles/r04/hwq_bench.jsonl).
 os.environ.setdefault("MXD_HW_QUEUES", "16")
+# e2e_jpeg's progressive leg measures the device decode of every scan
+# (jpeg_prog) against the host entropy decode: force the device choice, which
+# the library's default leaves to the host above 11 host CPUs
+os.environ.setdefault("MXD_DEVICE_PROGRESSIVE", "1")
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 C = 3
@@ -813,6 +817,18 @@ def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False):
 
         value, n, dt, split = leg("device")
         hostent, n2, dt2, split2 = leg("device_hostent")
+        # the same files saved progressive: every scan decoded on the device
+        # (jpeg_prog; MXD_DEVICE_PROGRESSIVE above) against the host entropy
+        # decode
+        files_c4 = files
+        files = bp.make_files(root, "c4p", batch)
+        pvalue, pn, pdt, psplit = leg("device")
+        phost, _, _, _ = leg("device_hostent")
+        dprog = capi.JpegCoefs(open(files[0], "rb").read(), device_entropy=True).entropy_progressive
+        progressive = {"value": pvalue, "images": pn, "seconds": pdt, "host_entropy_value": phost,
+                       "device_progressive": dprog, "host_split": psplit,
+                       "files": "the e2e files saved progressive (libjpeg's default progression)"}
+        files = files_c4
         cpu = None
         if not no_cpu:
             sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -840,7 +856,7 @@ def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False):
     return {"value": value, "unit": "images/s", "images": n, "seconds": dt, "workers": workers, "cores": cores,
             "batch": batch, "files": len(files), "file_mb": round(mb, 2),
             "host_entropy_value": hostent, "host_entropy_seconds": dt2, "cpu_restatement": cpu,
-            "host_split": split, "host_entropy_split": split2,
+            "host_split": split, "host_entropy_split": split2, "progressive": progressive,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "devices": dx.devices(),
             "device_entropy": dx.device_entropy(), "abi": capi.lib().mxd_abi_version(),
             "chain": "files -> load_image -> image_resize_smallest_side(256) -> image_center_crop(224, 224) -> "

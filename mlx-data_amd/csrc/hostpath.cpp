@@ -1293,5 +1293,8 @@ int pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device)
 }
 
 
+// (jpeg.cpp's choice of the progressive device decode)
+int host_cpus() { return host_cpu_budget(); }
+
 }  // namespace capi
 }  // namespace mxd

@@ -40,5 +40,5 @@ if __name__ == "__main__":
     with tempfile.TemporaryDirectory() as root:
         bp.make_files(root, "c4p", 128)
         for skip in (0, 1, 2, 4, 6, 7):
-            env = dict(os.environ, MXD_PROG_SKIP=str(skip))
+            env = dict(os.environ, MXD_PROG_SKIP=str(skip), MXD_DEVICE_PROGRESSIVE="1")
             subprocess.run([sys.executable, __file__, root], env=env, check=True, timeout=240)

@@ -20,8 +20,8 @@ run() {  # name limit cmd...
 run pytest_prog 300 python -u -m pytest tests/test_gpu_jpeg_progressive.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 run pytest_jpeg 400 python -u -m pytest tests/test_gpu_jpeg.py tests/test_gpu_jpeg_entropy.py tests/test_gpu_c4_full.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 if [ "${2:-}" = "tests-only" ]; then exit 0; fi
-run pipe_dev 300 python tools/bench_pipeline.py --datasets c4p --images 256 --workers 1,16,32 --variants device --min-seconds 3 --stats
+MXD_DEVICE_PROGRESSIVE=1 run pipe_dev 300 python tools/bench_pipeline.py --datasets c4p --images 256 --workers 1,16,32 --variants device --min-seconds 3 --stats
 MXD_NO_DEVICE_PROGRESSIVE=1 run pipe_host 300 python tools/bench_pipeline.py --datasets c4p --images 256 --workers 1,16,32 --variants device --min-seconds 3 --stats
-run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 tools/bench_pipeline.py --datasets c4p --images 256 --workers 16 --variants device --min-seconds 2
+MXD_DEVICE_PROGRESSIVE=1 run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 tools/bench_pipeline.py --datasets c4p --images 256 --workers 16 --variants device --min-seconds 2
 cut -c1-250 gpurun_out/${TAG}_prof/run_kernel_stats.csv
 exit 0
