@@ -155,3 +155,16 @@ def test_progressive_mixed_batch_and_resize():
     _, dev = _decode_gpu(datas, geoms)
     for i, (g, (w_, _)) in enumerate(zip(dev, want)):
         assert np.array_equal(g, w_), i
+
+
+def test_progressive_large_images_read_device_memory():
+    """Photos whose scans do not fit the kernel's LDS staging (48 KB per
+    phase) read their segments from device memory (the prefetching reader):
+    1600x1200 and 2400x1800 progressive files, one with restart markers,
+    equal to the host decoder and Pillow."""
+    rng = np.random.default_rng(14)
+    datas = [_encode(_smooth(rng, 1200, 1600), quality=95, progressive=True, subsampling=2),
+             _encode(_smooth(rng, 1800, 2400), quality=92, progressive=True, subsampling=0),
+             _encode(_smooth(rng, 1200, 1600, 1), quality=97, progressive=True, restart_marker_blocks=5)]
+    coefs = _check_identity(datas)
+    assert all(c.entropy_progressive for c in coefs)
