@@ -37,8 +37,9 @@ extern "C" {
  * mxd_device_synchronize, and the tuning knobs MXD_TUNE_HUFF_BITS,
  * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS,
  * MXD_TUNE_HUFF_JOB, MXD_TUNE_JPEG_RGB, mxd_jpeg_plane_sources,
- * mxd_host_stats, mxd_jpeg_coefs_load. */
-#define MXD_ABI_VERSION 5
+ * mxd_host_stats, mxd_jpeg_coefs_load.
+ * 6 (round 6): the knob MXD_TUNE_DEVICE_TIMING and mxd_device_stats. */
+#define MXD_ABI_VERSION 6
 
 enum mxd_status {
   MXD_OK = 0,
@@ -189,7 +190,11 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_JPEG_RGB: 1 = every device-finished JPEG goes through an RGB
  * frame (jpeg_color) before the resize; 0 (default) = a 4:2:0 image whose
  * resize runs on a scatter wave kernel is resized straight from its sample
- * planes (no RGB frame). */
+ * planes (no RGB frame);
+ * MXD_TUNE_DEVICE_TIMING: 1 = every host-path chunk records two timing events
+ * on its stream, before its first kernel and after its last, and
+ * mxd_device_stats sums the span between them (diagnostics: what the batch
+ * calls cost the device; read when a chunk is launched). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -202,7 +207,8 @@ enum mxd_tune {
   MXD_TUNE_HOST_STREAMS = 8,
   MXD_TUNE_HUFF_JOB = 9,
   MXD_TUNE_JPEG_RGB = 10,
-  MXD_TUNE_COUNT = 11
+  MXD_TUNE_DEVICE_TIMING = 11,
+  MXD_TUNE_COUNT = 12
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 
@@ -388,6 +394,13 @@ int mxd_jpeg_plane_sources(int64_t* count, int32_t reset);
  * out[4] mxd_jpeg_coefs_parse / mxd_jpeg_coefs_load calls, out[5] their time
  * in ns (a load's includes its file read). */
 int mxd_host_stats(int64_t* out6, int32_t reset);
+
+/* Diagnostics (ABI 6): with MXD_TUNE_DEVICE_TIMING 1, out[0] = host-path
+ * chunks timed, out[1] = the summed device time in ns from each chunk's
+ * first kernel to the end of its last (entropy decode, IDCT, colour, resize;
+ * the staged input copy before them and the result copy after them are
+ * outside), since the last reset (reset != 0 zeroes them after reading). */
+int mxd_device_stats(int64_t* out2, int32_t reset);
 
 /* ---- pixel maps: rotate / affine and channel reduction --
  *

@@ -519,6 +519,12 @@ int mxd_host_stats(int64_t* out6, int32_t reset) {
   return MXD_OK;
 }
 
+int mxd_device_stats(int64_t* out2, int32_t reset) {
+  if (!out2) return fail(MXD_ERR_INVALID, "mxd: null out2");
+  for (int i = 0; i < 2; i++) out2[i] = reset ? g_device_stats[i].exchange(0) : g_device_stats[i].load();
+  return MXD_OK;
+}
+
 int mxd_jpeg_plane_sources(int64_t* count, int32_t reset) {
   if (!count) return fail(MXD_ERR_INVALID, "mxd: null count");
   *count = reset ? g_plane_sources.exchange(0) : g_plane_sources.load();

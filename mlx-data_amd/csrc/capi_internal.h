@@ -243,6 +243,7 @@ int jpeg_path(const mxd_jpeg_image* jimg, int32_t n, int32_t out_dtype, int32_t 
 // mxd_host_stats counters: host-path calls, images, wall ns, device-wait ns,
 // coefficient parses, parse ns
 extern std::atomic<int64_t> g_host_stats[6];
+extern std::atomic<int64_t> g_device_stats[2];  // mxd_device_stats: timed chunks, device ns
 int64_t now_ns();
 extern std::atomic<int64_t> g_plane_sources;  // images resized from their JPEG sample planes (mxd_jpeg_plane_sources)
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c);

@@ -39,6 +39,10 @@ struct Slot {
   uint8_t* dev_mid = nullptr;  // JPEG chunks: IDCT samples + decoded RGB images
   size_t dev_mid_cap = 0;
   int32_t* huff_err = nullptr;  // page-locked: the entropy decode's error word, copied back with the chunk
+  // MXD_TUNE_DEVICE_TIMING: events around the chunk's kernels (timed: this
+  // chunk recorded them)
+  hipEvent_t k0 = nullptr, k1 = nullptr;
+  bool timed = false;
 };
 
 struct HostCtx {
@@ -171,8 +175,10 @@ class Helpers {
 // the mask does not show: the GPU boxes give every process the whole
 // machine's mask and a 16-CPU quota, and sizing helpers by the mask put
 // 16 prefetch workers x 8 staging threads on 16 CPUs -- and by
-// OMP_NUM_THREADS when the environment sets it (the boxes' per-GPU share).
-// MXD_HOST_CPUS overrides all of it.
+// OMP_NUM_THREADS when the environment sets it above 1 (the boxes' per-GPU
+// share; torchrun and similar launchers export 1 to every rank by default,
+// which says nothing about the host's CPUs and is ignored).
+// MXD_HOST_CPUS overrides all of it (tuning knobs).
 int host_cpu_budget() {
   if (const char* e = std::getenv("MXD_HOST_CPUS"))
     if (std::atoi(e) > 0) return std::atoi(e);
@@ -200,7 +206,7 @@ int host_cpu_budget() {
   }
   if (const char* e = std::getenv("OMP_NUM_THREADS")) {
     const int k = std::atoi(e);
-    if (k > 0) n = std::min(n, k);
+    if (k > 1) n = std::min(n, k);
   }
   return std::max(1, n);
 }
@@ -413,6 +419,7 @@ struct JpegChunk {
 
 std::atomic<int64_t> g_plane_sources{0};
 std::atomic<int64_t> g_host_stats[6] = {};
+std::atomic<int64_t> g_device_stats[2] = {};
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -623,19 +630,23 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       c.hsegs.push_back(sd);
     }
     sub_first.push_back(nsub_img);
-    // jobs: runs of at most kHuffThreads - kHuffWarm own subsequences, evenly
+    // jobs: runs of at most kHuffThreads - kJobSlack own subsequences, evenly
     // sized; a cut inside a segment gives the next job a warm-up of up to
-    // kHuffWarm subsequences before its own (jpeghuff.h); cuts within a few
-    // subsequences of a segment start move there (restart markers: no warm-up)
+    // kHuffWarm subsequences before its own (jpeghuff.h); cuts within
+    // kCutMove subsequences of a segment start move there (restart markers: no
+    // warm-up), which lengthens the job after the cut by up to kCutMove.  The
+    // slack covers both, so no job exceeds one workgroup's kHuffThreads.
+    constexpr int64_t kCutMove = 32;
+    constexpr int64_t kJobSlack = std::max<int64_t>(mxd::kHuffWarm, kCutMove);
     const int32_t job_knob = g_tune[MXD_TUNE_HUFF_JOB].load();
-    const int64_t cap = job_knob > 0 ? std::min<int64_t>(job_knob, mxd::kHuffThreads - mxd::kHuffWarm)
-                                     : mxd::kHuffThreads - mxd::kHuffWarm;
+    const int64_t cap = job_knob > 0 ? std::min<int64_t>(job_knob, mxd::kHuffThreads - kJobSlack)
+                                     : mxd::kHuffThreads - kJobSlack;
     const int64_t njob = (nsub_img + cap - 1) / cap;
     std::vector<int64_t> cuts{0};
     for (int64_t q = 1; q < njob; q++) {
       int64_t cut = q * nsub_img / njob;
       const int64_t sgi = std::upper_bound(sub_first.begin(), sub_first.end(), cut) - sub_first.begin() - 1;
-      if (cut - sub_first[sgi] <= 32 && sub_first[sgi] > cuts.back()) cut = sub_first[sgi];
+      if (cut - sub_first[sgi] <= kCutMove && sub_first[sgi] > cuts.back()) cut = sub_first[sgi];
       cuts.push_back(cut);
     }
     cuts.push_back(nsub_img);
@@ -890,6 +901,14 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     MXD_HIP(hipEventSynchronize(sl.done));
     waited(t0);
     pending[k & 1] = -1;
+    if (sl.timed) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, sl.k0, sl.k1) == hipSuccess) {
+        g_device_stats[0].fetch_add(1, std::memory_order_relaxed);
+        g_device_stats[1].fetch_add((int64_t)((double)ms * 1e6), std::memory_order_relaxed);
+      }
+      sl.timed = false;
+    }
     if (sl.huff_err && *sl.huff_err) {
       *sl.huff_err = 0;
       return fail(MXD_ERR_DEVICE, "jpeg entropy decode: a job never received its predecessor's state");
@@ -1086,8 +1105,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         // page-locked host twin in the control record
         if (!sl.huff_err) {
           MXD_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.huff_err), 64, hipHostMallocDefault));
-          *sl.huff_err = 0;
         }
+        // cleared for every staged chunk: a call that left early (another
+        // chunk's error, a failed launch) never read the word back, and a job
+        // that gave up there must not fail this call
+        *sl.huff_err = 0;
         std::memset(sl.pin_in + jc.pub_off, 0, (size_t)(jc.coef_off - jc.pub_off));
         mxd::HuffCtlDev ctl{};
         ctl.err_host = const_cast<int32_t*>(reinterpret_cast<const int32_t*>(host_device_ptr(sl.huff_err)));
@@ -1096,8 +1118,19 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     }
     if (in_staged > 0 && !pin_in_dev)
       MXD_HIP(hipMemcpyAsync(sl.dev_in, sl.pin_in, in_staged, hipMemcpyHostToDevice, sl.stream));
+    sl.timed = g_tune[MXD_TUNE_DEVICE_TIMING].load() == 1;
+    if (sl.timed) {
+      if (!sl.k0) MXD_HIP(hipEventCreate(&sl.k0));
+      if (!sl.k1) MXD_HIP(hipEventCreate(&sl.k1));
+      if (jpeg) MXD_HIP(hipEventRecord(sl.k0, sl.stream));  // (else after the source row copies below)
+    }
     if (jpeg) {
       if (!jc.hjobs.empty()) {
+        // jpeg_chunk's job sizing keeps every job within one workgroup; a
+        // larger one would leave subsequences undecoded and never publish
+        if (jc.huff_threads > mxd::kHuffThreads)
+          return fail(MXD_ERR_DEVICE, "jpeg entropy decode: a job of " + std::to_string(jc.huff_threads) +
+                                          " subsequences exceeds a workgroup");
         // (the publication records and the ticket came zero with the staged
         // copy; the decode zeroes every block it starts, and the blocks
         // insufficient data leaves undecoded)
@@ -1158,7 +1191,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       MXD_HIP(hipMemcpy2DAsync(sl.dev_in + s.in_off, s.pitch, from, im.src_stride, s.copy, s.rows,
                                hipMemcpyHostToDevice, sl.stream));
     }
+    if (sl.timed && !jpeg) MXD_HIP(hipEventRecord(sl.k0, sl.stream));
     if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
+    if (sl.timed) MXD_HIP(hipEventRecord(sl.k1, sl.stream));
     if (!dst_device) {
       if (out_staged > 0 && !pin_out_dev)
         MXD_HIP(hipMemcpyAsync(sl.pin_out, sl.dev_out, out_staged, hipMemcpyDeviceToHost, sl.stream));

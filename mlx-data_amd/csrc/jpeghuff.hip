@@ -1361,6 +1361,13 @@ __device__ void prog_dc_refine(const uint32_t* words, const ProgImgDev& im, cons
   }
 }
 
+// Diagnostic builds only (-DMXD_PROG_SKIP=<bits>; wrong output, never in the
+// product library): bit 0 skips DC-first scans, bit 1 AC-first, bit 2 AC
+// refinements -- tools/prog_breakdown.py times them with variant builds.
+#ifndef MXD_PROG_SKIP
+#define MXD_PROG_SKIP 0
+#endif
+
 constexpr int kProgLdsWords = 12288;  // the phase's staged segments (48 KB of dynamic LDS)
 constexpr int kProgScansLds = 64;     // scans of an image that can be staged
 
@@ -1435,7 +1442,7 @@ __global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ wor
         const ProgScanDev sc = scans[mine];
         const ProgSrc src{words, staged, mine - im.scan0 < kProgScansLds ? scan_at[mine - im.scan0] : -1};
         const int kind = sc.ss == 0 ? 1 : sc.ah == 0 ? 2 : 4;
-        if (skip & kind) continue;  // (diagnostic: MXD_PROG_SKIP, timing breakdowns only)
+        if (skip & kind) continue;  // (diagnostic builds: MXD_PROG_SKIP)
         if (src.at >= 0) {
           if (sc.ss == 0) prog_dc_first<LdsBits>(src, im, sc, segs, sh, coef);
           else if (sc.ah == 0) prog_ac_first<LdsBits>(src, im, sc, segs, sh, coef);
@@ -1497,11 +1504,8 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
 int launch_jpeg_prog(const uint32_t* words, const ProgTabDev* tabs, const ProgImgDev* imgs, const ProgScanDev* scans,
                      const ProgSegDev* segs, int32_t nimg, int16_t* coef, void* stream) {
   if (nimg <= 0) return 0;
-  // MXD_PROG_SKIP (diagnostic; wrong output): bit 0 skips DC-first scans,
-  // bit 1 AC-first, bit 2 AC refinements -- tools/prog_breakdown.py times them
-  static const int skip = std::getenv("MXD_PROG_SKIP") ? std::atoi(std::getenv("MXD_PROG_SKIP")) : 0;
   hipLaunchKernelGGL(jpeg_prog, dim3(nimg), dim3(64), (size_t)kProgLdsWords * 4, reinterpret_cast<hipStream_t>(stream),
-                     words, tabs, imgs, scans, segs, coef, skip);
+                     words, tabs, imgs, scans, segs, coef, MXD_PROG_SKIP);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

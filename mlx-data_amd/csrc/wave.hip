@@ -189,6 +189,14 @@ __device__ __forceinline__ void store_out(V* p, T v) {
     *p = v;
 }
 
+// Cache policy of every source row load (the aux operand of the buffer
+// loads; tuning builds -DMXD_LOAD_AUX=<n>: 2 = nt (streaming), 1 = sc0,
+// 16 = sc1, 3 = sc0 nt).  0, the default policy, is the product setting:
+// profiles/r06/README.md has the in-process A/B over C2..C5.
+#ifndef MXD_LOAD_AUX
+#define MXD_LOAD_AUX 0
+#endif
+
 // A voffset past any image (images are < 2^31 bytes): the buffer range check
 // turns the load into zeros without a memory request.
 constexpr int kNoLoad = 0x7ffffff0;
@@ -210,17 +218,17 @@ __device__ __forceinline__ void to_planes(const Raw<P * C / 4>& v, float (&x)[C]
 template <int N>
 __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_t* w) {
   if constexpr (N >= 4) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, MXD_LOAD_AUX);
     w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
     if constexpr (N > 4) load_dwords<N - 4>(rs, voff + 16, soff, w + 4);
   } else if constexpr (N == 3) {
-    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, voff, soff, 0);
+    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, voff, soff, MXD_LOAD_AUX);
     w[0] = v.x, w[1] = v.y, w[2] = v.z;
   } else if constexpr (N == 2) {
-    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, MXD_LOAD_AUX);
     w[0] = v.x, w[1] = v.y;
   } else if constexpr (N == 1) {
-    w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+    w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, MXD_LOAD_AUX);
   }
 }
 
@@ -307,13 +315,13 @@ struct YccSrc {
     const uint32_t c0 = (uint32_t)(min(iy, dh - 1) * cstride) + (uint32_t)coff;
     const uint32_t c1 = (uint32_t)(min(max((ry & 1) ? iy + 1 : iy - 1, 0), dh - 1) * cstride) + (uint32_t)coff;
     YccRaw v;
-    v.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((uint32_t)yoff + (uint32_t)((ok ? r : 0) * ystride)), 0, 0);
+    v.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((uint32_t)yoff + (uint32_t)((ok ? r : 0) * ystride)), 0, MXD_LOAD_AUX);
     const uint32_t offs[2][2] = {{c0 + (uint32_t)cb, c1 + (uint32_t)cb}, {c0 + (uint32_t)cr, c1 + (uint32_t)cr}};
 #pragma unroll
     for (int k = 0; k < 2; k++)
 #pragma unroll
       for (int j = 0; j < 2; j++) {
-        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)offs[k][j], 0, 0);
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)offs[k][j], 0, MXD_LOAD_AUX);
         v.c[k][j][0] = t.x;
         v.c[k][j][1] = t.y;
       }

@@ -32,7 +32,7 @@ EXPORTS = (
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
     "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_load", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
     "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
-    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources", "mxd_host_stats",
+    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources", "mxd_host_stats", "mxd_device_stats",
 )
 
 MXD_AFFINE = 0
@@ -60,6 +60,7 @@ MXD_TUNE_HOST_WAIT = 7
 MXD_TUNE_HOST_STREAMS = 8
 MXD_TUNE_HUFF_JOB = 9
 MXD_TUNE_JPEG_RGB = 10
+MXD_TUNE_DEVICE_TIMING = 11
 
 
 class MxdImage(ctypes.Structure):
@@ -356,6 +357,15 @@ def host_stats(reset=False):
     check(lib().mxd_host_stats(v, 1 if reset else 0))
     return {"calls": v[0], "images": v[1], "call_s": v[2] * 1e-9, "wait_s": v[3] * 1e-9,
             "parses": v[4], "parse_s": v[5] * 1e-9}
+
+
+def device_stats(reset=False):
+    """Device time of the host-path calls' chunks since the last reset
+    (mxd_device_stats; counted while MXD_TUNE_DEVICE_TIMING is 1): a dict of
+    timed chunks and their summed seconds from first kernel to last."""
+    v = (ctypes.c_int64 * 2)()
+    check(lib().mxd_device_stats(v, 1 if reset else 0))
+    return {"chunks": v[0], "device_s": v[1] * 1e-9}
 
 
 def jpeg_resize_crop_to_device(images, n, out_dtype, device=0):

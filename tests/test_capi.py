@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(capi.EXPORTS) == syms
-    assert L.mxd_abi_version() == 5
+    assert L.mxd_abi_version() == 6
 
 
 @pytest.mark.parametrize("w,h,size", [(1280, 960, 256), (375, 500, 256), (500, 375, 256), (300, 200, 256),

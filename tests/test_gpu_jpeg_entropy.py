@@ -335,3 +335,86 @@ def test_arithmetic_coded_files_finish_on_the_device():
              A.encode(_smooth(rng, 33, 47)[:, :, 0], q=5, dac=(1, 6, 9))]
     coefs = _check_identity(datas)
     assert [c.entropy_pending for c in coefs] == [False, False, True, False]
+
+
+def _segment_bytes(d):
+    """Unstuffed bytes of each restart interval of a one-scan file (what
+    jpeg.cpp record_segments counts: stuffed 0x00 and fill 0xFF dropped)."""
+    i = 2
+    while True:
+        m, n = d[i + 1], d[i + 2] * 256 + d[i + 3]
+        if m == 0xDA:
+            p = i + 2 + n
+            break
+        i += 2 + n
+    out, cur = [], 0
+    while True:
+        if d[p] == 0xFF:
+            m = d[p + 1]
+            if m == 0x00:
+                cur, p = cur + 1, p + 2
+            elif 0xD0 <= m <= 0xD7:
+                out.append(cur)
+                cur, p = 0, p + 2
+            elif m == 0xFF:
+                p += 1
+            else:
+                out.append(cur)
+                return out
+        else:
+            cur, p = cur + 1, p + 1
+
+
+def _job_sizes(subs, cap, move=32, warm=24):
+    """hostpath.cpp jpeg_chunk's job split (subsequences per job, warm-up
+    included) for segments of `subs` subsequences at a per-job cap."""
+    import bisect
+
+    sf = [0]
+    for s in subs:
+        sf.append(sf[-1] + s)
+    n = sf[-1]
+    njob = -(-n // cap)
+    cuts = [0]
+    for q in range(1, njob):
+        cut = q * n // njob
+        g = bisect.bisect_right(sf, cut) - 1
+        if cut - sf[g] <= move and sf[g] > cuts[-1]:
+            cut = sf[g]
+        cuts.append(cut)
+    cuts.append(n)
+    return [b - a + min(warm, a - sf[bisect.bisect_right(sf, a) - 1]) for a, b in zip(cuts, cuts[1:])]
+
+
+def test_cut_moved_to_a_segment_start_stays_within_a_workgroup():
+    """a job cut moved back to a restart-segment start (no
+    warm-up) lengthens the next job by up to 32 subsequences; with the old
+    per-job cap of 1000 that job could hold 1025..1032 subsequences, past the
+    1024-thread workgroup -- its tail never decoded and the next job waiting
+    for a state that never came.  Search (seeded) for a restart-interval file
+    and subsequence length where the old split overflows, then decode it on
+    the device with that length: bit-exact to the host decoder and Pillow."""
+    rng = np.random.default_rng(7)
+    found = None
+    for _ in range(60):
+        h, w = 64 * int(rng.integers(2, 8)), 64 * int(rng.integers(2, 8))
+        a = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        d = _encode(a, quality=int(rng.integers(60, 100)), subsampling=2,
+                    restart_marker_blocks=int(rng.integers(4, 40)))
+        sb = _segment_bytes(d)
+        for bits in range(32, 2049, 32):
+            subs = [max(1, -(-8 * b // bits)) for b in sb]
+            if max(_job_sizes(subs, 1000)) > 1024:
+                found = (d, bits, subs)
+                break
+        if found:
+            break
+    assert found, "no overflowing split found"
+    d, bits, subs = found
+    assert max(_job_sizes(subs, 1024 - 32)) <= 1024  # the fixed cap
+    prev = capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, bits)
+    try:
+        coefs = _check_identity([d])
+    finally:
+        capi.set_tuning(capi.MXD_TUNE_HUFF_BITS, prev)
+    assert coefs[0].entropy_pending
