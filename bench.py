@@ -79,10 +79,6 @@ import numpy as np  # noqa: E402
 # 9); e2e_jpeg adds the device-batch rate at 16 queues from a child process
 # (`hwq16`), since the setting is read once, when HIP initialises.  The C2
 # line does not depend on it (profiles/r04/hwq_bench.jsonl).
-# e2e_jpeg's progressive leg measures the device decode of every scan
-# (jpeg_prog) against the host entropy decode: force the device choice, which
-# the library's default leaves to the host above 11 host CPUs
-os.environ.setdefault("MXD_DEVICE_PROGRESSIVE", "1")
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 C = 3
@@ -932,17 +928,15 @@ def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False, device_only=Fa
                     "d2h_bytes_per_image": out_b, "host_split": hsplit,
                     "chain": "as `chain`, but batch(128) into host memory (no device=): the f32 batch is copied "
                              "device -> page-locked staging -> the batch array inside the timed run"}
-        # the same files saved progressive: every scan decoded on the device
-        # (jpeg_prog; MXD_DEVICE_PROGRESSIVE above) against the host entropy
-        # decode
+        # the same files saved progressive: entropy-decoded on the host
+        # (round 6 retired the device decode of progressive scans), finished
+        # and resized on the GPU
         files_c4 = files
         files = bp.make_files(root, "c4p", batch)
         pvalue, pn, pdt, psplit = leg("device")
-        phost, _, _, _ = leg("device_hostent")
-        dprog = capi.JpegCoefs(open(files[0], "rb").read(), device_entropy=True).entropy_progressive
-        progressive = {"value": pvalue, "images": pn, "seconds": pdt, "host_entropy_value": phost,
-                       "device_progressive": dprog, "host_split": psplit,
-                       "files": "the e2e files saved progressive (libjpeg's default progression)"}
+        progressive = {"value": pvalue, "images": pn, "seconds": pdt, "host_split": psplit,
+                       "files": "the e2e files saved progressive (libjpeg's default progression); Huffman decode "
+                                "of every scan on the host, IDCT + colour + resize on the GPU"}
         files = files_c4
         hwq16 = e2e_jpeg_hwq16()
         cpu = None

@@ -38,7 +38,9 @@ extern "C" {
  * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS,
  * MXD_TUNE_HUFF_JOB, MXD_TUNE_JPEG_RGB, mxd_jpeg_plane_sources,
  * mxd_host_stats, mxd_jpeg_coefs_load.
- * 6 (round 6): the knob MXD_TUNE_DEVICE_TIMING and mxd_device_stats. */
+ * 6 (round 6): the knob MXD_TUNE_DEVICE_TIMING and mxd_device_stats;
+ * mxd_jpeg_coefs_entropy_pending no longer reports 2 (progressive files are
+ * entropy-decoded on the host). */
 #define MXD_ABI_VERSION 6
 
 enum mxd_status {
@@ -347,8 +349,9 @@ int mxd_jpeg_coefs_parse(const uint8_t* data, size_t size, int32_t device_entrop
  * reference's exact message. */
 int mxd_jpeg_coefs_load(const char* path, int32_t device_entropy, mxd_jpeg_coefs** out);
 /* *pending = 1 when the coefficients will come from the device entropy decode
- * of a sequential file's one scan, 2 when from the device decode of every scan
- * of a progressive file (round 5), 0 when the host decoded them. */
+ * of a sequential file's one scan, 0 when the host decoded them (progressive
+ * files always: round 5's value 2, every scan of a progressive file decoded
+ * on the device, was retired in round 6 -- DESIGN.md section 8). */
 int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending);
 int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs);
 

@@ -478,7 +478,7 @@ int mxd_jpeg_coefs_load(const char* path, int32_t device_entropy, mxd_jpeg_coefs
 int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending) {
   if (!coefs || !pending) return fail(MXD_ERR_INVALID, "mxd: null argument");
   const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(coefs));
-  *pending = info.entropy_progressive ? 2 : info.entropy_pending ? 1 : 0;
+  *pending = info.entropy_pending ? 1 : 0;
   return MXD_OK;
 }
 

@@ -400,7 +400,7 @@ struct JpegChunk {
     const uint8_t *b, *e;  // raw segment bytes
     int64_t at;            // staged byte offset (relative to words_off)
   };
-  std::vector<Raw> raw;              // per staged segment (hsegs entries, then those of progressive images)
+  std::vector<Raw> raw;              // per staged segment (hsegs entries)
   std::vector<int32_t> seg_first;    // per chunk image: its first raw entry (-1: not pending)
   std::vector<int32_t> seg_count;    // and their number
   int64_t words_off = 0, words_bytes = 0, htabs_off = 0, himgs_off = 0, hsegs_off = 0, hjobs_off = 0;
@@ -409,12 +409,6 @@ struct JpegChunk {
   int32_t huff_threads = 0;
   int64_t huff_lds = 0;  // the largest job's dynamic LDS (its words included when they fit)
   bool huff_search = false;  // some table needs the searching kernel (HuffDev::search)
-  // progressive images decoded on the device (jpeghuff.h jpeg_prog)
-  std::vector<mxd::ProgTabDev> ptabs;
-  std::vector<mxd::ProgImgDev> pimgs;
-  std::vector<mxd::ProgScanDev> pscans;
-  std::vector<mxd::ProgSegDev> psegs;
-  int64_t ptabs_off = 0, pimgs_off = 0, pscans_off = 0, psegs_off = 0;
 };
 
 std::atomic<int64_t> g_plane_sources{0};
@@ -429,110 +423,6 @@ const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c) { return reinterpret_c
 
 int64_t rgb_pitch(int32_t w) { return (((int64_t)w * 3 + 63) & ~(int64_t)63) + 64; }
 
-// A progressive image's scans for jpeg_prog (jpeghuff.h): its tables, scan
-// records in phases, segments (staged like the sequential ones: unstuffed,
-// zero padded, 16-byte aligned); coefficients at coef_rel (coef_off added
-// later).  Phases: a run of single-component scans, each on its component's
-// lane in file order, until an interleaved DC-first scan (lane 0) or a DC
-// refinement (every lane) -- each a phase of its own -- or the LDS table
-// slots run out.
-void prog_image(const mxd::jpeg::Coefs* co, const mxd::jpeg::CoefInfo& info, int64_t coef_rel, int32_t ci,
-                JpegChunk& c) {
-  auto up = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
-  const mxd::jpeg::ProgScans ps = mxd::jpeg::prog_scans(co);
-  const int32_t tab0 = (int32_t)c.ptabs.size(), seg0 = (int32_t)c.psegs.size();
-  const auto* tabs = static_cast<const mxd::ProgTabDev*>(ps.tabs);
-  c.ptabs.insert(c.ptabs.end(), tabs, tabs + ps.ntab);
-  mxd::ProgImgDev im{};
-  im.coef = coef_rel / 2;
-  im.coef_count = info.coef_count;
-  im.aux = (coef_rel + (info.coef_count * 2 + 255) / 256 * 256) / 2;  // the refinement aux area after the planes
-  im.ncomp = (int8_t)info.ncomp;
-  for (int k = 0; k < info.ncomp && k < 3; k++) {
-    im.plane[k] = info.comp[k].off;
-    im.bw[k] = info.comp[k].bw;
-    im.wib[k] = ps.wib[k];
-    im.hib[k] = ps.hib[k];
-    im.h[k] = (int8_t)info.comp[k].h;
-    im.v[k] = (int8_t)info.comp[k].v;
-  }
-  im.mcux = ps.mcux;
-  im.mcuy = ps.mcuy;
-  im.scan0 = (int32_t)c.pscans.size();
-  im.nscan = ps.nscan;
-  // phases: scans of different components run together, one lane per
-  // component, its scans in file order (a first scan may write past its band
-  // on corrupt data: the component's order is kept); an AC refinement reads
-  // the coefficients before its phase starts and writes them after its
-  // decode, so it comes first among its component's scans of a phase and
-  // nothing of that component follows it there
-  int phase = 0, slots = 0;
-  int steps[3] = {0, 0, 0};
-  bool refined[3] = {false, false, false};
-  auto close = [&]() {
-    if (steps[0] + steps[1] + steps[2]) phase++;
-    slots = 0;
-    steps[0] = steps[1] = steps[2] = 0;
-    refined[0] = refined[1] = refined[2] = false;
-  };
-  for (int q = 0; q < ps.nscan; q++) {
-    const mxd::jpeg::ProgScan& r = ps.scans[q];
-    mxd::ProgScanDev d{};
-    d.ns = (int8_t)r.ns;
-    d.ss = (int8_t)r.ss;
-    d.se = (int8_t)r.se;
-    d.ah = (int8_t)r.ah;
-    d.al = (int8_t)r.al;
-    d.rst = r.rst;
-    d.seg0 = seg0 + r.seg0;
-    d.nseg = r.nseg;
-    d.mcus = r.mcus;
-    int ntab = 0;
-    for (int j = 0; j < 4; j++) {
-      d.comp[j] = (int8_t)(j < r.ns ? r.comp[j] : 0);
-      d.tab[j] = j < r.ns && r.tab[j] >= 0 ? tab0 + r.tab[j] : -1;
-      d.slot[j] = -1;
-      ntab += d.tab[j] >= 0;
-    }
-    const bool own = r.ns > 1 || (r.ss == 0 && r.ah != 0);
-    const int cc = r.comp[0];
-    const bool refine = r.ss > 0 && r.ah != 0;
-    if (own || slots + ntab > mxd::kProgSlots || refined[cc] || (refine && steps[cc]) || steps[cc] == 127) close();
-    for (int j = 0; j < r.ns; j++)
-      if (d.tab[j] >= 0) d.slot[j] = (int8_t)slots++;
-    d.phase = phase;
-    d.step = 0;
-    if (own) {
-      d.lane = (int8_t)(r.ss == 0 && r.ah != 0 ? -1 : 0);
-      phase++;
-      slots = 0;
-    } else {
-      d.lane = (int8_t)cc;
-      d.step = (int8_t)steps[cc]++;
-      refined[cc] = refine;
-    }
-    c.pscans.push_back(d);
-  }
-  close();
-  im.nphase = phase;
-  c.pimgs.push_back(im);
-  c.seg_first[ci] = (int32_t)c.raw.size();
-  c.seg_count[ci] = 0;
-  for (int q = 0; q < ps.nscan; q++) {
-    const mxd::jpeg::ProgScan& r = ps.scans[q];
-    for (int g = r.seg0; g < r.seg0 + r.nseg; g++) {
-      mxd::ProgSegDev sd{};
-      sd.word = c.words_bytes / 4;
-      sd.bits = (int32_t)(8 * ps.seg_bytes[g]);
-      c.psegs.push_back(sd);
-      const int64_t raw = ps.seg_end[g] - ps.seg_begin[g];
-      c.raw.push_back({ps.data + ps.seg_begin[g], ps.data + ps.seg_end[g], c.words_bytes});
-      c.words_bytes += up(raw + 4, 16);
-      c.seg_count[ci]++;
-    }
-  }
-}
-
 // Lays out the chunk [first, end) of a JPEG batch whose coefficients are staged
 // at in_off[i]; the tables follow at `tables_at`.
 // foot[i]: image i's resize footprint (x0, x1, y0, y1, inclusive, in image
@@ -544,19 +434,11 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
   auto up = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
   int64_t coef_rel = 0;  // pending images' coefficients, relative to coef_off
   std::vector<int64_t> pend_rel(end - first, -1);
-  std::vector<char> natural(end - first, 0);  // pending coefficients in natural order (progressive)
   c.seg_first.assign(end - first, -1);
   c.seg_count.assign(end - first, 0);
   for (int32_t i = first; i < end; i++) {
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
     if (!info.entropy_pending) continue;
-    if (info.entropy_progressive) {
-      pend_rel[i - first] = coef_rel;
-      natural[i - first] = 1;
-      prog_image(coefs_of(jimg[i].coefs), info, coef_rel, i - first, c);
-      coef_rel += up(info.coef_count * 2, 256) + up(info.coef_count / 2, 256);  // planes, refinement aux
-      continue;
-    }
     const mxd::jpeg::EntropyScan es = mxd::jpeg::entropy_scan(coefs_of(jimg[i].coefs));
     pend_rel[i - first] = coef_rel;
     mxd::HuffImgDev h{};
@@ -702,7 +584,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
       p.bh = cp.bh;
       p.qtab = (int32_t)c.qtabs.size();
       p.coded = cp.coded ? 1 : 0;
-      p.zigzag = pend_rel[i - first] >= 0 && !natural[i - first] ? 1 : 0;  // decoded by jpeg_huff: zig-zag order
+      p.zigzag = pend_rel[i - first] >= 0 ? 1 : 0;  // decoded by jpeg_huff: zig-zag order
       {
         // the footprint on this component's sample grid, one sample wider on
         // each side (fancy upsampling reads a neighbour), in whole blocks
@@ -746,11 +628,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
   c.himgs_off = up(c.htabs_off + (int64_t)(c.htabs.size() * sizeof(mxd::HuffDev)), 256);
   c.hsegs_off = up(c.himgs_off + (int64_t)(c.himgs.size() * sizeof(mxd::HuffImgDev)), 256);
   c.hjobs_off = up(c.hsegs_off + (int64_t)(c.hsegs.size() * sizeof(mxd::HuffSegDev)), 256);
-  c.ptabs_off = up(c.hjobs_off + (int64_t)(c.hjobs.size() * sizeof(mxd::HuffJobDev)), 256);
-  c.pimgs_off = up(c.ptabs_off + (int64_t)(c.ptabs.size() * sizeof(mxd::ProgTabDev)), 256);
-  c.pscans_off = up(c.pimgs_off + (int64_t)(c.pimgs.size() * sizeof(mxd::ProgImgDev)), 256);
-  c.psegs_off = up(c.pscans_off + (int64_t)(c.pscans.size() * sizeof(mxd::ProgScanDev)), 256);
-  c.planes_off = up(c.psegs_off + (int64_t)(c.psegs.size() * sizeof(mxd::ProgSegDev)), 256);
+  c.planes_off = up(c.hjobs_off + (int64_t)(c.hjobs.size() * sizeof(mxd::HuffJobDev)), 256);
   c.imgs_off = up(c.planes_off + (int64_t)(c.planes.size() * sizeof(mxd::JpegPlaneDev)), 256);
   c.q_off = up(c.imgs_off + (int64_t)(c.imgs.size() * sizeof(mxd::JpegImgDev)), 256);
   c.ycc.assign(c.imgs.size(), mxd::YccDev{});
@@ -761,10 +639,6 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
                   256);
   c.dev_end = c.coef_off + coef_rel;
   for (mxd::HuffImgDev& h : c.himgs) h.coef += c.coef_off / 2;
-  for (mxd::ProgImgDev& h : c.pimgs) {
-    h.coef += c.coef_off / 2;
-    h.aux += c.coef_off / 2;
-  }
   for (size_t k = 0, pi = 0; k < (size_t)(end - first); k++) {
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[first + k].coefs));
     const int np = info.ncomp == 1 ? 1 : 3;
@@ -1026,12 +900,6 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         std::memcpy(sl.pin_in + jc.hsegs_off, jc.hsegs.data(), jc.hsegs.size() * sizeof(mxd::HuffSegDev));
         std::memcpy(sl.pin_in + jc.hjobs_off, jc.hjobs.data(), jc.hjobs.size() * sizeof(mxd::HuffJobDev));
       }
-      if (!jc.pimgs.empty()) {
-        std::memcpy(sl.pin_in + jc.ptabs_off, jc.ptabs.data(), jc.ptabs.size() * sizeof(mxd::ProgTabDev));
-        std::memcpy(sl.pin_in + jc.pimgs_off, jc.pimgs.data(), jc.pimgs.size() * sizeof(mxd::ProgImgDev));
-        std::memcpy(sl.pin_in + jc.pscans_off, jc.pscans.data(), jc.pscans.size() * sizeof(mxd::ProgScanDev));
-        std::memcpy(sl.pin_in + jc.psegs_off, jc.psegs.data(), jc.psegs.size() * sizeof(mxd::ProgSegDev));
-      }
       std::memcpy(sl.pin_in + jc.planes_off, jc.planes.data(), jc.planes.size() * sizeof(mxd::JpegPlaneDev));
       for (auto& m : jc.imgs) m.out += jc.rgb_off;
       std::memcpy(sl.pin_in + jc.q_off, jc.qtabs.data(), jc.qtabs.size() * sizeof(uint16_t));
@@ -1164,14 +1032,6 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         }
 #endif
       }
-      if (!jc.pimgs.empty() &&
-          mxd::launch_jpeg_prog(reinterpret_cast<const uint32_t*>(sl.dev_in + jc.words_off),
-                                reinterpret_cast<const mxd::ProgTabDev*>(sl.dev_in + jc.ptabs_off),
-                                reinterpret_cast<const mxd::ProgImgDev*>(sl.dev_in + jc.pimgs_off),
-                                reinterpret_cast<const mxd::ProgScanDev*>(sl.dev_in + jc.pscans_off),
-                                reinterpret_cast<const mxd::ProgSegDev*>(sl.dev_in + jc.psegs_off),
-                                (int32_t)jc.pimgs.size(), reinterpret_cast<int16_t*>(sl.dev_in), sl.stream))
-        return fail(MXD_ERR_DEVICE, std::string("jpeg progressive decode launch: ") + hipGetErrorString(hipGetLastError()));
       mxd::launch_jpeg_idct(reinterpret_cast<const int16_t*>(sl.dev_in),
                             reinterpret_cast<const uint16_t*>(sl.dev_in + jc.q_off),
                             reinterpret_cast<const mxd::JpegPlaneDev*>(sl.dev_in + jc.planes_off),
@@ -1327,9 +1187,6 @@ int pixmap_host(const mxd_pixmap* images, int32_t n, int32_t op, int32_t device)
   return MXD_OK;
 }
 
-
-// (jpeg.cpp's choice of the progressive device decode)
-int host_cpus() { return host_cpu_budget(); }
 
 }  // namespace capi
 }  // namespace mxd

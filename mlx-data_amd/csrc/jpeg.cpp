@@ -28,14 +28,6 @@
 
 #include "jpeghuff.h"
 
-namespace mxd {
-namespace capi {
-// hostpath.cpp: the CPUs this process may keep busy (this weak stand-in
-// serves builds of the decoder alone: tests/native, tools/jpeg_fuzz.cpp)
-__attribute__((weak)) int host_cpus() { return 1; }
-}  // namespace capi
-}  // namespace mxd
-
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -967,26 +959,6 @@ size_t scan_to_marker_avx512(const uint8_t* data, size_t p, size_t size, int64_t
   return scan_to_marker_scalar(data, p, size, dropped);
 }
 
-static_assert(kLook == kProgLook, "ProgTabDev copies Huff::look");
-
-// Progressive files' scans decoded on the device (jpeghuff.h jpeg_prog) or
-// on the host.  The device decode is one serial chain per component: 3.7x
-// the host entropy decode with one pipeline worker, but at 16 workers the
-// host's cores overtake it (6.2-7.8 k against 7.5-8.5 k
-// img/s on C4-shape files).  So by default it runs on the device when the
-// process has fewer than 12 CPUs to spend (the crossover), on the host
-// otherwise; MXD_DEVICE_PROGRESSIVE=1 / 0 forces it either way
-// (MXD_NO_DEVICE_PROGRESSIVE=1 is the same as =0).
-bool device_progressive() {
-  static const bool on = [] {
-    if (const char* e = std::getenv("MXD_DEVICE_PROGRESSIVE")) return std::atoi(e) != 0;
-    if (const char* e = std::getenv("MXD_NO_DEVICE_PROGRESSIVE"))
-      if (std::atoi(e) == 1) return false;
-    return capi::host_cpus() < 12;
-  }();
-  return on;
-}
-
 bool have_avx512_bytes() {  // (MXD_NO_AVX512=1: the scalar forms, for A/Bs)
   static const bool ok = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vbmi2") &&
                          !(std::getenv("MXD_NO_AVX512") && std::atoi(std::getenv("MXD_NO_AVX512")) == 1);
@@ -1041,13 +1013,7 @@ struct Decoder {
   bool device_entropy = false;
   bool pending = false;
   int scans = 0;
-  // device_entropy on a progressive Huffman file: every scan recorded
-  // (record_prog_scan), its tables snapshotted; pending once parse_held finds
-  // the progression complete (jpeghuff.h jpeg_prog)
-  bool prog_dev = false;
   bool eoi = false;
-  std::vector<ProgScan> prog;
-  std::vector<ProgTabDev> prog_tabs;
   std::vector<int64_t> seg_begin, seg_end;
   std::vector<int64_t> seg_bytes;  // unstuffed bytes of each segment (what unstuff() writes)
   int scan_ns = 0;
@@ -1162,9 +1128,10 @@ struct Decoder {
     progressive = marker == 0xC2 || marker == 0xCA;
     arith = marker == 0xC9 || marker == 0xCA;
     lossless = marker == 0xC3;
-    if ((arith || lossless) && device_entropy) throw NotDevice{};
-    prog_dev = progressive && device_entropy;
-    if (prog_dev && !device_progressive()) throw NotDevice{};
+    // progressive files: every scan's entropy decode on the host (round 5's
+    // device form, one serial chain per component, lost to the host decode
+    // at 16 workers and was retired in round 6: DESIGN.md section 8)
+    if ((arith || lossless || progressive) && device_entropy) throw NotDevice{};
     for (int i = 0; i < ncomp; i++) {
       Component& c = comp[i];
       c.id = u8();
@@ -1243,8 +1210,7 @@ struct Decoder {
     const int ss = u8(), se = u8(), a = u8();
     const int ah = a >> 4, al = a & 15;
     if (device_entropy) {
-      if (prog_dev) record_prog_scan(sc, ns, ss, se, ah, al);
-      else record_scan(sc, ns);
+      record_scan(sc, ns);
       any_scan = true;
       return;
     }
@@ -1354,64 +1320,6 @@ struct Decoder {
     }
     if ((int64_t)seg_begin.size() - seg0 != nseg) throw NotDevice{};
     pos = seg_end.back();  // marker parsing resumes at the marker
-  }
-
-  // One scan of a progressive file for the device (jpeghuff.h jpeg_prog):
-  // parameters, progression status (as read_sos keeps it for the host
-  // decode), table snapshots and segments.  Whatever the host decoder would
-  // refuse, or that the device decode does not cover, throws NotDevice (the
-  // host decodes the file and reports its own error).
-  void record_prog_scan(Component** sc, int ns, int ss, int se, int ah, int al) {
-    if (ncomp != 1 && ncomp != 3) throw NotDevice{};
-    if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || ah > 13 || al > 13) throw NotDevice{};
-    input_scans++;
-    for (int i = 0; i < ns; i++) {
-      const int ci = (int)(sc[i] - comp);
-      for (int k = std::min(ss, 1); k <= std::min(std::max(se, 9), 9); k++)
-        coef_bits[4 + ci][k] = input_scans > 1 ? coef_bits[ci][k] : 0;
-      for (int k = ss; k <= std::min(se, 9); k++) coef_bits[ci][k] = al;
-    }
-    ProgScan r{};
-    r.ns = ns;
-    r.ss = ss;
-    r.se = se;
-    r.ah = ah;
-    r.al = al;
-    r.rst = restart_interval;
-    int bpm = 0;
-    for (int i = 0; i < 4; i++) r.tab[i] = -1;
-    auto snapshot = [&](const Huff& h) {
-      ProgTabDev t;
-      std::memset(&t, 0, sizeof t);
-      std::memcpy(t.look, h.look, sizeof t.look);
-      std::memcpy(t.maxcode, h.maxcode, sizeof t.maxcode);
-      std::memcpy(t.valoffset, h.valoffset, sizeof t.valoffset);
-      std::memcpy(t.vals, h.vals, (size_t)h.nvals);
-      for (size_t q = 0; q < prog_tabs.size(); q++)
-        if (std::memcmp(&prog_tabs[q], &t, sizeof t) == 0) return (int)q;
-      prog_tabs.push_back(t);
-      return (int)prog_tabs.size() - 1;
-    };
-    for (int i = 0; i < ns; i++) {
-      Component& c = *sc[i];
-      r.comp[i] = (int)(sc[i] - comp);
-      bpm += ns == 1 ? 1 : c.h * c.v;
-      if (ss == 0 && ah == 0) {
-        if (c.dc_tbl > 3 || !dc[c.dc_tbl].present) throw NotDevice{};
-        for (int q = 0; q < dc[c.dc_tbl].nvals; q++)
-          if (dc[c.dc_tbl].vals[q] > 15) throw NotDevice{};  // check_dc_table's failure
-        r.tab[i] = snapshot(dc[c.dc_tbl]);
-      } else if (ss > 0) {
-        if (c.ac_tbl > 3 || !ac[c.ac_tbl].present) throw NotDevice{};
-        r.tab[i] = snapshot(ac[c.ac_tbl]);
-      }
-    }
-    if (bpm > 10) throw NotDevice{};
-    r.mcus = ns == 1 ? (int64_t)sc[0]->wib * sc[0]->hib : (int64_t)mcux * mcuy;
-    r.seg0 = (int)seg_begin.size();
-    record_segments(r.mcus);
-    r.nseg = (int)seg_begin.size() - r.seg0;
-    prog.push_back(r);
   }
 
   // R: Bits or Arith (restart(), insufficient)
@@ -2160,17 +2068,6 @@ Coefs* parse_held(std::unique_ptr<Coefs> c, std::string* err) {
     d.parse();
     if (!d.frame) fail("Invalid JPEG file structure: missing SOF marker");
     if (d.color_space() < 0) fail("unhandled format");
-    if (d.prog_dev) {
-      // every scan recorded: on the device when the file ends at EOI and its
-      // progression leaves the first ten coefficients of every component
-      // exact (libjpeg's block smoothing has nothing to estimate: smoothing_ok)
-      if (!d.eoi || d.prog.empty()) throw NotDevice{};
-      for (int ci = 0; ci < d.ncomp; ci++)
-        for (int k = 0; k < 10; k++)
-          if (d.coef_bits[ci][k] != 0) throw NotDevice{};
-      d.finalize_quant();
-      d.pending = true;
-    }
     if (!d.pending) throw NotDevice{};  // no scan
     // decode_coefs' check: output() reaches it exactly for non-integral factors
     if (d.ncomp > 1)
@@ -2450,7 +2347,6 @@ CoefInfo coef_info(const Coefs* c) {
   r.coef = d.pending ? nullptr : d.coefbuf.data();
   r.coef_count = d.coef_total;
   r.entropy_pending = d.pending;
-  r.entropy_progressive = d.pending && d.prog_dev;
   for (int i = 0; i < d.ncomp; i++) {
     const Component& k = d.comp[i];
     CoefPlane& p = r.comp[i];
@@ -2468,25 +2364,6 @@ CoefInfo coef_info(const Coefs* c) {
   return r;
 }
 
-ProgScans prog_scans(const Coefs* c) {
-  const Decoder& d = c->d;
-  ProgScans r{};
-  r.nscan = (int)d.prog.size();
-  r.scans = d.prog.data();
-  r.ntab = (int)d.prog_tabs.size();
-  r.tabs = d.prog_tabs.data();
-  r.seg_begin = d.seg_begin.data();
-  r.seg_end = d.seg_end.data();
-  r.seg_bytes = d.seg_bytes.data();
-  r.data = d.data;
-  r.mcux = d.mcux;
-  r.mcuy = d.mcuy;
-  for (int i = 0; i < d.ncomp && i < 4; i++) {
-    r.wib[i] = d.comp[i].wib;
-    r.hib[i] = d.comp[i].hib;
-  }
-  return r;
-}
 
 bool finish(const Coefs* c, uint8_t* dst, int64_t dst_stride, std::string* err) {
   try {

@@ -46,7 +46,6 @@ struct CoefInfo {
   CoefPlane comp[4];
   bool device_ok;   // grey, YCbCr or RGB: the device kernels can finish it
   bool entropy_pending;  // the coefficients come from the device entropy decode (jpeghuff.h)
-  bool entropy_progressive;  // ... of every scan of a progressive file (jpeghuff.h jpeg_prog; prog_scans)
 };
 
 // Entropy decode (every error decode() reports, from here); nullptr + *err.
@@ -93,27 +92,6 @@ EntropyScan entropy_scan(const Coefs* c);
 // small per-thread cache of built tables: two calls on one thread that
 // return the same serial gave the same table.
 uint64_t device_table(const Coefs* c, int cls, int table_id, void* huff_dev);
-// The scans of a progressive file pending on the device (entropy_progressive):
-// per scan its parameters, its tables (ProgTabDev, snapshotted at its SOS)
-// and its segments (raw byte ranges of `data`, unstuffed sizes).
-struct ProgScan {
-  int ns, comp[4], ss, se, ah, al;
-  int tab[4];      // index into tabs per scan component (-1: none)
-  int rst;         // restart interval at the scan
-  int seg0, nseg;  // its segments
-  int64_t mcus;
-};
-struct ProgScans {
-  int nscan;
-  const ProgScan* scans;
-  int ntab;
-  const void* tabs;  // ProgTabDev[ntab]
-  const int64_t *seg_begin, *seg_end, *seg_bytes;
-  const uint8_t* data;
-  int mcux, mcuy;
-  int wib[4], hib[4];
-};
-ProgScans prog_scans(const Coefs* c);
 // Unstuffed bytes of the raw segment [b, e) (0xFF 0x00 -> 0xFF, fill 0xFF
 // bytes dropped) into dst (>= e - b bytes); returns their count.
 int64_t unstuff(const uint8_t* b, const uint8_t* e, uint8_t* dst);

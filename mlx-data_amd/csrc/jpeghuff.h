@@ -188,65 +188,5 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
                      const HuffJobDev* jobs, int32_t njobs, int32_t threads, int64_t lds_bytes, HuffPubDev* pub,
                      HuffCtlDev* ctl, int16_t* coef, bool search, void* stream);
 
-// ---- progressive files (round 5; jpeghuff.hip
-// jpeg_prog).  Every scan of a progressive Huffman-coded file (jdphuff.c:
-// DC first / refine, AC first with EOB runs, AC refinement) decoded on the
-// device, one workgroup (one wave) per image.  The scans run in PHASES:
-// single-component scans of different components have no data in common, so
-// a phase runs them at once, one lane per component, each lane its
-// component's scans in file order.  An interleaved DC-first scan is a phase of its
-// own on lane 0, a DC refinement (one bit per block, no Huffman code) a
-// phase of its own over all 64 lanes, and an AC refinement's coefficient
-// reads and writes are done by the whole wave before and after its lane
-// decodes the symbols (jpeghuff.hip prog_ac_refine).  Coefficients
-// are written in natural order (the host decoder's layout, which jpeg_idct
-// reads with zigzag = 0).  The host parses the markers, snapshots each
-// scan's tables at its SOS (later DHTs may replace them) and stages the
-// unstuffed segments like the sequential path's; files whose scans leave
-// any of the first ten coefficients inexact (block smoothing applies) or
-// whose data does not end at a marker are decoded on the host.
-constexpr int kProgLook = 9;  // lookahead bits of ProgTabDev (jpeg.cpp's Huff)
-constexpr int kProgSlots = 8;  // LDS table slots of a phase
-struct ProgTabDev {            // jdhuff.c derived table: (length << 8) | symbol per 9-bit prefix, 0 = longer
-  uint16_t look[1 << kProgLook];
-  int32_t maxcode[18];
-  int32_t valoffset[18];
-  uint8_t vals[256];
-};
-static_assert(sizeof(ProgTabDev) % 16 == 0, "ProgTabDev: whole 16-byte chunks");
-struct ProgScanDev {
-  int8_t ns, ss, se, ah, al;
-  int8_t lane;   // its component's lane in the phase, -1: every lane (DC refinement)
-  int8_t step;   // its place among its lane's scans of the phase
-  int8_t pad0;
-  int8_t comp[4];  // frame components, SOS order
-  int8_t slot[4];  // LDS slot of each component's table (-1: none)
-  int32_t tab[4];  // ProgTabDev index of each (launch-wide; -1: none)
-  int32_t phase;
-  int32_t rst;     // MCUs per segment (0: one segment)
-  int32_t seg0, nseg;  // ProgSegDev range (launch-wide)
-  int64_t mcus;
-};
-static_assert(sizeof(ProgScanDev) == 56, "ProgScanDev layout");
-struct ProgImgDev {
-  int64_t coef;        // first coefficient (int16 elements of the coefficient buffer)
-  int64_t coef_count;  // its coefficients (a multiple of 64), zeroed by the kernel first
-  int64_t plane[3];    // each component's first coefficient, relative to coef
-  int32_t bw[3], wib[3], hib[3];  // blocks per plane row; blocks of the component proper
-  int8_t h[3], v[3];
-  int8_t ncomp, pad0;
-  int32_t mcux, mcuy;
-  int32_t scan0, nscan, nphase, pad1;
-  int64_t aux;  // refinement scratch: per block a nonzero mask and a 3-word delta (coef_count / 2 bytes, 8-aligned)
-};
-static_assert(sizeof(ProgImgDev) == 120, "ProgImgDev layout");
-struct ProgSegDev {
-  int64_t word;  // first 32-bit word of its unstuffed bytes (16-byte aligned)
-  int32_t bits;  // data bits; past them zeros (libjpeg's insufficient-data rule)
-  int32_t pad;
-};
-// Enqueues the decode of `nimg` progressive images (coefficients in `coef`).
-int launch_jpeg_prog(const uint32_t* words, const ProgTabDev* tabs, const ProgImgDev* imgs, const ProgScanDev* scans,
-                     const ProgSegDev* segs, int32_t nimg, int16_t* coef, void* stream);
 
 }  // namespace mxd

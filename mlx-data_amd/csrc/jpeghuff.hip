@@ -17,8 +17,9 @@
 //      again from the true state;
 //   3. block counts prefix-summed per segment -> each subsequence's first
 //      block; the job's exit state and block index published;
-//   4. the job's blocks zeroed by the whole workgroup (whole lines);
-//   5. write pass: decode again, storing AC coefficients and DC differences;
+//   4. (round 6: no separate zeroing pass, see decode_job)
+//   5. write pass: decode again, each block's own positions zeroed as the
+//      subsequence enters it, then its AC coefficients and DC differences;
 //   6. DC: per-component sums of the differences prefix-summed per segment
 //      (the continued segment's from the previous job's published sums),
 //      then each subsequence turns its blocks' differences into values.
@@ -207,8 +208,6 @@ struct Shared {
   int3 scan3[kHuffThreads / 64];
   int32_t flag[2];
   int64_t pred_blocks;             // the previous job's published block index
-  int64_t zero_range[2];           // the job's first and last block (jpeghuff.hip step 4)
-  int32_t zero_k[2];               // the job's part of them starts at / ends before these positions
   int32_t pred_dc[3];
 #ifdef MXD_HUFF_STAMPS
   // diagnostic build: s_memtime at the phase boundaries ([0] start, [1]
@@ -404,22 +403,6 @@ struct Dec {
     return end;
   }
 };
-
-// Coefficient offset of block g (decode order) of the image: blocks number
-// < 2^31 (the host refuses larger images), so 32-bit divisions.
-__device__ __forceinline__ int64_t block_addr(const HuffImgDev& im, int64_t g64) {
-  const uint32_t g = (uint32_t)g64;
-  if (!im.interleaved) {
-    const uint32_t by = g / (uint32_t)im.mcux, bx = g - by * (uint32_t)im.mcux;
-    return im.coef + im.plane[0] + ((int64_t)by * im.bw[0] + bx) * 64;
-  }
-  const uint32_t m = g / (uint32_t)im.bpm;
-  const int j = (int)(g - m * (uint32_t)im.bpm);
-  const int c = im.blk_comp[j];
-  const uint32_t my = m / (uint32_t)im.mcux, mx = m - my * (uint32_t)im.mcux;
-  const int64_t bx = (int64_t)mx * im.comp_h[c] + im.blk_dx[j], by = (int64_t)my * im.comp_v[c] + im.blk_dy[j];
-  return im.coef + im.plane[c] + (by * im.bw[c] + bx) * 64;
-}
 
 // Dynamic LDS of a job: its tables, its segment records, then (job.lds)
 // its words.
@@ -650,60 +633,48 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
                       ((uint64_t)(uint8_t)sh.out_k[t] << 40));
   }
 
-  // 4. Zero the job's blocks (the write pass stores only the symbols'
-  // positions): every block it decodes whole or in part -- [z0, z1) in decode
-  // order, contiguous over the job's segments; the segment's last
-  // subsequence's range runs to the segment's end, which leaves the blocks of
-  // data that ran out early zero (libjpeg's insufficient-data rule) -- by the
-  // whole workgroup in 16-byte pieces, consecutive threads on consecutive
-  // pieces, so a block's 128 bytes go out as one line.  Not the first block
-  // when the previous job decodes its start, nor the last when the next job
-  // decodes its end: the neighbouring job writes into those with no barrier
-  // in between, so their owners here zero them position by position.
+  // 4. (no separate zeroing pass) The write pass stores only the symbols'
+  // positions, so each own subsequence zeroes, as it enters a block, the
+  // positions of that block it decodes -- [ke, 64) of its first block, [0, kx)
+  // of the block it ends inside, whole blocks in between -- immediately
+  // before its stores into them: a block's 128 bytes are written whole while
+  // the line is in the XCD's L2, instead of zeroed for the whole job first
+  // (72 MB per C4 call, more than the L2s hold) and then reached by scattered
+  // 2-byte stores that HBM took as partial-line writes (round 5: 2.8x the
+  // coefficient bytes written).  Neighbouring subsequences' ranges are
+  // disjoint, so no ordering between threads is needed; a thread's zeros
+  // precede its own stores to the same addresses in program order.  A
+  // segment's last subsequence also zeroes the blocks to the segment's end
+  // that data running out early leaves undecoded (libjpeg's insufficient-data
+  // rule).
   const int ke = sh.in_k[t];
   const int32_t start_pos = sh.in_pos[t];
   const int64_t gx = g + my_done;                   // the block it ends inside (non-last)
   const int kx = u.seg_last ? 0 : sh.out_k[t];
   const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
   int16_t* const icoef = coef + im.coef;            // the image's coefficients
-  // the job's first block (from position kf on: the previous job decodes its
-  // start) and its last (to position kl: the next job decodes the rest)
-  if (act && t == job.warm) {
-    sh.zero_range[0] = g;
-    sh.zero_k[0] = g < seg_block1 ? ke : 0;
-  }
-  if (act && u.job_last) {
-    sh.zero_range[1] = u.seg_last ? seg_block1 : gx;
-    sh.zero_k[1] = gx < seg_block1 ? kx : 0;
-  }
-  __syncthreads();
-  {
-    const int64_t first = sh.zero_range[0], last = sh.zero_range[1];
-    const int kf = sh.zero_k[0], kl = sh.zero_k[1];
-    const int64_t z0 = first + (kf != 0 ? 1 : 0), pieces = (last - z0) * 8;
-    if (t < pieces) {
-      // thread t's pieces: t, t + blockDim, ... -- blocks blockDim / 8 apart,
-      // reached by a cursor jump instead of a division per piece
-      const uint32_t jump = blockDim.x >> 3, jq = jump / bpm, jr = jump - jq * bpm;
-      BlockCursor zc;
-      zc.set((uint32_t)(z0 + (t >> 3)), bpm, mcux);
-      for (int64_t c = t; c < pieces; c += blockDim.x) {
-        reinterpret_cast<uint4*>(icoef + zc.off(sh))[t & 7] = uint4{0u, 0u, 0u, 0u};
-        zc.advance(jq, jr, bpm, mcux);
+  // positions [k0, k1) of block b: whole 16-byte pieces, 2-byte stores at the ends
+  auto zero_own = [](int16_t* b, int k0, int k1) {
+    if (k0 == 0 && k1 == 64) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) reinterpret_cast<uint4*>(b)[i] = uint4{0u, 0u, 0u, 0u};
+      return;
+    }
+    for (int q = k0; q < k1;) {
+      if ((q & 7) == 0 && q + 8 <= k1) {
+        *reinterpret_cast<uint4*>(b + q) = uint4{0u, 0u, 0u, 0u};
+        q += 8;
+      } else {
+        b[q++] = 0;
       }
     }
-    auto zero = [&](int64_t b, int k0, int k1) {
-      int16_t* d = coef + block_addr(im, b);
-      for (int q = k0; q < k1; q++) d[q] = 0;
-    };
-    if (t == job.warm && kf != 0) zero(first, kf, last == first && kl != 0 ? kl : 64);
-    if (act && u.job_last && kl != 0 && !(last == first && kf != 0)) zero(last, 0, kl);
-  }
-  // the start / exit / block-count arrays are free from here on: each thread
-  // keeps its DC-difference sums per component in its own slots of them
+  };
+  // the start / exit / block-count arrays are free from here on (after every
+  // thread has read its segment's first prefix above): each thread keeps its
+  // DC-difference sums per component in its own slots of them
+  __syncthreads();
   int* const dcslot[3] = {&sh.done[t], &sh.in_pos[t], &sh.out_pos[t]};
   *dcslot[0] = *dcslot[1] = *dcslot[2] = 0;
-  __syncthreads();  // the zeros land before the coefficients
 
   // 5. write pass (own subsequences)
   Dec<SEARCH> dec;
@@ -720,6 +691,10 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     cur.set((uint32_t)min(g, seg_block1 - 1), bpm, mcux);
     cur0 = cur;
     int16_t* blk = icoef + cur.off(sh);
+    // the positions of block g this subsequence decodes: to kx in the block it
+    // ends inside, else to the block's end
+    auto own_end = [&](int64_t gb) { return !u.seg_last && gb == gx ? kx : 64; };
+    if (g < seg_block1) zero_own(blk, ke, own_end(g));
     int32_t rem = u.end - start_pos;
     for (;;) {
       if (rem <= 0 || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && u.end - rem > u.sg.bits)) break;
@@ -736,6 +711,15 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
         g++;
         cur.next(bpm, mcux);
         blk = icoef + cur.off(sh);  // past the segment's last block when g == seg_block1: never stored through
+        if (g < seg_block1) zero_own(blk, 0, own_end(g));
+      }
+    }
+    if (u.seg_last && g < seg_block1) {
+      // data ran out at an MCU boundary: the rest of the segment stays zero
+      BlockCursor zc = cur;
+      for (int64_t q = g; q < seg_block1; q++) {
+        zero_own(icoef + zc.off(sh), 0, 64);
+        zc.next(bpm, mcux);
       }
     }
     dc0 = g_first + (ke != 0 ? 1 : 0);
@@ -927,542 +911,6 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
 }
 
 
-// ---------------------------------------------------------------- progressive
-// jpeg_prog (jpeghuff.h): one wave per image; the scans of a phase run on
-// the lanes of their components, each scan in the host decoder's order of
-// operations (jpeg.cpp Decoder::decode_scan, jdphuff.c), so the coefficients
-// are the host's bit for bit.
-
-// jpeg_natural_order with libjpeg's 16 extra entries (a corrupt run past 63
-// lands on 63)
-__device__ constexpr int8_t kNat80[80] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
-    6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
-    39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
-
-struct ProgShared {
-  ProgTabDev tab[kProgSlots];
-  int8_t nat[80];
-};
-
-// One symbol (jpeg.cpp Bits::decode: the 9-bit lookahead, then the canonical
-// search; no code within 16 bits: 16 bits consumed, symbol 0)
-template <class R>
-__device__ __forceinline__ int prog_sym(R& r, const ProgTabDev& t) {
-  const uint32_t w = r.win();
-  const int e = t.look[w >> (32 - kProgLook)];
-  if (e) {
-    r.advance(e >> 8);
-    return e & 0xff;
-  }
-  int l = kProgLook + 1;
-  while (l <= 16 && (int32_t)(w >> (32 - l)) > t.maxcode[l]) l++;
-  if (l > 16) {
-    r.advance(16);
-    return 0;
-  }
-  r.advance(l);
-  return t.vals[((int32_t)(w >> (32 - l)) + t.valoffset[l]) & 0xff];
-}
-template <class R>
-__device__ __forceinline__ int prog_get(R& r, int n) {  // n <= 16
-  const int v = n ? (int)(r.win() >> (32 - n)) : 0;
-  r.advance(n);
-  return v;
-}
-__device__ __forceinline__ int prog_extend(int v, int s) { return s ? extend_nz((uint32_t)v, s) : 0; }
-
-// Per-component fields picked by selects (a dynamic index into the image
-// record would put it in scratch memory, a load per use)
-template <class T>
-__device__ __forceinline__ T pick3(const T (&a)[3], int c) {
-  return c == 0 ? a[0] : c == 1 ? a[1] : a[2];
-}
-struct CompGeom {
-  int64_t base;  // first coefficient of the component's plane
-  int32_t bw, wib, h, v;
-  __device__ __forceinline__ CompGeom(const ProgImgDev& im, int c)
-      : base(im.coef + pick3(im.plane, c)), bw(pick3(im.bw, c)), wib(pick3(im.wib, c)), h(pick3(im.h, c)),
-        v(pick3(im.v, c)) {}
-};
-
-// One lane's bit reader over a segment staged in LDS (byte-swapped words, a
-// zero word after them): a 64-bit buffer refilled a word at a time when 32 or
-// fewer bits remain, the next word's LDS load issued one refill ahead -- so
-// a step waits on LDS only when its lookup does (LdsReader, built for the
-// many-lane sequential kernel, loads a word per step)
-struct LdsBits {
-  const uint32_t* w;
-  int32_t nw, q;  // words: staged (w[nw] is the zero word), taken into buf
-  uint64_t buf;
-  int32_t cnt;    // bits of buf not yet consumed (33..64 between steps)
-  uint32_t nxt;   // w[q], loaded ahead
-  __device__ __forceinline__ uint32_t word(int32_t i) const { return w[min(i, nw)]; }
-  __device__ __forceinline__ void init(const void* base, int32_t w0, int32_t nwords, int32_t) {
-    w = static_cast<const uint32_t*>(base) + w0;
-    nw = nwords;
-  }
-  __device__ __forceinline__ void seek(int32_t) {  // (segment start only)
-    buf = (uint64_t)word(0) << 32 | word(1);
-    cnt = 64;
-    q = 2;
-    nxt = word(2);
-  }
-  __device__ __forceinline__ uint32_t win() const { return (uint32_t)(buf >> 32); }
-  __device__ __forceinline__ void advance(int n) {  // n <= 31
-    buf <<= n;
-    cnt -= n;
-    if (cnt <= 32) {
-      buf |= (uint64_t)nxt << (32 - cnt);
-      cnt += 32;
-      q++;
-      nxt = word(q);
-    }
-  }
-  __device__ __forceinline__ int32_t pos() const { return q * 32 - cnt; }
-};
-
-// Where a lane's scan reads its segments: the words in device memory, or
-// (at >= 0) the copy the wave staged in LDS for the phase -- each segment's
-// words byte-swapped and followed by a zero word, the scan's segments one
-// after another from `at` (an LDS read has no wait on outstanding stores,
-// while a device-memory reader's refills wait for every memory operation in
-// flight: the coefficient stores included)
-struct ProgSrc {
-  const uint32_t* words;
-  const uint32_t* lds;
-  int32_t at;
-};
-template <class R>
-struct ProgSeg {
-  R r;
-  int32_t bits;
-  __device__ __forceinline__ void open(const ProgSrc& src, const ProgSegDev& sg, int32_t& at) {
-    bits = sg.bits;
-    const int32_t nw = (bits + 31) >> 5;
-    if constexpr (std::is_same<R, GlobalReader>::value) {
-      r.init(src.words, (int32_t)sg.word, nw, 0);
-    } else {
-      r.init(src.lds, at, nw, nw);
-      at += nw + 1;
-    }
-    r.seek(0);
-  }
-  // libjpeg's insufficient data: some symbol read past the segment's end
-  __device__ __forceinline__ bool out() const { return r.pos() > bits; }
-};
-
-// DC first (Ah = 0), any number of components, on one lane.
-template <class R>
-__device__ void prog_dc_first(const ProgSrc& src, const ProgImgDev& im, const ProgScanDev& sc,
-                              const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
-  int32_t at = src.at;
-  const int ns = sc.ns;
-  const CompGeom g0(im, sc.comp[0]), g1(im, sc.comp[1]), g2(im, sc.comp[2]);
-  const int t0 = sc.slot[0], t1 = sc.slot[1], t2 = sc.slot[2];
-  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
-  const int mult = 1 << sc.al;
-  const int64_t row = ns == 1 ? g0.wib : im.mcux;
-  for (int s = 0; s < sc.nseg; s++) {
-    ProgSeg<R> g;
-    g.open(src, segs[sc.seg0 + s], at);
-    int pred0 = 0, pred1 = 0, pred2 = 0;
-    const int64_t m0 = (int64_t)s * per, m1 = min(sc.mcus, m0 + per);
-    int64_t my = m0 / row, mx = m0 - my * row;
-    for (int64_t m = m0; m < m1; m++) {
-      if (g.out()) break;
-#pragma unroll
-      for (int i = 0; i < 3; i++) {
-        if (i >= ns) break;
-        const CompGeom& cg = i == 0 ? g0 : i == 1 ? g1 : g2;
-        const ProgTabDev& t = sh.tab[i == 0 ? t0 : i == 1 ? t1 : t2];
-        int& pred = i == 0 ? pred0 : i == 1 ? pred1 : pred2;
-        const int nh = ns > 1 ? cg.h : 1, nv = ns > 1 ? cg.v : 1;
-        for (int y = 0; y < nv; y++)
-          for (int x = 0; x < nh; x++) {
-            const int z = prog_sym(g.r, t);
-            pred += prog_extend(prog_get(g.r, z), z);
-            const int64_t bx = mx * nh + x, by = my * nv + y;
-            coef[cg.base + (by * cg.bw + bx) * 64] = (int16_t)(pred * mult);
-          }
-      }
-      if (++mx == row) {
-        mx = 0;
-        my++;
-      }
-    }
-  }
-}
-
-// AC first (Ah = 0) of one component.
-template <class R>
-__device__ void prog_ac_first(const ProgSrc& src, const ProgImgDev& im, const ProgScanDev& sc,
-                              const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
-  int32_t at = src.at;
-  const CompGeom cg(im, sc.comp[0]);
-  const ProgTabDev& t = sh.tab[sc.slot[0]];
-  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
-  const int ss = sc.ss, se = sc.se, al = sc.al;
-  for (int s = 0; s < sc.nseg; s++) {
-    ProgSeg<R> g;
-    g.open(src, segs[sc.seg0 + s], at);
-    int eobrun = 0;
-    const int64_t m0 = (int64_t)s * per, m1 = min(sc.mcus, m0 + per);
-    int64_t by = m0 / cg.wib, bx = m0 - by * cg.wib;
-    for (int64_t m = m0; m < m1; m++) {
-      if (g.out()) break;
-      int16_t* blk = coef + cg.base + (by * cg.bw + bx) * 64;
-      if (++bx == cg.wib) {
-        bx = 0;
-        by++;
-      }
-      if (eobrun > 0) {
-        eobrun--;
-        continue;
-      }
-      for (int k = ss; k <= se; k++) {
-        const int rs = prog_sym(g.r, t);
-        const int r = rs >> 4, z = rs & 15;
-        if (z) {
-          k += r;
-          blk[sh.nat[k]] = (int16_t)(prog_extend(prog_get(g.r, z), z) * (1 << al));
-        } else if (r == 15) {
-          k += 15;
-        } else {
-          eobrun = 1 << r;
-          if (r) eobrun += prog_get(g.r, r);
-          eobrun--;
-          break;
-        }
-      }
-    }
-  }
-}
-
-// AC refinement (Ah != 0) of one component (jpeg.cpp Bits::block_refine),
-// in three steps so that the lane decoding the symbols never waits on
-// coefficient memory:
-//   1. (every lane) each block's nonzero history as a 64-bit mask in zigzag
-//      order into the image's aux area, its delta record zeroed;
-//   2. (the scan's lane) the symbols: per symbol the zero-history positions
-//      it skips and the position of a new coefficient found with mask
-//      arithmetic, the correction bits of the nonzero positions passed read
-//      together (they come in position order: one bit per nonzero position
-//      of the band, EOB runs included) -- per block a delta record (the
-//      correction bits packed, new positions, their signs);
-//   3. (every lane) the deltas applied to the blocks (jpeg.cpp's fix(): a
-//      correction bit adds p1 / m1 to a coefficient whose Al bit is clear).
-__device__ __forceinline__ uint64_t zz_band(int a, int b) {  // zigzag positions a..b (empty when a > b)
-  return a > b ? 0ull : (~0ull >> (63 - b)) & (~0ull << a);
-}
-struct ProgAux {  // the image's aux area: per block of the image (coefficient block index)
-  uint64_t* mask;   // nonzero history
-  uint64_t* delta;  // 3 per block: correction bits (first read at the top), new positions, their signs
-  __device__ __forceinline__ ProgAux(const ProgImgDev& im, int16_t* coef) {
-    mask = reinterpret_cast<uint64_t*>(coef + im.aux);
-    delta = mask + im.coef_count / 64;
-  }
-};
-
-__device__ void prog_refine_masks(const ProgImgDev& im, const ProgScanDev& sc, int16_t* coef) {
-  const CompGeom cg(im, sc.comp[0]);
-  const ProgAux ax(im, coef);
-  const int64_t g0 = (cg.base - im.coef) / 64, n = (int64_t)cg.wib * pick3(im.hib, sc.comp[0]);
-  for (int64_t q = threadIdx.x; q < n; q += 64) {
-    const int64_t by = q / cg.wib, bx = q - by * cg.wib, g = g0 + by * cg.bw + bx;
-    const uint4* p = reinterpret_cast<const uint4*>(coef + cg.base + (by * cg.bw + bx) * 64);
-    uint32_t w[32];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint4 v = p[u];
-      w[4 * u] = v.x;
-      w[4 * u + 1] = v.y;
-      w[4 * u + 2] = v.z;
-      w[4 * u + 3] = v.w;
-    }
-    uint64_t nz = 0;
-#pragma unroll
-    for (int k = 1; k < 64; k++) {
-      const int nn = kNat80[k];
-      nz |= (uint64_t)(((w[nn >> 1] >> ((nn & 1) * 16)) & 0xffffu) != 0) << k;
-    }
-    ax.mask[g] = nz;
-    ax.delta[3 * g] = ax.delta[3 * g + 1] = ax.delta[3 * g + 2] = 0;
-  }
-}
-
-template <class R>
-__device__ __forceinline__ void prog_bits(R& r, int c, uint64_t& acc) {  // c <= 63 bits appended
-  while (c > 0) {
-    const int n = min(c, 16);
-    acc = (acc << n) | (uint64_t)prog_get(r, n);
-    c -= n;
-  }
-}
-
-template <class R>
-__device__ void prog_ac_refine(const ProgSrc& src, const ProgImgDev& im, const ProgScanDev& sc,
-                               const ProgSegDev* segs, const ProgShared& sh, int16_t* coef) {
-  int32_t at = src.at;
-  const CompGeom cg(im, sc.comp[0]);
-  const ProgAux ax(im, coef);
-  const ProgTabDev& t = sh.tab[sc.slot[0]];
-  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
-  const int ss = sc.ss, se = sc.se;
-  const int64_t g0 = (cg.base - im.coef) / 64;
-  const int wib = cg.wib;
-  constexpr int kAhead = 8;  // masks loaded ahead of the block being decoded
-  for (int s = 0; s < sc.nseg; s++) {
-    ProgSeg<R> g;
-    g.open(src, segs[sc.seg0 + s], at);
-    int eobrun = 0;
-    const int64_t m0 = (int64_t)s * per, m1b = min(sc.mcus, m0 + per);
-    int64_t by = m0 / wib, bx = m0 - by * wib;
-    // a ring of the next kAhead blocks' masks (block m + u at ring[u])
-    uint64_t ring[kAhead];
-    int64_t fy = by, fx = bx;  // the block the next ring load reads
-    auto fetch = [&](int64_t m) -> uint64_t {
-      uint64_t v = 0;
-      if (m < m1b) v = ax.mask[g0 + fy * cg.bw + fx];
-      if (++fx == wib) {
-        fx = 0;
-        fy++;
-      }
-      return v;
-    };
-#pragma unroll
-    for (int u = 0; u < kAhead; u++) ring[u] = fetch(m0 + u);
-    for (int64_t m = m0; m < m1b; m++) {
-      if (g.out()) break;
-      const uint64_t nz = ring[0];
-#pragma unroll
-      for (int u = 0; u + 1 < kAhead; u++) ring[u] = ring[u + 1];
-      ring[kAhead - 1] = fetch(m + kAhead);
-      const int64_t gb = g0 + by * cg.bw + bx;
-      if (++bx == wib) {
-        bx = 0;
-        by++;
-      }
-      uint64_t acc = 0, newm = 0, negm = 0;
-      int k = ss;
-      if (eobrun == 0) {
-        for (; k <= se; k++) {
-          const int rs = prog_sym(g.r, t);
-          const int r = rs >> 4, z = rs & 15;
-          int neg = 0;
-          if (z) {
-            neg = prog_get(g.r, 1) ? 0 : 1;
-          } else if (r != 15) {
-            eobrun = 1 << r;
-            if (r) eobrun += prog_get(g.r, r);
-            break;
-          }
-          // past r zero-history positions to the next one (the new
-          // coefficient's place), or to the band's end
-          uint64_t zeros = ~nz & zz_band(k, se);
-          for (int q = 0; q < r && zeros; q++) zeros &= zeros - 1;
-          const int p = zeros ? __builtin_ctzll(zeros) : se + 1;
-          prog_bits(g.r, __builtin_popcountll(nz & zz_band(k, p - 1)), acc);
-          k = p;
-          if (z) {  // k <= 64; 64 is libjpeg's extra entry: natural position 63
-            const uint64_t bit = (uint64_t)1 << min(k, 63);
-            newm |= bit;
-            negm = neg ? negm | bit : negm & ~bit;
-          }
-        }
-      }
-      if (eobrun > 0) {
-        prog_bits(g.r, __builtin_popcountll(nz & zz_band(k, se)), acc);
-        eobrun--;
-      }
-      if (acc | newm) {
-        ax.delta[3 * gb] = acc;
-        ax.delta[3 * gb + 1] = newm;
-        ax.delta[3 * gb + 2] = negm;
-      }
-    }
-  }
-}
-
-__device__ void prog_refine_apply(const ProgImgDev& im, const ProgScanDev& sc, int16_t* coef) {
-  const CompGeom cg(im, sc.comp[0]);
-  const ProgAux ax(im, coef);
-  const int64_t g0 = (cg.base - im.coef) / 64, n = (int64_t)cg.wib * pick3(im.hib, sc.comp[0]);
-  const int p1 = 1 << sc.al, m1 = -(1 << sc.al);
-  const uint64_t band = zz_band(sc.ss, sc.se);
-  for (int64_t q = threadIdx.x; q < n; q += 64) {
-    const int64_t by = q / cg.wib, bx = q - by * cg.wib, g = g0 + by * cg.bw + bx;
-    const uint64_t acc = ax.delta[3 * g], newm = ax.delta[3 * g + 1], negm = ax.delta[3 * g + 2];
-    if (!(acc | newm)) continue;
-    const uint64_t nzb = ax.mask[g] & band;
-    int rem = __builtin_popcountll(nzb);
-    uint4* p = reinterpret_cast<uint4*>(coef + cg.base + (by * cg.bw + bx) * 64);
-    uint32_t w[32];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint4 v = p[u];
-      w[4 * u] = v.x;
-      w[4 * u + 1] = v.y;
-      w[4 * u + 2] = v.z;
-      w[4 * u + 3] = v.w;
-    }
-#pragma unroll
-    for (int k = 1; k < 64; k++) {
-      const int nn = kNat80[k];
-      const int sh16 = (nn & 1) * 16;
-      int v = (int16_t)(w[nn >> 1] >> sh16);
-      if ((nzb >> k) & 1) {
-        rem--;
-        if (((acc >> rem) & 1) && (v & p1) == 0) v = v >= 0 ? v + p1 : v + m1;
-      }
-      if ((newm >> k) & 1) v = ((negm >> k) & 1) ? m1 : p1;
-      w[nn >> 1] = (w[nn >> 1] & ~(0xffffu << sh16)) | (((uint32_t)v & 0xffffu) << sh16);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u++) p[u] = make_uint4(w[4 * u], w[4 * u + 1], w[4 * u + 2], w[4 * u + 3]);
-  }
-}
-
-// DC refinement: one bit per block in scan order, no Huffman code; spread
-// over the wave's lanes (bits past a segment's end are zeros: no change).
-__device__ void prog_dc_refine(const uint32_t* words, const ProgImgDev& im, const ProgScanDev& sc,
-                               const ProgSegDev* segs, int16_t* coef) {
-  const int ns = sc.ns;
-  const CompGeom g0(im, sc.comp[0]), g1(im, sc.comp[1]), g2(im, sc.comp[2]);
-  const int n0 = ns > 1 ? g0.h * g0.v : 1, n1 = ns > 1 ? g1.h * g1.v : 0, n2 = ns > 2 ? g2.h * g2.v : 0;
-  const int bpm = n0 + n1 + n2;
-  const int64_t per = sc.rst > 0 ? sc.rst : sc.mcus;
-  const int16_t p1 = (int16_t)(1 << sc.al);
-  const uint8_t* bytes = reinterpret_cast<const uint8_t*>(words);
-  for (int s = 0; s < sc.nseg; s++) {
-    const ProgSegDev sg = segs[sc.seg0 + s];
-    const int64_t m0 = (int64_t)s * per, nm = min(sc.mcus, m0 + per) - m0;
-    const int64_t nb = min(nm * bpm, (int64_t)sg.bits);  // blocks with a bit of data
-    for (int64_t q = threadIdx.x; q < nb; q += 64) {
-      if (!((bytes[sg.word * 4 + (q >> 3)] >> (7 - (q & 7))) & 1)) continue;
-      const int64_t m = m0 + q / bpm;
-      int j = (int)(q % bpm);
-      const int i = j < n0 ? 0 : j < n0 + n1 ? 1 : 2;
-      j -= i == 0 ? 0 : i == 1 ? n0 : n0 + n1;
-      const CompGeom& cg = i == 0 ? g0 : i == 1 ? g1 : g2;
-      int64_t bx, by;
-      if (ns == 1) {
-        by = m / cg.wib;
-        bx = m - by * cg.wib;
-      } else {
-        const int64_t my = m / im.mcux, mx = m - my * im.mcux;
-        const int dy = j / cg.h;
-        bx = mx * cg.h + (j - dy * cg.h);
-        by = my * cg.v + dy;
-      }
-      int16_t* d = coef + cg.base + (by * cg.bw + bx) * 64;
-      *d = (int16_t)(*d | p1);
-    }
-  }
-}
-
-// Diagnostic builds only (-DMXD_PROG_SKIP=<bits>; wrong output, never in the
-// product library): bit 0 skips DC-first scans, bit 1 AC-first, bit 2 AC
-// refinements -- tools/prog_breakdown.py times them with variant builds.
-#ifndef MXD_PROG_SKIP
-#define MXD_PROG_SKIP 0
-#endif
-
-constexpr int kProgLdsWords = 12288;  // the phase's staged segments (48 KB of dynamic LDS)
-constexpr int kProgScansLds = 64;     // scans of an image that can be staged
-
-__global__ __launch_bounds__(64) void jpeg_prog(const uint32_t* __restrict__ words, const ProgTabDev* __restrict__ tabs,
-                                                const ProgImgDev* __restrict__ imgs,
-                                                const ProgScanDev* __restrict__ scans,
-                                                const ProgSegDev* __restrict__ segs, int16_t* __restrict__ coef,
-                                                int skip) {
-  __shared__ ProgShared sh;
-  __shared__ int32_t scan_at[kProgScansLds];
-  extern __shared__ uint32_t staged[];
-  const ProgImgDev im = imgs[blockIdx.x];
-  const int lane = threadIdx.x;
-  for (int i = lane; i < 80; i += 64) sh.nat[i] = kNat80[i];
-  {
-    uint4* z = reinterpret_cast<uint4*>(coef + im.coef);
-    const int64_t n16 = im.coef_count / 8;
-    for (int64_t i = lane; i < n16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
-  }
-  __syncthreads();
-  for (int ph = 0; ph < im.nphase; ph++) {
-    // the phase's tables into their slots, refinement masks (the whole wave)
-    bool refine_all = false, refine_ac = false;
-    for (int si = im.scan0; si < im.scan0 + im.nscan; si++) {
-      const ProgScanDev& sc = scans[si];
-      if (sc.phase != ph) continue;
-      refine_all = refine_all || sc.lane < 0;
-      for (int j = 0; j < sc.ns; j++) {
-        if (sc.tab[j] < 0) continue;
-        const uint4* from = reinterpret_cast<const uint4*>(tabs + sc.tab[j]);
-        uint4* to = reinterpret_cast<uint4*>(&sh.tab[sc.slot[j]]);
-        for (int q = lane; q < (int)(sizeof(ProgTabDev) / 16); q += 64) to[q] = from[q];
-      }
-      if (sc.ss > 0 && sc.ah != 0) {
-        prog_refine_masks(im, sc, coef);
-        refine_ac = true;
-      }
-    }
-    // the phase's Huffman-coded segments into LDS while they fit
-    {
-      int32_t at = 0;
-      for (int si = im.scan0; si < im.scan0 + im.nscan && si - im.scan0 < kProgScansLds; si++) {
-        const ProgScanDev& sc = scans[si];
-        if (sc.phase != ph || sc.lane < 0) continue;
-        int64_t need = 0;
-        for (int q = sc.seg0; q < sc.seg0 + sc.nseg; q++) need += ((segs[q].bits + 31) >> 5) + 1;
-        const bool fits = at + need <= kProgLdsWords;
-        if (lane == 0) scan_at[si - im.scan0] = fits ? at : -1;
-        if (!fits) continue;
-        for (int q = sc.seg0; q < sc.seg0 + sc.nseg; q++) {
-          const int32_t nw = (segs[q].bits + 31) >> 5;
-          const uint32_t* from = words + segs[q].word;
-          for (int u = lane; u <= nw; u += 64) staged[at + u] = u < nw ? __builtin_bswap32(from[u]) : 0u;
-          at += nw + 1;
-        }
-      }
-    }
-    __syncthreads();
-    if (refine_all) {
-      for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
-        if (scans[si].phase == ph) prog_dc_refine(words, im, scans[si], segs, coef);
-    } else {
-      // each component's scans of the phase on its lane, in file order
-      int steps = 0;
-      for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
-        if (scans[si].phase == ph) steps = max(steps, scans[si].step + 1);
-      for (int st = 0; st < steps; st++) {
-        int mine = -1;
-        for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
-          if (scans[si].phase == ph && scans[si].lane == lane && scans[si].step == st) mine = si;
-        if (mine < 0) continue;
-        const ProgScanDev sc = scans[mine];
-        const ProgSrc src{words, staged, mine - im.scan0 < kProgScansLds ? scan_at[mine - im.scan0] : -1};
-        const int kind = sc.ss == 0 ? 1 : sc.ah == 0 ? 2 : 4;
-        if (skip & kind) continue;  // (diagnostic builds: MXD_PROG_SKIP)
-        if (src.at >= 0) {
-          if (sc.ss == 0) prog_dc_first<LdsBits>(src, im, sc, segs, sh, coef);
-          else if (sc.ah == 0) prog_ac_first<LdsBits>(src, im, sc, segs, sh, coef);
-          else prog_ac_refine<LdsBits>(src, im, sc, segs, sh, coef);
-        } else {
-          if (sc.ss == 0) prog_dc_first<GlobalReader>(src, im, sc, segs, sh, coef);
-          else if (sc.ah == 0) prog_ac_first<GlobalReader>(src, im, sc, segs, sh, coef);
-          else prog_ac_refine<GlobalReader>(src, im, sc, segs, sh, coef);
-        }
-      }
-    }
-    __syncthreads();
-    if (refine_ac) {
-      for (int si = im.scan0; si < im.scan0 + im.nscan; si++)
-        if (scans[si].phase == ph && scans[si].ss > 0 && scans[si].ah != 0) prog_refine_apply(im, scans[si], coef);
-      __syncthreads();
-    }
-  }
-}
-
 }  // namespace
 
 int64_t jpeg_huff_lds_budget() { return 160 * 1024 - (int64_t)sizeof(Shared) - 1024; }
@@ -1498,14 +946,6 @@ int launch_jpeg_huff(const uint32_t* words, const HuffDev* tables, const HuffImg
   if (set_rc[dev]) return -1;
   hipLaunchKernelGGL(k, dim3(njobs), dim3(threads), (size_t)lds_bytes, reinterpret_cast<hipStream_t>(stream), words,
                      tables, imgs, segs, jobs, pub, ctl, coef);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_jpeg_prog(const uint32_t* words, const ProgTabDev* tabs, const ProgImgDev* imgs, const ProgScanDev* scans,
-                     const ProgSegDev* segs, int32_t nimg, int16_t* coef, void* stream) {
-  if (nimg <= 0) return 0;
-  hipLaunchKernelGGL(jpeg_prog, dim3(nimg), dim3(64), (size_t)kProgLdsWords * 4, reinterpret_cast<hipStream_t>(stream),
-                     words, tabs, imgs, scans, segs, coef, MXD_PROG_SKIP);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

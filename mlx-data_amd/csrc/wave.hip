@@ -189,6 +189,28 @@ __device__ __forceinline__ void store_out(V* p, T v) {
     *p = v;
 }
 
+// Tuning builds (-DMXD_STORE_AUX=<n>, e.g. 18 = nt sc1): the f32 output
+// stores as buffer stores with that cache policy instead of store_out.
+#ifndef MXD_STORE_AUX
+#define MXD_STORE_AUX 0
+#endif
+template <int C>
+__device__ __forceinline__ void store_row_px(char* drow, int px, const float (&s)[C]) {
+  const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc(drow, (short)0, 0x7ffffff0, 0x00020000);
+  if constexpr (C == 3) {
+    const u32x3 v = {__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2])};
+    __builtin_amdgcn_raw_buffer_store_b96(v, rs, px * 12, 0, MXD_STORE_AUX);
+  } else if constexpr (C == 4) {
+    const u32x4 v = {__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, px * 16, 0, MXD_STORE_AUX);
+  } else if constexpr (C == 2) {
+    const u32x2 v = {__float_as_uint(s[0]), __float_as_uint(s[1])};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, px * 8, 0, MXD_STORE_AUX);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s[0]), rs, px * 4, 0, MXD_STORE_AUX);
+  }
+}
+
 // Cache policy of every source row load (the aux operand of the buffer
 // loads; tuning builds -DMXD_LOAD_AUX=<n>: 2 = nt (streaming), 1 = sc0,
 // 16 = sc1, 3 = sc0 nt).  0, the default policy, is the product setting:
@@ -399,8 +421,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // u8 outputs are stored one byte per channel: dword stores of 4 packed bytes
-// gathered across lanes measured no better (round 4, profiles/r04/ring_pack_b.jsonl:
-// 480p 0.0898 vs 0.0903 ms per launch, C5 0.3249 vs 0.3203).
+// gathered across lanes through LDS measured no better (round 4,
+// profiles/r04/ring_pack_b.jsonl: 480p 0.0898 vs 0.0903 ms per launch, C5
+// 0.3249 vs 0.3203).  Tuning builds (-DMXD_U8_BPERM=1, round 6): RGB u8
+// rows packed across lanes with ds_bpermute (no LDS memory): lane l gathers
+// the two pixels its output dword at byte 4 l overlaps and stores one dword,
+// 48 lanes x 4 bytes per instruction instead of 3 x 64 single bytes.
+#ifndef MXD_U8_BPERM
+#define MXD_U8_BPERM 0
+#endif
 
 // Horizontal pass of one strip: lane l owns output pixels l + 64 q (q < Q).
 template <class L, bool F32, int T, int Q>
@@ -443,8 +472,30 @@ struct HStrip {
       }
       if (q > 0 && kLanes * q >= npx) break;  // uniform: no lane has pixels left
       if ((MXD_ABLATE & 2) && s[0] != -1.0f) continue;
+      if constexpr (!F32 && C == 3 && MXD_U8_BPERM != 0) {
+        char* row = drow + kLanes * q * 3;  // the chunk's 192 bytes (4-aligned when drow is)
+        if ((reinterpret_cast<uintptr_t>(drow) & 3) == 0) {  // uniform
+          const int pk = (int)((uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16));
+          const int p0 = (4 * lane) / 3, r = 4 * lane - 3 * p0;
+          const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(p0, kLanes - 1), pk);
+          const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(p0 + 1, kLanes - 1), pk);
+          const uint32_t w = (uint32_t)((((uint64_t)b << 24) | a) >> (8 * r));
+          const int nbytes = 3 * min(kLanes, npx - kLanes * q);
+          if (4 * lane + 4 <= nbytes) {
+            *GLOBAL_PTR(uint32_t, row + 4 * lane) = w;
+          } else if (4 * lane < nbytes) {
+            for (int i = 0; i < nbytes - 4 * lane; i++) GLOBAL_PTR(uint8_t, row)[4 * lane + i] = (uint8_t)(w >> (8 * i));
+          }
+          continue;
+        }
+      }
       if (px < npx) {
-        if constexpr (F32) {
+        if constexpr (F32 && MXD_STORE_AUX != 0) {
+          float q[C];
+#pragma unroll
+          for (int c = 0; c < C; c++) q[c] = div255(s[c]);
+          store_row_px<C>(drow, px, q);
+        } else if constexpr (F32) {
           auto* d = GLOBAL_PTR(float, drow) + px * C;
           if constexpr (C == 1) {
             store_out(d, div255(s[0]));

@@ -291,7 +291,6 @@ class JpegCoefs:
         pend = ctypes.c_int32()
         check(lib().mxd_jpeg_coefs_entropy_pending(ctypes.c_void_p(self.handle), ctypes.byref(pend)))
         self.entropy_pending = bool(pend.value)
-        self.entropy_progressive = pend.value == 2  # every scan of a progressive file on the device
         w, hh, ok = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib().mxd_jpeg_coefs_info(ctypes.c_void_p(self.handle), ctypes.byref(w), ctypes.byref(hh),
                                         ctypes.byref(ok)))

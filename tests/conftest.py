@@ -8,11 +8,6 @@ for p in (REPO, os.path.join(REPO, "oracle"), os.path.join(REPO, "mlx-data_amd")
     if p not in sys.path:
         sys.path.insert(0, p)
 
-# Progressive JPEGs on the device decode whatever this machine's CPU count
-# (jpeg.cpp device_progressive's default picks the host above 11 CPUs): the
-# tests cover that path; MXD_DEVICE_PROGRESSIVE=0 in the environment keeps it off.
-os.environ.setdefault("MXD_DEVICE_PROGRESSIVE", "1")
-
 # Bind the product library (and with it /opt/rocm's HIP runtime) before any
 # test module imports torch, which bundles its own libamdhip64.so.7.
 try:

@@ -1,19 +1,19 @@
-"""GPU: progressive JPEGs entropy-decoded on the device (csrc/jpeghuff.hip
-jpeg_prog).  With mxd_jpeg_coefs_parse(device_entropy=1)
-a progressive Huffman-coded file whose progression is complete (ends at EOI,
-every scan's data ends at a marker, the first ten coefficients of every
-component exact, so libjpeg's block smoothing has nothing to do) is only
-parsed on the host; every scan -- DC first / refinement, AC first with EOB
-runs, AC refinement -- is decoded on the GPU, then finished and resized there.
+"""GPU: progressive JPEGs through the device route.  Round 5 decoded every
+scan of a complete progressive file on the GPU (jpeg_prog, one serial chain
+per component); it lost to the host entropy decode at 16 pipeline workers
+and was retired in round 6, so with
+mxd_jpeg_coefs_parse(device_entropy=1) a progressive file is entropy-decoded
+on the host (jpeg.cpp, libjpeg-turbo's jdphuff.c semantics) and its
+coefficients -- natural order -- are finished (IDCT, upsampling, colour) and
+resized on the GPU.
 
 Bit-exact against the host decoder (pinned to libjpeg-turbo through Pillow by
 tests/test_jpeg.py) and against Pillow's decode of the same file, at identity
 geometry: the committed progressive fixtures, seeded Pillow progressive
 encodes (sizes 1..600, qualities 5..100, 4:4:4 / 4:2:2 / 4:2:0 / grey,
 restart intervals), corrupt scan data, scans whose data runs out before
-their last block (libjpeg's insufficient-data rule inside one scan while the
-later scans still arrive), and batches that mix progressive, sequential and
-host-decoded files."""
+their last block, batches that mix progressive, sequential and host-decoded
+files, and large photos."""
 import io
 import os
 
@@ -72,14 +72,14 @@ def test_progressive_fixtures_identity():
         if f"{k}_rgb" in GOLD.files:
             assert np.array_equal(g.reshape(c.height, c.width, 3), GOLD[f"{k}_rgb"]), k
     for k, c in zip(keys, coefs):
-        assert c.entropy_progressive or "prog0" in k, k
+        assert not c.entropy_pending or "prog0" in k, k
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_progressive_sweep_matches_pillow(seed):
     datas = _sweep(seed)
     coefs = _check_identity(datas)
-    assert all(c.entropy_progressive for c in coefs)
+    assert not any(c.entropy_pending for c in coefs)
 
 
 def test_progressive_corrupt_scan_data():
@@ -99,7 +99,7 @@ def test_progressive_corrupt_scan_data():
                     d[at] = int(rng.integers(0, 0xFF))
         datas.append(bytes(d))
     coefs = _check_identity(datas, pillow=False)
-    assert sum(c.entropy_progressive for c in coefs) >= 8
+    assert not any(c.entropy_pending for c in coefs)
 
 
 def test_progressive_scan_data_runs_out():
@@ -121,7 +121,7 @@ def test_progressive_scan_data_runs_out():
             cut += 1
         datas.append(d[:cut] + d[keep:] if d[keep - 1] != 0xFF else d)
     coefs = _check_identity(datas, pillow=False)
-    assert sum(c.entropy_progressive for c in coefs) >= 5
+    assert not any(c.entropy_pending for c in coefs)
 
 
 def test_progressive_mixed_batch_and_resize():
@@ -157,14 +157,12 @@ def test_progressive_mixed_batch_and_resize():
         assert np.array_equal(g, w_), i
 
 
-def test_progressive_large_images_read_device_memory():
-    """Photos whose scans do not fit the kernel's LDS staging (48 KB per
-    phase) read their segments from device memory (the prefetching reader):
-    1600x1200 and 2400x1800 progressive files, one with restart markers,
-    equal to the host decoder and Pillow."""
+def test_progressive_large_images():
+    """1600x1200 and 2400x1800 progressive photos, one grey with restart
+    markers, finished on the device: equal to the host decoder and Pillow."""
     rng = np.random.default_rng(14)
     datas = [_encode(_smooth(rng, 1200, 1600), quality=95, progressive=True, subsampling=2),
              _encode(_smooth(rng, 1800, 2400), quality=92, progressive=True, subsampling=0),
              _encode(_smooth(rng, 1200, 1600, 1), quality=97, progressive=True, restart_marker_blocks=5)]
     coefs = _check_identity(datas)
-    assert all(c.entropy_progressive for c in coefs)
+    assert not any(c.entropy_pending for c in coefs)

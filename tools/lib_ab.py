@@ -54,7 +54,10 @@ def main():
     args = ap.parse_args()
     names = args.variants.split(",")
     for wl in args.workloads.split(","):
-        capi, PL, stream, sets, mode, alg, sizes, geoms, f32 = band_sweep.setup(wl)
+        # "c3:640x480" = C3's batch drawn from that one size
+        name, _, only = wl.partition(":")
+        c3 = [tuple(int(v) for v in only.split("x"))] if only else None
+        capi, PL, stream, sets, mode, alg, sizes, geoms, f32 = band_sweep.setup(name, c3_sizes=c3)
         libs = {n: load_variant(n, capi) for n in names}
         for L in libs.values():
             L.mxd_set_kernel_policy(args.policy)

@@ -2,12 +2,17 @@
 arguments) and grid size, from a rocprofv3 --pmc counter_collection.csv.
   python tools/pmc_kernels.py FILE"""
 import csv
+import glob
+import os
 import sys
 from collections import defaultdict
 
 
 def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
+    path = sys.argv[1]
+    if os.path.isdir(path):  # rocprofv3 -d DIR: the counter file may sit in a host / pid subdirectory
+        path = sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True))[0]
+    rows = list(csv.DictReader(open(path)))
     per = defaultdict(float)  # (dispatch, kernel, grid, counter) -> summed over the row's instances
     for r in rows:
         short = r["Kernel_Name"].split("(")[0][:90]
