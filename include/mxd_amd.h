@@ -38,7 +38,8 @@ extern "C" {
  * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS,
  * MXD_TUNE_HUFF_JOB, MXD_TUNE_JPEG_RGB, mxd_jpeg_plane_sources,
  * mxd_host_stats, mxd_jpeg_coefs_load.
- * 6 (round 6): the knob MXD_TUNE_DEVICE_TIMING and mxd_device_stats;
+ * 6 (round 6): the knobs MXD_TUNE_DEVICE_TIMING, MXD_TUNE_LOAD_POLICY and
+ * mxd_device_stats;
  * mxd_jpeg_coefs_entropy_pending no longer reports 2 (progressive files are
  * entropy-decoded on the host). */
 #define MXD_ABI_VERSION 6
@@ -196,7 +197,10 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_DEVICE_TIMING: 1 = every host-path chunk records two timing events
  * on its stream, before its first kernel and after its last, and
  * mxd_device_stats sums the span between them (diagnostics: what the batch
- * calls cost the device; read when a chunk is launched). */
+ * calls cost the device; read when a chunk is launched);
+ * MXD_TUNE_LOAD_POLICY: cache policy of the scatter wave kernels' source
+ * loads (0 = automatic: streaming (nt) when the call's sources total >= 128
+ * MiB, else the default policy; 1 = default policy always; 2 = nt always). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -210,7 +214,8 @@ enum mxd_tune {
   MXD_TUNE_HUFF_JOB = 9,
   MXD_TUNE_JPEG_RGB = 10,
   MXD_TUNE_DEVICE_TIMING = 11,
-  MXD_TUNE_COUNT = 12
+  MXD_TUNE_LOAD_POLICY = 12,
+  MXD_TUNE_COUNT = 13
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 

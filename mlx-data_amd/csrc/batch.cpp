@@ -10,6 +10,10 @@ namespace mxd {
 namespace capi {
 namespace {
 
+// A call whose wave-kernel sources total at least this many bytes loads them
+// with the streaming (nt) policy (half the 256 MB Infinity Cache).
+constexpr int64_t kNtSourceBytes = (int64_t)128 << 20;
+
 struct Workspace {
   std::mutex mu;
   // Descriptor slots: each launch reads its descriptors from one slot.  A
@@ -491,8 +495,19 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                     p.ycc ? 1 : 0}});
     groups.back().count++;
   }
+  // Source load policy (wave.hip LAUX): streaming (nt) loads when the
+  // call's sources are far past what the 256 MB Infinity Cache could hold
+  // for a re-read (sources just written by a decode or a copy stay there,
+  // and nt loads would bypass them: C4's 128 small images measured 45 %
+  // slower with nt, C2 / C3 / C5 2-7 % faster; profiles/r06/README.md).
+  // MXD_TUNE_LOAD_POLICY: 1 = default policy always, 2 = nt always.
+  int64_t src_bytes = 0;
+  for (int32_t i : order) src_bytes += (int64_t)images[i].src_w * images[i].src_h * images[i].channels;
+  const int32_t load_knob = g_tune[MXD_TUNE_LOAD_POLICY].load();
+  const int32_t nt = load_knob == 2 ? 1 : load_knob == 1 ? 0 : src_bytes >= kNtSourceBytes ? 1 : 0;
   for (Group& g : groups) {
     g.cfg.nimgs = g.count;
+    g.cfg.nt = g.cfg.ycc ? 0 : nt;
     std::vector<std::pair<int32_t, int32_t>> strips;  // (nstrips, crop_h) per image
     for (int32_t k = g.first; k < g.first + g.count; k++) strips.push_back({plans[order[k]].nstrips, images[order[k]].crop_h});
     g.ty = band_rows(strips, wave_capacity_cached(g.cfg, device));

@@ -17,9 +17,8 @@
 //      again from the true state;
 //   3. block counts prefix-summed per segment -> each subsequence's first
 //      block; the job's exit state and block index published;
-//   4. (round 6: no separate zeroing pass, see decode_job)
-//   5. write pass: decode again, each block's own positions zeroed as the
-//      subsequence enters it, then its AC coefficients and DC differences;
+//   4. the job's blocks zeroed by the whole workgroup (whole lines);
+//   5. write pass: decode again, storing AC coefficients and DC differences;
 //   6. DC: per-component sums of the differences prefix-summed per segment
 //      (the continued segment's from the previous job's published sums),
 //      then each subsequence turns its blocks' differences into values.
@@ -208,6 +207,8 @@ struct Shared {
   int3 scan3[kHuffThreads / 64];
   int32_t flag[2];
   int64_t pred_blocks;             // the previous job's published block index
+  int64_t zero_range[2];           // the job's first and last block (jpeghuff.hip step 4)
+  int32_t zero_k[2];               // the job's part of them starts at / ends before these positions
   int32_t pred_dc[3];
 #ifdef MXD_HUFF_STAMPS
   // diagnostic build: s_memtime at the phase boundaries ([0] start, [1]
@@ -403,6 +404,22 @@ struct Dec {
     return end;
   }
 };
+
+// Coefficient offset of block g (decode order) of the image: blocks number
+// < 2^31 (the host refuses larger images), so 32-bit divisions.
+__device__ __forceinline__ int64_t block_addr(const HuffImgDev& im, int64_t g64) {
+  const uint32_t g = (uint32_t)g64;
+  if (!im.interleaved) {
+    const uint32_t by = g / (uint32_t)im.mcux, bx = g - by * (uint32_t)im.mcux;
+    return im.coef + im.plane[0] + ((int64_t)by * im.bw[0] + bx) * 64;
+  }
+  const uint32_t m = g / (uint32_t)im.bpm;
+  const int j = (int)(g - m * (uint32_t)im.bpm);
+  const int c = im.blk_comp[j];
+  const uint32_t my = m / (uint32_t)im.mcux, mx = m - my * (uint32_t)im.mcux;
+  const int64_t bx = (int64_t)mx * im.comp_h[c] + im.blk_dx[j], by = (int64_t)my * im.comp_v[c] + im.blk_dy[j];
+  return im.coef + im.plane[c] + (by * im.bw[c] + bx) * 64;
+}
 
 // Dynamic LDS of a job: its tables, its segment records, then (job.lds)
 // its words.
@@ -633,48 +650,60 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
                       ((uint64_t)(uint8_t)sh.out_k[t] << 40));
   }
 
-  // 4. (no separate zeroing pass) The write pass stores only the symbols'
-  // positions, so each own subsequence zeroes, as it enters a block, the
-  // positions of that block it decodes -- [ke, 64) of its first block, [0, kx)
-  // of the block it ends inside, whole blocks in between -- immediately
-  // before its stores into them: a block's 128 bytes are written whole while
-  // the line is in the XCD's L2, instead of zeroed for the whole job first
-  // (72 MB per C4 call, more than the L2s hold) and then reached by scattered
-  // 2-byte stores that HBM took as partial-line writes (round 5: 2.8x the
-  // coefficient bytes written).  Neighbouring subsequences' ranges are
-  // disjoint, so no ordering between threads is needed; a thread's zeros
-  // precede its own stores to the same addresses in program order.  A
-  // segment's last subsequence also zeroes the blocks to the segment's end
-  // that data running out early leaves undecoded (libjpeg's insufficient-data
-  // rule).
+  // 4. Zero the job's blocks (the write pass stores only the symbols'
+  // positions): every block it decodes whole or in part -- [z0, z1) in decode
+  // order, contiguous over the job's segments; the segment's last
+  // subsequence's range runs to the segment's end, which leaves the blocks of
+  // data that ran out early zero (libjpeg's insufficient-data rule) -- by the
+  // whole workgroup in 16-byte pieces, consecutive threads on consecutive
+  // pieces, so a block's 128 bytes go out as one line.  Not the first block
+  // when the previous job decodes its start, nor the last when the next job
+  // decodes its end: the neighbouring job writes into those with no barrier
+  // in between, so their owners here zero them position by position.
   const int ke = sh.in_k[t];
   const int32_t start_pos = sh.in_pos[t];
   const int64_t gx = g + my_done;                   // the block it ends inside (non-last)
   const int kx = u.seg_last ? 0 : sh.out_k[t];
   const uint32_t bpm = (uint32_t)im.bpm, mcux = (uint32_t)im.mcux;
   int16_t* const icoef = coef + im.coef;            // the image's coefficients
-  // positions [k0, k1) of block b: whole 16-byte pieces, 2-byte stores at the ends
-  auto zero_own = [](int16_t* b, int k0, int k1) {
-    if (k0 == 0 && k1 == 64) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) reinterpret_cast<uint4*>(b)[i] = uint4{0u, 0u, 0u, 0u};
-      return;
-    }
-    for (int q = k0; q < k1;) {
-      if ((q & 7) == 0 && q + 8 <= k1) {
-        *reinterpret_cast<uint4*>(b + q) = uint4{0u, 0u, 0u, 0u};
-        q += 8;
-      } else {
-        b[q++] = 0;
+  // the job's first block (from position kf on: the previous job decodes its
+  // start) and its last (to position kl: the next job decodes the rest)
+  if (act && t == job.warm) {
+    sh.zero_range[0] = g;
+    sh.zero_k[0] = g < seg_block1 ? ke : 0;
+  }
+  if (act && u.job_last) {
+    sh.zero_range[1] = u.seg_last ? seg_block1 : gx;
+    sh.zero_k[1] = gx < seg_block1 ? kx : 0;
+  }
+  __syncthreads();
+  {
+    const int64_t first = sh.zero_range[0], last = sh.zero_range[1];
+    const int kf = sh.zero_k[0], kl = sh.zero_k[1];
+    const int64_t z0 = first + (kf != 0 ? 1 : 0), pieces = (last - z0) * 8;
+    if (t < pieces) {
+      // thread t's pieces: t, t + blockDim, ... -- blocks blockDim / 8 apart,
+      // reached by a cursor jump instead of a division per piece
+      const uint32_t jump = blockDim.x >> 3, jq = jump / bpm, jr = jump - jq * bpm;
+      BlockCursor zc;
+      zc.set((uint32_t)(z0 + (t >> 3)), bpm, mcux);
+      for (int64_t c = t; c < pieces; c += blockDim.x) {
+        reinterpret_cast<uint4*>(icoef + zc.off(sh))[t & 7] = uint4{0u, 0u, 0u, 0u};
+        zc.advance(jq, jr, bpm, mcux);
       }
     }
-  };
-  // the start / exit / block-count arrays are free from here on (after every
-  // thread has read its segment's first prefix above): each thread keeps its
-  // DC-difference sums per component in its own slots of them
-  __syncthreads();
+    auto zero = [&](int64_t b, int k0, int k1) {
+      int16_t* d = coef + block_addr(im, b);
+      for (int q = k0; q < k1; q++) d[q] = 0;
+    };
+    if (t == job.warm && kf != 0) zero(first, kf, last == first && kl != 0 ? kl : 64);
+    if (act && u.job_last && kl != 0 && !(last == first && kf != 0)) zero(last, 0, kl);
+  }
+  // the start / exit / block-count arrays are free from here on: each thread
+  // keeps its DC-difference sums per component in its own slots of them
   int* const dcslot[3] = {&sh.done[t], &sh.in_pos[t], &sh.out_pos[t]};
   *dcslot[0] = *dcslot[1] = *dcslot[2] = 0;
+  __syncthreads();  // the zeros land before the coefficients
 
   // 5. write pass (own subsequences)
   Dec<SEARCH> dec;
@@ -691,10 +720,6 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
     cur.set((uint32_t)min(g, seg_block1 - 1), bpm, mcux);
     cur0 = cur;
     int16_t* blk = icoef + cur.off(sh);
-    // the positions of block g this subsequence decodes: to kx in the block it
-    // ends inside, else to the block's end
-    auto own_end = [&](int64_t gb) { return !u.seg_last && gb == gx ? kx : 64; };
-    if (g < seg_block1) zero_own(blk, ke, own_end(g));
     int32_t rem = u.end - start_pos;
     for (;;) {
       if (rem <= 0 || g >= seg_block1 || (dec.b == 0 && dec.k == 0 && u.end - rem > u.sg.bits)) break;
@@ -711,15 +736,6 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
         g++;
         cur.next(bpm, mcux);
         blk = icoef + cur.off(sh);  // past the segment's last block when g == seg_block1: never stored through
-        if (g < seg_block1) zero_own(blk, 0, own_end(g));
-      }
-    }
-    if (u.seg_last && g < seg_block1) {
-      // data ran out at an MCU boundary: the rest of the segment stays zero
-      BlockCursor zc = cur;
-      for (int64_t q = g; q < seg_block1; q++) {
-        zero_own(icoef + zc.off(sh), 0, 64);
-        zc.next(bpm, mcux);
       }
     }
     dc0 = g_first + (ke != 0 ? 1 : 0);

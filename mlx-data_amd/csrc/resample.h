@@ -82,6 +82,7 @@ struct WaveCfg {
   int32_t per_img = 0;  // units of every image when all images of the launch have the same count, else 0
   int32_t prio = 1;     // progress-based wave priority (off for the concurrent launches of a mixed batch)
   int32_t ycc = 0;      // sources are JPEG sample planes (ImgDev::ycc; scatter, p = 4, no shift)
+  int32_t nt = 0;       // streaming (nt) source loads (scatter kernels; wave.hip LAUX)
 };
 
 // Scatter schedule geometry, shared by the kernel and the host builder:

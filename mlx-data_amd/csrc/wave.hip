@@ -211,13 +211,19 @@ __device__ __forceinline__ void store_row_px(char* drow, int px, const float (&s
   }
 }
 
-// Cache policy of every source row load (the aux operand of the buffer
-// loads; tuning builds -DMXD_LOAD_AUX=<n>: 2 = nt (streaming), 1 = sc0,
-// 16 = sc1, 3 = sc0 nt).  0, the default policy, is the product setting:
-// profiles/r06/README.md has the in-process A/B over C2..C5.
+// Cache policy of the source row loads (the aux operand of the buffer loads).
+// Kernels come in two forms (template argument LAUX): the default policy,
+// and nt (2, streaming) for calls whose sources are far larger than the
+// Infinity Cache -- the planner's choice (batch.cpp, MXD_TUNE_LOAD_POLICY).
+// Measured in one process (profiles/r06/README.md): nt reads stream at
+// 7.0-7.2 TB/s against 6.2-6.4 default (tools/nt_ceiling.hip), and the wave
+// kernels gain 2-7 % on C2 / C3 / C5, while C4's 128 small images, which the
+// Infinity Cache holds, lose 45 % with nt.  Tuning builds: -DMXD_LOAD_AUX=<n>
+// replaces the default form's policy (1 = sc0, 16 = sc1, ...).
 #ifndef MXD_LOAD_AUX
 #define MXD_LOAD_AUX 0
 #endif
+constexpr int kLoadNt = 2;
 
 // A voffset past any image (images are < 2^31 bytes): the buffer range check
 // turns the load into zeros without a memory request.
@@ -236,21 +242,21 @@ __device__ __forceinline__ void to_planes(const Raw<P * C / 4>& v, float (&x)[C]
   for (int i = 0; i < P * C; i++) x[i % C][i / C] = (float)((v.d[i >> 2] >> (8 * (i & 3))) & 0xffu);
 }
 
-// n consecutive dwords of a buffer row into w[0..n).
-template <int N>
+// n consecutive dwords of a buffer row into w[0..n) (cache policy AUX).
+template <int N, int AUX>
 __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_t* w) {
   if constexpr (N >= 4) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, MXD_LOAD_AUX);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX);
     w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-    if constexpr (N > 4) load_dwords<N - 4>(rs, voff + 16, soff, w + 4);
+    if constexpr (N > 4) load_dwords<N - 4, AUX>(rs, voff + 16, soff, w + 4);
   } else if constexpr (N == 3) {
-    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, voff, soff, MXD_LOAD_AUX);
+    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, voff, soff, AUX);
     w[0] = v.x, w[1] = v.y, w[2] = v.z;
   } else if constexpr (N == 2) {
-    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, MXD_LOAD_AUX);
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, AUX);
     w[0] = v.x, w[1] = v.y;
   } else if constexpr (N == 1) {
-    w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, MXD_LOAD_AUX);
+    w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, AUX);
   }
 }
 
@@ -261,7 +267,7 @@ __device__ __forceinline__ void load_dwords(Rsrc rs, int voff, int soff, uint32_
 // Row offsets go into the VGPR offset (r - y0) * stride + lane offset, which
 // the buffer range check covers (the scalar offset is not checked): rows
 // outside the stored region read zeros, never other memory.
-template <class L, bool SHIFT>
+template <class L, bool SHIFT, int AUX>
 struct Src {
   using RawT = Raw<L::ND>;
   static constexpr int kLaneBytes = L::LB;  // (its scatter ring: resample.h scatter_ring_slots)
@@ -281,12 +287,12 @@ struct Src {
       const int off2 = (int)((uint32_t)voff2 + roff);
       constexpr int NH = ND / 2;
       if constexpr (!SHIFT) {
-        load_dwords<NH>(rs, off, 0, x.d);
-        load_dwords<NH>(rs, off2, 0, x.d + NH);
+        load_dwords<NH, AUX>(rs, off, 0, x.d);
+        load_dwords<NH, AUX>(rs, off2, 0, x.d + NH);
       } else {
         uint32_t w[NH + 1], v[NH + 1];
-        load_dwords<NH + 1>(rs, off, 0, w);
-        load_dwords<NH + 1>(rs, off2, 0, v);
+        load_dwords<NH + 1, AUX>(rs, off, 0, w);
+        load_dwords<NH + 1, AUX>(rs, off2, 0, v);
 #pragma unroll
         for (int j = 0; j < NH; j++) {
           x.d[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
@@ -296,10 +302,10 @@ struct Src {
       return x;
     }
     if constexpr (!SHIFT) {
-      load_dwords<ND>(rs, off, 0, x.d);
+      load_dwords<ND, AUX>(rs, off, 0, x.d);
     } else {
       uint32_t w[ND + 1];
-      load_dwords<ND + 1>(rs, off, 0, w);
+      load_dwords<ND + 1, AUX>(rs, off, 0, w);
 #pragma unroll
       for (int j = 0; j < ND; j++) x.d[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
     }
@@ -593,7 +599,7 @@ constexpr int min_waves(int c, int p, int kind, int dmax) {
 }
 
 // One unit (image, band, strip) by the calling wave; planes = its LDS rows.
-template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC>
+template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC, int LAUX>
 __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int nimgs, int per_img, int unit,
                                          float* __restrict__ planes, int lane, bool prio) {
   using L = Lay<C, P>;
@@ -632,7 +638,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
   int lo, hi;
   strip_span(xtab, xs, crop_w, flip, ox0, ox1, &lo, &hi);
   const int sx0 = __builtin_amdgcn_readfirstlane(im.src_x0);
-  Src<L, SHIFT> src;
+  Src<L, SHIFT, LAUX> src;
   int hbase;  // HStrip base (see HStrip::init)
   {
     void* base = uniform_ptr<void*>(im.src);
@@ -775,7 +781,8 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
 #endif
 }
 
-template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC = false>
+template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC = false,
+          int LAUX = MXD_LOAD_AUX>
 __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void resample_wave(
     const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -790,7 +797,7 @@ __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void r
     for (int i = 0; i < L::PAD; i += kLanes)
       if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
   if (unit < nunits)
-    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC>(imgs, nimgs, per_img, unit, planes, lane,
+    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC, LAUX>(imgs, nimgs, per_img, unit, planes, lane,
                                                     __builtin_amdgcn_readfirstlane(prio) != 0);
 }
 
@@ -842,12 +849,15 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == P_)              \
     return cfg.ycc ? (P_ == 4 && !cfg.shift ? resample_wave<3, 4, F32, T_, Q_, kScatter, S_, D_, false, true> \
                                             : nullptr)                                            \
-           : cfg.shift ? resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, true>                \
-                       : resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, false>;
+           : cfg.shift ? (cfg.nt ? resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, true, false, kLoadNt> \
+                                 : resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, true>)     \
+                       : (cfg.nt ? resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, false, false, kLoadNt> \
+                                 : resample_wave<3, P_, F32, T_, Q_, kScatter, S_, D_, false>);
   // byte lanes (P = 16): any base alignment, no realignment variant
 #define MXD_SCATTER_B(S_, D_, T_, Q_)                                                             \
   if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == 16 && !cfg.ycc)  \
-    return resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false>;
+    return cfg.nt ? resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false, false, kLoadNt>    \
+                  : resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false>;
   MXD_SCATTER(2, 4, 8, 2, 8)    // 960 -> 256 (C2)
   MXD_SCATTER(2, 4, 8, 1, 4)
   MXD_SCATTER(2, 5, 10, 2, 8)   // 1080 -> 256, 2160 -> 512 (C5)

@@ -61,6 +61,7 @@ MXD_TUNE_HOST_STREAMS = 8
 MXD_TUNE_HUFF_JOB = 9
 MXD_TUNE_JPEG_RGB = 10
 MXD_TUNE_DEVICE_TIMING = 11
+MXD_TUNE_LOAD_POLICY = 12
 
 
 class MxdImage(ctypes.Structure):

@@ -8,7 +8,7 @@ Settings are measured round-robin (rep 1 of every setting, then rep 2, ...)
 after a --warm-s warm-up, so clock / cache drift does not favour any of them.
 Each --set is a comma list of knob=value (rows -> MXD_TUNE_BAND_ROWS, la ->
 MXD_TUNE_BAND_LA, grid -> MXD_TUNE_BAND_GRID, desc -> MXD_TUNE_DESC, streams ->
-MXD_TUNE_STREAMS, policy -> mxd_set_kernel_policy).  Inputs are bench.py's
+MXD_TUNE_STREAMS, load -> MXD_TUNE_LOAD_POLICY, policy -> mxd_set_kernel_policy).  Inputs are bench.py's
 workload (two alternating source/output sets, resident in HBM); the time is
 HIP events around `launches` back-to-back launches on one stream, after 3
 warm-up launches, repeated `--reps` times (median reported).  Prints one JSON
@@ -92,6 +92,7 @@ def main():
         capi.set_tuning(capi.MXD_TUNE_BAND_GRID, int(kv.get("grid", 0)))
         capi.set_tuning(capi.MXD_TUNE_DESC, int(kv.get("desc", 0)))
         capi.set_tuning(capi.MXD_TUNE_STREAMS, int(kv.get("streams", 0)))
+        capi.set_tuning(capi.MXD_TUNE_LOAD_POLICY, int(kv.get("load", 0)))
         capi.set_kernel_policy(int(kv.get("policy", 0)))
         # wrows: the wave kernels' band height, read from the environment by
         # tuning builds only (-DMXD_TUNING_ENV; tools/variants.sh build tenv)
