@@ -39,8 +39,9 @@ extern "C" {
  * MXD_TUNE_HUFF_JOB, MXD_TUNE_JPEG_RGB, mxd_jpeg_plane_sources,
  * mxd_host_stats, mxd_jpeg_coefs_load.
  * 6 (round 6): the knobs MXD_TUNE_DEVICE_TIMING, MXD_TUNE_LOAD_POLICY and
- * mxd_device_stats;
- * mxd_jpeg_coefs_entropy_pending no longer reports 2 (progressive files are
+ * mxd_device_stats; CMYK / YCCK files finish (and sequential ones
+ * entropy-decode) on the device; mxd_jpeg_coefs_entropy_pending no longer
+ * reports 2 (progressive files are
  * entropy-decoded on the host). */
 #define MXD_ABI_VERSION 6
 
@@ -360,8 +361,9 @@ int mxd_jpeg_coefs_load(const char* path, int32_t device_entropy, mxd_jpeg_coefs
 int mxd_jpeg_coefs_entropy_pending(const mxd_jpeg_coefs* coefs, int32_t* pending);
 int mxd_jpeg_coefs_free(mxd_jpeg_coefs* coefs);
 
-/* Image size; *device_ok = 1 when the GPU can finish it (grey, YCbCr or RGB;
- * CMYK / YCCK finish on the host only). */
+/* Image size; *device_ok = 1 when the GPU can finish it (grey, YCbCr, RGB
+ * and, since ABI 6, CMYK / YCCK -- their first three output channels; lossless
+ * files finish on the host only). */
 int mxd_jpeg_coefs_info(const mxd_jpeg_coefs* coefs, int32_t* width, int32_t* height, int32_t* device_ok);
 
 /* Host finish: height rows of width*3 bytes at dst_stride (thread-safe; the

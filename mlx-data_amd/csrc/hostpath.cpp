@@ -443,7 +443,7 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     pend_rel[i - first] = coef_rel;
     mxd::HuffImgDev h{};
     h.coef = coef_rel / 2;  // coef_off added below
-    for (int k = 0; k < info.ncomp && k < 3; k++) {
+    for (int k = 0; k < info.ncomp && k < 4; k++) {
       h.plane[k] = info.comp[k].off;
       h.bw[k] = info.comp[k].bw;
       h.comp_h[k] = (int8_t)info.comp[k].h;
@@ -567,7 +567,9 @@ void jpeg_chunk(const mxd_jpeg_image* jimg, int32_t first, int32_t end, const st
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(jimg[i].coefs));
     mxd::JpegImgDev m{};
     m.ncomp = info.ncomp == 1 ? 1 : 3;
-    m.rgb = info.color_space == 2 ? 1 : 0;
+    // 0 YCbCr -> RGB; 1 the components as they are (RGB, CMYK's C M Y);
+    // 2 YCCK: YCbCr -> RGB inverted (jdcolor.c ycck_cmyk_convert's C M Y)
+    m.rgb = info.color_space == 2 || info.color_space == 3 ? 1 : info.color_space == 4 ? 2 : 0;
     m.width = info.width;
     m.height = info.height;
     m.pitch = (int32_t)rgb_pitch(info.width);
@@ -1106,7 +1108,7 @@ int jpeg_path(const mxd_jpeg_image* jimg, int32_t n, int32_t out_dtype, int32_t 
     if (!j.coefs) return fail(MXD_ERR_INVALID, "mxd: null coefs" + at);
     const mxd::jpeg::CoefInfo info = mxd::jpeg::coef_info(coefs_of(j.coefs));
     if (!info.device_ok)
-      return fail(MXD_ERR_UNSUPPORTED, "mxd: CMYK / YCCK JPEGs finish on the host (mxd_jpeg_coefs_finish)" + at);
+      return fail(MXD_ERR_UNSUPPORTED, "mxd: this JPEG finishes on the host (mxd_jpeg_coefs_finish)" + at);
     if (j.win_w <= 0 || j.win_h <= 0)
       return fail(MXD_ERR_INVALID, "image: cannot create image with 0 or negative dimension" + at);
     if (j.win_x < 0 || j.win_y < 0 || (int64_t)j.win_x + j.win_w > info.width ||

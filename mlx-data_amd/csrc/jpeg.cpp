@@ -1270,7 +1270,7 @@ struct Decoder {
   // component of a grey (1) or YCbCr / RGB (3) image, its entropy-coded data
   // ending at a marker, restart markers RST0..7 in sequence, one per interval.
   void record_scan(Component** sc, int ns) {
-    if (scans++ > 0 || progressive || ns != ncomp || (ncomp != 1 && ncomp != 3)) throw NotDevice{};
+    if (scans++ > 0 || progressive || ns != ncomp || (ncomp != 1 && ncomp != 3 && ncomp != 4)) throw NotDevice{};
     int bpm = 0;
     for (int i = 0; i < ns; i++) {
       if (sc[i]->dc_tbl > 3 || sc[i]->ac_tbl > 3 || !dc[sc[i]->dc_tbl].present || !ac[sc[i]->ac_tbl].present)
@@ -2360,7 +2360,11 @@ CoefInfo coef_info(const Coefs* c) {
     p.off = k.off;
     p.q = k.q;
   }
-  r.device_ok = !d.lossless && (d.ncomp == 1 || (d.ncomp == 3 && (r.color_space == 1 || r.color_space == 2)));
+  // grey, YCbCr, RGB, and (round 6) CMYK / YCCK: their first three output
+  // channels come from the first three components (ImageJPEG.cpp:112-124
+  // keeps C, M, Y of libjpeg's CMYK output; K is never read)
+  r.device_ok = !d.lossless && (d.ncomp == 1 || (d.ncomp == 3 && (r.color_space == 1 || r.color_space == 2)) ||
+                                (d.ncomp == 4 && (r.color_space == 3 || r.color_space == 4)));
   return r;
 }
 

@@ -44,7 +44,7 @@ struct CoefInfo {
   const int16_t* coef;  // nullptr while the entropy decode is pending (decoded on the device)
   int64_t coef_count;
   CoefPlane comp[4];
-  bool device_ok;   // grey, YCbCr or RGB: the device kernels can finish it
+  bool device_ok;   // grey, YCbCr, RGB, CMYK, YCCK (not lossless): the device kernels can finish it
   bool entropy_pending;  // the coefficients come from the device entropy decode (jpeghuff.h)
 };
 

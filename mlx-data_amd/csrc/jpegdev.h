@@ -46,8 +46,9 @@ struct JpegImgDev {
   int32_t dw[3], dh[3];
   int32_t mode[3];   // JpegUp
   int32_t hx[3], vx[3];
-  int32_t ncomp;     // 1 (grey, replicated) or 3
-  int32_t rgb;       // 1: the components are R, G, B (no YCbCr conversion)
+  int32_t ncomp;     // 1 (grey, replicated) or 3 (a CMYK / YCCK file's first three)
+  int32_t rgb;       // 0: YCbCr -> RGB; 1: the components as they are (RGB; CMYK's C, M, Y);
+                     // 2: YCCK, YCbCr -> RGB inverted (libjpeg's C, M, Y)
   int32_t width, height;
   int32_t pitch;     // bytes per RGB row (a multiple of 64, >= 3 * round_up(width, 8))
   int32_t skip;      // 1: a wave kernel reads the planes itself (ImgDev::ycc): no RGB frame

@@ -346,12 +346,17 @@ __global__ __launch_bounds__(256) void jpeg_color(const uint8_t* __restrict__ sa
       const int c0 = sample_at(samples + m.plane[0], m, 0, x, y);
       const int c1 = sample_at(samples + m.plane[1], m, 1, x, y);
       const int c2 = sample_at(samples + m.plane[2], m, 2, x, y);
-      if (m.rgb) {
+      if (m.rgb == 1) {
         px[j][0] = (uint32_t)c0;
         px[j][1] = (uint32_t)c1;
         px[j][2] = (uint32_t)c2;
       } else {
         ycc_to_rgb(c0, c1, c2, px[j]);
+        if (m.rgb == 2) {  // YCCK: the C, M, Y libjpeg outputs are 255 - R, G, B
+          px[j][0] = 255u - px[j][0];
+          px[j][1] = 255u - px[j][1];
+          px[j][2] = 255u - px[j][2];
+        }
       }
     }
   }

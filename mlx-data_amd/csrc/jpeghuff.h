@@ -100,8 +100,8 @@ static_assert(sizeof(HuffDev) % 16 == 0, "HuffDev keeps 16-byte alignment");
 // One image of a device entropy-decode launch.
 struct HuffImgDev {
   int64_t coef;            // first coefficient of the image's planes (int16 elements of the coefficient buffer)
-  int64_t plane[3];        // first coefficient of each component plane, relative to coef
-  int32_t bw[3];           // blocks per plane row (MCU-padded grid)
+  int64_t plane[4];        // first coefficient of each component plane, relative to coef (4: CMYK / YCCK)
+  int32_t bw[4];           // blocks per plane row (MCU-padded grid)
   int32_t tables;          // first HuffDev of the image (index into the launch's table array)
   int32_t ntables;         // HuffDev the image uses (<= 8)
   int32_t bpm;             // blocks per MCU (1 for a single-component scan)
@@ -115,8 +115,7 @@ struct HuffImgDev {
   int8_t blk_ac[kHuffMaxBlocks];
   int8_t blk_dx[kHuffMaxBlocks];    // its block offset inside the MCU (component blocks)
   int8_t blk_dy[kHuffMaxBlocks];
-  int8_t comp_h[3], comp_v[3];     // sampling factors (blocks per MCU per component)
-  int8_t pad[3];
+  int8_t comp_h[4], comp_v[4];     // sampling factors (blocks per MCU per component)
 };
 
 // One entropy-coded segment (restart interval) of one image.

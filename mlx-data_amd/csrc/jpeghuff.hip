@@ -729,7 +729,10 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
         if (sz != 0) {
           const int v = extend_nz(raw, sz);
           blk[kk] = (int16_t)v;
-          if (dc) __hip_atomic_fetch_add(dcslot[dec.comp()], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          // (component 3, a CMYK / YCCK file's K: decoded, never output -- its
+          // DC values are not summed)
+          if (dc && dec.comp() < 3)
+            __hip_atomic_fetch_add(dcslot[dec.comp()], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       });
       if (fin) {
@@ -802,7 +805,7 @@ __device__ void decode_job(const void* wbase, Shared& sh, const HuffDev* tab, co
       for (int r = 0; r < 4; r++) v[r] = q + r < dc1 ? a[r][0] : (int16_t)0;
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        if (q + r < dc1) {
+        if (q + r < dc1 && cc[r] < 3) {  // (K's DC differences stay as they are: never output)
           const int x = (cc[r] == 0 ? (p0 += v[r]) : cc[r] == 1 ? (p1 += v[r]) : (p2 += v[r]));
           a[r][0] = (int16_t)x;
         }

@@ -84,13 +84,15 @@ def _dct_blocks(plane, q):
     return np.clip(z, -1023, 1023)
 
 
-def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0, coefs=None):
+def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0, coefs=None, adobe=None):
     """pixels: (H, W) or (H, W, 3) uint8 -> baseline JPEG bytes (4:4:4 when
     three components, which are written as given: Y, Cb, Cr).  q: the flat
     quantiser (int) or a 64-entry table in natural order.  coefs: the
     quantised blocks to write instead of the pixels' -- per component a
     (rows, cols, 64) zig-zag array (DC within +-2047 of its neighbour, AC
-    within +-1023) -- pixels then only gives the frame size."""
+    within +-1023) -- pixels then only gives the frame size.  adobe: write an
+    Adobe APP14 marker with this colour transform (0: RGB / CMYK as stored,
+    1: YCbCr, 2: YCCK for four components)."""
     a = pixels if pixels.ndim == 3 else pixels[:, :, None]
     h, w, nc = a.shape
     qt = np.full(64, q, np.int64) if np.isscalar(q) else np.asarray(q, np.int64)
@@ -138,6 +140,8 @@ def encode(pixels, dc=DEEP_DC, ac=DEEP_AC, q=2, restart_mcus=0, coefs=None):
         return bytes([0xFF, marker]) + (len(body) + 2).to_bytes(2, "big") + body
 
     out = bytearray(b"\xff\xd8")
+    if adobe is not None:
+        out += seg(0xEE, b"Adobe" + (100).to_bytes(2, "big") + bytes(4) + bytes([adobe]))
     out += seg(0xDB, bytes([0]) + bytes(qt[ZIGZAG].astype(np.uint8).tolist()))
     out += seg(0xC0, bytes([8]) + h.to_bytes(2, "big") + w.to_bytes(2, "big") + bytes([nc]) +
                b"".join(bytes([i + 1, 0x11, 0]) for i in range(nc)))

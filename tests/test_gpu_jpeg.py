@@ -202,8 +202,67 @@ def test_chunked_batch_of_large_images():
         assert np.array_equal(g, w_)
 
 
-def test_host_only_colour_spaces_are_refused():
-    c = capi.JpegCoefs(GOLD["cmyk_jpg"])
+def _cmyk_files(seed):
+    """Four-component files: Pillow CMYK (Adobe transform 0, 1x1 sampling;
+    baseline, restart intervals, progressive), and tests/jpeg_enc.py files
+    with an Adobe marker of transform 2 (YCCK) and 0 (CMYK), with restarts."""
+    import jpeg_enc as J
+    from PIL import Image
+
+    rng = np.random.default_rng(seed)
+    out = [bytes(GOLD["cmyk_jpg"])]
+    for i in range(6):
+        h, w = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        kw = dict(quality=int(rng.integers(20, 101)), progressive=i % 3 == 2)
+        if i % 3 == 1:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 6))
+        b = io.BytesIO()
+        Image.fromarray(_smooth(rng, h, w, 4), "CMYK").save(b, "JPEG", **kw)
+        out.append(b.getvalue())
+    for i in range(4):
+        h, w = int(rng.integers(8, 200)), int(rng.integers(8, 200))
+        out.append(J.encode(_smooth(rng, h, w, 4), q=int(rng.integers(1, 6)), adobe=2 if i % 2 == 0 else 0,
+                            restart_mcus=3 if i >= 2 else 0))
+    return out
+
+
+def test_cmyk_and_ycck_finish_on_the_device():
+    """four-component JPEGs (CMYK and YCCK) finish on the
+    device -- their first three components through the IDCT and the colour
+    step (YCCK: YCbCr -> RGB inverted, jdcolor.c ycck_cmyk_convert), the
+    reference's first three channels of libjpeg's CMYK output
+    (ImageJPEG.cpp:112-124) -- with the sequential ones' Huffman data decoded
+    on the device too (K decoded and dropped).  Identity geometry: equal to
+    the host decoder and to libjpeg's raw output through Pillow (255 - Pillow's
+    un-inverted Adobe CMYK), then resized + cropped like the host bytes."""
+    from PIL import Image
+
+    datas = _cmyk_files(41)
+    coefs = [capi.JpegCoefs(d, device_entropy=True) for d in datas]
+    assert all(c.device_ok for c in coefs)
+    assert sum(c.entropy_pending for c in coefs) >= 6  # the sequential ones
+    got = _gpu(coefs, [_identity(c) for c in coefs], False)
+    for i, (d, g, c) in enumerate(zip(datas, got, coefs)):
+        img = g.reshape(c.height, c.width, 3)
+        assert np.array_equal(img, capi.jpeg_decode(d)), i
+        pil = Image.open(io.BytesIO(d))
+        assert pil.mode == "CMYK"
+        assert np.array_equal(img, 255 - np.asarray(pil)[:, :, :3]), i
+    geoms = []
+    for c in coefs:
+        rw, rh = capi.resize_smallest_side_dims(c.width, c.height, 48)
+        cw, ch = min(40, rw), min(40, rh)
+        geoms.append((0, 0, c.width, c.height, rw, rh, (rw - cw) // 2, (rh - ch) // 2, cw, ch, 1))
+    for f32 in (False, True):
+        want = _host_ref([capi.jpeg_decode(d) for d in datas], geoms, f32)
+        for g, w_ in zip(_gpu(coefs, geoms, f32), want):
+            assert np.array_equal(g, w_)
+
+
+def test_lossless_files_are_refused_on_the_device():
+    import jpeg_enc as J
+
+    c = capi.JpegCoefs(J.encode_lossless(_smooth(np.random.default_rng(3), 20, 30), psv=1))
     assert not c.device_ok
     with pytest.raises(capi.MxdError, match="host"):
         _gpu([c], [_identity(c)], False)

@@ -345,8 +345,10 @@ def test_device_entropy_parse_routes_and_host_finish():
     for k in [k[:-4] for k in GOLD.files if k.endswith("_jpg")]:
         data = bytes(GOLD[f"{k}_jpg"])
         c = capi.JpegCoefs(data, device_entropy=True)
-        if "cmyk" in k or "trunc" in k or ("prog" in k and "prog0" not in k):
+        if "trunc" in k or ("prog" in k and "prog0" not in k):
             assert not c.entropy_pending, k
+        if "cmyk" in k:  # (round 6: four-component sequential files decode on the device too)
+            assert c.entropy_pending and c.device_ok, k
         if c.device_ok:
             assert np.array_equal(c.finish(), GOLD[f"{k}_rgb"]), k
 
@@ -467,3 +469,25 @@ def test_scalar_byte_scans_match_avx512(tmp_path):
         out[flag] = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True,
                                    check=True, timeout=300).stdout.strip()
     assert out["0"] == out["1"] and len(out["0"]) == 64
+
+
+def test_ycck_and_cmyk_decode_like_libjpeg():
+    """Four-component files (Adobe transform 2 = YCCK, 0 = CMYK; tests/
+    jpeg_enc.py) decode to the first three channels of libjpeg's CMYK output
+    (ImageJPEG.cpp:112-124): YCCK through jdcolor.c ycck_cmyk_convert (C, M,
+    Y = 255 - R, G, B).  Pinned to libjpeg-turbo through Pillow, whose Adobe
+    CMYK comes un-inverted (255 - libjpeg's raw values)."""
+    Image = pytest.importorskip("PIL.Image")
+    import jpeg_enc as J
+
+    rng = np.random.default_rng(43)
+    for i in range(8):
+        h, w = int(rng.integers(1, 90)), int(rng.integers(1, 90))
+        d = J.encode(_smooth(rng, h, w, 4), q=int(rng.integers(1, 8)), adobe=2 if i % 2 == 0 else 0,
+                     restart_mcus=2 if i % 4 == 3 else 0)
+        pil = Image.open(io.BytesIO(d))
+        assert pil.mode == "CMYK"
+        assert np.array_equal(capi.jpeg_decode(d), 255 - np.asarray(pil)[:, :, :3]), i
+        c = capi.JpegCoefs(d, device_entropy=True)
+        assert c.device_ok and c.entropy_pending, i
+        assert np.array_equal(c.finish(), 255 - np.asarray(pil)[:, :, :3]), i
