@@ -23,7 +23,7 @@ def test_host_finish_equals_decode(case):
     c = capi.JpegCoefs(data)
     want = GOLD[f"{case}_rgb"]
     assert (c.height, c.width) == want.shape[:2]
-    assert c.device_ok == (case != "cmyk")
+    assert c.device_ok  # (CMYK too, since round 6; only lossless files finish on the host alone)
     got = c.finish()
     assert np.array_equal(got, want)
     assert np.array_equal(c.finish(), got)  # the handle stays valid
