@@ -64,18 +64,20 @@ res = {
     "us_below_50pct_of_peak_at_end": round(float(span - max(t for t, r in zip(grid, running) if r >= 0.5 * peak)), 2),
     "running_every_5us": running[::5],
 }
-# units are laid out XCD by XCD (wave.hip xcd_remap): unit u ran on XCD
-# (u // 4) // ceil(blocks / 8) (blocks = ceil(units / 4)), roughly
-nb = (len(a) + 3) // 4
+# units are laid out XCD by XCD (wave.hip xcd_remap, kWaves = 8 waves per
+# workgroup): unit u ran on XCD (u // 8) // ceil(blocks / 8) (blocks =
+# ceil(units / 8)), roughly
+WAVES = 8
+nb = (len(a) + WAVES - 1) // WAVES
 q = (nb + 7) // 8
 ids = np.nonzero(np.frombuffer(buf, np.uint64).reshape(N, 2)[:, 0] > 0)[0]
-xcd = np.minimum((ids // 4) // q, 7) if os.environ.get("NO_XCD_REMAP") is None else (ids // 4) % 8
+xcd = np.minimum((ids // WAVES) // q, 7) if os.environ.get("NO_XCD_REMAP") is None else (ids // WAVES) % 8
 img = ids // max(1, len(a) // bench.WORKLOADS[w]["batch"])
 res["image_octile_unit_us_median"] = [round(float(np.median(dur[(img * 8 // bench.WORKLOADS[w]["batch"]) == k])), 1)
                                       for k in range(8)]
 res["xcd_unit_us_median"] = [round(float(np.median(dur[xcd == x])), 1) for x in range(8)]
 res["xcd_end_us_max"] = [round(float(en[xcd == x].max()), 1) for x in range(8)]
-res["wave_in_block_median"] = [round(float(np.median(dur[ids % 4 == k])), 1) for k in range(4)]
+res["wave_in_block_median"] = [round(float(np.median(dur[ids % WAVES == k])), 1) for k in range(WAVES)]
 # within one XCD: block order (dispatch order) vs duration
 x0 = ids[xcd == 0]
 res["xcd0_first_vs_last_blocks_us"] = [round(float(np.median(dur[(xcd == 0) & (ids < x0.min() + 128)])), 1),

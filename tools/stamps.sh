@@ -9,8 +9,9 @@ if [ "$1" = build ]; then
   cd mlx-data_amd
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -I../include -Icsrc --offload-arch=gfx950 -ffp-contract=fast \
     -DMXD_STAMPS=1 ${STAMP_FLAGS:-} -c csrc/wave.hip -o build/wave_stamps.o || exit 1
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave_stamps.o build/pixmap.o \
-    build/capi.o build/plan.o build/batch.o build/hostpath.o build/taps.o build/jpeg.o build/jpegdev.o -o ../tools/libmxd_amd_stamps.so || exit 1
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/resample.o build/wave_stamps.o build/band.o \
+    build/band_plan.o build/pixmap.o build/capi.o build/plan.o build/batch.o build/hostpath.o build/taps.o \
+    build/jpeg.o build/jpegdev.o build/jpeghuff.o -o ../tools/libmxd_amd_stamps.so || exit 1
   exit 0
 fi
 shift
