@@ -188,21 +188,6 @@ struct SegLds {
   int32_t pad[2];
 };
 
-// Sync-round trails (see sync_rounds): kTrail block ends per subsequence,
-// packed as position offset (14 bits) | block of the MCU (5 bits) | blocks
-// completed (13 bits); subsequences longer than kTrailMaxBits decode without
-// them.
-// Tuning builds: -DMXD_HUFF_TRAILS=0 decodes every round in full (the A/B).
-#ifndef MXD_HUFF_TRAILS
-#define MXD_HUFF_TRAILS 1
-#endif
-constexpr int kTrail = 3;
-constexpr int kTrailCountBits = 13, kTrailPosBits = 14;
-constexpr uint32_t kTrailCountMask = (1u << kTrailCountBits) - 1u;
-constexpr int kTrailMaxCount = (int)kTrailCountMask - 1;
-constexpr int kTrailMaxBits = (1 << kTrailPosBits) - 512;
-constexpr uint32_t kNoTrail = 0xffffffffu;  // (block field 31: no real state, b <= 27)
-
 // Per-job shared state (static part; the tables, segment records and, when
 // they fit, the job's words follow in dynamic LDS: jpeg_huff_lds_bytes).
 struct Shared {
@@ -213,11 +198,6 @@ struct Shared {
   int32_t in_pos[kHuffThreads], out_pos[kHuffThreads];
   int8_t in_b[kHuffThreads], in_k[kHuffThreads], out_b[kHuffThreads], out_k[kHuffThreads];
   int32_t done[kHuffThreads];      // blocks a subsequence completes (sync pass)
-  // the first kTrail block ends of each subsequence's latest decode (sync
-  // rounds' early exit): position past its nominal start << 18 | block of
-  // the MCU (3 j) << 13 | blocks completed there
-  uint32_t trail[kTrail][kHuffThreads];
-  int8_t trail_n[kHuffThreads];
   int32_t blk_off[kHuffMaxBlocks];  // block j of an MCU: offset of MCU (0, 0)'s block j in the image's coefficients,
   int32_t blk_mxs[kHuffMaxBlocks];  // and its steps per MCU column / row (non-interleaved: per block)
   int32_t blk_mys[kHuffMaxBlocks];
@@ -488,17 +468,8 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
 #ifdef MXD_HUFF_STAMPS
   int round = 0;
 #endif
-  // Decodes subsequence id from its start state to its end: exit state and
-  // blocks completed.  Early exit (round 6): the decode keeps its first
-  // kTrail block-end states (bit position, block of the MCU) with the blocks
-  // completed up to each (sh.trail); a later round's decode of the same
-  // subsequence from a changed start stops as soon as it reaches one of
-  // them -- the decoder's whole state then equals the earlier path's, so the
-  // rest of the path, its exit and its remaining block count are the earlier
-  // decode's.  A decode whose start changed by a few bits typically joins its
-  // old path within a block or two instead of re-decoding all sub_bits.
-  const bool trails = MXD_HUFF_TRAILS != 0 && sh.img.sub_bits <= kTrailMaxBits;
-  auto decode_one = [&](int id, const Sub& v) __attribute__((always_inline)) {
+  // decodes subsequence id from its start state to its end: exit state and blocks completed
+  auto decode_one = [&](int id, const Sub& v) {
     rd.init(wbase, v.sg.word, (v.sg.bits + 31) >> 5, v.sg.lim);
     rd.seek(sh.in_pos[id]);
     dec.b = sh.in_b[id];
@@ -506,90 +477,17 @@ __device__ void sync_rounds(const void* wbase, Shared& sh, const HuffDev* tab, c
     int done = 0;
     const auto nop = [](bool, int, uint32_t, int) {};
     int32_t rem = v.end - sh.in_pos[id];
-    const int nold = trails ? sh.trail_n[id] : 0;
-    const uint32_t o0 = nold > 0 ? sh.trail[0][id] : kNoTrail;
-    const uint32_t o1 = nold > 1 ? sh.trail[1][id] : kNoTrail;
-    const uint32_t o2 = nold > 2 ? sh.trail[2][id] : kNoTrail;
-    uint32_t f0 = kNoTrail, f1 = kNoTrail, f2 = kNoTrail;  // this decode's block ends
-    int nnew = 0, mi = -1;                                 // mi: the old block end it joined
-    // a block-end state (k = 0) at the current position: record it, look it up
-    auto at_state = [&](bool record) __attribute__((always_inline)) {
-      const int32_t off = v.end - rem - v.start;
-      if (!trails || off < 0 || off >= (1 << kTrailPosBits) || done > kTrailMaxCount) {
-        nnew += record ? 1 : 0;  // (counted, so the lookups stop as they would)
-        return;
-      }
-      const uint32_t key = (uint32_t)off << 5 | (uint32_t)dec.b;
-      if (record) {  // (selects, not an indexed store: that would put f0..f2 in scratch memory)
-        const uint32_t e = key << kTrailCountBits | (uint32_t)done;
-        f0 = nnew == 0 ? e : f0;
-        f1 = nnew == 1 ? e : f1;
-        f2 = nnew == 2 ? e : f2;
-        nnew++;
-      }
-      mi = (o0 >> kTrailCountBits) == key ? 0 : (o1 >> kTrailCountBits) == key ? 1 : (o2 >> kTrailCountBits) == key ? 2 : -1;
-    };
-    if (dec.k == 0) at_state(false);  // a start on an old block end
-    // Only the first kTrail + 1 block ends are recorded and looked up: a
-    // changed start lies within one step of the old one (both are the
-    // nominal start, or a predecessor's exit within 31 bits past it), so
-    // the paths join early or not at all -- and work done at a block end
-    // runs, divergent, on almost every step of the wave, so it stops once
-    // every lane is past that point.
-    // A step consumes <= 31 bits: while the end is further than one step,
-    // two steps both start before it.
-    while (rem > 31 && mi < 0) {
-      if (dec.step(rd, rem, nop)) {
-        done++;
-        if (nnew <= kTrail) {
-          at_state(true);
-          if (mi >= 0) break;
-        }
-      }
-      if (dec.step(rd, rem, nop)) {
-        done++;
-        if (nnew <= kTrail) at_state(true);
-      }
+    // a step consumes <= 31 bits: while the end is further than one step,
+    // two steps both start before it
+    while (rem > 31) {
+      done += dec.step(rd, rem, nop) ? 1 : 0;
+      done += dec.step(rd, rem, nop) ? 1 : 0;
     }
-    while (rem > 0 && mi < 0) {
-      if (dec.step(rd, rem, nop)) {
-        done++;
-        if (nnew <= kTrail) at_state(true);
-      }
-    }
-    if (mi >= 0) {
-      // joined the old path at its block end mi: the old exit stands; the
-      // blocks are this decode's so far plus the old path's after that point
-      const uint32_t om = mi == 0 ? o0 : mi == 1 ? o1 : o2;
-      const int base = done - (int)(om & kTrailCountMask);
-      sh.done[id] += base;
-      // the new trail: this decode's block ends, then the old ones past mi
-      // with their counts rebased
-      auto rebase = [&](uint32_t o) __attribute__((always_inline)) {  // (an entry whose count would leave its field is dropped)
-        const int c = (int)(o & kTrailCountMask) + base;
-        return o == kNoTrail || c < 0 || c > kTrailMaxCount ? kNoTrail : (o & ~kTrailCountMask) | (uint32_t)c;
-      };
-      const uint32_t r1 = mi < 1 ? rebase(o1) : kNoTrail;
-      const uint32_t r2 = mi < 2 ? rebase(o2) : kNoTrail;
-      // the old entries past mi, in order: a, then b
-      const uint32_t a = mi == 0 ? r1 : r2, b = mi == 0 ? r2 : kNoTrail;
-      const uint32_t t0 = nnew == 0 ? a : f0;
-      const uint32_t t1 = nnew == 0 ? b : nnew == 1 ? a : f1;
-      const uint32_t t2 = nnew == 1 ? b : nnew == 2 ? a : nnew == 0 ? kNoTrail : f2;
-      sh.trail[0][id] = t0;
-      sh.trail[1][id] = t1;
-      sh.trail[2][id] = t2;
-      sh.trail_n[id] = (int8_t)((t0 != kNoTrail) + (t1 != kNoTrail) + (t2 != kNoTrail));
-      return;
-    }
+    while (rem > 0) done += dec.step(rd, rem, nop) ? 1 : 0;
     sh.out_pos[id] = v.end - rem;
     sh.out_b[id] = (int8_t)dec.b;
     sh.out_k[id] = (int8_t)dec.k;
     sh.done[id] = done;
-    sh.trail[0][id] = f0;
-    sh.trail[1][id] = f1;
-    sh.trail[2][id] = f2;
-    sh.trail_n[id] = (int8_t)min(nnew, kTrail);
   };
   for (;;) {
     // this round's subsequences, compacted onto the first threads, so a
@@ -1022,7 +920,6 @@ __global__ __launch_bounds__(kHuffThreads) void jpeg_huff(const uint32_t* __rest
     sh.in_b[t] = 0;
     sh.in_k[t] = 0;
     sh.done[t] = 0;
-    sh.trail_n[t] = 0;
   }
   __syncthreads();
   HUFF_STAMP(1);
