@@ -613,6 +613,11 @@ def main():
     alg_bytes = sum(footprint_bytes(capi, sw, sh, C, *g[:6]) for (sw, sh), g in zip(sizes, geoms)) + sum(out_bytes)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     copy_gbs = capi.copy_bandwidth(1 << 30, dev, 20) if not args.no_copy else None
+    # the streaming forms (nontemporal loads and stores, + sc1): the ceiling
+    # the nt-load kernels are held to
+    copy_nt = ({p: capi.copy_bandwidth(1 << 30, dev, 20, policy=p) for p in (1, 2)}
+               if not args.no_copy else None)
+    best_copy = max(copy_nt.values()) if copy_nt else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.workload),
                 "alg_bytes_per_launch": int(alg_bytes), "alg_bytes_per_image": round(alg_bytes / B, 1),
@@ -625,7 +630,12 @@ def main():
                 "host_ms_per_call_fresh": round(fresh_host_ms, 5) if fresh_host_ms else None,
                 "kernel": kernel_name(capi, sizes[0], geoms[0], f32, args.policy),
                 "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
-                "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None}
+                "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs else None,
+                "copy_ceiling_nt_gbs": round(copy_nt[1], 1) if copy_nt else None,
+                "copy_ceiling_nt_sc1_gbs": round(copy_nt[2], 1) if copy_nt else None,
+                "frac_of_streaming_copy_ceiling": round(achieved / best_copy, 4) if best_copy else None,
+                # the planner's choice (batch.cpp: nt when the call's sources total >= 128 MiB)
+                "load_policy": "nt" if sum(sw * sh * C for sw, sh in sizes) >= (128 << 20) else "default"}
 
     # the other single-GPU BASELINE configs' kernels on this box and build
     # (rank 0 of a single-rank C2 run; each a few seconds)

@@ -38,8 +38,8 @@ extern "C" {
  * MXD_TUNE_HUFF_GLOBAL, MXD_TUNE_HOST_WAIT; round 5: MXD_TUNE_HOST_STREAMS,
  * MXD_TUNE_HUFF_JOB, MXD_TUNE_JPEG_RGB, mxd_jpeg_plane_sources,
  * mxd_host_stats, mxd_jpeg_coefs_load.
- * 6 (round 6): the knobs MXD_TUNE_DEVICE_TIMING, MXD_TUNE_LOAD_POLICY and
- * mxd_device_stats; CMYK / YCCK files finish (and sequential ones
+ * 6 (round 6): the knobs MXD_TUNE_DEVICE_TIMING, MXD_TUNE_LOAD_POLICY,
+ * mxd_device_stats and mxd_copy_bandwidth_policy; CMYK / YCCK files finish (and sequential ones
  * entropy-decode) on the device; mxd_jpeg_coefs_entropy_pending no longer
  * reports 2 (progressive files are
  * entropy-decoded on the host). */
@@ -238,6 +238,9 @@ int mxd_describe_band_plan(const mxd_image* image, int32_t out_dtype, int32_t* i
 /* Measured device-memory ceiling: a 16-byte-per-lane streaming copy of `bytes`
  * (read + write counted), averaged over `iters` launches, in GB/s. */
 int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps);
+/* The same copy with a cache policy on its loads and stores (ABI 6): 0 the
+ * default (= mxd_copy_bandwidth), 1 nontemporal, 2 nontemporal + sc1. */
+int mxd_copy_bandwidth_policy(size_t bytes, int32_t device, int32_t iters, int32_t policy, float* gbps);
 
 /* ---- device memory / streams / events (so a C or C++ host needs no torch) */
 int mxd_set_device(int32_t device);

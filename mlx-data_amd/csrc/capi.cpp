@@ -275,7 +275,12 @@ int mxd_describe_plan(const mxd_image* image, int32_t out_dtype, int32_t device,
 }
 
 int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps) {
-  if (!gbps || bytes < 16 || iters <= 0) return fail(MXD_ERR_INVALID, "mxd: bad copy_bandwidth arguments");
+  return mxd_copy_bandwidth_policy(bytes, device, iters, 0, gbps);
+}
+
+int mxd_copy_bandwidth_policy(size_t bytes, int32_t device, int32_t iters, int32_t policy, float* gbps) {
+  if (!gbps || bytes < 16 || iters <= 0 || policy < 0 || policy > 2)
+    return fail(MXD_ERR_INVALID, "mxd: bad copy_bandwidth arguments");
   if (int rc = check_device(device)) return rc;
   DeviceGuard g(device);
   void *a = nullptr, *b = nullptr;
@@ -287,9 +292,9 @@ int mxd_copy_bandwidth(size_t bytes, int32_t device, int32_t iters, float* gbps)
   MXD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   MXD_HIP(hipEventCreate(&e0));
   MXD_HIP(hipEventCreate(&e1));
-  mxd::launch_copy(a, b, bytes, s);
+  mxd::launch_copy(a, b, bytes, s, policy);
   MXD_HIP(hipEventRecord(e0, s));
-  for (int32_t i = 0; i < iters; i++) mxd::launch_copy(a, b, bytes, s);
+  for (int32_t i = 0; i < iters; i++) mxd::launch_copy(a, b, bytes, s, policy);
   MXD_HIP(hipEventRecord(e1, s));
   MXD_HIP(hipEventSynchronize(e1));
   float ms = 0.0f;

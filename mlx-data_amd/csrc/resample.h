@@ -148,7 +148,8 @@ int wave_capacity(const WaveCfg& cfg, int device);
 // Diagnostics: the occupancy API's blocks per CU, the kernel's VGPRs and LDS
 // bytes per block; returns waves per block (-1: no kernel / error).
 int wave_kernel_info(const WaveCfg& cfg, int device, int* api_blocks, int* vgprs, int* lds);
-int launch_copy(const void* src, void* dst, size_t bytes, void* stream);
+// policy: 0 default (16-B loads / stores per thread), 1 nt, 2 nt sc1 (buffer forms)
+int launch_copy(const void* src, void* dst, size_t bytes, void* stream, int policy = 0);
 
 // Dynamic LDS bytes the kernel needs for cfg.
 int resample_smem_bytes(const LaunchCfg& cfg);

@@ -113,10 +113,20 @@ constexpr int kPad = 32;  // floats after each plane: padded taps read zeros the
 #define MXD_PRIO 1
 #endif
 
+// Tuning builds (-DMXD_PRIO_MODE=<n>, round 6; the unit stamps show a
+// workgroup's waves 4-7 finishing ~3 % after waves 0-3): 1 = waves 4-7 one
+// level above the others at equal progress (capped at 3); 2 = levels in
+// eighths of the band, cycling 3, 2, 1, 0, 3, 2, 1, 0 (a wave that falls
+// behind its neighbours wins ties within the cycle).
+#ifndef MXD_PRIO_MODE
+#define MXD_PRIO_MODE 0
+#endif
 __device__ __forceinline__ void progress_prio(bool on, int done, int total) {
   if (!on) return;
   if constexpr (MXD_PRIO != 0) {
-    const int level = 3 - (4 * done) / (total + 1);  // 3 at the start .. 0 in the last quarter
+    int level = 3 - (4 * done) / (total + 1);  // 3 at the start .. 0 in the last quarter
+    if constexpr (MXD_PRIO_MODE == 1) level = min(3, level + ((threadIdx.x >> 6) >= kWaves / 2 ? 1 : 0));
+    if constexpr (MXD_PRIO_MODE == 2) level = 3 - ((8 * done) / (total + 1)) % 4;
     switch (level) {
       case 3: __builtin_amdgcn_s_setprio(3); break;
       case 2: __builtin_amdgcn_s_setprio(2); break;
@@ -954,10 +964,33 @@ __global__ __launch_bounds__(256) void copy_f4(const f32x4* __restrict__ a, f32x
   if (i < n) b[i] = a[i];
 }
 
-int launch_copy(const void* src, void* dst, size_t bytes, void* stream) {
+// The same copy with a cache policy on both sides (buffer loads / stores,
+// one 4-KiB window per block): AUX 2 = nt, 18 = nt sc1 -- the streaming forms
+// tools/nt_ceiling.hip measured fastest (round 6), so bench.py can quote the
+// ceiling the nt-load kernels are held to on the box it runs on.
+template <int AUX>
+__global__ __launch_bounds__(256) void copy_policy(const char* __restrict__ a, char* __restrict__ b, size_t bytes) {
+  const size_t base = (size_t)blockIdx.x * 4096;
+  const int n = (int)min((size_t)4096, bytes - base);
+  const Rsrc ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a) + base, (short)0, n, 0x00020000);
+  const Rsrc rb = __builtin_amdgcn_make_buffer_rsrc(b + base, (short)0, n, 0x00020000);
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ra, threadIdx.x * 16, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rb, threadIdx.x * 16, 0, AUX);
+}
+
+int launch_copy(const void* src, void* dst, size_t bytes, void* stream, int policy) {
   const size_t n = bytes / 16;
-  hipLaunchKernelGGL(copy_f4, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const f32x4*>(src), reinterpret_cast<f32x4*>(dst), n);
+  const auto s = reinterpret_cast<hipStream_t>(stream);
+  if (policy == 0) {
+    hipLaunchKernelGGL(copy_f4, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const f32x4*>(src), reinterpret_cast<f32x4*>(dst), n);
+  } else {
+    const unsigned blocks = (unsigned)((n * 16 + 4095) / 4096);
+    const auto* a = static_cast<const char*>(src);
+    auto* b = static_cast<char*>(dst);
+    if (policy == 1) hipLaunchKernelGGL(copy_policy<2>, dim3(blocks), dim3(256), 0, s, a, b, n * 16);
+    else hipLaunchKernelGGL(copy_policy<18>, dim3(blocks), dim3(256), 0, s, a, b, n * 16);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -32,7 +32,7 @@ EXPORTS = (
     "mxd_is_jpeg", "mxd_jpeg_info", "mxd_jpeg_decode",
     "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_load", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
     "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
-    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources", "mxd_host_stats", "mxd_device_stats",
+    "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources", "mxd_host_stats", "mxd_device_stats", "mxd_copy_bandwidth_policy",
 )
 
 MXD_AFFINE = 0
@@ -496,9 +496,11 @@ class DeviceBuffer:
             pass
 
 
-def copy_bandwidth(nbytes=1 << 30, device=0, iters=20):
+def copy_bandwidth(nbytes=1 << 30, device=0, iters=20, policy=0):
+    """Streaming copy rate in GB/s (read + written bytes); policy 0 default,
+    1 nontemporal, 2 nontemporal + sc1 (mxd_copy_bandwidth_policy)."""
     g = ctypes.c_float()
-    check(lib().mxd_copy_bandwidth(ctypes.c_size_t(nbytes), device, iters, ctypes.byref(g)))
+    check(lib().mxd_copy_bandwidth_policy(ctypes.c_size_t(nbytes), device, iters, policy, ctypes.byref(g)))
     return g.value
 
 
