@@ -13,6 +13,10 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "libmxd_amd.so")
 
 MXD_OK = 0
+MXD_ERR_INVALID = 1
+MXD_ERR_UNSUPPORTED = 2
+MXD_ERR_DEVICE = 3
+MXD_ERR_NOMEM = 4
 MXD_U8 = 0
 MXD_F32_DIV255 = 1
 

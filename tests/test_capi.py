@@ -1,6 +1,7 @@
 """CPU-side checks of the C ABI (no device work): the library loads, exports
 every symbol include/mxd_amd.h declares, its host logic (geometry, tap tables,
 argument validation) matches the reference rules and the oracle."""
+import ctypes
 import os
 import re
 
@@ -169,3 +170,18 @@ def test_every_downscale_ratio_up_to_16_has_a_wave_kernel():
     assert (p["taps"], p["dmax"], p["p"], p["nstrips"]) == (24, 12, 8, 6)
     p = _plan(_entry(6000, 4000, 6000 * 3, 384, 256, cx=80, cy=16))
     assert (p["taps"], p["dmax"]) == (32, 16)
+
+
+def test_round6_knobs_and_counters_without_a_device():
+    """ABI 6 (host side, no GPU call): MXD_TUNE_LOAD_POLICY and
+    MXD_TUNE_DEVICE_TIMING are knobs (set returns the previous value, an
+    unknown knob -1), mxd_device_stats reads and resets, and
+    mxd_copy_bandwidth_policy refuses bad arguments with the ABI's status."""
+    for knob in (capi.MXD_TUNE_LOAD_POLICY, capi.MXD_TUNE_DEVICE_TIMING):
+        assert capi.set_tuning(knob, 2) == 0
+        assert capi.set_tuning(knob, 0) == 2
+    assert capi.lib().mxd_set_tuning(capi.MXD_TUNE_LOAD_POLICY + 1, 0) == -1  # MXD_TUNE_COUNT
+    assert capi.device_stats(reset=True) == {"chunks": 0, "device_s": 0.0}
+    g = ctypes.c_float()
+    assert capi.lib().mxd_copy_bandwidth_policy(ctypes.c_size_t(1 << 20), 0, 1, 3, ctypes.byref(g)) == capi.MXD_ERR_INVALID
+    assert capi.lib().mxd_copy_bandwidth_policy(ctypes.c_size_t(8), 0, 1, 0, ctypes.byref(g)) == capi.MXD_ERR_INVALID

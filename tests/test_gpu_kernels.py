@@ -2,7 +2,8 @@
 mlx-data_amd/csrc/wave.hip (scatter schedule with byte lanes or pixel lanes,
 gather) and the general tile
 kernel of resample.hip -- give bit-identical outputs on the same inputs (each
-sums an output row's taps in the same order from 0), and the default choice
+sums an output row's taps in the same order from 0), in both source-load
+cache policies of the scatter kernels, and the default choice
 matches the oracle (+-1 per channel, < 0.2 % of channels differing).  The
 kernel is chosen through mxd_set_kernel_policy (include/mxd_amd.h)."""
 import numpy as np
@@ -15,12 +16,18 @@ pytestmark = pytest.mark.gpu
 
 from mlx_data_amd import capi
 
+# (name, kernel policy, source-load policy: MXD_TUNE_LOAD_POLICY 0 auto /
+# 1 default / 2 streaming (nt) -- round 6's second form of every scatter
+# kernel, which the planner takes for calls with >= 128 MiB of sources)
 KINDS = [
-    ("default", capi.MXD_POLICY_AUTO),
-    ("pixel_lanes", capi.MXD_POLICY_NO_BYTES),
-    ("byte_lanes", capi.MXD_POLICY_BYTES),
-    ("gather", capi.MXD_POLICY_NO_SCATTER),
-    ("general", capi.MXD_POLICY_NO_WAVE),
+    ("default", capi.MXD_POLICY_AUTO, 1),
+    ("pixel_lanes", capi.MXD_POLICY_NO_BYTES, 1),
+    ("byte_lanes", capi.MXD_POLICY_BYTES, 1),
+    ("gather", capi.MXD_POLICY_NO_SCATTER, 1),
+    ("general", capi.MXD_POLICY_NO_WAVE, 1),
+    ("nt_default", capi.MXD_POLICY_AUTO, 2),
+    ("nt_pixel_lanes", capi.MXD_POLICY_NO_BYTES, 2),
+    ("nt_byte_lanes", capi.MXD_POLICY_BYTES, 2),
 ]
 
 
@@ -47,11 +54,13 @@ CASES = {"c2": c2, "mixed": mixed, "c5": c5}
 def run_kinds(imgs, geoms, f32):
     outs = {}
     try:
-        for name, policy in KINDS:
+        for name, policy, load in KINDS:
             capi.set_kernel_policy(policy)
+            capi.set_tuning(capi.MXD_TUNE_LOAD_POLICY, load)
             outs[name] = run_device(imgs, geoms, f32=f32)
     finally:
         capi.set_kernel_policy(capi.MXD_POLICY_AUTO)
+        capi.set_tuning(capi.MXD_TUNE_LOAD_POLICY, 0)
     return outs
 
 
