@@ -8,7 +8,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/r06
 export TMPDIR=/tmp
-TAG=${1:-r06c}
+TAG=${1:-r06z}
 O=gpurun_out/r06/$TAG
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
