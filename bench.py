@@ -37,7 +37,14 @@ Extra fields:
                 / the timed wall per step (streams overlapped); `traffic` = HBM bytes
                 per launch from the PMC summary recorded for this workload in
                 profiles/traffic.json; `copy_ceiling_gbs` = the measured
-                streaming-copy rate of this box.
+                streaming-copy rate of this box (default cache policy),
+                `copy_ceiling_nt_gbs` / `copy_ceiling_nt_sc1_gbs` the same
+                copy with nontemporal (+ sc1) loads and stores, and
+                `frac_of_streaming_copy_ceiling` the kernel against the
+                better of those; `load_policy` the planner's choice for the
+                kernel's source loads (nt for >= 128 MiB of sources).
+  workloads     (c2 runs) per-launch records of C3 / C4 / C5 on the same box
+                and build: kernel ms per launch, frac of 8 TB/s, traffic.
   cpu_baseline  the oracle's C restatement of the reference CPU path
                 (stbir-semantics resize -> crop -> batch -> numpy /255) on a
                 bounded sample at 1, 8 and all of this rank's cores (rank 0,
@@ -48,10 +55,17 @@ Extra fields:
                 2, Pillow q=90) through the operator surface -- load_image ->
                 image_resize_smallest_side(256) -> image_center_crop(224) ->
                 image_to_float -> batch(128, device=0) -> prefetch(16, 16) --
-                repeated for >= 3 s; beside it the same with the Huffman
-                decode on the host, and the reference-algorithm CPU
-                restatement (Pillow's libjpeg-turbo decode -> the oracle's C
-                stbir -> crop -> /255) on the same files and this rank's cores.
+                repeated for >= 3 s, at the box's GPU_MAX_HW_QUEUES;
+                `device_busy` (isolated device time per image x the rate) and
+                the `bound` it implies; `host_out` the host-ending form
+                (batch(128) into host memory, D2H inside the timed run) with
+                its D2H GB/s; `hwq16` the device leg in a child process with
+                16 hardware queues; `progressive` the files saved progressive
+                (host entropy decode, device finish); beside them the same
+                chain with the Huffman decode on the host, and the
+                reference-algorithm CPU restatement (Pillow's libjpeg-turbo
+                decode -> the oracle's C stbir -> crop -> /255) on the same
+                files and this rank's cores.
   e2e           the product's host-resident path (mxd_resize_crop_host: host
                 images in, host batch out; the kernel reads each image's
                 source footprint and writes results over PCIe, from / to

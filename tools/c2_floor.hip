@@ -1,0 +1,165 @@
+// tools/c2_floor.hip -- the floor of C2's access pattern on this box
+// (diagnostic, not product; round 6).
+//
+// The product's C2 launch (resample_wave<3, 8, true, 8, 2, kScatter, 2, 4>,
+// split pixel lanes) with its arithmetic removed: 256 images of 960 rows x
+// 3840 B; 4,096 units = image x 8 bands x 2 strips, one 64-lane wave each, 8
+// waves per 512-thread workgroup (2 per CU, one occupancy round), XCD-
+// contiguous workgroup order as wave.hip's xcd_remap; per unit the band's
+// ~109 source rows (its 28 output rows x 3.768 + the 8-tap halo), each row one
+// 1,536-B window per wave read as two dwordx3 loads per lane over two
+// contiguous 768-B halves, a 4-slot register ring (3 rows ahead); per output
+// row a 1,344-B strip row of f32 stored as f32x3 per lane (2 per lane).  The
+// same bytes as the kernel (547 MB read, 154 MB written per launch).
+// Variants: source-load policy (default / nt), stores (nt / none), loads
+// (on / none), and a light "V pass" (convert + 2 FMAs per byte) to see how
+// much of the kernel's VALU the pattern hides.  Median of 7 x 20 launches
+// over two alternating source / output sets.
+//
+//   hipcc --offload-arch=gfx950 -O3 tools/c2_floor.hip -o tools/c2_floor && tools/c2_floor
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                    \
+  do {                                                              \
+    hipError_t e = (x);                                             \
+    if (e != hipSuccess) {                                          \
+      fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e)); \
+      exit(1);                                                      \
+    }                                                               \
+  } while (0)
+
+typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+using Rsrc = __amdgpu_buffer_rsrc_t;
+
+constexpr int kImgs = 256, kRows = 960, kStride = 3840;
+constexpr int kBands = 8, kStrips = 2, kOutRows = 224, kOutRowBytes = 224 * 12;
+constexpr int kFy0 = 58, kFy1 = 902;                 // footprint rows [58, 902)
+constexpr int kFx0 = 218 * 3;                        // footprint's first byte in a row
+constexpr int kWin = 1536, kHalf = 768;              // bytes per wave row window, per half
+constexpr int kStripStep = 422 * 3;                  // the second strip's window start (bytes)
+constexpr int kWaves = 8, kUnits = kImgs * kBands * kStrips;
+
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int q = n >> 3, r = n & 7;
+  const int xcd = b & 7, idx = b >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int AUX, bool LOADS, bool STORES, bool VALU>
+__global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restrict__ src, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
+  if (unit >= kUnits) return;
+  const int img = unit / (kBands * kStrips), rest = unit % (kBands * kStrips);
+  const int band = rest / kStrips, strip = rest % kStrips;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)img * kRows * kStride), (short)0,
+                                                   kRows * kStride, 0x00020000);
+  const int w0 = kFx0 + strip * kStripStep;
+  const int v0 = w0 + 12 * lane, v1 = w0 + kHalf + 12 * lane;
+  const int oy0 = band * (kOutRows / kBands), oy1 = oy0 + kOutRows / kBands;
+  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
+  float* orow0 = out + ((size_t)img * kOutRows) * (kOutRowBytes / 4) + strip * (kOutRowBytes / 8);
+  constexpr int R = 4;
+  u32x3 ring[R][2];
+  auto load = [&](int row, u32x3 (&d)[2]) {
+    if constexpr (LOADS) {
+      d[0] = __builtin_amdgcn_raw_buffer_load_b96(r, v0 + row * kStride, 0, AUX);
+      d[1] = __builtin_amdgcn_raw_buffer_load_b96(r, v1 + row * kStride, 0, AUX);
+    } else {
+      d[0] = u32x3{(unsigned)row, 0u, 0u};
+      d[1] = d[0];
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < R - 1; d++) load(min(r0 + d, r1 - 1), ring[d]);
+  float acc[2][12] = {};
+  int oy = oy0;
+  for (int row = r0; row < r1; row += R) {
+#pragma unroll
+    for (int d = 0; d < R; d++) {
+      load(min(row + d + R - 1, r1 - 1), ring[(d + R - 1) % R]);
+      const u32x3* x = ring[d];
+      if constexpr (VALU) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int i = 0; i < 12; i++) {
+            const float f = (float)((x[h][i >> 2] >> (8 * (i & 3))) & 255u);
+            acc[h][i] = __builtin_fmaf(f, 0.25f, acc[h][i]);
+            acc[(h + 1) & 1][i] = __builtin_fmaf(f, 0.125f, acc[(h + 1) & 1][i]);
+          }
+      } else {
+        acc[0][0] += (float)(x[0].x & 255u);
+        acc[1][0] += (float)(x[1].y >> 24);
+      }
+      const int want = (int)((row + d - r0) / 3.768f) + oy0;
+      if (want > oy && oy < oy1) {
+        if constexpr (STORES) {
+          float* o = orow0 + (size_t)oy * (kOutRowBytes / 4);
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const int px = lane + 64 * q;
+            if (px < 112)
+              __builtin_nontemporal_store(f32x3{acc[0][q], acc[1][q], acc[0][q + 2]},
+                                          reinterpret_cast<f32x3*>(o + 3 * px));
+          }
+        }
+        oy++;
+      }
+    }
+  }
+  if (acc[0][0] == -1.0f) out[lane] = acc[1][1];
+}
+
+template <class K>
+static float time_us(K kernel, unsigned char** src, float** out, int iters = 20, int reps = 7) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const unsigned blocks = kUnits / kWaves;
+  for (int i = 0; i < 4; i++) hipLaunchKernelGGL(kernel, dim3(blocks), dim3(512), 0, 0, src[i & 1], out[i & 1]);
+  std::vector<float> t;
+  for (int r = 0; r < reps; r++) {
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL(kernel, dim3(blocks), dim3(512), 0, 0, src[i & 1], out[i & 1]);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    t.push_back(ms * 1000.0f / iters);
+  }
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+int main() {
+  unsigned char* src[2];
+  float* out[2];
+  const size_t sb = (size_t)kImgs * kRows * kStride, ob = (size_t)kImgs * kOutRows * kOutRowBytes;
+  for (int i = 0; i < 2; i++) {
+    CHECK(hipMalloc(&src[i], sb));
+    CHECK(hipMalloc(&out[i], ob));
+    CHECK(hipMemset(src[i], 7 + i, sb));
+  }
+  CHECK(hipDeviceSynchronize());
+  const double alg = 256.0 * (844.0 * 844 * 3 + 224.0 * 224 * 3 * 4);
+  auto report = [&](const char* name, float us) {
+    printf("{\"probe\": \"%s\", \"us\": %.1f, \"alg_TBps\": %.3f, \"frac_of_8TBps\": %.3f}\n", name, us,
+           alg / (us * 1e-6) / 1e12, alg / (us * 1e-6) / 8e12);
+    fflush(stdout);
+  };
+  for (int round = 0; round < 2; round++) {
+    report("nt loads + nt stores", time_us(c2_floor<2, true, true, false>, src, out));
+    report("default loads + nt stores", time_us(c2_floor<0, true, true, false>, src, out));
+    report("nt loads, no stores", time_us(c2_floor<2, true, false, false>, src, out));
+    report("no loads, nt stores", time_us(c2_floor<2, false, true, false>, src, out));
+    report("nt loads + nt stores + V-pass VALU", time_us(c2_floor<2, true, true, true>, src, out));
+  }
+  return 0;
+}
