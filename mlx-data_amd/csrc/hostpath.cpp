@@ -779,7 +779,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     pending[k & 1] = -1;
     if (sl.timed) {
       float ms = 0.0f;
-      if (hipEventElapsedTime(&ms, sl.k0, sl.k1) == hipSuccess) {
+      if (hipEventElapsedTime(&ms, sl.k0, sl.k1) == hipSuccess && ms > 0.0f) {
         g_device_stats[0].fetch_add(1, std::memory_order_relaxed);
         g_device_stats[1].fetch_add((int64_t)((double)ms * 1e6), std::memory_order_relaxed);
       }
@@ -1054,7 +1054,10 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                hipMemcpyHostToDevice, sl.stream));
     }
     if (sl.timed && !jpeg) MXD_HIP(hipEventRecord(sl.k0, sl.stream));
-    if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) return rc;
+    if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) {
+      sl.timed = false;  // (k1 not recorded for this chunk)
+      return rc;
+    }
     if (sl.timed) MXD_HIP(hipEventRecord(sl.k1, sl.stream));
     if (!dst_device) {
       if (out_staged > 0 && !pin_out_dev)
