@@ -42,8 +42,10 @@ extern "C" {
  * mxd_device_stats and mxd_copy_bandwidth_policy; CMYK / YCCK files finish (and sequential ones
  * entropy-decode) on the device; mxd_jpeg_coefs_entropy_pending no longer
  * reports 2 (progressive files are
- * entropy-decoded on the host). */
-#define MXD_ABI_VERSION 6
+ * entropy-decoded on the host).
+ * 7 (round 6, later): the knobs MXD_TUNE_STEAL and MXD_TUNE_STEAL_MIN (work
+ * stealing in the scatter wave launches). */
+#define MXD_ABI_VERSION 7
 
 enum mxd_status {
   MXD_OK = 0,
@@ -201,7 +203,14 @@ int mxd_set_kernel_policy(int32_t policy);
  * calls cost the device; read when a chunk is launched);
  * MXD_TUNE_LOAD_POLICY: cache policy of the scatter wave kernels' source
  * loads (0 = automatic: streaming (nt) when the call's sources total >= 128
- * MiB, else the default policy; 1 = default policy always; 2 = nt always). */
+ * MiB, else the default policy; 1 = default policy always; 2 = nt always);
+ * MXD_TUNE_STEAL (ABI 7): work stealing between the units of a scatter wave
+ * launch -- a wave done with its band runs the last blocks of the band
+ * furthest behind (0 = automatic: on; 1 = off; 2 = on; 3 = on, with the
+ * owners of odd units starting ~80 us late so that thieves run their last
+ * blocks -- a test mode: timing changes, the bytes written do not);
+ * MXD_TUNE_STEAL_MIN (ABI 7): fewest blocks (two output rows each at C2's
+ * shape) a stealing wave takes from one band (0 = 2). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -216,7 +225,9 @@ enum mxd_tune {
   MXD_TUNE_JPEG_RGB = 10,
   MXD_TUNE_DEVICE_TIMING = 11,
   MXD_TUNE_LOAD_POLICY = 12,
-  MXD_TUNE_COUNT = 13
+  MXD_TUNE_STEAL = 13,
+  MXD_TUNE_STEAL_MIN = 14,
+  MXD_TUNE_COUNT = 15
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 

@@ -534,32 +534,103 @@ struct HStrip {
   }
 };
 
+// Work stealing over the blocks of scatter bands (round 6).  All units of a
+// launch start together, but they do not end together: C2's units end
+// between 115 and 145 us (profiles/r06/r06f_unit_stamps.jsonl: XCD medians
+// 128-138 us), and a wave that is done idles its share of HBM for the rest of
+// the launch.  So a wave that finishes its own band (the OWNER's part) turns
+// THIEF: it takes the last blocks of the band whose owner is furthest from
+// its limit and runs them itself, from the same schedule.
+//
+// A block is BG groups of the schedule (the unrolled loop body).  Rows done
+// in block b get contributions only from groups >= the first group of block
+// b - 1 (S - 1 < BG), so a thief that runs blocks [b0 - 1, b1) from zeroed
+// sums and writes the rows of blocks [b0, b1) writes exactly the bytes the
+// owner would have: same loads, same FMAs in the same order from 0.
+//
+// Two 64-bit words per unit, tagged with the launch's generation `gen` (a
+// word with another generation is a previous launch's, i.e. "untouched"):
+//   word 0, LIMIT: the owner stops before this block (untouched: all of them);
+//     thieves lower it with a compare-and-swap and run [new, old);
+//   word 1, PROGRESS: (blocks << 16 | the block the owner is starting),
+//     published by the owner at every block (blocks when it is done).
+// The owner reads LIMIT once per block, one block ahead of its use, so a
+// read can be stale by a block: it then runs rows a thief runs too, and both
+// write the same bytes.  Correctness never depends on timing: every row below
+// the last LIMIT the owner read is the owner's, every range a compare-and-swap
+// removed is its thief's, and an owner that reads a stale word runs on.
+// Tuning builds: -DMXD_STEAL=0 compiles stealing out.
+#ifndef MXD_STEAL
+#define MXD_STEAL 1
+#endif
+struct Steal {
+  unsigned long long* word;  // the unit's two words (null: no stealing)
+  uint32_t gen;
+  int b0, b1;  // thief: blocks whose rows it writes (it starts one block earlier)
+  bool thief;
+  bool delay;  // test mode (MXD_TUNE_STEAL 3): the owners of odd units start ~80 us late
+};
+
+// Kernel argument `steal`: fewest blocks worth taking (bits 0-15) and the
+// test mode (bit 16).
+constexpr int kStealDelay = 1 << 16;
+
+__device__ __forceinline__ unsigned long long claim_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Runs a band's scatter schedule (see the top of the file); on_row(acc, y) is
 // called with the V sums of every completed output row y.
 template <class L, int S, int DMAX, class SrcT, class OnRow, class Start>
 __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const SrcT& src, OnRow&& on_row,
-                                             Start&& start, bool prio, bool sync = false) {
+                                             Start&& start, bool prio, bool sync, const Steal& st, int lane) {
   constexpr int C = L::VC;
   constexpr int R = scatter_ring_slots(DMAX, SrcT::kLaneBytes);
   constexpr int LA = R - 1;  // iterations loaded ahead
   constexpr int BG = scatter_block_groups(S, DMAX, SrcT::kLaneBytes);
   constexpr int E = scatter_entry_words(S);
   constexpr int P = L::VP;
+  static_assert(S - 1 <= BG, "a thief warms up over one block");
   const int ngroups = sched[0];
+  const int nblk = ngroups / BG;
   kint* gout = sched + 1;
   kint* itab = sched + entry_off;
+  const int bbeg = MXD_STEAL != 5 && st.thief ? max(st.b0 - 1, 0) : 0;
+  const int bend = st.thief ? min(st.b1, nblk) : nblk;
+  const bool owner = MXD_STEAL != 3 && st.word != nullptr && !st.thief;
+  if (owner && st.delay) {
+    // test mode: announce block 0, then sleep so that thieves take this band's
+    // last blocks before its owner runs (timing only: the bytes are the same)
+    if (lane == 0)
+      __hip_atomic_store(st.word + 1, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 24; i++) __builtin_amdgcn_s_sleep(127);
+  }
   float acc[S][C][P];
 #pragma unroll
   for (int s = 0; s < S; s++) zero_planes<C, P>(acc[s]);
   typename SrcT::RawT ring[R];
+  kint* it0 = itab + bbeg * BG * DMAX * E;
   static_for<LA>([&](auto ic) {
     __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's counted waits assume it
-    ring[decltype(ic)::value] = src.load(itab[decltype(ic)::value * E + 1]);
+    ring[decltype(ic)::value] = src.load(it0[decltype(ic)::value * E + 1]);
   });
   __builtin_amdgcn_sched_barrier(0);
   start();  // after the prologue loads (see resample_wave)
   __builtin_amdgcn_sched_barrier(0);
-  for (int gb = 0; gb < ngroups; gb += BG) {
+  unsigned long long lword = 0;  // the LIMIT word as read one block earlier (owner)
+  for (int b = bbeg; b < bend; b++) {
+    const int gb = b * BG;
+    if (owner) {
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lword >> 32));
+      const int lim = hi == st.gen ? __builtin_amdgcn_readfirstlane((int)(uint32_t)lword) : nblk;
+      if (b >= lim) break;
+      if (lane == 0)
+        __hip_atomic_store(st.word + 1, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16) | (uint32_t)b,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lword = claim_load(st.word);
+    }
+    const bool write = !st.thief || b >= st.b0;
     kint* blk = itab + gb * DMAX * E;
     static_for<BG>([&](auto gc) {
       constexpr int gi = decltype(gc)::value;
@@ -588,13 +659,16 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
         }
       });
       const int y = gout[gb + gi];
-      if (y >= 0) on_row(acc[gi % S], y);
+      if (y >= 0 && write) on_row(acc[gi % S], y);
       zero_planes<C, P>(acc[gi % S]);
       if constexpr (MXD_SYNC_STRIPS != 0)
         if (sync) __builtin_amdgcn_s_barrier();
     });
     progress_prio(prio, gb + BG, ngroups);
   }
+  if (owner && lane == 0)  // done: nothing left to take
+    __hip_atomic_store(st.word + 1, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16) | (uint32_t)nblk,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // bytes per lane of Lay<c, p> (a plain function: template arguments do not
@@ -602,16 +676,27 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
 constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; }
 
 // Minimum waves per SIMD the register allocation must allow, by lane width.
+// Scatter kernels (round 6): the stealing loop adds ~10 VGPRs, which would
+// take the kernels that ran at 117-127 VGPRs -- two 8-wave workgroups per CU
+// -- past 128 (one workgroup per CU); those (the narrow, byte-lane and JPEG
+// plane kernels up to DMAX 9, and the wide ones of DMAX 4: C2's 960 -> 256
+// at 122-125) are held to 4 waves per SIMD, i.e. 128 VGPRs.  Tuning builds:
+// -DMXD_FORCE_WIDE5=1 holds the wide DMAX 5 kernels (C5's, 129-131 VGPRs:
+// one workgroup per CU before stealing) to 128 as well.
+#ifndef MXD_FORCE_WIDE5
+#define MXD_FORCE_WIDE5 0
+#endif
 constexpr int min_waves(int c, int p, int kind, int dmax) {
-  (void)kind;
-  (void)dmax;
+  if (MXD_STEAL != 0 && kind == 2) {
+    if (lane_bytes(c, p) <= 16 ? dmax <= 9 : dmax == 4 || (MXD_FORCE_WIDE5 != 0 && dmax == 5)) return 4;
+  }
   return lane_bytes(c, p) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES;
 }
 
 // One unit (image, band, strip) by the calling wave; planes = its LDS rows.
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC, int LAUX>
 __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int nimgs, int per_img, int unit,
-                                         float* __restrict__ planes, int lane, bool prio) {
+                                         float* __restrict__ planes, int lane, bool prio, const Steal& st) {
   using L = Lay<C, P>;
   constexpr int VC = L::VC, VP = L::VP;
   progress_prio(prio, 0, 1);
@@ -754,7 +839,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    const bool sync = nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
+    const bool sync = st.word == nullptr && nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
     if constexpr (YCC) {
       static_assert(C == 3 && P == 4 && !SHIFT, "JPEG plane sources: RGB pixel lanes, P = 4, aligned windows");
       // the same window as the RGB source would have (hbase = wp0), read from the planes
@@ -778,23 +863,86 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
       ys.coff = on ? 4 * d : kNoLoad;
       ys.e = c - 1 - 4 * d;
       ys.ci = c;
-      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), ys, finish_row, start, prio, sync);
+      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), ys, finish_row, start, prio, sync, st,
+                               lane);
     } else {
-      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio, sync);
+      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio, sync, st,
+                               lane);
     }
   }
 #if MXD_STAMPS
-  if (lane == 0 && unit < kMaxStamped) {
+  if (lane == 0 && unit < kMaxStamped && !st.thief) {
     g_stamps[2 * unit] = t_start;
     g_stamps[2 * unit + 1] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
 
+// The thief's choice (see Steal): among 64 units spread over the launch
+// (every XCD's share), the one with the most blocks past its owner's next;
+// it takes half of them (at least one) when there are >= `min_avail`.
+// Returns the victim unit and sets *b0 / *b1, or returns -1 (nothing worth
+// taking: the wave exits).
+__device__ __forceinline__ int steal_pick(unsigned long long* claims, uint32_t gen, int nunits, int self, int round,
+                                          int min_avail, int lane, int* b0, int* b1) {
+#if MXD_STEAL == 6
+  const unsigned long long w = claim_load(claims + 2 * self);
+  *b0 = (int)(uint32_t)w;
+  *b1 = (int)(w >> 32);
+  return __builtin_amdgcn_readfirstlane((int)(uint32_t)w) - 1;
+#endif
+  for (int attempt = 0; attempt < 4; attempt++) {
+    const int stride = max(1, nunits >> 6);
+    const int cand = (int)(((uint32_t)self * 2654435761u + (uint32_t)(round * 4 + attempt) * 40503u +
+                            (uint32_t)lane * (uint32_t)stride) % (uint32_t)nunits);
+    const unsigned long long pw = claim_load(claims + 2 * cand + 1);
+    const unsigned long long lw = claim_load(claims + 2 * cand);
+    int avail = -1, limit = 0;
+    if ((uint32_t)(pw >> 32) == gen) {
+      const int nb = (int)((pw >> 16) & 0xffffu), at = (int)(pw & 0xffffu);
+      limit = (uint32_t)(lw >> 32) == gen ? (int)(uint32_t)lw : nb;
+      avail = limit - at - 2;  // past the block the owner runs and the one it may start
+    }
+    // the wave's best: (avail, lane) packed, max over the 64 lanes
+    // (ds_swizzle's xor patterns within each 32 lanes: immediate patterns,
+    // no per-lane address registers for the compiler to keep)
+    int key = (min(max(avail, -1), 0xffff) + 1) << 6 | lane;
+    key = max(key, __builtin_amdgcn_ds_swizzle(key, (1 << 10) | 0x1f));
+    key = max(key, __builtin_amdgcn_ds_swizzle(key, (2 << 10) | 0x1f));
+    key = max(key, __builtin_amdgcn_ds_swizzle(key, (4 << 10) | 0x1f));
+    key = max(key, __builtin_amdgcn_ds_swizzle(key, (8 << 10) | 0x1f));
+    key = max(key, __builtin_amdgcn_ds_swizzle(key, (16 << 10) | 0x1f));
+    key = max(__builtin_amdgcn_readlane(key, 0), __builtin_amdgcn_readlane(key, 32));
+    const int best = (key >> 6) - 1, who = key & 63;
+    if (best < min_avail) return -1;
+    const int v = __builtin_amdgcn_readlane(cand, who);
+    const int lim = __builtin_amdgcn_readlane(limit, who);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lw, who);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lw >> 32), who);
+    const int take = max(1, best / 2);
+    const int nl = lim - take;
+    int ok = 0;
+    if (lane == 0) {
+      unsigned long long expect = ((unsigned long long)hi << 32) | lo;
+      ok = __hip_atomic_compare_exchange_strong(claims + 2 * v, &expect, ((unsigned long long)gen << 32) | (uint32_t)nl,
+                                                __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               ? 1
+               : 0;
+    }
+    if (__builtin_amdgcn_readfirstlane(ok)) {
+      *b0 = nl;
+      *b1 = lim;
+      return v;
+    }
+  }
+  return -1;
+}
+
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC = false,
           int LAUX = MXD_LOAD_AUX>
 __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void resample_wave(
-    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio) {
+    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio, unsigned long long* claims,
+    uint32_t gen, int steal) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = Lay<C, P>;
   constexpr int PL = L::PL;
@@ -806,12 +954,30 @@ __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void r
 #pragma unroll
     for (int i = 0; i < L::PAD; i += kLanes)
       if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
-  if (unit < nunits)
-    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC, LAUX>(imgs, nimgs, per_img, unit, planes, lane,
-                                                    __builtin_amdgcn_readfirstlane(prio) != 0);
+  if (unit >= nunits) return;
+  const bool on = MXD_STEAL != 0 && KIND == kScatter && uniform_ptr<unsigned long long*>(claims) != nullptr;
+  const int sflags = __builtin_amdgcn_readfirstlane(steal);
+  Steal st{on ? uniform_ptr<unsigned long long*>(claims) + 2 * unit : nullptr,
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)gen), 0, 0, false, (sflags & kStealDelay) != 0 && (unit & 1)};
+  // the owner's band, then (stealing on) other owners' last blocks: a
+  // bounded number of rounds, each of which took at least one block
+  int u = unit;
+  bool pr = __builtin_amdgcn_readfirstlane(prio) != 0;
+  for (int round = 0;; round++) {
+    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC, LAUX>(imgs, nimgs, per_img, u, planes, lane, pr, st);
+    if (!on || MXD_STEAL == 2 || round >= 64) break;
+    int b0 = 0, b1 = 0;
+    const int v = steal_pick(uniform_ptr<unsigned long long*>(claims), st.gen, nunits, unit, round,
+                             max(1, sflags & 0xffff), lane, &b0, &b1);
+    if (v < 0) break;
+    u = __builtin_amdgcn_readfirstlane(v);
+    st = Steal{uniform_ptr<unsigned long long*>(claims) + 2 * u, st.gen, __builtin_amdgcn_readfirstlane(b0),
+               __builtin_amdgcn_readfirstlane(b1), true, false};
+    pr = false;
+  }
 }
 
-using WaveKernel = void (*)(const ImgDev*, int, int, int, int);
+using WaveKernel = void (*)(const ImgDev*, int, int, int, int, unsigned long long*, uint32_t, int);
 
 constexpr int default_p(int c) { return c == 1 ? 16 : c == 2 ? 8 : 4; }
 
@@ -869,6 +1035,7 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
     return cfg.nt ? resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false, false, kLoadNt>    \
                   : resample_wave<3, 16, F32, T_, Q_, kScatter, S_, D_, false>;
   MXD_SCATTER(2, 4, 8, 2, 8)    // 960 -> 256 (C2)
+#ifndef MXD_ONLY_C2  // register-count checks of one kernel (tools/wave_regs.sh)
   MXD_SCATTER(2, 4, 8, 1, 4)
   MXD_SCATTER(2, 5, 10, 2, 8)   // 1080 -> 256, 2160 -> 512 (C5)
   MXD_SCATTER(2, 5, 10, 1, 4)
@@ -901,12 +1068,16 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   MXD_SCATTER_B(2, 2, 3, 4)     // 375 / 333 -> 256 (C4: one strip)
   MXD_SCATTER_B(2, 2, 3, 2)
   MXD_SCATTER_B(3, 1, 2, 4)     // upsampling (200 -> 256)
+#endif
 #undef MXD_SCATTER_B
 #undef MXD_SCATTER
   return nullptr;
 }
 
 WaveKernel select_kernel(const WaveCfg& cfg) {
+#ifdef MXD_ONLY_C2
+  return cfg.kind == kScatter && cfg.f32 ? select_scatter<true>(cfg) : nullptr;
+#endif
   if (cfg.kind == kScatter) return cfg.f32 ? select_scatter<true>(cfg) : select_scatter<false>(cfg);
   if (cfg.ycc) return nullptr;  // JPEG plane sources: scatter kernels only
   switch (cfg.channels * 2 + (cfg.f32 ? 1 : 0)) {
@@ -999,7 +1170,9 @@ int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
   if (!k) return -2;
   const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
-                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.prio);
+                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.prio,
+                     cfg.kind == kScatter ? static_cast<unsigned long long*>(cfg.claims) : nullptr, cfg.gen,
+                     (cfg.steal_min & 0xffff) | (cfg.steal_delay ? kStealDelay : 0));
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -66,6 +66,8 @@ MXD_TUNE_HUFF_JOB = 9
 MXD_TUNE_JPEG_RGB = 10
 MXD_TUNE_DEVICE_TIMING = 11
 MXD_TUNE_LOAD_POLICY = 12
+MXD_TUNE_STEAL = 13
+MXD_TUNE_STEAL_MIN = 14
 
 
 class MxdImage(ctypes.Structure):

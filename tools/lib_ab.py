@@ -32,7 +32,21 @@ import numpy as np  # noqa: E402
 import band_sweep  # noqa: E402
 
 
+# "NAME@knob=v,knob=v": a library with tuning knobs set around its runs
+KNOBS = {"load": 12, "steal": 13, "steal_min": 14}
+
+
+def parse_variant(spec):
+    name, _, knobs = spec.partition("@")
+    kv = {}
+    for item in filter(None, knobs.split(",")):
+        k, _, v = item.partition("=")
+        kv[KNOBS[k]] = int(v)
+    return name, kv
+
+
 def load_variant(name, capi):
+    name = parse_variant(name)[0]
     if name == "product":
         return capi.lib()
     path = os.path.join(REPO, "tools", f"libmxd_amd_var_{name}.so")
@@ -64,7 +78,18 @@ def main():
         hs = ctypes.c_void_p(stream.handle)
         e0, e1 = capi.Event(), capi.Event()
 
-        def run(L, i):
+        knobs = {n: parse_variant(n)[1] for n in names}
+        cur = {"n": None}
+
+        def run(L, i, n=None):
+            if n is not None and cur["n"] != n:
+                # the previous variant's knobs back to 0, this one's set
+                if cur["n"] is not None:
+                    for k in knobs[cur["n"]]:
+                        libs[cur["n"]].mxd_set_tuning(k, 0)
+                for k, v in knobs[n].items():
+                    L.mxd_set_tuning(k, v)
+                cur["n"] = n
             rc = L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, 0, hs)
             if rc != 0:
                 raise RuntimeError(L.mxd_last_error().decode())
@@ -75,24 +100,24 @@ def main():
         same = {}
         for n, L in libs.items():
             sets[0][1].memset(0, stream=stream)
-            run(L, 0)
+            run(L, 0, n)
             stream.synchronize()
             got = sets[0][1].download((out_bytes,), np.uint8, stream=stream)
             if ref is None:
                 ref = got
             same[n] = bool(np.array_equal(got, ref))
             for i in range(20):
-                run(L, i)
+                run(L, i, n)
         stream.synchronize()
         times = {n: [] for n in names}
         for _ in range(args.reps):
             for n, L in libs.items():
                 for i in range(3):
-                    run(L, i)
+                    run(L, i, n)
                 stream.synchronize()
                 e0.record(stream)
                 for i in range(args.launches):
-                    run(L, i)
+                    run(L, i, n)
                 e1.record(stream)
                 stream.synchronize()
                 times[n].append(e0.elapsed_ms(e1) / args.launches)
