@@ -206,7 +206,8 @@ int mxd_set_kernel_policy(int32_t policy);
  * MiB, else the default policy; 1 = default policy always; 2 = nt always);
  * MXD_TUNE_STEAL (ABI 7): work stealing between the units of a scatter wave
  * launch -- a wave done with its band runs the last blocks of the band
- * furthest behind (0 = automatic: on; 1 = off; 2 = on; 3 = on, with the
+ * furthest behind (0 = automatic: on for a wave launch that runs alone as
+ * one occupancy round of RGB-source units; 1 = off; 2 = on; 3 = on, with the
  * owners of odd units starting ~80 us late so that thieves run their last
  * blocks -- a test mode: timing changes, the bytes written do not);
  * MXD_TUNE_STEAL_MIN (ABI 7): fewest blocks (two output rows each at C2's

@@ -697,11 +697,15 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       g.cfg.prio = nfork == 0 ? 1 : 0;  // priorities only where launches never overlap
       // Work stealing (wave.hip Steal) in scatter launches: MXD_TUNE_STEAL
       // 1 = off, 2 = on, 3 = on with the test mode (odd units' owners start
-      // late), 0 = automatic (on); MXD_TUNE_STEAL_MIN = fewest blocks worth
-      // taking from one owner (0: 2).
+      // late), 0 = automatic: on for a launch that runs alone (no forked
+      // launches beside it) as one occupancy round of RGB-source units -- with
+      // more rounds the dispatcher already hands freed slots to the waiting
+      // units, and a JPEG-plane launch's bands are a few blocks long;
+      // MXD_TUNE_STEAL_MIN = fewest blocks worth taking from one owner (0: 2).
       const int32_t steal = g_tune[MXD_TUNE_STEAL].load();
       g.cfg.claims = nullptr;
-      if (g.cfg.kind == 2 && steal != 1) {
+      const bool auto_on = nfork == 0 && !g.cfg.ycc && g.units <= wave_capacity_cached(g.cfg, device);
+      if (g.cfg.kind == 2 && (steal >= 2 || (steal == 0 && auto_on))) {
         unsigned long long* words = nullptr;
         if (int crc = claims_for(ws, lane, g.units, reinterpret_cast<hipStream_t>(s), &words)) {
           launch_rc = crc;

@@ -549,22 +549,33 @@ struct HStrip {
 // owner would have: same loads, same FMAs in the same order from 0.
 //
 // Two 64-bit words per unit, tagged with the launch's generation `gen` (a
-// word with another generation is a previous launch's, i.e. "untouched"):
-//   word 0, LIMIT: the owner stops before this block (untouched: all of them);
-//     thieves lower it with a compare-and-swap and run [new, old);
-//   word 1, PROGRESS: (blocks << 16 | the block the owner is starting),
-//     published by the owner at every block (blocks when it is done).
-// The owner reads LIMIT once per block, one block ahead of its use, so a
-// read can be stale by a block: it then runs rows a thief runs too, and both
-// write the same bytes.  Correctness never depends on timing: every row below
-// the last LIMIT the owner read is the owner's, every range a compare-and-swap
-// removed is its thief's, and an owner that reads a stale word runs on.
+// word with another generation is a previous launch's, i.e. "untouched"), in
+// two arrays of the launch's `claims` buffer (nunits words each):
+//   LIMIT[unit]: the owner stops before this block (untouched: all of them);
+//     thieves lower it with a compare-and-swap (executed at the memory side)
+//     and run [new, old);
+//   PROGRESS[unit]: (blocks << 16 | the block the owner is starting).
+// The owner reads LIMIT once per block (sc1: from its XCD's L2 while the line
+// is there, which C2's stream turns over within microseconds) and writes
+// PROGRESS with plain stores (they reach memory when the L2 writes the line
+// back): an sc1 store per block, which drops the line and goes to memory,
+// cost C2 7 % and C4 25 % (profiles/r06/r06u_lib_ab.jsonl).  So both words
+// lag, by about a block: a thief leaves the owner's next two blocks alone, an
+// owner that read a stale LIMIT runs rows a thief runs too, and both write the
+// same bytes.  Correctness never depends on timing: every row below the last
+// LIMIT the owner read is the owner's, every range a compare-and-swap removed
+// is its thief's, and an owner that reads a stale word runs on.
 // Tuning builds: -DMXD_STEAL=0 compiles stealing out.
 #ifndef MXD_STEAL
 #define MXD_STEAL 1
 #endif
+// The words live in global memory and are reached through global-space
+// pointers: a generic (flat) access would count in lgkmcnt as well as vmcnt,
+// and every scalar schedule read of the band loop would then wait for it.
+using cword = __attribute__((address_space(1))) unsigned long long;
 struct Steal {
-  unsigned long long* word;  // the unit's two words (null: no stealing)
+  cword* lim;   // the unit's LIMIT word (null: no stealing)
+  cword* prog;  // its PROGRESS word
   uint32_t gen;
   int b0, b1;  // thief: blocks whose rows it writes (it starts one block earlier)
   bool thief;
@@ -575,8 +586,14 @@ struct Steal {
 // test mode (bit 16).
 constexpr int kStealDelay = 1 << 16;
 
-__device__ __forceinline__ unsigned long long claim_load(const unsigned long long* p) {
+__device__ __forceinline__ unsigned long long claim_load(const cword* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The owner's progress: a plain (L2 write-back) store.
+__device__ __forceinline__ void publish(const Steal& st, int nblk, int b) {
+  __hip_atomic_store(st.prog, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16) | (uint32_t)b,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 // Runs a band's scatter schedule (see the top of the file); on_row(acc, y) is
@@ -597,12 +614,13 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
   kint* itab = sched + entry_off;
   const int bbeg = MXD_STEAL != 5 && st.thief ? max(st.b0 - 1, 0) : 0;
   const int bend = st.thief ? min(st.b1, nblk) : nblk;
-  const bool owner = MXD_STEAL != 3 && st.word != nullptr && !st.thief;
+  const bool owner = MXD_STEAL != 3 && st.lim != nullptr && !st.thief;
   if (owner && st.delay) {
-    // test mode: announce block 0, then sleep so that thieves take this band's
-    // last blocks before its owner runs (timing only: the bytes are the same)
+    // test mode: announce block 0 (written through, so thieves see it), then
+    // sleep so that thieves take this band's last blocks before its owner
+    // runs (timing only: the bytes are the same)
     if (lane == 0)
-      __hip_atomic_store(st.word + 1, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16), __ATOMIC_RELAXED,
+      __hip_atomic_store(st.prog, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     for (int i = 0; i < 24; i++) __builtin_amdgcn_s_sleep(127);
   }
@@ -618,17 +636,18 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
   __builtin_amdgcn_sched_barrier(0);
   start();  // after the prologue loads (see resample_wave)
   __builtin_amdgcn_sched_barrier(0);
-  unsigned long long lword = 0;  // the LIMIT word as read one block earlier (owner)
+  // Owner: the LIMIT word is loaded at the start of a block and read into a
+  // scalar at its end, so the wait for it is a counted one inside the block
+  // (a value loaded in one iteration and first used at the next one's top
+  // makes the compiler drain every load in flight there).
+  int lim = nblk;
+  unsigned long long lword = 0;
   for (int b = bbeg; b < bend; b++) {
     const int gb = b * BG;
     if (owner) {
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lword >> 32));
-      const int lim = hi == st.gen ? __builtin_amdgcn_readfirstlane((int)(uint32_t)lword) : nblk;
       if (b >= lim) break;
-      if (lane == 0)
-        __hip_atomic_store(st.word + 1, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16) | (uint32_t)b,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lword = claim_load(st.word);
+      if (lane == 0) publish(st, nblk, b);
+      lword = claim_load(st.lim);
     }
     const bool write = !st.thief || b >= st.b0;
     kint* blk = itab + gb * DMAX * E;
@@ -664,11 +683,13 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
       if constexpr (MXD_SYNC_STRIPS != 0)
         if (sync) __builtin_amdgcn_s_barrier();
     });
+    if (owner) {
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lword >> 32));
+      lim = hi == st.gen ? __builtin_amdgcn_readfirstlane((int)(uint32_t)lword) : nblk;
+    }
     progress_prio(prio, gb + BG, ngroups);
   }
-  if (owner && lane == 0)  // done: nothing left to take
-    __hip_atomic_store(st.word + 1, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16) | (uint32_t)nblk,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (owner && lane == 0) publish(st, nblk, nblk);  // done: nothing left to take
 }
 
 // bytes per lane of Lay<c, p> (a plain function: template arguments do not
@@ -839,7 +860,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    const bool sync = st.word == nullptr && nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
+    const bool sync = st.lim == nullptr && nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
     if constexpr (YCC) {
       static_assert(C == 3 && P == 4 && !SHIFT, "JPEG plane sources: RGB pixel lanes, P = 4, aligned windows");
       // the same window as the RGB source would have (hbase = wp0), read from the planes
@@ -878,30 +899,26 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
 #endif
 }
 
-// The thief's choice (see Steal): among 64 units spread over the launch
-// (every XCD's share), the one with the most blocks past its owner's next;
-// it takes half of them (at least one) when there are >= `min_avail`.
-// Returns the victim unit and sets *b0 / *b1, or returns -1 (nothing worth
-// taking: the wave exits).
-__device__ __forceinline__ int steal_pick(unsigned long long* claims, uint32_t gen, int nunits, int self, int round,
+// The thief's choice (see Steal): a window of 64 consecutive units (a few
+// lines of each word array; the units of one XCD's range, since workgroups
+// map to XCDs in contiguous unit ranges), up to 4 windows at pseudo-random
+// places; the unit with the most blocks past its owner's next two gives half
+// of them (at least one) when that is >= `min_avail`.  Returns the victim
+// unit and sets *b0 / *b1, or returns -1 (nothing worth taking: the wave
+// exits).
+__device__ __forceinline__ int steal_pick(cword* lims, cword* progs, uint32_t gen, int nunits, int self, int round,
                                           int min_avail, int lane, int* b0, int* b1) {
-#if MXD_STEAL == 6
-  const unsigned long long w = claim_load(claims + 2 * self);
-  *b0 = (int)(uint32_t)w;
-  *b1 = (int)(w >> 32);
-  return __builtin_amdgcn_readfirstlane((int)(uint32_t)w) - 1;
-#endif
   for (int attempt = 0; attempt < 4; attempt++) {
-    const int stride = max(1, nunits >> 6);
-    const int cand = (int)(((uint32_t)self * 2654435761u + (uint32_t)(round * 4 + attempt) * 40503u +
-                            (uint32_t)lane * (uint32_t)stride) % (uint32_t)nunits);
-    const unsigned long long pw = claim_load(claims + 2 * cand + 1);
-    const unsigned long long lw = claim_load(claims + 2 * cand);
+    const uint32_t h = ((uint32_t)self * 2654435761u) ^ ((uint32_t)(round * 4 + attempt + 1) * 40503u);
+    const int first = nunits > kLanes ? (int)(h % (uint32_t)(nunits - kLanes + 1)) : 0;
+    const int cand = min(first + lane, nunits - 1);
+    const unsigned long long pw = claim_load(progs + cand);
+    const unsigned long long lw = claim_load(lims + cand);
     int avail = -1, limit = 0;
     if ((uint32_t)(pw >> 32) == gen) {
       const int nb = (int)((pw >> 16) & 0xffffu), at = (int)(pw & 0xffffu);
       limit = (uint32_t)(lw >> 32) == gen ? (int)(uint32_t)lw : nb;
-      avail = limit - at - 2;  // past the block the owner runs and the one it may start
+      avail = limit - at - 3;  // past the block the owner runs, the next one, and a block of lag
     }
     // the wave's best: (avail, lane) packed, max over the 64 lanes
     // (ds_swizzle's xor patterns within each 32 lanes: immediate patterns,
@@ -914,7 +931,7 @@ __device__ __forceinline__ int steal_pick(unsigned long long* claims, uint32_t g
     key = max(key, __builtin_amdgcn_ds_swizzle(key, (16 << 10) | 0x1f));
     key = max(__builtin_amdgcn_readlane(key, 0), __builtin_amdgcn_readlane(key, 32));
     const int best = (key >> 6) - 1, who = key & 63;
-    if (best < min_avail) return -1;
+    if (best < min_avail) continue;
     const int v = __builtin_amdgcn_readlane(cand, who);
     const int lim = __builtin_amdgcn_readlane(limit, who);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lw, who);
@@ -924,7 +941,7 @@ __device__ __forceinline__ int steal_pick(unsigned long long* claims, uint32_t g
     int ok = 0;
     if (lane == 0) {
       unsigned long long expect = ((unsigned long long)hi << 32) | lo;
-      ok = __hip_atomic_compare_exchange_strong(claims + 2 * v, &expect, ((unsigned long long)gen << 32) | (uint32_t)nl,
+      ok = __hip_atomic_compare_exchange_strong(lims + v, &expect, ((unsigned long long)gen << 32) | (uint32_t)nl,
                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                ? 1
                : 0;
@@ -955,9 +972,11 @@ __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void r
     for (int i = 0; i < L::PAD; i += kLanes)
       if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
   if (unit >= nunits) return;
-  const bool on = MXD_STEAL != 0 && KIND == kScatter && uniform_ptr<unsigned long long*>(claims) != nullptr;
+  cword* const lims = MXD_GLOBAL_PTR(unsigned long long, uniform_ptr<unsigned long long*>(claims));
+  cword* const progs = lims + nunits;
+  const bool on = MXD_STEAL != 0 && KIND == kScatter && lims != nullptr;
   const int sflags = __builtin_amdgcn_readfirstlane(steal);
-  Steal st{on ? uniform_ptr<unsigned long long*>(claims) + 2 * unit : nullptr,
+  Steal st{on ? lims + unit : nullptr, progs + unit,
            (uint32_t)__builtin_amdgcn_readfirstlane((int)gen), 0, 0, false, (sflags & kStealDelay) != 0 && (unit & 1)};
   // the owner's band, then (stealing on) other owners' last blocks: a
   // bounded number of rounds, each of which took at least one block
@@ -967,11 +986,11 @@ __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void r
     run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC, LAUX>(imgs, nimgs, per_img, u, planes, lane, pr, st);
     if (!on || MXD_STEAL == 2 || round >= 64) break;
     int b0 = 0, b1 = 0;
-    const int v = steal_pick(uniform_ptr<unsigned long long*>(claims), st.gen, nunits, unit, round,
+    const int v = steal_pick(lims, progs, st.gen, nunits, unit, round,
                              max(1, sflags & 0xffff), lane, &b0, &b1);
     if (v < 0) break;
     u = __builtin_amdgcn_readfirstlane(v);
-    st = Steal{uniform_ptr<unsigned long long*>(claims) + 2 * u, st.gen, __builtin_amdgcn_readfirstlane(b0),
+    st = Steal{lims + u, progs + u, st.gen, __builtin_amdgcn_readfirstlane(b0),
                __builtin_amdgcn_readfirstlane(b1), true, false};
     pr = false;
   }

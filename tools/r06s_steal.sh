@@ -10,7 +10,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r06s}
-VARS=${2:-nosteal,product@steal=1,product,product@steal_min=1,product@steal_min=4,product@steal=3,wide5}
+VARS=${2:-nosteal,product@steal=1,product,product@steal_min=1,product@steal_min=4}
 mkdir -p gpurun_out/r06
 O=gpurun_out/r06/$TAG
 timeout -k 10 400 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_gpu_steal.py \
