@@ -945,13 +945,27 @@ def e2e_jpeg(dev, workers=16, batch=128, min_s=3.0, no_cpu=False, device_only=Fa
         # memory): the f32 batch written to host memory -- page-locked
         # staging, D2H inside the timed run -- the reference consumer's numpy
         # batch (benchmarks/comparative/caltech101/mlx_data.py:40-51)
+        capi.narrow_returns(reset=True)
         hvalue, hn, hdt, hsplit = leg("fused")
         hsplit["bound"] = bound_of(hsplit, None)
-        out_b = 224 * 224 * C * 4
+        # ABI 7: the f32 results cross the link as their u8 bytes and the host
+        # writes u8 / 255 into the batch (MXD_TUNE_F32_LINK 0, the default)
+        narrowed = capi.narrow_returns(reset=True)
+        out_b = 224 * 224 * C * (1 if narrowed else 4)
         host_out = {"value": hvalue, "images": hn, "seconds": hdt, "d2h_gbs": round(hvalue * out_b / 1e9, 2),
-                    "d2h_bytes_per_image": out_b, "host_split": hsplit,
-                    "chain": "as `chain`, but batch(128) into host memory (no device=): the f32 batch is copied "
-                             "device -> page-locked staging -> the batch array inside the timed run"}
+                    "d2h_bytes_per_image": out_b, "narrow_return": bool(narrowed), "host_split": hsplit,
+                    "chain": "as `chain`, but batch(128) into host memory (no device=): the batch's results are "
+                             "copied device -> page-locked staging (as u8 when narrow_return: the host then "
+                             "writes u8 / 255) -> the f32 batch array inside the timed run"}
+        # the same leg with the f32 results over the link (MXD_TUNE_F32_LINK 1,
+        # the pre-ABI-7 form), for the comparison
+        prev_link = capi.set_tuning(capi.MXD_TUNE_F32_LINK, 1)
+        try:
+            wvalue, _, _, wsplit = leg("fused")
+        finally:
+            capi.set_tuning(capi.MXD_TUNE_F32_LINK, prev_link)
+        host_out["f32_link"] = {"value": wvalue, "d2h_gbs": round(wvalue * 224 * 224 * C * 4 / 1e9, 2),
+                                "worker_busy": wsplit["worker_busy"]}
         # the same files saved progressive: entropy-decoded on the host
         # (round 6 retired the device decode of progressive scans), finished
         # and resized on the GPU

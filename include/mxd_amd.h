@@ -43,8 +43,9 @@ extern "C" {
  * entropy-decode) on the device; mxd_jpeg_coefs_entropy_pending no longer
  * reports 2 (progressive files are
  * entropy-decoded on the host).
- * 7 (round 6, later): the knobs MXD_TUNE_STEAL and MXD_TUNE_STEAL_MIN (work
- * stealing in the scatter wave launches). */
+ * 7 (round 6, later): f32 results bound for host memory cross the link as
+ * u8 and are expanded (x / 255) on the host -- the knob MXD_TUNE_F32_LINK and
+ * the counter mxd_narrow_returns. */
 #define MXD_ABI_VERSION 7
 
 enum mxd_status {
@@ -204,14 +205,12 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_LOAD_POLICY: cache policy of the scatter wave kernels' source
  * loads (0 = automatic: streaming (nt) when the call's sources total >= 128
  * MiB, else the default policy; 1 = default policy always; 2 = nt always);
- * MXD_TUNE_STEAL (ABI 7): work stealing between the units of a scatter wave
- * launch -- a wave done with its band runs the last blocks of the band
- * furthest behind (0 = automatic: on for a wave launch that runs alone as
- * one occupancy round of RGB-source units; 1 = off; 2 = on; 3 = on, with the
- * owners of odd units starting ~80 us late so that thieves run their last
- * blocks -- a test mode: timing changes, the bytes written do not);
- * MXD_TUNE_STEAL_MIN (ABI 7): fewest blocks (two output rows each at C2's
- * shape) a stealing wave takes from one band (0 = 2). */
+ * MXD_TUNE_F32_LINK (ABI 7): how a host-ending call returns MXD_F32_DIV255
+ * results staged through page-locked memory (0 = automatic: the kernels'
+ * u8 bytes cross the link and the host writes u8 / 255 -- the same f32 bytes,
+ * a quarter of the D2H traffic; 1 = the f32 results cross the link).  Calls
+ * whose destinations are all page-locked are always written by the device
+ * in place. */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,
@@ -226,9 +225,8 @@ enum mxd_tune {
   MXD_TUNE_JPEG_RGB = 10,
   MXD_TUNE_DEVICE_TIMING = 11,
   MXD_TUNE_LOAD_POLICY = 12,
-  MXD_TUNE_STEAL = 13,
-  MXD_TUNE_STEAL_MIN = 14,
-  MXD_TUNE_COUNT = 15
+  MXD_TUNE_F32_LINK = 13,
+  MXD_TUNE_COUNT = 14
 };
 int mxd_set_tuning(int32_t knob, int32_t value);
 
@@ -410,6 +408,12 @@ int mxd_jpeg_resize_crop_to_device(const mxd_jpeg_image* images, int32_t n, int3
  * their sample planes (4:2:0 on a scatter wave kernel, MXD_TUNE_JPEG_RGB 0:
  * no RGB frame) since the last reset; reset != 0 zeroes it after reading. */
 int mxd_jpeg_plane_sources(int64_t* count, int32_t reset);
+
+/* Diagnostics (ABI 7): images whose MXD_F32_DIV255 results a host-ending
+ * call (mxd_resize_crop_host, mxd_jpeg_resize_crop_host) returned over the
+ * link as u8 and expanded on the host (see MXD_TUNE_F32_LINK) since the last
+ * reset; reset != 0 zeroes it after reading. */
+int mxd_narrow_returns(int64_t* count, int32_t reset);
 
 /* Diagnostics: where a host-side pipeline's time goes, summed over every
  * thread since the last reset (reset != 0 zeroes them after reading).

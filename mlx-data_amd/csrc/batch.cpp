@@ -57,34 +57,7 @@ struct Workspace {
   static constexpr int kHelpers = 3;
   hipStream_t helper[kHelpers] = {};
   hipEvent_t fork = nullptr, join[kHelpers] = {};
-  // Work-stealing words of the scatter launches (wave.hip Steal), one buffer
-  // per stream lane (the caller's stream, then the helpers): launches on one
-  // stream run one after the other, and each launch tags its words with a
-  // generation of its own, so a buffer needs no clearing between launches.
-  unsigned long long* claims[1 + kHelpers] = {};
-  size_t claims_cap[1 + kHelpers] = {};
 };
-
-// Launch generations of the stealing words: never 0 (a cleared word), never
-// reused within a process (2^32 launches).
-std::atomic<uint32_t> g_claim_gen{0};
-
-// The lane's stealing words for `units` units (grown, and cleared on the
-// lane's stream, when too small).
-int claims_for(Workspace* ws, int lane, int64_t units, hipStream_t s, unsigned long long** out) {
-  const size_t need = (size_t)std::max<int64_t>(units, 1) * 2;
-  if (ws->claims_cap[lane] < need) {
-    const size_t cap = std::max<size_t>(need, (size_t)1 << 15);
-    if (ws->claims[lane]) MXD_HIP(hipFree(ws->claims[lane]));  // waits for the launches that used it
-    ws->claims[lane] = nullptr;
-    ws->claims_cap[lane] = 0;
-    MXD_HIP(hipMalloc(reinterpret_cast<void**>(&ws->claims[lane]), cap * sizeof(unsigned long long)));
-    MXD_HIP(hipMemsetAsync(ws->claims[lane], 0, cap * sizeof(unsigned long long), s));
-    ws->claims_cap[lane] = cap;
-  }
-  *out = ws->claims[lane];
-  return MXD_OK;
-}
 
 // Records a fence covering every batch launched so far on the stream.
 int record_fence(Workspace* ws, hipStream_t s) {
@@ -695,30 +668,6 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     } else if (launches[k].kind == 1) {
       Group& g = groups[launches[k].group];
       g.cfg.prio = nfork == 0 ? 1 : 0;  // priorities only where launches never overlap
-      // Work stealing (wave.hip Steal) in scatter launches: MXD_TUNE_STEAL
-      // 1 = off, 2 = on, 3 = on with the test mode (odd units' owners start
-      // late), 0 = automatic: on for a launch that runs alone (no forked
-      // launches beside it) as one occupancy round of RGB-source units -- with
-      // more rounds the dispatcher already hands freed slots to the waiting
-      // units, and a JPEG-plane launch's bands are a few blocks long;
-      // MXD_TUNE_STEAL_MIN = fewest blocks worth taking from one owner (0: 2).
-      const int32_t steal = g_tune[MXD_TUNE_STEAL].load();
-      g.cfg.claims = nullptr;
-      const bool auto_on = nfork == 0 && !g.cfg.ycc && g.units <= wave_capacity_cached(g.cfg, device);
-      if (g.cfg.kind == 2 && (steal >= 2 || (steal == 0 && auto_on))) {
-        unsigned long long* words = nullptr;
-        if (int crc = claims_for(ws, lane, g.units, reinterpret_cast<hipStream_t>(s), &words)) {
-          launch_rc = crc;
-          break;
-        }
-        uint32_t gen = ++g_claim_gen;
-        if (gen == 0) gen = ++g_claim_gen;
-        g.cfg.claims = words;
-        g.cfg.gen = gen;
-        const int32_t smin = g_tune[MXD_TUNE_STEAL_MIN].load();
-        g.cfg.steal_min = smin > 0 ? std::min(smin, 0xffff) : 2;
-        g.cfg.steal_delay = steal == 3 ? 1 : 0;
-      }
       rc = mxd::launch_wave(g.cfg, dev + wbase + g.first, s);
     } else {
       rc = mxd::launch_resample(cfg, dev + wbase + nw, s);

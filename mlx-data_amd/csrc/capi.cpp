@@ -536,6 +536,12 @@ int mxd_jpeg_plane_sources(int64_t* count, int32_t reset) {
   return MXD_OK;
 }
 
+int mxd_narrow_returns(int64_t* count, int32_t reset) {
+  if (!count) return fail(MXD_ERR_INVALID, "mxd: null count");
+  *count = reset ? g_narrow_images.exchange(0) : g_narrow_images.load();
+  return MXD_OK;
+}
+
 int mxd_release_host_buffers(void) {
   host_trim();
   return MXD_OK;

@@ -246,6 +246,7 @@ extern std::atomic<int64_t> g_host_stats[6];
 extern std::atomic<int64_t> g_device_stats[2];  // mxd_device_stats: timed chunks, device ns
 int64_t now_ns();
 extern std::atomic<int64_t> g_plane_sources;  // images resized from their JPEG sample planes (mxd_jpeg_plane_sources)
+extern std::atomic<int64_t> g_narrow_images;  // f32 results returned to the host as u8 (mxd_narrow_returns)
 const mxd::jpeg::Coefs* coefs_of(const mxd_jpeg_coefs* c);
 // Frees the buffers of every idle host-path context (mxd_release_host_buffers).
 void host_trim();

@@ -12,6 +12,7 @@
 #include <deque>
 #include <functional>
 
+#include <immintrin.h>
 #include <sched.h>
 
 namespace mxd {
@@ -209,6 +210,26 @@ int host_cpu_budget() {
     if (k > 1) n = std::min(n, k);
   }
   return std::max(1, n);
+}
+
+// dst[j] = src[j] / 255 in f32 (IEEE division: the bytes of the kernels'
+// MXD_F32_DIV255 output and of the reference's astype(float32) / 255 for the
+// same u8 value; multiplying by 1/255 differs for 126 of the 256 values).
+__attribute__((target("avx2"))) void div255_avx2(const uint8_t* src, float* dst, int64_t n) {
+  const __m256 k = _mm256_set1_ps(255.0f);
+  int64_t j = 0;
+  for (; j + 16 <= n; j += 16) {
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + j));
+    _mm256_storeu_ps(dst + j, _mm256_div_ps(_mm256_cvtepi32_ps(_mm256_cvtepu8_epi32(b)), k));
+    _mm256_storeu_ps(dst + j + 8, _mm256_div_ps(_mm256_cvtepi32_ps(_mm256_cvtepu8_epi32(_mm_srli_si128(b, 8))), k));
+  }
+  for (; j < n; j++) dst[j] = (float)src[j] / 255.0f;
+}
+
+void div255_row(const uint8_t* src, float* dst, int64_t n) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2) return div255_avx2(src, dst, n);
+  for (int64_t j = 0; j < n; j++) dst[j] = (float)src[j] / 255.0f;
 }
 
 template <class F>
@@ -412,6 +433,7 @@ struct JpegChunk {
 };
 
 std::atomic<int64_t> g_plane_sources{0};
+std::atomic<int64_t> g_narrow_images{0};
 std::atomic<int64_t> g_host_stats[6] = {};
 std::atomic<int64_t> g_device_stats[2] = {};
 int64_t now_ns() {
@@ -662,6 +684,14 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   for (int32_t i = 0; i < n; i++)
     if (int rc = validate(images[i], i)) return rc;
   if (int rc = check_device(device)) return rc;
+  // Narrow return (round 6): f32 results bound for host memory cross the link
+  // as the u8 bytes the same kernels compute before their exact /255 (the
+  // f32 output is LUT[u8] bit for bit), and the host expands them while it
+  // copies them into place -- a quarter of the D2H bytes (150 instead of 602
+  // KB per 224x224 RGB image), the host's staging-to-destination pass reading
+  // a quarter as much.  Not for page-locked destinations (written by the
+  // device in place) or MXD_TUNE_F32_LINK 1.
+  bool narrow = out_dtype == MXD_F32_DIV255 && !dst_device && g_tune[MXD_TUNE_F32_LINK].load() != 1;
   DeviceGuard g(device);
   g_host_calls.fetch_add(1);
   struct CallCount {
@@ -679,6 +709,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   struct Stage {
     int32_t x0, y0, rows;
     int64_t pitch, copy, in_off, out_off, out_row;
+    int64_t stage_row;            // an output row as staged (u8 for a narrow return)
     int64_t in_size;              // staged bytes (footprint rows, or a JPEG's coefficients)
     bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
     bool pending = false;         // JPEG whose entropy decode runs on the device (nothing staged at in_off)
@@ -704,6 +735,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                       ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
       if (!dst_device && im.dst_stride < s.out_row)
         return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+      narrow = narrow && !s.dst_pinned;
       continue;
     }
     const DevTable *xt = nullptr, *yt = nullptr;
@@ -732,7 +764,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                     ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
     if (!dst_device && im.dst_stride < s.out_row)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
+    narrow = narrow && !s.dst_pinned;
   }
+  const int32_t launch_dtype = narrow ? MXD_U8 : out_dtype;
+  for (int32_t i = 0; i < n; i++) st[i].stage_row = narrow ? st[i].out_row / 4 : st[i].out_row;
+  if (narrow) g_narrow_images.fetch_add(n, std::memory_order_relaxed);
   // Chunks of about kChunk staged bytes (at least one image each).  A JPEG
   // whose entropy decode runs on the device stages only its compressed
   // segments, and counts an eighth of its coefficient bytes (device memory):
@@ -797,7 +833,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const mxd_image& im = images[i];
       uint8_t* d = static_cast<uint8_t*>(im.dst);
       const uint8_t* src = sl.pin_out + st[i].out_off;
-      if (im.dst_stride == st[i].out_row) {
+      if (narrow) {
+        for (int32_t r = 0; r < im.crop_h; r++)
+          div255_row(src + (size_t)r * st[i].stage_row, reinterpret_cast<float*>(d + (size_t)r * im.dst_stride),
+                     st[i].stage_row);
+      } else if (im.dst_stride == st[i].out_row) {
         std::memcpy(d, src, (size_t)st[i].out_row * im.crop_h);
       } else {
         for (int32_t r = 0; r < im.crop_h; r++)
@@ -850,11 +890,11 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         if (st[i].dst_pinned == (pass == 1) && !st[i].dst_dev) {
           st[i].out_off = out_bytes;
           // page-locked destinations back to back (one copy per contiguous run)
-          const int64_t b = st[i].out_row * images[i].crop_h;
-          out_bytes += pass == 1 && (st[i].out_row & 3) == 0 ? b : (b + 255) & ~(int64_t)255;
+          const int64_t b = st[i].stage_row * images[i].crop_h;
+          out_bytes += pass == 1 && (st[i].stage_row & 3) == 0 ? b : (b + 255) & ~(int64_t)255;
         }
     for (int32_t i = chunks[k].first; i < chunks[k].second; i++)
-      if (!st[i].dst_pinned) out_staged = std::max(out_staged, st[i].out_off + st[i].out_row * images[i].crop_h);
+      if (!st[i].dst_pinned) out_staged = std::max(out_staged, st[i].out_off + st[i].stage_row * images[i].crop_h);
     if (int rc = grow_pinned(&sl.pin_in, &sl.pin_in_cap, in_bytes)) return rc;
     if (int rc = grow_device(&sl.dev_in, &sl.dev_in_cap, std::max(in_bytes, dev_in_bytes))) return rc;
     if (!dst_device) {
@@ -918,7 +958,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         dev_imgs[j].src_stride = m.pitch;
         if (!dst_device && !s.dst_dev) {
           dev_imgs[j].dst = sl.dev_out + s.out_off;
-          dev_imgs[j].dst_stride = s.out_row;
+          dev_imgs[j].dst_stride = s.stage_row;
         } else if (s.dst_dev) {
           dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
         }
@@ -940,7 +980,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
           y.records = (int32_t)std::min<int64_t>(y.cr + (int64_t)y.cstride * y.dh, INT32_MAX);
           const Stored planes{sl.dev_mid + m.plane[0], m.stride[0], 0, 0, im.src_h,
                               reinterpret_cast<const mxd::YccDev*>(sl.dev_in + jc.ycc_off) + j};
-          if (y.cr + (int64_t)y.cstride * y.dh < INT32_MAX && ycc_plan_ok(dev_imgs[j], planes, out_dtype, device)) {
+          if (y.cr + (int64_t)y.cstride * y.dh < INT32_MAX && ycc_plan_ok(dev_imgs[j], planes, launch_dtype, device)) {
             where[j] = planes;  // (dev_imgs[j] keeps the RGB frame's geometry, which run_batch validates)
             m.skip = 1;
             g_plane_sources.fetch_add(1, std::memory_order_relaxed);
@@ -961,7 +1001,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       dev_imgs[j].src_stride = std::max<int64_t>(s.pitch, (int64_t)im.src_w * im.channels);
       if (!dst_device && !s.dst_dev) {
         dev_imgs[j].dst = (pin_out_dev ? pin_out_dev : sl.dev_out) + s.out_off;
-        dev_imgs[j].dst_stride = s.out_row;
+        dev_imgs[j].dst_stride = s.stage_row;
       } else if (s.dst_dev) {
         dev_imgs[j].dst = s.dst_dev;  // written in place over PCIe
       }
@@ -1054,7 +1094,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                hipMemcpyHostToDevice, sl.stream));
     }
     if (sl.timed && !jpeg) MXD_HIP(hipEventRecord(sl.k0, sl.stream));
-    if (int rc = run_batch(dev_imgs.data(), cn, out_dtype, device, sl.stream, where.data())) {
+    if (int rc = run_batch(dev_imgs.data(), cn, launch_dtype, device, sl.stream, where.data())) {
       sl.timed = false;  // (k1 not recorded for this chunk)
       return rc;
     }

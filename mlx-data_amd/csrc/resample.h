@@ -83,14 +83,6 @@ struct WaveCfg {
   int32_t prio = 1;     // progress-based wave priority (off for the concurrent launches of a mixed batch)
   int32_t ycc = 0;      // sources are JPEG sample planes (ImgDev::ycc; scatter, p = 4, no shift)
   int32_t nt = 0;       // streaming (nt) source loads (scatter kernels; wave.hip LAUX)
-  // Work stealing between the units of a scatter launch (wave.hip Steal):
-  // claims = 2 * nunits device words of this launch's stream (null: off),
-  // gen = the launch's generation (never 0, never reused), steal_min = fewest
-  // blocks worth taking.
-  void* claims = nullptr;
-  uint32_t gen = 0;
-  int32_t steal_min = 2;
-  int32_t steal_delay = 0;  // test mode: odd units' owners start late, so thieves run their last blocks
 };
 
 // Scatter schedule geometry, shared by the kernel and the host builder:

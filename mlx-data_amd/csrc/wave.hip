@@ -534,122 +534,32 @@ struct HStrip {
   }
 };
 
-// Work stealing over the blocks of scatter bands (round 6).  All units of a
-// launch start together, but they do not end together: C2's units end
-// between 115 and 145 us (profiles/r06/r06f_unit_stamps.jsonl: XCD medians
-// 128-138 us), and a wave that is done idles its share of HBM for the rest of
-// the launch.  So a wave that finishes its own band (the OWNER's part) turns
-// THIEF: it takes the last blocks of the band whose owner is furthest from
-// its limit and runs them itself, from the same schedule.
-//
-// A block is BG groups of the schedule (the unrolled loop body).  Rows done
-// in block b get contributions only from groups >= the first group of block
-// b - 1 (S - 1 < BG), so a thief that runs blocks [b0 - 1, b1) from zeroed
-// sums and writes the rows of blocks [b0, b1) writes exactly the bytes the
-// owner would have: same loads, same FMAs in the same order from 0.
-//
-// Two 64-bit words per unit, tagged with the launch's generation `gen` (a
-// word with another generation is a previous launch's, i.e. "untouched"), in
-// two arrays of the launch's `claims` buffer (nunits words each):
-//   LIMIT[unit]: the owner stops before this block (untouched: all of them);
-//     thieves lower it with a compare-and-swap (executed at the memory side)
-//     and run [new, old);
-//   PROGRESS[unit]: (blocks << 16 | the block the owner is starting).
-// The owner reads LIMIT once per block (sc1: from its XCD's L2 while the line
-// is there, which C2's stream turns over within microseconds) and writes
-// PROGRESS with plain stores (they reach memory when the L2 writes the line
-// back): an sc1 store per block, which drops the line and goes to memory,
-// cost C2 7 % and C4 25 % (profiles/r06/r06u_lib_ab.jsonl).  So both words
-// lag, by about a block: a thief leaves the owner's next two blocks alone, an
-// owner that read a stale LIMIT runs rows a thief runs too, and both write the
-// same bytes.  Correctness never depends on timing: every row below the last
-// LIMIT the owner read is the owner's, every range a compare-and-swap removed
-// is its thief's, and an owner that reads a stale word runs on.
-// Tuning builds: -DMXD_STEAL=0 compiles stealing out.
-#ifndef MXD_STEAL
-#define MXD_STEAL 1
-#endif
-// The words live in global memory and are reached through global-space
-// pointers: a generic (flat) access would count in lgkmcnt as well as vmcnt,
-// and every scalar schedule read of the band loop would then wait for it.
-using cword = __attribute__((address_space(1))) unsigned long long;
-struct Steal {
-  cword* lim;   // the unit's LIMIT word (null: no stealing)
-  cword* prog;  // its PROGRESS word
-  uint32_t gen;
-  int b0, b1;  // thief: blocks whose rows it writes (it starts one block earlier)
-  bool thief;
-  bool delay;  // test mode (MXD_TUNE_STEAL 3): the owners of odd units start ~80 us late
-};
-
-// Kernel argument `steal`: fewest blocks worth taking (bits 0-15) and the
-// test mode (bit 16).
-constexpr int kStealDelay = 1 << 16;
-
-__device__ __forceinline__ unsigned long long claim_load(const cword* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The owner's progress: a plain (L2 write-back) store.
-__device__ __forceinline__ void publish(const Steal& st, int nblk, int b) {
-  __hip_atomic_store(st.prog, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16) | (uint32_t)b,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
 // Runs a band's scatter schedule (see the top of the file); on_row(acc, y) is
 // called with the V sums of every completed output row y.
 template <class L, int S, int DMAX, class SrcT, class OnRow, class Start>
 __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const SrcT& src, OnRow&& on_row,
-                                             Start&& start, bool prio, bool sync, const Steal& st, int lane) {
+                                             Start&& start, bool prio, bool sync = false) {
   constexpr int C = L::VC;
   constexpr int R = scatter_ring_slots(DMAX, SrcT::kLaneBytes);
   constexpr int LA = R - 1;  // iterations loaded ahead
   constexpr int BG = scatter_block_groups(S, DMAX, SrcT::kLaneBytes);
   constexpr int E = scatter_entry_words(S);
   constexpr int P = L::VP;
-  static_assert(S - 1 <= BG, "a thief warms up over one block");
   const int ngroups = sched[0];
-  const int nblk = ngroups / BG;
   kint* gout = sched + 1;
   kint* itab = sched + entry_off;
-  const int bbeg = MXD_STEAL != 5 && st.thief ? max(st.b0 - 1, 0) : 0;
-  const int bend = st.thief ? min(st.b1, nblk) : nblk;
-  const bool owner = MXD_STEAL != 3 && st.lim != nullptr && !st.thief;
-  if (owner && st.delay) {
-    // test mode: announce block 0 (written through, so thieves see it), then
-    // sleep so that thieves take this band's last blocks before its owner
-    // runs (timing only: the bytes are the same)
-    if (lane == 0)
-      __hip_atomic_store(st.prog, ((unsigned long long)st.gen << 32) | ((uint32_t)nblk << 16), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    for (int i = 0; i < 24; i++) __builtin_amdgcn_s_sleep(127);
-  }
   float acc[S][C][P];
 #pragma unroll
   for (int s = 0; s < S; s++) zero_planes<C, P>(acc[s]);
   typename SrcT::RawT ring[R];
-  kint* it0 = itab + bbeg * BG * DMAX * E;
   static_for<LA>([&](auto ic) {
     __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's counted waits assume it
-    ring[decltype(ic)::value] = src.load(it0[decltype(ic)::value * E + 1]);
+    ring[decltype(ic)::value] = src.load(itab[decltype(ic)::value * E + 1]);
   });
   __builtin_amdgcn_sched_barrier(0);
   start();  // after the prologue loads (see resample_wave)
   __builtin_amdgcn_sched_barrier(0);
-  // Owner: the LIMIT word is loaded at the start of a block and read into a
-  // scalar at its end, so the wait for it is a counted one inside the block
-  // (a value loaded in one iteration and first used at the next one's top
-  // makes the compiler drain every load in flight there).
-  int lim = nblk;
-  unsigned long long lword = 0;
-  for (int b = bbeg; b < bend; b++) {
-    const int gb = b * BG;
-    if (owner) {
-      if (b >= lim) break;
-      if (lane == 0) publish(st, nblk, b);
-      lword = claim_load(st.lim);
-    }
-    const bool write = !st.thief || b >= st.b0;
+  for (int gb = 0; gb < ngroups; gb += BG) {
     kint* blk = itab + gb * DMAX * E;
     static_for<BG>([&](auto gc) {
       constexpr int gi = decltype(gc)::value;
@@ -678,18 +588,13 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
         }
       });
       const int y = gout[gb + gi];
-      if (y >= 0 && write) on_row(acc[gi % S], y);
+      if (y >= 0) on_row(acc[gi % S], y);
       zero_planes<C, P>(acc[gi % S]);
       if constexpr (MXD_SYNC_STRIPS != 0)
         if (sync) __builtin_amdgcn_s_barrier();
     });
-    if (owner) {
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lword >> 32));
-      lim = hi == st.gen ? __builtin_amdgcn_readfirstlane((int)(uint32_t)lword) : nblk;
-    }
     progress_prio(prio, gb + BG, ngroups);
   }
-  if (owner && lane == 0) publish(st, nblk, nblk);  // done: nothing left to take
 }
 
 // bytes per lane of Lay<c, p> (a plain function: template arguments do not
@@ -697,27 +602,16 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
 constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; }
 
 // Minimum waves per SIMD the register allocation must allow, by lane width.
-// Scatter kernels (round 6): the stealing loop adds ~10 VGPRs, which would
-// take the kernels that ran at 117-127 VGPRs -- two 8-wave workgroups per CU
-// -- past 128 (one workgroup per CU); those (the narrow, byte-lane and JPEG
-// plane kernels up to DMAX 9, and the wide ones of DMAX 4: C2's 960 -> 256
-// at 122-125) are held to 4 waves per SIMD, i.e. 128 VGPRs.  Tuning builds:
-// -DMXD_FORCE_WIDE5=1 holds the wide DMAX 5 kernels (C5's, 129-131 VGPRs:
-// one workgroup per CU before stealing) to 128 as well.
-#ifndef MXD_FORCE_WIDE5
-#define MXD_FORCE_WIDE5 0
-#endif
 constexpr int min_waves(int c, int p, int kind, int dmax) {
-  if (MXD_STEAL != 0 && kind == 2) {
-    if (lane_bytes(c, p) <= 16 ? dmax <= 9 : dmax == 4 || (MXD_FORCE_WIDE5 != 0 && dmax == 5)) return 4;
-  }
+  (void)kind;
+  (void)dmax;
   return lane_bytes(c, p) > 16 ? MXD_MIN_WAVES_WIDE : MXD_MIN_WAVES;
 }
 
 // One unit (image, band, strip) by the calling wave; planes = its LDS rows.
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC, int LAUX>
 __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int nimgs, int per_img, int unit,
-                                         float* __restrict__ planes, int lane, bool prio, const Steal& st) {
+                                         float* __restrict__ planes, int lane, bool prio) {
   using L = Lay<C, P>;
   constexpr int VC = L::VC, VP = L::VP;
   progress_prio(prio, 0, 1);
@@ -860,7 +754,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
   } else {
     // ---- scatter: follow the band's schedule ----
     kint* sched = reinterpret_cast<kint*>(ytab) + band * __builtin_amdgcn_readfirstlane(im.ywidth);
-    const bool sync = st.lim == nullptr && nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
+    const bool sync = nstrips == kWaves && ((unit - local + band * nstrips) & (kWaves - 1)) == 0;
     if constexpr (YCC) {
       static_assert(C == 3 && P == 4 && !SHIFT, "JPEG plane sources: RGB pixel lanes, P = 4, aligned windows");
       // the same window as the RGB source would have (hbase = wp0), read from the planes
@@ -884,82 +778,23 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
       ys.coff = on ? 4 * d : kNoLoad;
       ys.e = c - 1 - 4 * d;
       ys.ci = c;
-      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), ys, finish_row, start, prio, sync, st,
-                               lane);
+      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), ys, finish_row, start, prio, sync);
     } else {
-      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio, sync, st,
-                               lane);
+      scatter_band<L, S, DMAX>(sched, __builtin_amdgcn_readfirstlane(im.group), src, finish_row, start, prio, sync);
     }
   }
 #if MXD_STAMPS
-  if (lane == 0 && unit < kMaxStamped && !st.thief) {
+  if (lane == 0 && unit < kMaxStamped) {
     g_stamps[2 * unit] = t_start;
     g_stamps[2 * unit + 1] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
 
-// The thief's choice (see Steal): a window of 64 consecutive units (a few
-// lines of each word array; the units of one XCD's range, since workgroups
-// map to XCDs in contiguous unit ranges), up to 4 windows at pseudo-random
-// places; the unit with the most blocks past its owner's next two gives half
-// of them (at least one) when that is >= `min_avail`.  Returns the victim
-// unit and sets *b0 / *b1, or returns -1 (nothing worth taking: the wave
-// exits).
-__device__ __forceinline__ int steal_pick(cword* lims, cword* progs, uint32_t gen, int nunits, int self, int round,
-                                          int min_avail, int lane, int* b0, int* b1) {
-  for (int attempt = 0; attempt < 4; attempt++) {
-    const uint32_t h = ((uint32_t)self * 2654435761u) ^ ((uint32_t)(round * 4 + attempt + 1) * 40503u);
-    const int first = nunits > kLanes ? (int)(h % (uint32_t)(nunits - kLanes + 1)) : 0;
-    const int cand = min(first + lane, nunits - 1);
-    const unsigned long long pw = claim_load(progs + cand);
-    const unsigned long long lw = claim_load(lims + cand);
-    int avail = -1, limit = 0;
-    if ((uint32_t)(pw >> 32) == gen) {
-      const int nb = (int)((pw >> 16) & 0xffffu), at = (int)(pw & 0xffffu);
-      limit = (uint32_t)(lw >> 32) == gen ? (int)(uint32_t)lw : nb;
-      avail = limit - at - 3;  // past the block the owner runs, the next one, and a block of lag
-    }
-    // the wave's best: (avail, lane) packed, max over the 64 lanes
-    // (ds_swizzle's xor patterns within each 32 lanes: immediate patterns,
-    // no per-lane address registers for the compiler to keep)
-    int key = (min(max(avail, -1), 0xffff) + 1) << 6 | lane;
-    key = max(key, __builtin_amdgcn_ds_swizzle(key, (1 << 10) | 0x1f));
-    key = max(key, __builtin_amdgcn_ds_swizzle(key, (2 << 10) | 0x1f));
-    key = max(key, __builtin_amdgcn_ds_swizzle(key, (4 << 10) | 0x1f));
-    key = max(key, __builtin_amdgcn_ds_swizzle(key, (8 << 10) | 0x1f));
-    key = max(key, __builtin_amdgcn_ds_swizzle(key, (16 << 10) | 0x1f));
-    key = max(__builtin_amdgcn_readlane(key, 0), __builtin_amdgcn_readlane(key, 32));
-    const int best = (key >> 6) - 1, who = key & 63;
-    if (best < min_avail) continue;
-    const int v = __builtin_amdgcn_readlane(cand, who);
-    const int lim = __builtin_amdgcn_readlane(limit, who);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lw, who);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lw >> 32), who);
-    const int take = max(1, best / 2);
-    const int nl = lim - take;
-    int ok = 0;
-    if (lane == 0) {
-      unsigned long long expect = ((unsigned long long)hi << 32) | lo;
-      ok = __hip_atomic_compare_exchange_strong(lims + v, &expect, ((unsigned long long)gen << 32) | (uint32_t)nl,
-                                                __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-               ? 1
-               : 0;
-    }
-    if (__builtin_amdgcn_readfirstlane(ok)) {
-      *b0 = nl;
-      *b1 = lim;
-      return v;
-    }
-  }
-  return -1;
-}
-
 template <int C, int P, bool F32, int T, int Q, int KIND, int S, int DMAX, bool SHIFT, bool YCC = false,
           int LAUX = MXD_LOAD_AUX>
 __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void resample_wave(
-    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio, unsigned long long* claims,
-    uint32_t gen, int steal) {
+    const ImgDev* __restrict__ imgs, int nimgs, int nunits, int per_img, int prio) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = Lay<C, P>;
   constexpr int PL = L::PL;
@@ -971,32 +806,12 @@ __global__ __launch_bounds__(kWaves* kLanes, min_waves(C, P, KIND, DMAX)) void r
 #pragma unroll
     for (int i = 0; i < L::PAD; i += kLanes)
       if (i + lane < L::PAD) planes[c * PL + L::WPX + i + lane] = 0.0f;  // padded taps read zeros
-  if (unit >= nunits) return;
-  cword* const lims = MXD_GLOBAL_PTR(unsigned long long, uniform_ptr<unsigned long long*>(claims));
-  cword* const progs = lims + nunits;
-  const bool on = MXD_STEAL != 0 && KIND == kScatter && lims != nullptr;
-  const int sflags = __builtin_amdgcn_readfirstlane(steal);
-  Steal st{on ? lims + unit : nullptr, progs + unit,
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)gen), 0, 0, false, (sflags & kStealDelay) != 0 && (unit & 1)};
-  // the owner's band, then (stealing on) other owners' last blocks: a
-  // bounded number of rounds, each of which took at least one block
-  int u = unit;
-  bool pr = __builtin_amdgcn_readfirstlane(prio) != 0;
-  for (int round = 0;; round++) {
-    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC, LAUX>(imgs, nimgs, per_img, u, planes, lane, pr, st);
-    if (!on || MXD_STEAL == 2 || round >= 64) break;
-    int b0 = 0, b1 = 0;
-    const int v = steal_pick(lims, progs, st.gen, nunits, unit, round,
-                             max(1, sflags & 0xffff), lane, &b0, &b1);
-    if (v < 0) break;
-    u = __builtin_amdgcn_readfirstlane(v);
-    st = Steal{lims + u, progs + u, st.gen, __builtin_amdgcn_readfirstlane(b0),
-               __builtin_amdgcn_readfirstlane(b1), true, false};
-    pr = false;
-  }
+  if (unit < nunits)
+    run_unit<C, P, F32, T, Q, KIND, S, DMAX, SHIFT, YCC, LAUX>(imgs, nimgs, per_img, unit, planes, lane,
+                                                    __builtin_amdgcn_readfirstlane(prio) != 0);
 }
 
-using WaveKernel = void (*)(const ImgDev*, int, int, int, int, unsigned long long*, uint32_t, int);
+using WaveKernel = void (*)(const ImgDev*, int, int, int, int);
 
 constexpr int default_p(int c) { return c == 1 ? 16 : c == 2 ? 8 : 4; }
 
@@ -1189,9 +1004,7 @@ int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream) {
   if (!k) return -2;
   const int blocks = (cfg.nunits + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kWaves * kLanes), lds_bytes(cfg), reinterpret_cast<hipStream_t>(stream),
-                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.prio,
-                     cfg.kind == kScatter ? static_cast<unsigned long long*>(cfg.claims) : nullptr, cfg.gen,
-                     (cfg.steal_min & 0xffff) | (cfg.steal_delay ? kStealDelay : 0));
+                     imgs, cfg.nimgs, cfg.nunits, cfg.per_img, cfg.prio);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -37,6 +37,7 @@ EXPORTS = (
     "mxd_jpeg_coefs_decode", "mxd_jpeg_coefs_parse", "mxd_jpeg_coefs_load", "mxd_jpeg_coefs_entropy_pending", "mxd_jpeg_coefs_free",
     "mxd_jpeg_coefs_info", "mxd_jpeg_coefs_finish",
     "mxd_jpeg_resize_crop_host", "mxd_jpeg_resize_crop_to_device", "mxd_jpeg_plane_sources", "mxd_host_stats", "mxd_device_stats", "mxd_copy_bandwidth_policy",
+    "mxd_narrow_returns",
 )
 
 MXD_AFFINE = 0
@@ -66,8 +67,7 @@ MXD_TUNE_HUFF_JOB = 9
 MXD_TUNE_JPEG_RGB = 10
 MXD_TUNE_DEVICE_TIMING = 11
 MXD_TUNE_LOAD_POLICY = 12
-MXD_TUNE_STEAL = 13
-MXD_TUNE_STEAL_MIN = 14
+MXD_TUNE_F32_LINK = 13
 
 
 class MxdImage(ctypes.Structure):
@@ -352,6 +352,14 @@ def jpeg_plane_sources(reset=False):
     reset (mxd_jpeg_plane_sources)."""
     c = ctypes.c_int64()
     check(lib().mxd_jpeg_plane_sources(ctypes.byref(c), 1 if reset else 0))
+    return c.value
+
+
+def narrow_returns(reset=False):
+    """Images whose f32 results a host-ending call returned over the link as
+    u8 and expanded on the host since the last reset (mxd_narrow_returns)."""
+    c = ctypes.c_int64()
+    check(lib().mxd_narrow_returns(ctypes.byref(c), 1 if reset else 0))
     return c.value
 
 

@@ -177,10 +177,10 @@ def test_round6_knobs_and_counters_without_a_device():
     MXD_TUNE_DEVICE_TIMING are knobs (set returns the previous value, an
     unknown knob -1), mxd_device_stats reads and resets, and
     mxd_copy_bandwidth_policy refuses bad arguments with the ABI's status."""
-    for knob in (capi.MXD_TUNE_LOAD_POLICY, capi.MXD_TUNE_DEVICE_TIMING, capi.MXD_TUNE_STEAL, capi.MXD_TUNE_STEAL_MIN):
+    for knob in (capi.MXD_TUNE_LOAD_POLICY, capi.MXD_TUNE_DEVICE_TIMING, capi.MXD_TUNE_F32_LINK):
         assert capi.set_tuning(knob, 2) == 0
         assert capi.set_tuning(knob, 0) == 2
-    assert capi.lib().mxd_set_tuning(capi.MXD_TUNE_STEAL_MIN + 1, 0) == -1  # MXD_TUNE_COUNT
+    assert capi.lib().mxd_set_tuning(capi.MXD_TUNE_F32_LINK + 1, 0) == -1  # MXD_TUNE_COUNT
     assert capi.device_stats(reset=True) == {"chunks": 0, "device_s": 0.0}
     g = ctypes.c_float()
     assert capi.lib().mxd_copy_bandwidth_policy(ctypes.c_size_t(1 << 20), 0, 1, 3, ctypes.byref(g)) == capi.MXD_ERR_INVALID

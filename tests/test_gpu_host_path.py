@@ -175,3 +175,63 @@ def test_zero_copy_bottom_right_crops_of_page_aligned_buffers(f32):
     finally:
         for p in pins:
             p.free()
+
+
+def test_narrow_return_equals_f32_over_the_link():
+    """ABI 7: f32 results bound for pageable host memory cross the link as the
+    kernels' u8 bytes and are expanded (x / 255, IEEE f32 division) on the host
+    (MXD_TUNE_F32_LINK 0, the default): the bytes equal the f32-over-the-link
+    form (MXD_TUNE_F32_LINK 1) and the numpy LUT of the u8 call, and
+    mxd_narrow_returns counts the images; a call whose destinations are all
+    page-locked (written by the device in place) is not narrowed."""
+    imgs = [synth(960, 1280, 3, 31), synth(375, 500, 3, 32), synth(61, 47, 3, 33), synth(720, 1280, 3, 34)]
+    geoms = []
+    for k, im in enumerate(imgs):
+        h, w = im.shape[:2]
+        rw, rh = capi.resize_smallest_side_dims(w, h, 256 if k != 2 else 40)
+        cw, ch = min(rw, 224 if k != 2 else 33), min(rh, 224 if k != 2 else 37)
+        geoms.append((rw, rh, (rw - cw) // 2, (rh - ch) // 2, cw, ch, k % 2))
+    pins = []
+
+    def run(dtype, link, pinned=False, pad=0):
+        prev = capi.set_tuning(capi.MXD_TUNE_F32_LINK, link)
+        try:
+            elem = 4 if dtype == capi.MXD_F32_DIV255 else 1
+            entries, outs = [], []
+            for im, g in zip(imgs, geoms):
+                h, w, c = im.shape
+                row = g[4] * c * elem + pad
+                if pinned:
+                    pd = Pinned(row * g[5])
+                    pins.append(pd)
+                    dst, dp = pd.a.reshape(g[5], row), pd.p.value
+                else:
+                    dst = np.zeros((g[5], row), np.uint8)
+                    dp = dst.ctypes.data
+                outs.append((dst, g[4] * c * elem))
+                entries.append(dict(src=im.ctypes.data, src_stride=w * c, src_w=w, src_h=h, channels=c,
+                                    resize_w=g[0], resize_h=g[1], crop_x=g[2], crop_y=g[3], crop_w=g[4],
+                                    crop_h=g[5], flip=g[6], dst=dp, dst_stride=row))
+            arr, n = capi.make_images(entries)
+            capi.resize_crop_host(arr, n, dtype, 0)
+            return [d[:, :r].copy() for d, r in outs]
+        finally:
+            capi.set_tuning(capi.MXD_TUNE_F32_LINK, prev)
+
+    lut = np.arange(256, dtype=np.uint8).astype(np.float32) / np.float32(255)
+    try:
+        u8 = run(capi.MXD_U8, 0)
+        capi.narrow_returns(reset=True)
+        narrow = run(capi.MXD_F32_DIV255, 0)
+        assert capi.narrow_returns(reset=True) == len(imgs)
+        wide = run(capi.MXD_F32_DIV255, 1)
+        padded = run(capi.MXD_F32_DIV255, 0, pad=20)  # destination rows longer than the output row
+        assert capi.narrow_returns(reset=True) == len(imgs)
+        pinned = run(capi.MXD_F32_DIV255, 0, pinned=True)
+        assert capi.narrow_returns(reset=True) == 0
+        for a, b, c, d, u in zip(narrow, wide, padded, pinned, u8):
+            assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d)
+            assert np.array_equal(a.view(np.float32), lut[u])
+    finally:
+        for p in pins:
+            p.free()

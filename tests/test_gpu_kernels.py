@@ -3,8 +3,7 @@ mlx-data_amd/csrc/wave.hip (scatter schedule with byte lanes or pixel lanes,
 gather) and the general tile
 kernel of resample.hip -- give bit-identical outputs on the same inputs (each
 sums an output row's taps in the same order from 0), in both source-load
-cache policies of the scatter kernels and with work stealing between the
-scatter units off, on, and forced (late owners), and the default choice
+cache policies of the scatter kernels, and the default choice
 matches the oracle (+-1 per channel, < 0.2 % of channels differing).  The
 kernel is chosen through mxd_set_kernel_policy (include/mxd_amd.h)."""
 import numpy as np
@@ -20,23 +19,15 @@ from mlx_data_amd import capi
 # (name, kernel policy, source-load policy: MXD_TUNE_LOAD_POLICY 0 auto /
 # 1 default / 2 streaming (nt) -- round 6's second form of every scatter
 # kernel, which the planner takes for calls with >= 128 MiB of sources)
-# A fourth field: MXD_TUNE_STEAL (work stealing between the units of a
-# scatter launch, wave.hip Steal): 0 automatic (on), 1 off, 3 on with the
-# owners of odd units starting late, so that thieves run the last blocks of
-# their bands -- the bytes must not change.
 KINDS = [
-    ("default", capi.MXD_POLICY_AUTO, 1, 0),
-    ("pixel_lanes", capi.MXD_POLICY_NO_BYTES, 1, 0),
-    ("byte_lanes", capi.MXD_POLICY_BYTES, 1, 0),
-    ("gather", capi.MXD_POLICY_NO_SCATTER, 1, 0),
-    ("general", capi.MXD_POLICY_NO_WAVE, 1, 0),
-    ("nt_default", capi.MXD_POLICY_AUTO, 2, 0),
-    ("nt_pixel_lanes", capi.MXD_POLICY_NO_BYTES, 2, 0),
-    ("nt_byte_lanes", capi.MXD_POLICY_BYTES, 2, 0),
-    ("no_steal", capi.MXD_POLICY_AUTO, 1, 1),
-    ("steal_late_owners", capi.MXD_POLICY_AUTO, 1, 3),
-    ("nt_pixel_steal_late_owners", capi.MXD_POLICY_NO_BYTES, 2, 3),
-    ("byte_steal_late_owners", capi.MXD_POLICY_BYTES, 1, 3),
+    ("default", capi.MXD_POLICY_AUTO, 1),
+    ("pixel_lanes", capi.MXD_POLICY_NO_BYTES, 1),
+    ("byte_lanes", capi.MXD_POLICY_BYTES, 1),
+    ("gather", capi.MXD_POLICY_NO_SCATTER, 1),
+    ("general", capi.MXD_POLICY_NO_WAVE, 1),
+    ("nt_default", capi.MXD_POLICY_AUTO, 2),
+    ("nt_pixel_lanes", capi.MXD_POLICY_NO_BYTES, 2),
+    ("nt_byte_lanes", capi.MXD_POLICY_BYTES, 2),
 ]
 
 
@@ -63,15 +54,13 @@ CASES = {"c2": c2, "mixed": mixed, "c5": c5}
 def run_kinds(imgs, geoms, f32):
     outs = {}
     try:
-        for name, policy, load, steal in KINDS:
+        for name, policy, load in KINDS:
             capi.set_kernel_policy(policy)
             capi.set_tuning(capi.MXD_TUNE_LOAD_POLICY, load)
-            capi.set_tuning(capi.MXD_TUNE_STEAL, steal)
             outs[name] = run_device(imgs, geoms, f32=f32)
     finally:
         capi.set_kernel_policy(capi.MXD_POLICY_AUTO)
         capi.set_tuning(capi.MXD_TUNE_LOAD_POLICY, 0)
-        capi.set_tuning(capi.MXD_TUNE_STEAL, 0)
     return outs
 
 

@@ -33,7 +33,7 @@ import band_sweep  # noqa: E402
 
 
 # "NAME@knob=v,knob=v": a library with tuning knobs set around its runs
-KNOBS = {"load": 12, "steal": 13, "steal_min": 14}
+KNOBS = {"load": 12}
 
 
 def parse_variant(spec):
