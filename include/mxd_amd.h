@@ -208,9 +208,9 @@ int mxd_set_kernel_policy(int32_t policy);
  * MXD_TUNE_F32_LINK (ABI 7): how a host-ending call returns MXD_F32_DIV255
  * results staged through page-locked memory (0 = automatic: the kernels'
  * u8 bytes cross the link and the host writes u8 / 255 -- the same f32 bytes,
- * a quarter of the D2H traffic; 1 = the f32 results cross the link).  Calls
- * whose destinations are all page-locked are always written by the device
- * in place. */
+ * a quarter of the link traffic, page-locked destinations included; 1 = the
+ * f32 results cross the link, and page-locked destinations are written by
+ * the device in place). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,

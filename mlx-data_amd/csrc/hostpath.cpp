@@ -215,13 +215,18 @@ int host_cpu_budget() {
 // dst[j] = src[j] / 255 in f32 (IEEE division: the bytes of the kernels'
 // MXD_F32_DIV255 output and of the reference's astype(float32) / 255 for the
 // same u8 value; multiplying by 1/255 differs for 126 of the 256 values).
+// The f32 rows are written with streaming (non-temporal) stores from the
+// first 32-byte boundary on: the batch is written once here and read by the
+// consumer later, and ordinary stores would first read every destination
+// line into the cache (the pass is bound by host memory traffic).
 __attribute__((target("avx2"))) void div255_avx2(const uint8_t* src, float* dst, int64_t n) {
   const __m256 k = _mm256_set1_ps(255.0f);
   int64_t j = 0;
+  for (; j < n && (reinterpret_cast<uintptr_t>(dst + j) & 31) != 0; j++) dst[j] = (float)src[j] / 255.0f;
   for (; j + 16 <= n; j += 16) {
     const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + j));
-    _mm256_storeu_ps(dst + j, _mm256_div_ps(_mm256_cvtepi32_ps(_mm256_cvtepu8_epi32(b)), k));
-    _mm256_storeu_ps(dst + j + 8, _mm256_div_ps(_mm256_cvtepi32_ps(_mm256_cvtepu8_epi32(_mm_srli_si128(b, 8))), k));
+    _mm256_stream_ps(dst + j, _mm256_div_ps(_mm256_cvtepi32_ps(_mm256_cvtepu8_epi32(b)), k));
+    _mm256_stream_ps(dst + j + 8, _mm256_div_ps(_mm256_cvtepi32_ps(_mm256_cvtepu8_epi32(_mm_srli_si128(b, 8))), k));
   }
   for (; j < n; j++) dst[j] = (float)src[j] / 255.0f;
 }
@@ -687,11 +692,12 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   // Narrow return (round 6): f32 results bound for host memory cross the link
   // as the u8 bytes the same kernels compute before their exact /255 (the
   // f32 output is LUT[u8] bit for bit), and the host expands them while it
-  // copies them into place -- a quarter of the D2H bytes (150 instead of 602
-  // KB per 224x224 RGB image), the host's staging-to-destination pass reading
-  // a quarter as much.  Not for page-locked destinations (written by the
-  // device in place) or MXD_TUNE_F32_LINK 1.
-  bool narrow = out_dtype == MXD_F32_DIV255 && !dst_device && g_tune[MXD_TUNE_F32_LINK].load() != 1;
+  // copies them into place -- a quarter of the link bytes (150 instead of 602
+  // KB per 224x224 RGB image), for page-locked destinations too (instead of
+  // the kernels writing f32 into them over PCIe: the pipeline's host batches
+  // are page-locked, and that write was the host-ending C4 bound, 43 GB/s).
+  // MXD_TUNE_F32_LINK 1: the f32 results cross the link.
+  const bool narrow = out_dtype == MXD_F32_DIV255 && !dst_device && g_tune[MXD_TUNE_F32_LINK].load() != 1;
   DeviceGuard g(device);
   g_host_calls.fetch_add(1);
   struct CallCount {
@@ -733,9 +739,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       s.dst_pinned = !dst_device && host_pinned(im.dst);
       s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
                       ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
+      if (narrow) s.dst_pinned = false, s.dst_dev = nullptr;  // staged, then expanded into place
       if (!dst_device && im.dst_stride < s.out_row)
         return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
-      narrow = narrow && !s.dst_pinned;
       continue;
     }
     const DevTable *xt = nullptr, *yt = nullptr;
@@ -762,9 +768,9 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     s.dst_pinned = !dst_device && host_pinned(im.dst);
     s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
                     ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
+    if (narrow) s.dst_pinned = false, s.dst_dev = nullptr;  // staged, then expanded into place
     if (!dst_device && im.dst_stride < s.out_row)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
-    narrow = narrow && !s.dst_pinned;
   }
   const int32_t launch_dtype = narrow ? MXD_U8 : out_dtype;
   for (int32_t i = 0; i < n; i++) st[i].stage_row = narrow ? st[i].out_row / 4 : st[i].out_row;
@@ -837,6 +843,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         for (int32_t r = 0; r < im.crop_h; r++)
           div255_row(src + (size_t)r * st[i].stage_row, reinterpret_cast<float*>(d + (size_t)r * im.dst_stride),
                      st[i].stage_row);
+        _mm_sfence();  // the streaming stores are visible before the call returns
       } else if (im.dst_stride == st[i].out_row) {
         std::memcpy(d, src, (size_t)st[i].out_row * im.crop_h);
       } else {

@@ -181,9 +181,9 @@ def test_narrow_return_equals_f32_over_the_link():
     """ABI 7: f32 results bound for pageable host memory cross the link as the
     kernels' u8 bytes and are expanded (x / 255, IEEE f32 division) on the host
     (MXD_TUNE_F32_LINK 0, the default): the bytes equal the f32-over-the-link
-    form (MXD_TUNE_F32_LINK 1) and the numpy LUT of the u8 call, and
-    mxd_narrow_returns counts the images; a call whose destinations are all
-    page-locked (written by the device in place) is not narrowed."""
+    form (MXD_TUNE_F32_LINK 1, with page-locked destinations the device's
+    in-place f32 writes) and the numpy LUT of the u8 call, and
+    mxd_narrow_returns counts the images, page-locked destinations included."""
     imgs = [synth(960, 1280, 3, 31), synth(375, 500, 3, 32), synth(61, 47, 3, 33), synth(720, 1280, 3, 34)]
     geoms = []
     for k, im in enumerate(imgs):
@@ -228,9 +228,11 @@ def test_narrow_return_equals_f32_over_the_link():
         padded = run(capi.MXD_F32_DIV255, 0, pad=20)  # destination rows longer than the output row
         assert capi.narrow_returns(reset=True) == len(imgs)
         pinned = run(capi.MXD_F32_DIV255, 0, pinned=True)
+        assert capi.narrow_returns(reset=True) == len(imgs)
+        pinned_wide = run(capi.MXD_F32_DIV255, 1, pinned=True)
         assert capi.narrow_returns(reset=True) == 0
-        for a, b, c, d, u in zip(narrow, wide, padded, pinned, u8):
-            assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d)
+        for a, b, c, d, e, u in zip(narrow, wide, padded, pinned, pinned_wide, u8):
+            assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d) and np.array_equal(a, e)
             assert np.array_equal(a.view(np.float32), lut[u])
     finally:
         for p in pins:
