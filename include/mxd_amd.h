@@ -210,7 +210,8 @@ int mxd_set_kernel_policy(int32_t policy);
  * u8 bytes cross the link and the host writes u8 / 255 -- the same f32 bytes,
  * a quarter of the link traffic, page-locked destinations included; 1 = the
  * f32 results cross the link, and page-locked destinations are written by
- * the device in place). */
+ * the device in place; 2..99 = that percentage of a call's images narrowed,
+ * spread evenly, the rest as with 1). */
 enum mxd_tune {
   MXD_TUNE_BAND_ROWS = 0,
   MXD_TUNE_BAND_LA = 1,

@@ -696,8 +696,13 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
   // KB per 224x224 RGB image), for page-locked destinations too (instead of
   // the kernels writing f32 into them over PCIe: the pipeline's host batches
   // are page-locked, and that write was the host-ending C4 bound, 43 GB/s).
-  // MXD_TUNE_F32_LINK 1: the f32 results cross the link.
-  const bool narrow = out_dtype == MXD_F32_DIV255 && !dst_device && g_tune[MXD_TUNE_F32_LINK].load() != 1;
+  // MXD_TUNE_F32_LINK 1: the f32 results cross the link; 2..99: that
+  // percentage of the images is narrowed, spread evenly, the rest cross the
+  // link as f32 (the link and the host's writes share the work).
+  const int32_t link_knob = g_tune[MXD_TUNE_F32_LINK].load();
+  const int32_t narrow_pct = link_knob == 1 ? 0 : link_knob >= 2 && link_knob < 100 ? link_knob : 100;
+  const bool narrow_any = out_dtype == MXD_F32_DIV255 && !dst_device && narrow_pct > 0;
+  auto narrow_of = [&](int32_t i) { return narrow_any && (narrow_pct == 100 || (i * narrow_pct) % 100 < narrow_pct); };
   DeviceGuard g(device);
   g_host_calls.fetch_add(1);
   struct CallCount {
@@ -716,6 +721,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     int32_t x0, y0, rows;
     int64_t pitch, copy, in_off, out_off, out_row;
     int64_t stage_row;            // an output row as staged (u8 for a narrow return)
+    bool narrow = false;          // f32 results returned as u8, expanded on the host
     int64_t in_size;              // staged bytes (footprint rows, or a JPEG's coefficients)
     bool src_pinned, dst_pinned;  // page-locked host memory: DMA'd directly, no staging copy
     bool pending = false;         // JPEG whose entropy decode runs on the device (nothing staged at in_off)
@@ -739,7 +745,8 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       s.dst_pinned = !dst_device && host_pinned(im.dst);
       s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
                       ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
-      if (narrow) s.dst_pinned = false, s.dst_dev = nullptr;  // staged, then expanded into place
+      s.narrow = narrow_of(i);
+      if (s.narrow) s.dst_pinned = false, s.dst_dev = nullptr;  // staged, then expanded into place
       if (!dst_device && im.dst_stride < s.out_row)
         return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
       continue;
@@ -768,13 +775,18 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
     s.dst_pinned = !dst_device && host_pinned(im.dst);
     s.dst_dev = s.dst_pinned && !(g_policy.load() & MXD_POLICY_NO_ZERO_COPY)
                     ? const_cast<uint8_t*>(host_device_ptr(im.dst)) : nullptr;
-    if (narrow) s.dst_pinned = false, s.dst_dev = nullptr;  // staged, then expanded into place
+    s.narrow = narrow_of(i);
+    if (s.narrow) s.dst_pinned = false, s.dst_dev = nullptr;  // staged, then expanded into place
     if (!dst_device && im.dst_stride < s.out_row)
       return fail(MXD_ERR_INVALID, "mxd: dst_stride smaller than an output row");
   }
-  const int32_t launch_dtype = narrow ? MXD_U8 : out_dtype;
-  for (int32_t i = 0; i < n; i++) st[i].stage_row = narrow ? st[i].out_row / 4 : st[i].out_row;
-  if (narrow) g_narrow_images.fetch_add(n, std::memory_order_relaxed);
+  int64_t nnarrow = 0;
+  for (int32_t i = 0; i < n; i++) {
+    st[i].stage_row = st[i].narrow ? st[i].out_row / 4 : st[i].out_row;
+    nnarrow += st[i].narrow ? 1 : 0;
+  }
+  if (nnarrow) g_narrow_images.fetch_add(nnarrow, std::memory_order_relaxed);
+  auto launch_dtype = [&](int32_t i) { return st[i].narrow ? MXD_U8 : out_dtype; };
   // Chunks of about kChunk staged bytes (at least one image each).  A JPEG
   // whose entropy decode runs on the device stages only its compressed
   // segments, and counts an eighth of its coefficient bytes (device memory):
@@ -839,7 +851,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
       const mxd_image& im = images[i];
       uint8_t* d = static_cast<uint8_t*>(im.dst);
       const uint8_t* src = sl.pin_out + st[i].out_off;
-      if (narrow) {
+      if (st[i].narrow) {
         for (int32_t r = 0; r < im.crop_h; r++)
           div255_row(src + (size_t)r * st[i].stage_row, reinterpret_cast<float*>(d + (size_t)r * im.dst_stride),
                      st[i].stage_row);
@@ -987,7 +999,7 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
           y.records = (int32_t)std::min<int64_t>(y.cr + (int64_t)y.cstride * y.dh, INT32_MAX);
           const Stored planes{sl.dev_mid + m.plane[0], m.stride[0], 0, 0, im.src_h,
                               reinterpret_cast<const mxd::YccDev*>(sl.dev_in + jc.ycc_off) + j};
-          if (y.cr + (int64_t)y.cstride * y.dh < INT32_MAX && ycc_plan_ok(dev_imgs[j], planes, launch_dtype, device)) {
+          if (y.cr + (int64_t)y.cstride * y.dh < INT32_MAX && ycc_plan_ok(dev_imgs[j], planes, launch_dtype(i), device)) {
             where[j] = planes;  // (dev_imgs[j] keeps the RGB frame's geometry, which run_batch validates)
             m.skip = 1;
             g_plane_sources.fetch_add(1, std::memory_order_relaxed);
@@ -1101,9 +1113,32 @@ int host_path(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
                                hipMemcpyHostToDevice, sl.stream));
     }
     if (sl.timed && !jpeg) MXD_HIP(hipEventRecord(sl.k0, sl.stream));
-    if (int rc = run_batch(dev_imgs.data(), cn, launch_dtype, device, sl.stream, where.data())) {
-      sl.timed = false;  // (k1 not recorded for this chunk)
-      return rc;
+    // one launch per output dtype (a chunk mixes them only when a share of
+    // its images is narrowed)
+    {
+      const int32_t first = chunks[k].first;
+      bool mixed = false;
+      for (int32_t i = first + 1; i < chunks[k].second; i++) mixed = mixed || st[i].narrow != st[first].narrow;
+      int rc = MXD_OK;
+      if (!mixed) {
+        rc = run_batch(dev_imgs.data(), cn, launch_dtype(first), device, sl.stream, where.data());
+      } else {
+        for (int part = 0; part < 2 && rc == MXD_OK; part++) {
+          std::vector<mxd_image> pi;
+          std::vector<Stored> pw;
+          for (int32_t j = 0; j < cn; j++)
+            if (st[first + j].narrow == (part == 0)) {
+              pi.push_back(dev_imgs[j]);
+              pw.push_back(where[j]);
+            }
+          if (!pi.empty())
+            rc = run_batch(pi.data(), (int32_t)pi.size(), part == 0 ? MXD_U8 : out_dtype, device, sl.stream, pw.data());
+        }
+      }
+      if (rc) {
+        sl.timed = false;  // (k1 not recorded for this chunk)
+        return rc;
+      }
     }
     if (sl.timed) MXD_HIP(hipEventRecord(sl.k1, sl.stream));
     if (!dst_device) {

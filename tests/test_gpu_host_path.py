@@ -231,8 +231,14 @@ def test_narrow_return_equals_f32_over_the_link():
         assert capi.narrow_returns(reset=True) == len(imgs)
         pinned_wide = run(capi.MXD_F32_DIV255, 1, pinned=True)
         assert capi.narrow_returns(reset=True) == 0
-        for a, b, c, d, e, u in zip(narrow, wide, padded, pinned, pinned_wide, u8):
+        # a share of the images narrowed (MXD_TUNE_F32_LINK 2..99): two
+        # launches per chunk, one per output dtype
+        half = run(capi.MXD_F32_DIV255, 50)
+        half_pinned = run(capi.MXD_F32_DIV255, 50, pinned=True)
+        assert capi.narrow_returns(reset=True) == 2 * (len(imgs) // 2)
+        for a, b, c, d, e, f, g, u in zip(narrow, wide, padded, pinned, pinned_wide, half, half_pinned, u8):
             assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d) and np.array_equal(a, e)
+            assert np.array_equal(a, f) and np.array_equal(a, g)
             assert np.array_equal(a.view(np.float32), lut[u])
     finally:
         for p in pins:
