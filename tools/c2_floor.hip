@@ -51,7 +51,12 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <int AUX, bool LOADS, bool STORES, bool VALU>
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// STORES: 0 none, 1 f32x3 per pixel (the kernel's: 12 B per lane, 2 stores per
+// strip row), 2 the same bytes as 16 B per lane (84 x 16 B per strip row: one
+// full-wave and one 20-lane store)
+template <int AUX, bool LOADS, int STORES, bool VALU>
 __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restrict__ src, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restri
       }
       const int want = (int)((row + d - r0) / 3.768f) + oy0;
       if (want > oy && oy < oy1) {
-        if constexpr (STORES) {
+        if constexpr (STORES == 1) {
           float* o = orow0 + (size_t)oy * (kOutRowBytes / 4);
 #pragma unroll
           for (int q = 0; q < 2; q++) {
@@ -109,12 +114,27 @@ __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restri
               __builtin_nontemporal_store(f32x3{acc[0][q], acc[1][q], acc[0][q + 2]},
                                           reinterpret_cast<f32x3*>(o + 3 * px));
           }
+        } else if constexpr (STORES == 2) {
+          float* o = orow0 + (size_t)oy * (kOutRowBytes / 4);
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const int c = lane + 64 * q;  // 16-B chunk of the 1,344-B strip row
+            if (c < 84)
+              __builtin_nontemporal_store(f32x4{acc[0][q], acc[1][q], acc[0][q + 2], acc[1][q + 2]},
+                                          reinterpret_cast<f32x4*>(o + 4 * c));
+          }
         }
         oy++;
       }
     }
   }
-  if (acc[0][0] == -1.0f) out[lane] = acc[1][1];
+  // keeps every accumulated byte live without storing (no-store variants)
+  float t = 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int i = 0; i < 12; i++) t += acc[h][i];
+  if (t == -1.0f) out[lane] = acc[1][1];
 }
 
 template <class K>
@@ -138,7 +158,7 @@ static float time_us(K kernel, unsigned char** src, float** out, int iters = 20,
   return t[t.size() / 2];
 }
 
-int main() {
+int main(int argc, char** argv) {
   unsigned char* src[2];
   float* out[2];
   const size_t sb = (size_t)kImgs * kRows * kStride, ob = (size_t)kImgs * kOutRows * kOutRowBytes;
@@ -154,12 +174,21 @@ int main() {
            alg / (us * 1e-6) / 1e12, alg / (us * 1e-6) / 8e12);
     fflush(stdout);
   };
+  const bool only16 = argc > 1 && argv[1][0] == 's';  // round 6, later: the store-width A/B only
   for (int round = 0; round < 2; round++) {
-    report("nt loads + nt stores", time_us(c2_floor<2, true, true, false>, src, out));
-    report("default loads + nt stores", time_us(c2_floor<0, true, true, false>, src, out));
-    report("nt loads, no stores", time_us(c2_floor<2, true, false, false>, src, out));
-    report("no loads, nt stores", time_us(c2_floor<2, false, true, false>, src, out));
-    report("nt loads + nt stores + V-pass VALU", time_us(c2_floor<2, true, true, true>, src, out));
+    if (!only16) {
+      report("nt loads + nt stores", time_us(c2_floor<2, true, 1, false>, src, out));
+      report("default loads + nt stores", time_us(c2_floor<0, true, 1, false>, src, out));
+      report("nt loads, no stores", time_us(c2_floor<2, true, 0, false>, src, out));
+      report("no loads, nt stores", time_us(c2_floor<2, false, 1, false>, src, out));
+      report("nt loads + nt stores + V-pass VALU", time_us(c2_floor<2, true, 1, true>, src, out));
+    }
+    report("nt loads + V-pass VALU, no stores", time_us(c2_floor<2, true, 0, true>, src, out));
+    report("default loads + V-pass VALU, no stores", time_us(c2_floor<0, true, 0, true>, src, out));
+    report("no loads, nt stores 12 B / lane", time_us(c2_floor<2, false, 1, false>, src, out));
+    report("no loads, nt stores 16 B / lane", time_us(c2_floor<2, false, 2, false>, src, out));
+    report("nt loads + nt stores 12 B / lane + V-pass VALU", time_us(c2_floor<2, true, 1, true>, src, out));
+    report("nt loads + nt stores 16 B / lane + V-pass VALU", time_us(c2_floor<2, true, 2, true>, src, out));
   }
   return 0;
 }
