@@ -7,6 +7,8 @@
 #      (tools/variants.sh build nosteal "-DMXD_STEAL=0" wave), the product with
 #      stealing off / on / fewest blocks 1 and 4, on C2 / C3 / C4 / C5
 # Output: gpurun_out/r06/<tag>_*.
+# (Runs against the stealing builds only -- commits 2f4a86b and the one after
+# it; the product reverted to the static units)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r06s}
