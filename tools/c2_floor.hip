@@ -56,13 +56,29 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // STORES: 0 none, 1 f32x3 per pixel (the kernel's: 12 B per lane, 2 stores per
 // strip row), 2 the same bytes as 16 B per lane (84 x 16 B per strip row: one
 // full-wave and one 20-lane store)
-template <int AUX, bool LOADS, int STORES, bool VALU>
+// MAP (round 6, later): how units map to workgroups -- 0 the kernel's (a
+// workgroup = 4 bands x 2 strips of one image, XCD-contiguous workgroups);
+// 1 a workgroup = the 8 bands of one strip; 2 as 0 without the XCD remap;
+// 3 a workgroup = one band x 2 strips of 4 consecutive images
+template <int AUX, bool LOADS, int STORES, bool VALU, int MAP = 0>
 __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restrict__ src, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
-  const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
+  const int wg = MAP == 2 ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int unit = __builtin_amdgcn_readfirstlane(wg * kWaves + (threadIdx.x >> 6));
   if (unit >= kUnits) return;
-  const int img = unit / (kBands * kStrips), rest = unit % (kBands * kStrips);
-  const int band = rest / kStrips, strip = rest % kStrips;
+  int img = unit / (kBands * kStrips), rest = unit % (kBands * kStrips);
+  int band = rest / kStrips, strip = rest % kStrips;
+  if constexpr (MAP == 1) {
+    strip = rest / kBands;
+    band = rest % kBands;
+  } else if constexpr (MAP == 3) {
+    // workgroup w: images 4 (w / 4) .. + 3, band w % 4 * 2 + (wave >> 2 & 1)?  simpler:
+    // unit u -> group of 64 units = 4 images x 8 bands x 2 strips, band-major
+    const int grp = unit / 64, r = unit % 64;
+    band = r / 8;
+    img = grp * 4 + (r % 8) / 2;
+    strip = r % 2;
+  }
   const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)img * kRows * kStride), (short)0,
                                                    kRows * kStride, 0x00020000);
   const int w0 = kFx0 + strip * kStripStep;
@@ -175,6 +191,18 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const bool only16 = argc > 1 && argv[1][0] == 's';  // round 6, later: the store-width A/B only
+  if (argc > 1 && argv[1][0] == 'm') {  // round 6, later: unit -> workgroup maps, loads only
+    for (int round = 0; round < 2; round++) {
+      report("map 0 (kernel's), loads + VALU", time_us(c2_floor<2, true, 0, true, 0>, src, out));
+      report("map 1 (strip-major WG), loads + VALU", time_us(c2_floor<2, true, 0, true, 1>, src, out));
+      report("map 2 (no XCD remap), loads + VALU", time_us(c2_floor<2, true, 0, true, 2>, src, out));
+      report("map 3 (4 images per band group), loads + VALU", time_us(c2_floor<2, true, 0, true, 3>, src, out));
+      report("map 1, loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 1>, src, out));
+      report("map 3, loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 3>, src, out));
+      report("map 0, loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 0>, src, out));
+    }
+    return 0;
+  }
   for (int round = 0; round < 2; round++) {
     if (!only16) {
       report("nt loads + nt stores", time_us(c2_floor<2, true, 1, false>, src, out));
