@@ -60,7 +60,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // workgroup = 4 bands x 2 strips of one image, XCD-contiguous workgroups);
 // 1 a workgroup = the 8 bands of one strip; 2 as 0 without the XCD remap;
 // 3 a workgroup = one band x 2 strips of 4 consecutive images
-template <int AUX, bool LOADS, int STORES, bool VALU, int MAP = 0>
+// RING: register ring slots (rows loaded RING - 1 ahead; the kernel's 4)
+// STRIDE: bytes between source rows (the 1280-pixel frame's 3,840; 2,560 =
+// the 844-pixel footprint rows nearly back to back, a diagnostic layout)
+template <int AUX, bool LOADS, int STORES, bool VALU, int MAP = 0, int RING = 4, int STRIDE = kStride>
 __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restrict__ src, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int wg = MAP == 2 ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
@@ -79,19 +82,19 @@ __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restri
     img = grp * 4 + (r % 8) / 2;
     strip = r % 2;
   }
-  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)img * kRows * kStride), (short)0,
-                                                   kRows * kStride, 0x00020000);
-  const int w0 = kFx0 + strip * kStripStep;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)img * kRows * STRIDE), (short)0,
+                                                   kRows * STRIDE, 0x00020000);
+  const int w0 = (STRIDE == kStride ? kFx0 : 0) + strip * kStripStep;
   const int v0 = w0 + 12 * lane, v1 = w0 + kHalf + 12 * lane;
   const int oy0 = band * (kOutRows / kBands), oy1 = oy0 + kOutRows / kBands;
   const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
   float* orow0 = out + ((size_t)img * kOutRows) * (kOutRowBytes / 4) + strip * (kOutRowBytes / 8);
-  constexpr int R = 4;
+  constexpr int R = RING;
   u32x3 ring[R][2];
   auto load = [&](int row, u32x3 (&d)[2]) {
     if constexpr (LOADS) {
-      d[0] = __builtin_amdgcn_raw_buffer_load_b96(r, v0 + row * kStride, 0, AUX);
-      d[1] = __builtin_amdgcn_raw_buffer_load_b96(r, v1 + row * kStride, 0, AUX);
+      d[0] = __builtin_amdgcn_raw_buffer_load_b96(r, v0 + row * STRIDE, 0, AUX);
+      d[1] = __builtin_amdgcn_raw_buffer_load_b96(r, v1 + row * STRIDE, 0, AUX);
     } else {
       d[0] = u32x3{(unsigned)row, 0u, 0u};
       d[1] = d[0];
@@ -115,6 +118,10 @@ __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restri
             acc[h][i] = __builtin_fmaf(f, 0.25f, acc[h][i]);
             acc[(h + 1) & 1][i] = __builtin_fmaf(f, 0.125f, acc[(h + 1) & 1][i]);
           }
+      } else if constexpr (STORES == 0) {
+        // no stores: every loaded dword kept live by an xor (minimal VALU)
+        const uint32_t k = x[0].x ^ x[0].y ^ x[0].z ^ x[1].x ^ x[1].y ^ x[1].z;
+        acc[0][0] = __uint_as_float(__float_as_uint(acc[0][0]) ^ k);
       } else {
         acc[0][0] += (float)(x[0].x & 255u);
         acc[1][0] += (float)(x[1].y >> 24);
@@ -151,6 +158,42 @@ __global__ __launch_bounds__(512, 2) void c2_floor(const unsigned char* __restri
 #pragma unroll
     for (int i = 0; i < 12; i++) t += acc[h][i];
   if (t == -1.0f) out[lane] = acc[1][1];
+}
+
+// The same units and rows, read as two b128 loads per lane (2 KiB per wave
+// per row, 16 B per lane) instead of two b96 (1.5 KiB): is the load width
+// part of the pattern's ceiling?  Minimal VALU, no stores; reports its own
+// byte count.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(512, 2) void c2_read128(const unsigned char* __restrict__ src, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
+  if (unit >= kUnits) return;
+  const int img = unit / (kBands * kStrips), rest = unit % (kBands * kStrips);
+  const int band = rest / kStrips, strip = rest % kStrips;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)img * kRows * kStride), (short)0,
+                                                   kRows * kStride, 0x00020000);
+  const int v0 = (kFx0 & ~15) + strip * 1280 + 16 * lane, v1 = v0 + 1024;
+  const int oy0 = band * (kOutRows / kBands), oy1 = oy0 + kOutRows / kBands;
+  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
+  constexpr int R = 4;
+  u32x4 ring[R][2];
+  auto load = [&](int row, u32x4 (&d)[2]) {
+    d[0] = __builtin_amdgcn_raw_buffer_load_b128(r, v0 + row * kStride, 0, 2);
+    d[1] = __builtin_amdgcn_raw_buffer_load_b128(r, v1 + row * kStride, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < R - 1; d++) load(min(r0 + d, r1 - 1), ring[d]);
+  uint32_t k = 0;
+  for (int row = r0; row < r1; row += R) {
+#pragma unroll
+    for (int d = 0; d < R; d++) {
+      load(min(row + d + R - 1, r1 - 1), ring[(d + R - 1) % R]);
+      const u32x4* x = ring[d];
+      k ^= x[0].x ^ x[0].y ^ x[0].z ^ x[0].w ^ x[1].x ^ x[1].y ^ x[1].z ^ x[1].w;
+    }
+  }
+  if (k == 0x12345678u) out[lane] = 1.0f;
 }
 
 template <class K>
@@ -191,6 +234,49 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const bool only16 = argc > 1 && argv[1][0] == 's';  // round 6, later: the store-width A/B only
+  if (argc > 1 && argv[1][0] == 'l') {  // round 6, later: the read pattern with minimal VALU
+    for (int round = 0; round < 2; round++) {
+      {
+        const float us = time_us(c2_read128, src, out);
+        // rows per unit as the kernel computes them, 2 KiB per wave per row
+        double bytes = 0;
+        for (int b = 0; b < kBands; b++) {
+          const int oy0 = b * (kOutRows / kBands), oy1 = oy0 + kOutRows / kBands;
+          const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = std::min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
+          bytes += (double)(r1 - r0) * 2048.0 * kStrips * kImgs;
+        }
+        printf("{\"probe\": \"b128 loads, 2 KiB per wave-row (xor)\", \"us\": %.1f, \"read_TBps\": %.3f}\n", us,
+               bytes / (us * 1e-6) / 1e12);
+        double b96 = bytes * 1536.0 / 2048.0;
+        printf("{\"probe\": \"(b96 pattern's bytes for comparison)\", \"bytes\": %.0f}\n", b96);
+        fflush(stdout);
+      }
+      report("loads only (xor, minimal VALU)", time_us(c2_floor<2, true, 0, false, 0, 4, 3840>, src, out));
+      report("loads + V-pass VALU", time_us(c2_floor<2, true, 0, true, 0, 4, 3840>, src, out));
+      report("loads only (xor), footprint-row stride", time_us(c2_floor<2, true, 0, false, 0, 4, 2560>, src, out));
+    }
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'p') {  // round 6, later: row stride (DRAM page use), loads only
+    for (int round = 0; round < 2; round++) {
+      report("stride 3840 (frame), loads + VALU", time_us(c2_floor<2, true, 0, true, 0, 4, 3840>, src, out));
+      report("stride 2560 (footprint rows), loads + VALU", time_us(c2_floor<2, true, 0, true, 0, 4, 2560>, src, out));
+      report("stride 3840 (frame), loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 0, 4, 3840>, src, out));
+      report("stride 2560 (footprint rows), loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 0, 4, 2560>, src, out));
+    }
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'r') {  // round 6, later: rows in flight per wave, loads only
+    for (int round = 0; round < 2; round++) {
+      report("ring 2, loads + VALU", time_us(c2_floor<2, true, 0, true, 0, 2>, src, out));
+      report("ring 4 (kernel's), loads + VALU", time_us(c2_floor<2, true, 0, true, 0, 4>, src, out));
+      report("ring 6, loads + VALU", time_us(c2_floor<2, true, 0, true, 0, 6>, src, out));
+      report("ring 8, loads + VALU", time_us(c2_floor<2, true, 0, true, 0, 8>, src, out));
+      report("ring 8, loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 0, 8>, src, out));
+      report("ring 4, loads + stores + VALU", time_us(c2_floor<2, true, 1, true, 0, 4>, src, out));
+    }
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'm') {  // round 6, later: unit -> workgroup maps, loads only
     for (int round = 0; round < 2; round++) {
       report("map 0 (kernel's), loads + VALU", time_us(c2_floor<2, true, 0, true, 0>, src, out));
