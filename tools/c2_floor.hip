@@ -196,6 +196,42 @@ __global__ __launch_bounds__(512, 2) void c2_read128(const unsigned char* __rest
   if (k == 0x12345678u) out[lane] = 1.0f;
 }
 
+// The kernel's bytes (1.5 KiB per wave-row, two strips) read as one b128
+// (the first KiB, 16 B per lane) and one b64 (the last 512 B, 8 B per lane)
+// per lane instead of two b96 halves: a byte-order lane layout's loads.
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(512, 2) void c2_read_b128_b64(const unsigned char* __restrict__ src, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int unit = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6));
+  if (unit >= kUnits) return;
+  const int img = unit / (kBands * kStrips), rest = unit % (kBands * kStrips);
+  const int band = rest / kStrips, strip = rest % kStrips;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)img * kRows * kStride), (short)0,
+                                                   kRows * kStride, 0x00020000);
+  const int w0 = ((kFx0 + strip * kStripStep) & ~15);
+  const int v0 = w0 + 16 * lane, v1 = w0 + 1024 + 8 * lane;
+  const int oy0 = band * (kOutRows / kBands), oy1 = oy0 + kOutRows / kBands;
+  const int r0 = kFy0 + (int)(oy0 * 3.768f), r1 = min(kFy1, kFy0 + (int)(oy1 * 3.768f) + 4);
+  constexpr int R = 4;
+  u32x4 a[R];
+  u32x2 b[R];
+  auto load = [&](int row, int slot) {
+    a[slot] = __builtin_amdgcn_raw_buffer_load_b128(r, v0 + row * kStride, 0, 2);
+    b[slot] = __builtin_amdgcn_raw_buffer_load_b64(r, v1 + row * kStride, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < R - 1; d++) load(min(r0 + d, r1 - 1), d);
+  uint32_t k = 0;
+  for (int row = r0; row < r1; row += R) {
+#pragma unroll
+    for (int d = 0; d < R; d++) {
+      load(min(row + d + R - 1, r1 - 1), (d + R - 1) % R);
+      k ^= a[d].x ^ a[d].y ^ a[d].z ^ a[d].w ^ b[d].x ^ b[d].y;
+    }
+  }
+  if (k == 0x12345678u) out[lane] = 1.0f;
+}
+
 template <class K>
 static float time_us(K kernel, unsigned char** src, float** out, int iters = 20, int reps = 7) {
   hipEvent_t e0, e1;
@@ -234,6 +270,13 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const bool only16 = argc > 1 && argv[1][0] == 's';  // round 6, later: the store-width A/B only
+  if (argc > 1 && argv[1][0] == 'w') {  // round 6, later: load widths for the kernel's 1.5-KiB wave-rows
+    for (int round = 0; round < 3; round++) {
+      report("2 x b96 (the kernel's), loads only (xor)", time_us(c2_floor<2, true, 0, false, 0, 4, 3840>, src, out));
+      report("b128 + b64, loads only (xor)", time_us(c2_read_b128_b64, src, out));
+    }
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'l') {  // round 6, later: the read pattern with minimal VALU
     for (int round = 0; round < 2; round++) {
       {

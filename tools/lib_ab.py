@@ -33,7 +33,7 @@ import band_sweep  # noqa: E402
 
 
 # "NAME@knob=v,knob=v": a library with tuning knobs set around its runs
-KNOBS = {"load": 12}
+KNOBS = {"load": 12, "policy": -1}  # -1: mxd_set_kernel_policy
 
 
 def parse_variant(spec):
@@ -86,9 +86,15 @@ def main():
                 # the previous variant's knobs back to 0, this one's set
                 if cur["n"] is not None:
                     for k in knobs[cur["n"]]:
-                        libs[cur["n"]].mxd_set_tuning(k, 0)
+                        if k < 0:
+                            libs[cur["n"]].mxd_set_kernel_policy(args.policy)
+                        else:
+                            libs[cur["n"]].mxd_set_tuning(k, 0)
                 for k, v in knobs[n].items():
-                    L.mxd_set_tuning(k, v)
+                    if k < 0:
+                        L.mxd_set_kernel_policy(v)
+                    else:
+                        L.mxd_set_tuning(k, v)
                 cur["n"] = n
             rc = L.mxd_resize_crop_batch(sets[i % 2][2], sets[i % 2][3], mode, 0, hs)
             if rc != 0:
