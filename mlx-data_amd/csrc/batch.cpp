@@ -528,7 +528,7 @@ int run_batch(const mxd_image* images, int32_t n, int32_t out_dtype, int32_t dev
         if (!sc)
           if (int rc = scatter_schedule(device, *p.yt, im.src_h, im.resize_h, im.crop_y, im.crop_h, d.ty,
                                        ScatterShape{p.s, p.dmax, p.p,
-                                                    p.ycc ? mxd::kYccLaneBytes : mxd::wave_byte_lanes(channels, p.pp) ? p.pp : p.pp * channels},
+                                                    p.ycc ? mxd::kYccLaneBytes : p.pp == 16 ? 16 : p.pp * channels},
                                        &sc))
             return rc;
         d.ytab = reinterpret_cast<const float*>(sc->ptr);

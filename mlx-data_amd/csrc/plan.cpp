@@ -293,9 +293,9 @@ bool wave_layout_ok(const mxd_image& im, const Stored& st, int32_t out_dtype) {
 // aligned stored base), fits the byte window, and its 16-byte chunks rounded
 // up stay inside the row stride (so the last stored row never reads past the
 // buffer's records).  Fewest strips first, then the smallest q.
-bool wave_strips_bytes(const DevTable& xt, const mxd_image& im, const Stored& st, int32_t pp, int32_t* nstrips,
-                       int32_t* tx, int32_t* q) {
-  const int32_t c = im.channels, win = mxd::wave_byte_window(pp);
+bool wave_strips_bytes(const DevTable& xt, const mxd_image& im, const Stored& st, int32_t* nstrips, int32_t* tx,
+                       int32_t* q) {
+  const int32_t c = im.channels, win = mxd::wave_byte_window();
   const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(st.base) & 3);
   int32_t best = 0;
   for (int32_t qq : {1, 2, 4}) {
@@ -451,7 +451,7 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
   // 0.0908 vs 0.0977 ms, profiles/r03/c3_layouts.jsonl).
   if (c == 3 && sh.s > 0 && !(policy & (MXD_POLICY_NO_BYTES | MXD_POLICY_NARROW))) {
     int32_t ns = 0, tx = 0, q = 0, bt = 0, bd = 0;
-    if (wave_strips_bytes(*p.xt, im, st, 16, &ns, &tx, &q) &&
+    if (wave_strips_bytes(*p.xt, im, st, &ns, &tx, &q) &&
         ((policy & MXD_POLICY_BYTES) || !p.wave || p.kind != 2 || (p.pp == 8 && ns <= p.nstrips && q <= 2)) &&
         scatter_kernel_for(c, f32, p.xt->width, sh, q, 0, 16, &bt, &bd)) {
       p.wave = true;
@@ -465,23 +465,6 @@ void plan_wave(const mxd_image& im, const Stored& st, int32_t f32, int32_t out_d
       p.s = sh.s;
       p.dmax = bd;
       p.p = sh.p;
-    }
-  }
-  // RGB scatter still on wide pixel lanes (P = 8): the same 1.5-KiB window read as
-  // wide byte lanes (P = 24: a b128 and a b64 per lane instead of two 12-byte
-  // loads; round 6) when it takes no more strips at the same q.
-  // MXD_POLICY_NO_BYTES keeps pixel lanes.
-  if (c == 3 && p.wave && p.kind == 2 && p.pp == 8 && !(policy & (MXD_POLICY_NO_BYTES | MXD_POLICY_NARROW))) {
-    int32_t ns = 0, tx = 0, q = 0, bt = 0, bd = 0;
-    if (wave_strips_bytes(*p.xt, im, st, 24, &ns, &tx, &q) && ns <= p.nstrips && q <= p.q &&
-        scatter_kernel_for(c, f32, p.xt->width, sh, q, 0, 24, &bt, &bd)) {
-      p.nstrips = ns;
-      p.tx = tx;
-      p.q = q;
-      p.pp = 24;
-      p.shift = 0;
-      p.bucket = bt;
-      p.dmax = bd;
     }
   }
 }

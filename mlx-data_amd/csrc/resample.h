@@ -135,10 +135,10 @@ int wave_taps_bucket(int taps);            // supported padded tap count >= taps
 int wave_default_p(int channels);          // source pixels per lane of the gather kernels
 int wave_window_px(int channels, int p);   // source pixels one wave covers per row
 int wave_window_align(int channels);       // window start alignment (pixels)
-// RGB with p = 16 / 24: byte lanes (p bytes per lane, a wave_byte_window(p)-byte
+// RGB with p = 16: byte lanes (16 bytes per lane, a wave_byte_window()-byte
 // window starting at a 16-byte boundary past the 4-byte aligned base).
 bool wave_byte_lanes(int channels, int p);
-int wave_byte_window(int p);
+int wave_byte_window();
 int wave_plane_floats(int channels, int p);  // LDS floats per wave
 int wave_lanes();
 int launch_wave(const WaveCfg& cfg, const ImgDev* imgs, void* stream);

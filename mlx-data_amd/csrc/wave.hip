@@ -166,23 +166,13 @@ enum Kind { kGather = 0, kScatter = 2 };
 // per wave-instruction; the V pass runs on bytes in memory order (it is
 // per-byte anyway) and the LDS row keeps that order, so the H pass reads
 // channel c of pixel x at float C x + c.
-//
-// Wide byte lanes (RGB with P = 24, round 6): 24 bytes per lane over a 1.5-KiB
-// window -- lane l owns the 16 bytes at 16 l of its first KiB (one b128) and
-// the 8 bytes at 1024 + 8 l of its last 512 (one b64) -- the window of pixel
-// lanes at P = 8 with byte lanes' V pass, LDS order and H pass.  The same
-// bytes in the same sums; the loads are 16- and 8-byte ones instead of two
-// 12-byte ones, which C2's access pattern reads 11 % faster (tools/c2_floor,
-// profiles/r06/r06r_width.jsonl).
 template <int C_, int P_ = (C_ == 1 ? 16 : C_ == 2 ? 8 : 4)>
 struct Lay {
   static constexpr int C = C_;
   static constexpr int P = P_;
-  static constexpr bool B = C == 3 && (P == 16 || P == 24);  // byte lanes
-  static constexpr bool BSPLIT = C == 3 && P == 24;           // wide byte lanes: b128 + b64
-  static constexpr int BHEAD = 16;                           // BSPLIT: bytes per lane in the first KiB
-  static constexpr int VC = B ? 1 : C;                       // V-pass planes
-  static constexpr int LB = B ? P : P * C;                   // bytes per lane
+  static constexpr bool B = C == 3 && P == 16;  // byte lanes
+  static constexpr int VC = B ? 1 : C;          // V-pass planes
+  static constexpr int LB = B ? 16 : P * C;     // bytes per lane
   static constexpr int ND = LB / 4;             // dwords per lane
   static constexpr int VP = LB / VC;            // V-pass values per lane and plane
   static constexpr int WPX = kLanes * VP;       // window pixels (byte lanes: bytes)
@@ -303,12 +293,6 @@ struct Src {
     // unsigned: a row above the region wraps to a huge (out-of-range) offset
     const int off = (int)((uint32_t)voff + roff);
     Raw<ND> x;
-    if constexpr (L::BSPLIT) {
-      static_assert(!SHIFT, "byte lanes: the base offset folds into the H-pass positions");
-      load_dwords<L::BHEAD / 4, AUX>(rs, off, 0, x.d);
-      load_dwords<ND - L::BHEAD / 4, AUX>(rs, (int)((uint32_t)voff2 + roff), 0, x.d + L::BHEAD / 4);
-      return x;
-    }
     if constexpr (L::SPLIT) {
       const int off2 = (int)((uint32_t)voff2 + roff);
       constexpr int NH = ND / 2;
@@ -442,11 +426,7 @@ __device__ __forceinline__ void write_planes(float* planes, const float (&acc)[L
   for (int c = 0; c < C; c++)
 #pragma unroll
     for (int p = 0; p < P; p += 4)
-      *reinterpret_cast<f32x4*>(planes + c * L::PL +
-                                (L::BSPLIT ? (p < L::BHEAD ? L::BHEAD * lane + p
-                                                           : L::BHEAD * kLanes + (P - L::BHEAD) * lane + p - L::BHEAD)
-                                 : L::SPLIT ? (p / 4) * 4 * kLanes + 4 * lane
-                                            : P * lane + p)) =
+      *reinterpret_cast<f32x4*>(planes + c * L::PL + (L::SPLIT ? (p / 4) * 4 * kLanes + 4 * lane : P * lane + p)) =
           f32x4{acc[c][p], acc[c][p + 1], acc[c][p + 2], acc[c][p + 3]};
 }
 
@@ -619,7 +599,7 @@ __device__ __forceinline__ void scatter_band(kint* sched, int entry_off, const S
 
 // bytes per lane of Lay<c, p> (a plain function: template arguments do not
 // parse inside __launch_bounds__)
-constexpr int lane_bytes(int c, int p) { return c == 3 && (p == 16 || p == 24) ? p : p * c; }
+constexpr int lane_bytes(int c, int p) { return c == 3 && p == 16 ? 16 : p * c; }
 
 // Minimum waves per SIMD the register allocation must allow, by lane width.
 constexpr int min_waves(int c, int p, int kind, int dmax) {
@@ -689,13 +669,7 @@ __device__ __forceinline__ void run_unit(const ImgDev* __restrict__ imgs, int ni
       const int b0 = ((lo - sx0) * C + shift) & ~15;
       const int nb = (hi + 1 - sx0) * C + shift - b0;
       src.sh = 0;
-      if constexpr (L::BSPLIT) {
-        constexpr int TB = L::LB - L::BHEAD;  // bytes per lane past the first KiB
-        src.voff = L::BHEAD * lane < nb ? b0 + L::BHEAD * lane : kNoLoad;
-        src.voff2 = L::BHEAD * kLanes + TB * lane < nb ? b0 + L::BHEAD * kLanes + TB * lane : kNoLoad;
-      } else {
-        src.voff = L::LB * lane < nb ? b0 + L::LB * lane : kNoLoad;
-      }
+      src.voff = L::LB * lane < nb ? b0 + L::LB * lane : kNoLoad;
       hbase = sx0 * C - shift + b0;
     } else {
       constexpr int A = C == 2 ? 2 : C == 4 ? 1 : 4;  // wp0 * C a multiple of 4
@@ -929,23 +903,6 @@ WaveKernel select_scatter(const WaveCfg& cfg) {
   MXD_SCATTER_B(2, 2, 3, 2)
   MXD_SCATTER_B(3, 1, 2, 4)     // upsampling (200 -> 256)
 #endif
-  // wide byte lanes (P = 24): 1.5-KiB windows, the P = 8 pixel lanes' shapes
-#define MXD_SCATTER_W(S_, D_, T_, Q_)                                                             \
-  if (cfg.s == S_ && cfg.dmax == D_ && cfg.taps == T_ && cfg.q == Q_ && cfg.p == 24 && !cfg.ycc)  \
-    return cfg.nt ? resample_wave<3, 24, F32, T_, Q_, kScatter, S_, D_, false, false, kLoadNt>    \
-                  : resample_wave<3, 24, F32, T_, Q_, kScatter, S_, D_, false>;
-  MXD_SCATTER_W(2, 4, 8, 2)     // 960 -> 256 (C2)
-#ifndef MXD_ONLY_C2
-  MXD_SCATTER_W(2, 5, 10, 2)    // 1080 -> 256, 2160 -> 512 (C5)
-  MXD_SCATTER_W(2, 6, 12, 2)    // 1440 -> 256
-  MXD_SCATTER_W(2, 9, 17, 1)    // 2160 -> 256
-  MXD_SCATTER_W(2, 3, 6, 2)     // 720 -> 256
-  MXD_SCATTER_W(2, 2, 4, 4)     // 480 -> 256
-  MXD_SCATTER_W(2, 2, 3, 4)     // 375 / 333 -> 256
-  MXD_SCATTER_W(2, 12, 24, 1)   // 12 MP -> 256 (C6)
-  MXD_SCATTER_W(2, 16, 32, 1)   // 24 MP -> 256 (C7)
-#endif
-#undef MXD_SCATTER_W
 #undef MXD_SCATTER_B
 #undef MXD_SCATTER
   return nullptr;
@@ -990,12 +947,12 @@ int wave_window_px(int channels, int p) { return kLanes * p; }
 
 int wave_window_align(int channels) { return channels == 2 ? 2 : channels == 4 ? 1 : 4; }
 
-bool wave_byte_lanes(int channels, int p) { return channels == 3 && (p == 16 || p == 24); }
+bool wave_byte_lanes(int channels, int p) { return channels == 3 && p == 16; }
 
-int wave_byte_window(int p) { return kLanes * p; }
+int wave_byte_window() { return kLanes * 16; }
 
 int wave_plane_floats(int channels, int p) {
-  if (wave_byte_lanes(channels, p)) return p == 24 ? plane_floats<3, 24>() : plane_floats<3, 16>();
+  if (wave_byte_lanes(channels, p)) return plane_floats<3, 16>();
   return channels * (kLanes * p + kPad);
 }
 

@@ -122,13 +122,10 @@ def test_rgb_scatter_lane_layouts():
     three with byte lanes; ImageNet shapes (C4) two 256-pixel strips (one
     wide strip would run at 2-3 waves per SIMD, profiles/r03/onestrip.jsonl),
     one 1-KiB byte-lane strip when forced (profiles/r02/bytes_ab.txt).  MXD_POLICY_NO_BYTES keeps pixel lanes,
-    MXD_POLICY_BYTES takes byte lanes wherever a kernel exists.  Round 6: a
-    crop left on wide pixel lanes reads the same 1.5-KiB windows as wide byte
-    lanes (p = 24: a b128 and a b64 per lane) when they take no more strips."""
+    MXD_POLICY_BYTES takes byte lanes wherever a kernel exists."""
     p = _plan(_entry())
     assert (p["wave"], p["kind"], p["taps"], p["s"], p["dmax"]) == (1, 2, 8, 2, 4)
-    assert (p["p"], p["nstrips"], p["q"]) == (24, 2, 2)
-    assert (_plan(_entry(), capi.MXD_POLICY_NO_BYTES)["p"], _plan(_entry(), capi.MXD_POLICY_NO_BYTES)["nstrips"]) == (8, 2)
+    assert (p["p"], p["nstrips"], p["q"]) == (8, 2, 2)
     b = _plan(_entry(), capi.MXD_POLICY_BYTES)
     assert (b["p"], b["nstrips"], b["q"]) == (16, 3, 2)
     hd = _entry(1280, 720, 3840, 455, 256, cx=(455 - 224) // 2)
@@ -170,7 +167,7 @@ def test_every_downscale_ratio_up_to_16_has_a_wave_kernel():
         assert p["wave"] == 1 and p["kind"] == 2, (side, p)
         assert p["taps"] >= cnt.max(), (side, p)
     p = _plan(_entry(4032, 3024, 4032 * 3, 341, 256, cx=58, cy=16))
-    assert (p["taps"], p["dmax"], p["p"], p["nstrips"]) == (24, 12, 24, 6)
+    assert (p["taps"], p["dmax"], p["p"], p["nstrips"]) == (24, 12, 8, 6)
     p = _plan(_entry(6000, 4000, 6000 * 3, 384, 256, cx=80, cy=16))
     assert (p["taps"], p["dmax"]) == (32, 16)
 

@@ -28,8 +28,6 @@ KINDS = [
     ("nt_default", capi.MXD_POLICY_AUTO, 2),
     ("nt_pixel_lanes", capi.MXD_POLICY_NO_BYTES, 2),
     ("nt_byte_lanes", capi.MXD_POLICY_BYTES, 2),
-    # round 6: "default" now reads wide-pixel-lane crops as wide byte lanes
-    # (p = 24); pixel_lanes / nt_pixel_lanes (MXD_POLICY_NO_BYTES) keep p = 8
 ]
 
 
