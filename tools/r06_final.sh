@@ -25,6 +25,9 @@ for w in ${LOAD_AB:-}; do
   run load_ab_$w 200 python tools/band_sweep.py --workload $w --reps 5 --set load=0 --set load=1 --set load=2
 done
 run bench 600 python bench.py
+# the launcher the driver uses for N > 1, here with one rank (the only GPU)
+run bench_torchrun 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu --no-e2e --no-e2e-jpeg --no-others
 run bench_1stream 300 python bench.py --streams 1 --no-cpu --no-e2e --no-e2e-jpeg --no-others
 FLAGS="--no-cpu --no-e2e --no-e2e-jpeg --no-others"
 run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run -- python3 bench.py $FLAGS
